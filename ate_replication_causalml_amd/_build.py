@@ -1,0 +1,92 @@
+"""In-tree build of the native libraries.
+
+* ``_lib/libatehip.so`` — every ``csrc/*.hip`` file compiled for gfx950 with hipcc
+  (cross-compiles without a GPU) and linked into one shared object.
+* ``_lib/libatecpu.so`` — host C++ (``csrc/cpu/*.cpp``): CPU forest engine used by
+  the float64 reference path and as a host runtime.
+
+Usage: ``python -m ate_replication_causalml_amd._build`` (or ``__graft_entry__.build()``).
+Object files are cached under ``build/`` keyed by source mtime.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+LIBDIR = Path(__file__).resolve().parent / "_lib"
+BUILD = ROOT / "build"
+ARCH = os.environ.get("ATE_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-ffp-contract=fast", "-Wno-unused-result"]
+CPU_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-march=x86-64-v2"]
+
+
+def _headers(d: Path):
+    return [p for p in d.glob("*.hpp")] + [p for p in d.glob("*.h")]
+
+
+def _stale(obj: Path, deps) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build_hip(verbose: bool = False) -> Path:
+    srcs = sorted(CSRC.glob("*.hip"))
+    hdrs = _headers(CSRC)
+    BUILD.mkdir(exist_ok=True)
+    LIBDIR.mkdir(exist_ok=True)
+    objs = []
+    jobs = []
+    for s in srcs:
+        o = BUILD / (s.stem + ".hip.o")
+        objs.append(o)
+        if _stale(o, [s, *hdrs, Path(__file__)]):
+            jobs.append([HIPCC, *HIP_FLAGS, "-I", str(CSRC), "-c", str(s), "-o", str(o)])
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        list(ex.map(_run, jobs))
+    lib = LIBDIR / "libatehip.so"
+    if jobs or not lib.exists():
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)])
+    if verbose:
+        print(f"built {lib} ({len(jobs)} recompiled)")
+    return lib
+
+
+def build_cpu(verbose: bool = False) -> Path:
+    cdir = CSRC / "cpu"
+    srcs = sorted(cdir.glob("*.cpp"))
+    LIBDIR.mkdir(exist_ok=True)
+    lib = LIBDIR / "libatecpu.so"
+    if not srcs:
+        return lib
+    deps = [*srcs, *_headers(cdir), *_headers(CSRC), Path(__file__)]
+    if _stale(lib, deps):
+        _run(["g++", *CPU_FLAGS, "-I", str(CSRC), "-shared", "-o", str(lib), *map(str, srcs)])
+    if verbose:
+        print(f"built {lib}")
+    return lib
+
+
+def build_all(verbose: bool = False):
+    return build_hip(verbose), build_cpu(verbose)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True)
+    sys.exit(0)

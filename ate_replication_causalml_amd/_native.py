@@ -1,0 +1,122 @@
+"""ctypes bindings of the in-tree native libraries.
+
+``hip()`` returns the gfx950 kernel library (``_lib/libatehip.so``). It is loaded
+lazily, after ``import torch`` (torch's HIP runtime is the one the process uses;
+both share the ``libamdhip64.so.7`` soname). If the library is missing while a GPU
+op is requested, :class:`NativeMissing` is raised — there is no silent fallback.
+``cpu()`` returns the host C++ library (forest engine).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_LIBDIR = Path(__file__).resolve().parent / "_lib"
+_hip = None
+_cpu = None
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int64 = ctypes.c_int64
+c_uint64 = ctypes.c_uint64
+c_double = ctypes.c_double
+
+# name -> argtypes (restype int). 'p' pointer, 'i' int32, 'l' int64, 'u' uint64, 'd' double
+_SIGS = {
+    "ate_gram_bf16": "plipipipippp",
+    "ate_gram_f32": "plippipipipppp",
+    "ate_gram_f64": "plippipipipppp",
+    "ate_gram_tile_sizes": "pppp",
+    "ate_chol_solve": "pipiipdpppppp",
+    "ate_predict": "ipllppiidipp",
+    "ate_irls_update": "ipllppiiiiippppipp",
+    "ate_irls_check": "piidippp",
+    "ate_naive": "ippplpppp",
+    "ate_clip_propensity": "pplpp",
+    "ate_aipw": "ppppppldpppp",
+    "ate_dml_moments": "ppplppp",
+    "ate_dml_finalize": "pipp",
+    "ate_boot_multinomial": "ppluiipp",
+    "ate_boot_poisson": "ppluiilipp",
+    "ate_enet_prepare": "piipipiipippppppppp",
+    "ate_enet_path": "ppiippppidddipppppip",
+    "ate_enet_coef": "ppiiiipppppppp",
+    "ate_enet_cvloss_gauss": "pippiipppiipp",
+    "ate_cv_select": "pppiipipppp",
+    "ate_enet_pick": "ppiiiipp",
+    "ate_dml_resid_moments": "iplpipipiiiiiippp",
+    "ate_dgp_fill": "ipllllu" + "iip",
+}
+_CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}
+
+
+def _load(path: Path, sigs: dict):
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    for name, sig in sigs.items():
+        if hasattr(lib, name):
+            f = getattr(lib, name)
+            f.restype = c_int
+            f.argtypes = [_CT[ch] for ch in sig]
+    return lib
+
+
+def hip_available() -> bool:
+    return (_LIBDIR / "libatehip.so").exists()
+
+
+def hip():
+    """The gfx950 kernel library; raises NativeMissing if it was not built."""
+    global _hip
+    if _hip is None:
+        import torch  # noqa: F401  (ensure torch's HIP runtime is loaded first)
+        p = _LIBDIR / "libatehip.so"
+        if not p.exists():
+            raise NativeMissing(
+                f"{p} not found: build it with `python -m ate_replication_causalml_amd._build` "
+                "(hipcc --offload-arch=gfx950). GPU ops have no fallback.")
+        _hip = _load(p, _SIGS)
+    return _hip
+
+
+def cpu():
+    global _cpu
+    if _cpu is None:
+        p = _LIBDIR / "libatecpu.so"
+        if not p.exists():
+            from ._build import build_cpu
+            build_cpu()
+        _cpu = _load(p, {})
+    return _cpu
+
+
+def check(rc: int, name: str = "native call"):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def call(name: str, *args):
+    """Invoke a kernel-library entry point and raise on a non-zero status."""
+    f = getattr(hip(), name)
+    rc = f(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+    return rc
+
+
+def loaded_libraries():
+    """Paths of in-tree native libraries mapped into this process (diagnostics)."""
+    out = []
+    try:
+        with open(f"/proc/{os.getpid()}/maps") as f:
+            for line in f:
+                if str(_LIBDIR) in line:
+                    out.append(line.split()[-1])
+    except OSError:
+        pass
+    return sorted(set(out))

@@ -1,0 +1,168 @@
+"""Device LASSO-family estimators: E5 single-equation LASSO, E6 usual LASSO,
+E11 Belloni post-double-selection, and the K-fold cross-fit DML (partially
+linear model) with CV-LASSO nuisances — the north-star estimator.
+
+All LASSO fits run on the per-fold Gram stack (K01, one pass over the panel)
+followed by on-device coordinate descent, CV loss and lambda selection (K08/K09).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..ops import stats as S
+from ..ops.enet import cv_enet_gaussian
+from ..ops.gram import gram
+from ..ops.linalg import chol_solve
+from ..ops.panel import build_panel, dtype_code
+from ..parallel import rng
+from ..reference.estimators import lambda_interp
+from ..result import AteResult
+from .common import as_np, read_result, resolve_device
+
+
+def _lasso_w_coef(Y, W, X, pf_w, seed, nfolds, fold_stream, device, dtype):
+    dev = resolve_device(device)
+    Xn = np.column_stack([as_np(X), as_np(W)])
+    n, pp = Xn.shape
+    fid = rng.fold_ids(n, nfolds, seed, fold_stream)
+    pan = build_panel(Xn, None, as_np(Y), folds=fid, dtype=dtype, device=dev)
+    G = gram(pan)
+    pf = np.r_[np.ones(pp - 1), pf_w]
+    cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf)
+    return cv
+
+
+def lasso_single(Y, W, X, seed=1991, nfolds=10, fold_stream=5, method="Single-equation LASSO",
+                 device=None, dtype="f64"):
+    """E5 ``ate_condmean_lasso`` (ate_functions.R:89-108): W unpenalised, coef at lambda.1se."""
+    cv = _lasso_w_coef(Y, W, X, 0.0, seed, nfolds, fold_stream, device, dtype)
+    return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
+                          lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
+
+
+def lasso_usual(Y, W, X, seed=1991, nfolds=10, fold_stream=6, method="Usual LASSO", device=None,
+                dtype="f64"):
+    """E6 ``ate_lasso`` (ate_functions.R:111-130): W penalised."""
+    cv = _lasso_w_coef(Y, W, X, 1.0, seed, nfolds, fold_stream, device, dtype)
+    return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
+                          lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
+
+
+def interaction_expand(x: torch.Tensor) -> torch.Tensor:
+    """K21 (small p): [x, x_c1 * x_c2 for all ordered pairs incl. squares] (Q10)."""
+    n, p = x.shape
+    return torch.cat([x, (x[:, :, None] * x[:, None, :]).reshape(n, p * p)], 1)
+
+
+def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni et.al",
+            device=None, dtype="f64"):
+    """E11 ``belloni`` (ate_functions.R:286-328) with quirks Q10-Q13."""
+    dev = resolve_device(device)
+    Yn, Wn = as_np(Y), as_np(W)
+    xint = interaction_expand(torch.as_tensor(as_np(X), device=dev)).cpu().numpy()
+    n, q = xint.shape
+    fits = []
+    for target, stream in ((Wn, 8), (Yn, 9)):
+        fid = rng.fold_ids(n, nfolds, seed, stream)
+        pan = build_panel(xint, None, target, folds=fid, dtype=dtype, device=dev)
+        G = gram(pan)
+        fits.append((pan, G, cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]])))
+    (_, _, cw), (_, _, cy) = fits
+    s = float(cw.lambdas[0, int(cw.sel[0, 0])])
+    lw = cw.lambdas[0, :int(cw.nlam[0])].cpu().numpy()
+    ly = cy.lambdas[0, :int(cy.nlam[0])].cpu().numpy()
+    pw = cw.coef_path[0, :len(lw)].cpu().numpy()
+    py = cy.coef_path[0, :len(ly)].cpu().numpy()
+
+    def coef_at(lams, path, s_):
+        l, r, f = lambda_interp(lams, s_)
+        return path[l] * f + path[r] * (1 - f)
+
+    bw = coef_at(lw, pw, s)[1:]
+    by = coef_at(ly, py, s if compat == "reference" else float(cy.lambdas[0, int(cy.sel[0, 0])]))[1:]
+    if compat == "reference":
+        union = []
+        for v in np.concatenate([np.flatnonzero(bw > 0) + 1, np.flatnonzero(by > 0) + 1]):
+            if int(v) not in union:
+                union.append(int(v))
+        cols = [v - 2 for v in union if v - 1 >= 1]        # Q13 shift, index 0 dropped
+    else:
+        cols = sorted(set(np.flatnonzero(bw != 0)) | set(np.flatnonzero(by != 0)))
+    # post-selection OLS: y ~ 1 + x_int[:, cols] + W
+    pan = build_panel(np.column_stack([xint[:, cols], Wn]), None, Yn, dtype=dtype, device=dev)
+    G = gram(pan)[0]
+    dcols = [pan.cols["one"], *pan.xcols]
+    r = chol_solve(G, dcols, pan.cols["Y"])
+    se = torch.sqrt(r.aux[1] / (pan.n - r.aux[0]) * r.invdiag[-1])
+    return read_result(torch.stack([r.beta[-1], se]), method, n_selected=len(cols),
+                       rank=int(r.aux[0]))
+
+
+# ---------------------------------------------------------------- K-fold DML (PLR)
+def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None):
+    """DML-PLR on a fold-segmented panel (segment k = fold k). Returns (res[2], moments[7], cv).
+
+    comm: optional parallel.comm.Communicator — each rank holds a row shard of every
+    fold; the fold Gram stack and the score moments are all-reduced (C01, C06)."""
+    if G is None:
+        G = gram(pan)
+    if comm is not None and comm.world_size > 1:
+        comm.all_reduce_(G)
+    K = folds
+    full_sets = [[s for s in range(K) if s != k] for k in range(K)]
+    ycols = [pan.cols["Y"], pan.cols["W"]]
+    cv = cv_enet_gaussian(G, pan, pan.xcols, ycols, full_sets=full_sets)
+    coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1).contiguous()
+    mom = dml_residual_moments(pan, coef)
+    if comm is not None and comm.world_size > 1:
+        comm.all_reduce_(mom)
+    res = S.dml_finalize(mom, "plr")
+    return res, mom, cv
+
+
+def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
+    """Fused held-out residual pass (csrc/dml.hip) -> 7 fp64 moments."""
+    K = coef.shape[0]
+    p = len(pan.xcols)
+    if not pan.data.is_cuda:
+        X = pan.data.double()
+        moms = torch.zeros(7, dtype=torch.float64)
+        for k in range(K):
+            r0, r1 = pan.seg_bounds[k]
+            Xs = X[:, r0:r1]
+            v = Xs[pan.cols["one"]] != 0
+            xs = Xs[pan.xcols]
+            yv, wv = Xs[pan.cols["Y"]], Xs[pan.cols["W"]]
+            yr = yv - (coef[k, 0, 0] + coef[k, 0, 1:] @ xs)
+            wr = wv - (coef[k, 1, 0] + coef[k, 1, 1:] @ xs)
+            moms += S.dml_moments(yr[v], wr[v])
+        return moms
+    dev = pan.device
+    xc = torch.tensor(pan.xcols, dtype=torch.int32, device=dev)
+    segs = torch.tensor(np.asarray(pan.seg_bounds[:K], dtype=np.int64), device=dev)
+    nbx = 256
+    part = torch.empty(K * nbx * 7, dtype=torch.float64, device=dev)
+    mom = torch.empty(7, dtype=torch.float64, device=dev)
+    bf = pan.dtype == torch.bfloat16
+    # binary Y/W are exact in bf16; continuous targets use the hi+lo split columns
+    y0, y1 = (pan.cols["Y_hi"], pan.cols["Y_lo"]) if bf else (pan.cols["Y"], -1)
+    w0, w1 = (pan.cols["W_hi"], pan.cols["W_lo"]) if bf else (pan.cols["W"], -1)
+    _native.call("ate_dml_resid_moments", dtype_code(pan.data), pan.data.data_ptr(), pan.ld,
+                 xc.data_ptr(), p, segs.data_ptr(), K, coef.data_ptr(), y0, y1, w0, w1,
+                 pan.cols["one"], nbx, part.data_ptr(), mom.data_ptr(),
+                 torch.cuda.current_stream().cuda_stream)
+    return mom
+
+
+def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cross-fit (LASSO)",
+                  device=None, dtype="f64"):
+    """K-fold cross-fit partially-linear DML with CV-LASSO nuisances E[Y|X], E[W|X]
+    (inner CV over the other K-1 folds). Matches reference.estimators.dml_plr_lasso."""
+    dev = resolve_device(device)
+    Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
+    fid = rng.fold_ids(len(Yn), folds, seed, stream=0)
+    pan = build_panel(Xn, Wn, Yn, folds=fid, dtype=dtype, device=dev)
+    res, mom, _ = dml_crossfit_panel(pan, folds, lambda_rule)
+    return read_result(res, method, n=len(Yn))

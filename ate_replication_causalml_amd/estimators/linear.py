@@ -1,0 +1,132 @@
+"""Device estimators built on Gram / IRLS / score kernels:
+E1 naive, E2 OLS (Direct Method), E16 logistic propensity, E3 IPW, E4 PS-WLS,
+E9 doubly-robust (logistic), E10 bootstrap SE.
+
+Semantics follow ``ate_functions.R`` exactly (see reference/estimators.py for the
+float64 CPU oracle and SURVEY.md §2.7); each function takes ``(Y, W, X)``.
+Default precision is the fp64 parity panel (fp64 MFMA Gram), the right choice at
+tutorial scale (N ~ 1e4, p = 21); ``dtype="f32"`` uses fp32 MFMA.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import stats as S
+from ..ops.gram import gram
+from ..ops.linalg import chol_solve, logistic_irls, predict
+from ..ops.panel import build_panel
+from ..result import AteResult
+from .common import as_np, read_result, resolve_device
+
+
+def naive(Y, W, method="naive", device=None):
+    """E1 ``naive_ate`` (ate_functions.R:3-21)."""
+    dev = resolve_device(device)
+    y = torch.as_tensor(as_np(Y), device=dev)
+    w = torch.as_tensor(as_np(W), device=dev)
+    res, mom = S.naive(y, w)
+    return read_result(res, method)
+
+
+def ols(Y, W, X, method="Direct Method", device=None, dtype="f64"):
+    """E2 ``ate_condmean_ols`` (ate_functions.R:25-39): lm(Y ~ covariates + W)."""
+    dev = resolve_device(device)
+    pan = build_panel(as_np(X), as_np(W), as_np(Y), dtype=dtype, device=dev)
+    G = gram(pan)[0]
+    cols = [pan.cols["one"], *pan.xcols, pan.cols["W"]]
+    r = chol_solve(G, cols, pan.cols["Y"])
+    out = torch.stack([r.beta[-1], torch.sqrt(r.aux[1] / (pan.n - r.aux[0]) * r.invdiag[-1]),
+                       r.aux[0]])
+    v = out.cpu().numpy()
+    return AteResult.make(method, v[0], v[1], rank=int(v[2]))
+
+
+def propensity_logistic(W, X, device=None, dtype="f64", return_panel_order=False):
+    """E16: glm(W ~ covariates, binomial) fitted values (ate_replication.Rmd:165-168)."""
+    dev = resolve_device(device)
+    pan = build_panel(as_np(X), as_np(W), None, dtype=dtype, device=dev, extra_cols=("z",))
+    cols = [pan.cols["one"], *pan.xcols]
+    fit = logistic_irls(pan, cols, pan.cols["W"], pan.cols["z"])
+    if return_panel_order:
+        return fit.mu, pan
+    return pan.scatter_rows(fit.mu)
+
+
+def ipw(Y, W, X, p, method="Propensity_Weighting", compat="reference", device=None, dtype="f64"):
+    """E3 ``prop_score_weight`` (ate_functions.R:44-63) with the full-frame projection
+    design under compat="reference" (Q25; see reference.estimators.ipw_design)."""
+    dev = resolve_device(device)
+    Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
+    pt = torch.as_tensor(as_np(p), device=dev)
+    y = torch.as_tensor(Yn, device=dev)
+    w = torch.as_tensor(Wn, device=dev)
+    x = torch.as_tensor(Xn, device=dev)
+    ps = w - pt
+    tau = ps * y / (pt * (1 - pt))
+    frame = torch.cat([x, y[:, None], w[:, None], pt[:, None], tau[:, None], ps[:, None]], 1) \
+        if compat == "reference" else x
+    d = frame * ps[:, None]
+    pan = build_panel(d.cpu().numpy(), None, tau.cpu().numpy(), dtype=dtype, device=dev)
+    G = gram(pan)[0]
+    cols = [pan.cols["one"], *pan.xcols]
+    r = chol_solve(G, cols, pan.cols["Y"])
+    n = pan.n
+    ate = G[pan.cols["one"], pan.cols["Y"]] / n
+    se = torch.sqrt(r.aux[1] / n) / np.sqrt(n)
+    return read_result(torch.stack([ate, se]), method)
+
+
+def ipw_wls(Y, W, p, method="Propensity_Regression", device=None, dtype="f64"):
+    """E4 ``prop_score_ols`` (ate_functions.R:67-86): WLS of Y on W, weights W/p+(1-W)/(1-p)."""
+    dev = resolve_device(device)
+    Wn, pn = as_np(W), as_np(p)
+    wts = Wn / pn + (1 - Wn) / (1 - pn)
+    pan = build_panel(Wn[:, None], None, as_np(Y), dtype=dtype, device=dev)
+    wt = pan.gather_rows(torch.as_tensor(wts, device=dev).to(pan.dtype))
+    G = gram(pan, wt)[0]
+    cols = [pan.cols["one"], pan.xcols[0]]
+    r = chol_solve(G, cols, pan.cols["Y"])
+    se = torch.sqrt(r.aux[1] / (pan.n - r.aux[0]) * r.invdiag[1])
+    return read_result(torch.stack([r.beta[1], se]), method)
+
+
+def outcome_mu(Y, W, X, counterfactual_quirk, device=None, dtype="f64"):
+    """Outcome GLM Y ~ covariates + W (Q24); mu1/mu0 with W overridden to 1/0, or both
+    equal to mu(x, W_obs) under the ``mutate_("W = 1")`` quirk (Q6)."""
+    dev = resolve_device(device)
+    pan = build_panel(np.column_stack([as_np(X), as_np(W)]), None, as_np(Y), dtype=dtype,
+                      device=dev, extra_cols=("z",))
+    cols = [pan.cols["one"], *pan.xcols]
+    fit = logistic_irls(pan, cols, pan.cols["Y"], pan.cols["z"])
+    if counterfactual_quirk:
+        mu = pan.scatter_rows(fit.mu)
+        return mu, mu.clone()
+    widx = len(cols) - 1
+    mu1 = predict(pan, cols, fit.beta, override_idx=widx, override_val=1.0, link="logit")
+    mu1 = pan.scatter_rows(mu1.clone())
+    mu0 = predict(pan, cols, fit.beta, override_idx=widx, override_val=0.0, link="logit")
+    mu0 = pan.scatter_rows(mu0.clone())
+    return mu0, mu1
+
+
+def aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se=False, B=1000, seed=1991,
+                        compat="reference", device=None, **diag):
+    dev = resolve_device(device)
+    y = torch.as_tensor(as_np(Y), device=dev)
+    w = torch.as_tensor(as_np(W), device=dev)
+    p = p.to(dev).double()
+    res, _ = S.aipw(w, y, p, mu0.to(dev), mu1.to(dev), compat=compat)
+    if bootstrap_se:
+        e1, e2 = S.aipw_terms(w, y, p, mu0.to(dev), mu1.to(dev), compat)
+        taus = S.bootstrap_multinomial(e1.contiguous(), e2.contiguous(), B, seed)
+        res = torch.stack([res[0], taus.std(unbiased=True).to(res.device)])
+    return read_result(res, method, **diag)
+
+
+def aipw_glm(Y, W, X, bootstrap_se=False, B=1000, seed=1991, compat="reference",
+             method="Doubly Robust with logistic regression PS", device=None, dtype="f64"):
+    """E9 ``doubly_robust_glm`` (ate_functions.R:211-264)."""
+    mu0, mu1 = outcome_mu(Y, W, X, counterfactual_quirk=False, device=device, dtype=dtype)
+    p = propensity_logistic(W, X, device=device, dtype=dtype)
+    return aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se, B, seed, compat, device)

@@ -1,0 +1,279 @@
+"""K08/K09 elastic-net ops: glmnet-equivalent gaussian paths + cv.glmnet selection,
+computed from per-segment Gram matrices (K01) — no extra pass over the data.
+
+``cv_enet_gaussian`` covers both reference usages:
+
+* plain ``cv.glmnet`` (E5, E6, E11; ``ate_functions.R:101,123,304,305``): one full
+  training set = all segments, CV folds = the segments;
+* nested cross-fitting (DML nuisances): K full training sets (all segments but
+  k), each cross-validated over its own K-1 segments. Training sets that occur
+  twice (all \\ {k, s} = all \\ {s, k}) are prepared once.
+
+GPU: ``csrc/enet.hip``. CPU: numpy with the same algorithm (reference core).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..reference import glmnet as ref
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@dataclass
+class EnetCvResult:
+    lambdas: torch.Tensor     # [nfull, L] original scale (NaN beyond nlam)
+    nlam: torch.Tensor        # [nfull]
+    cvm: torch.Tensor         # [nfull, L]
+    cvsd: torch.Tensor
+    sel: torch.Tensor         # [nfull, 2] (idx_min, idx_1se)
+    coef_path: torch.Tensor   # [nfull, L, p+1] original-scale (intercept first)
+    coef_min: torch.Tensor    # [nfull, p+1]
+    coef_1se: torch.Tensor    # [nfull, p+1]
+    full_keys: list           # (full set index, y index) per full problem
+    npass: torch.Tensor
+
+
+def _rescale_vp(vp, p):
+    vp = np.ones(p) if vp is None else np.maximum(np.asarray(vp, float), 0)
+    return vp * p / vp.sum()
+
+
+def cv_enet_gaussian(G: torch.Tensor, panel, xcols, ycols, full_sets=None, penalty_factor=None,
+                     alpha=1.0, nlambda=100, lambda_min_ratio=None, thresh=1e-7,
+                     maxit=100000) -> EnetCvResult:
+    """Cross-validated gaussian elastic net from the segment Gram stack ``G`` [nseg,P,P].
+
+    full_sets: list of lists of segment ids (default: one set with all segments).
+    Problems are ordered (full set f, y index) for the result arrays."""
+    nseg = G.shape[0]
+    P = G.shape[1]
+    p = len(xcols)
+    ny = len(ycols)
+    if full_sets is None:
+        full_sets = [list(range(nseg))]
+    # training sets: each full set, then every (full set minus one segment)
+    tsets, tindex = [], {}
+
+    def tid(segs):
+        key = tuple(sorted(segs))
+        if key not in tindex:
+            tindex[key] = len(tsets)
+            tsets.append(key)
+        return tindex[key]
+
+    full_t = [tid(fs) for fs in full_sets]
+    fold_t, fold_hold = [], []
+    for fs in full_sets:
+        for s in fs:
+            fold_t.append(tid([q for q in fs if q != s]))
+            fold_hold.append(s)
+    K = len(full_sets[0])
+    assert all(len(fs) == K for fs in full_sets), "full sets must have equal fold counts"
+    masks = np.zeros((len(tsets), nseg), dtype=np.uint8)
+    for i, ts in enumerate(tsets):
+        masks[i, list(ts)] = 1
+    nreal = np.asarray(panel.seg_nreal, dtype=np.float64)
+    n_full = [nreal[list(fs)].sum() for fs in full_sets]
+    if lambda_min_ratio is None:
+        lambda_min_ratio = 1e-4 if min(n_full) > p else 1e-2
+    vp = _rescale_vp(penalty_factor, p)
+    L = nlambda
+    # problem tables
+    full_probs = [(full_t[f], y, -1, nlambda) for f in range(len(full_sets)) for y in range(ny)]
+    full_keys = [(f, y) for f in range(len(full_sets)) for y in range(ny)]
+    fold_probs, fold_ycol, fold_holds, fold_of_full = [], [], [], []
+    for f in range(len(full_sets)):
+        for k in range(K):
+            for y in range(ny):
+                src = f * ny + y
+                fold_probs.append((fold_t[f * K + k], y, src, 0))
+                fold_ycol.append(ycols[y])
+                fold_holds.append(fold_hold[f * K + k])
+    # fold_probs index for (full problem fp, k): order above is f, k, y
+    fold_index = np.zeros((len(full_probs), K), dtype=np.int32)
+    nfold = np.zeros((len(full_probs), K))
+    for f in range(len(full_sets)):
+        for k in range(K):
+            for y in range(ny):
+                fold_index[f * ny + y, k] = (f * K + k) * ny + y
+                nfold[f * ny + y, k] = nreal[fold_hold[f * K + k]]
+    if G.is_cuda:
+        return _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, panel.cols["one"], full_probs,
+                       fold_probs, fold_ycol, fold_holds, fold_index, nfold, alpha,
+                       lambda_min_ratio, thresh, maxit, L, full_keys)
+    return _cv_cpu(G, masks, xcols, ycols, p, ny, vp, panel.cols["one"], full_probs, fold_probs,
+                   fold_ycol, fold_holds, fold_index, nfold, alpha, lambda_min_ratio, thresh, maxit,
+                   L, full_keys)
+
+
+_PROB_DT = np.dtype([("train", "<i4"), ("y", "<i4"), ("src", "<i4"), ("nlam", "<i4")])
+
+
+def _probs_tensor(probs, dev):
+    a = np.array(probs, dtype=_PROB_DT)
+    return torch.from_numpy(a.view(np.uint8).copy()).to(dev)
+
+
+def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_probs, fold_ycol,
+            fold_holds, fold_index, nfold, alpha, flmin, thresh, maxit, L, full_keys):
+    dev = G.device
+    s = _stream()
+    f64 = dict(dtype=torch.float64, device=dev)
+    nt = masks.shape[0]
+    masks_t = torch.from_numpy(masks).to(dev)
+    xc = torch.tensor(xcols, dtype=torch.int32, device=dev)
+    yc = torch.tensor(ycols, dtype=torch.int32, device=dev)
+    C = torch.empty((nt, p, p), **f64)
+    g = torch.empty((nt, ny, p), **f64)
+    xm = torch.empty((nt, p), **f64)
+    xs = torch.empty((nt, p), **f64)
+    ju = torch.empty((nt, p), dtype=torch.uint8, device=dev)
+    ym = torch.empty((nt, ny), **f64)
+    ys = torch.empty((nt, ny), **f64)
+    nobs = torch.empty(nt, **f64)
+    _native.call("ate_enet_prepare", G.data_ptr(), nseg, P, masks_t.data_ptr(), nt, xc.data_ptr(),
+                 p, one, yc.data_ptr(), ny, C.data_ptr(), g.data_ptr(), xm.data_ptr(),
+                 xs.data_ptr(), ju.data_ptr(), ym.data_ptr(), ys.data_ptr(), nobs.data_ptr(), s)
+    vp_t = torch.tensor(vp, **f64)
+    outs = {}
+    for tag, probs in (("full", full_probs), ("fold", fold_probs)):
+        nq = len(probs)
+        pr = _probs_tensor(probs, dev)
+        apath = torch.zeros((nq, L, p), **f64)
+        lams = torch.full((nq, L), float("nan"), **f64)
+        rsq = torch.zeros((nq, L), **f64)
+        nlam = torch.zeros(nq, dtype=torch.int32, device=dev)
+        npass = torch.zeros(nq, dtype=torch.int32, device=dev)
+        if tag == "fold":
+            lams_src = outs["full"]["lams"]
+            nlam_src = outs["full"]["nlam"]
+            # the kernel reads the source lambdas from its own lams/nlam buffers at index src:
+            # place the full problems' values in a combined table
+            nf = lams_src.shape[0]
+            lams = torch.cat([lams_src, lams])
+            nlam = torch.cat([nlam_src, nlam])
+            apath = torch.cat([torch.zeros((nf, L, p), **f64), apath])
+            rsq = torch.cat([torch.zeros((nf, L), **f64), rsq])
+            npass = torch.cat([torch.zeros(nf, dtype=torch.int32, device=dev), npass])
+            probs2 = [(0, 0, -2, 0)] * nf + list(probs)
+            pr = _probs_tensor(probs2, dev)
+            nq = len(probs2)
+        _native.call("ate_enet_path", C.data_ptr(), g.data_ptr(), p, ny, ju.data_ptr(),
+                     ys.data_ptr(), vp_t.data_ptr(), pr.data_ptr(), nq, alpha, flmin, thresh,
+                     maxit, apath.data_ptr(), lams.data_ptr(), rsq.data_ptr(), nlam.data_ptr(),
+                     npass.data_ptr(), L, s)
+        coef = torch.empty((nq, L, p + 1), **f64)
+        _native.call("ate_enet_coef", apath.data_ptr(), pr.data_ptr(), nq, p, ny, L,
+                     nlam.data_ptr(), xm.data_ptr(), xs.data_ptr(), ju.data_ptr(), ym.data_ptr(),
+                     ys.data_ptr(), coef.data_ptr(), s)
+        outs[tag] = dict(lams=lams, nlam=nlam, coef=coef, npass=npass, probs=pr, nq=nq)
+    nf = len(full_probs)
+    fo = outs["fold"]
+    hold = torch.tensor([0] * nf + list(fold_holds), dtype=torch.int32, device=dev)
+    ycol_p = torch.tensor([0] * nf + list(fold_ycol), dtype=torch.int32, device=dev)
+    cvraw = torch.empty((fo["nq"], L), **f64)
+    _native.call("ate_enet_cvloss_gauss", G.data_ptr(), P, hold.data_ptr(), xc.data_ptr(), p, one,
+                 ycol_p.data_ptr(), fo["coef"].data_ptr(), fo["nlam"].data_ptr(), L, fo["nq"],
+                 cvraw.data_ptr(), s)
+    fidx = torch.from_numpy(fold_index + nf).to(dev)
+    nfold_t = torch.from_numpy(nfold).to(dev)
+    cvm = torch.empty((nf, L), **f64)
+    cvsd = torch.empty((nf, L), **f64)
+    sel = torch.empty((nf, 2), dtype=torch.int32, device=dev)
+    K = fold_index.shape[1]
+    fu = outs["full"]
+    _native.call("ate_cv_select", cvraw.data_ptr(), fidx.data_ptr(), nfold_t.data_ptr(), K, nf,
+                 fu["nlam"].data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), s)
+    cmin = torch.empty((nf, p + 1), **f64)
+    c1se = torch.empty((nf, p + 1), **f64)
+    _native.call("ate_enet_pick", fu["coef"].data_ptr(), sel.data_ptr(), 0, p, L, nf,
+                 cmin.data_ptr(), s)
+    _native.call("ate_enet_pick", fu["coef"].data_ptr(), sel.data_ptr(), 1, p, L, nf,
+                 c1se.data_ptr(), s)
+    return EnetCvResult(fu["lams"], fu["nlam"], cvm, cvsd, sel, fu["coef"], cmin, c1se, full_keys,
+                        fu["npass"])
+
+
+def _cv_cpu(G, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_probs, fold_ycol, fold_holds,
+            fold_index, nfold, alpha, flmin, thresh, maxit, L, full_keys):
+    Gn = G.double().cpu().numpy()
+    nt = masks.shape[0]
+    stats = []
+    for t in range(nt):
+        Gt = np.tensordot(masks[t].astype(float), Gn, axes=1)
+        n = Gt[one, one]
+        sx = Gt[one, xcols] / n
+        vx = np.diag(Gt)[xcols] / n - sx * sx
+        ju = vx > 0
+        xs = np.where(ju, np.sqrt(np.maximum(vx, 0)), 1.0)
+        Cm = (Gt[np.ix_(xcols, xcols)] / n - np.outer(sx, sx)) / np.outer(xs, xs)
+        Cm[~ju, :] = 0
+        Cm[:, ~ju] = 0
+        Cm[np.flatnonzero(~ju), np.flatnonzero(~ju)] = 1.0
+        gs, ymv, ysv = [], [], []
+        for yc in ycols:
+            my = Gt[one, yc] / n
+            vy = Gt[yc, yc] / n - my * my
+            sy = np.sqrt(vy) if vy > 0 else 1.0
+            gj = np.where(ju, (Gt[xcols, yc] / n - sx * my) / (xs * sy), 0.0)
+            gs.append(gj)
+            ymv.append(my)
+            ysv.append(sy)
+        stats.append(dict(C=Cm, g=gs, xm=sx, xs=xs, ju=ju, ym=ymv, ys=ysv, n=n))
+
+    def run(probs, src_paths):
+        res = []
+        for (t, y, src, nlam_req) in probs:
+            st = stats[t]
+            lam = None if src < 0 else src_paths[src].lambdas
+            path = ref._elnet_core(st["C"], st["g"][y], np.ones(p), st["xm"], st["xs"], st["ym"][y],
+                                   st["ys"][y], st["ju"], alpha, vp, lam, nlam_req or L, flmin,
+                                   thresh, maxit)
+            res.append(path)
+        return res
+
+    full = run(full_probs, None)
+    folds = run(fold_probs, full)
+    nf = len(full_probs)
+    K = fold_index.shape[1]
+    lams = np.full((nf, L), np.nan)
+    nlam = np.zeros(nf, dtype=np.int32)
+    coef = np.full((nf, L, p + 1), np.nan)
+    for f, path in enumerate(full):
+        m = len(path.lambdas)
+        lams[f, :m] = path.lambdas
+        nlam[f] = m
+        coef[f, :m, 0] = path.a0
+        coef[f, :m, 1:] = path.beta
+    cvraw = np.full((len(fold_probs), L), np.nan)
+    for q, path in enumerate(folds):
+        Gh = Gn[fold_holds[q]]
+        yc = fold_ycol[q]
+        n = Gh[one, one]
+        for m in range(len(path.lambdas)):
+            a0, b = path.a0[m], path.beta[m]
+            Gxx = Gh[np.ix_(xcols, xcols)]
+            sse = (Gh[yc, yc] - 2 * a0 * Gh[one, yc] - 2 * b @ Gh[xcols, yc] + n * a0 * a0
+                   + 2 * a0 * b @ Gh[xcols, one] + b @ Gxx @ b)
+            cvraw[q, m] = sse / n
+    cvm = np.full((nf, L), np.nan)
+    cvsd = np.full((nf, L), np.nan)
+    sel = np.zeros((nf, 2), dtype=np.int32)
+    for f in range(nf):
+        m = nlam[f]
+        raw = cvraw[fold_index[f]][:, :m]
+        cm, cs, i0, i1 = ref.cv_select(lams[f, :m], raw, nfold[f])
+        cvm[f, :m], cvsd[f, :m] = cm, cs
+        sel[f] = (i0, i1)
+    cmin = np.stack([coef[f, sel[f, 0]] for f in range(nf)])
+    c1se = np.stack([coef[f, sel[f, 1]] for f in range(nf)])
+    t = torch.from_numpy
+    return EnetCvResult(t(lams), t(nlam), t(cvm), t(cvsd), t(sel), t(coef), t(cmin), t(c1se),
+                        full_keys, t(np.array([pth.npasses for pth in full])))

@@ -1,0 +1,151 @@
+"""Communicator abstraction.
+
+* :class:`TorchComm` — ``torch.distributed``; on MI355X the ``nccl`` backend IS
+  RCCL over xGMI (one process per GPU), on CPU the ``gloo`` backend.
+  Collectives are enqueued on the current HIP stream (capturable in a graph).
+* :class:`ThreadSimComm` — in-process simulator: ranks are threads sharing host
+  memory, reductions run in RANK ORDER, so results are deterministic (CPU tests
+  of the distributed algorithms without any cluster).
+* :class:`LocalComm` — world size 1, no-op.
+
+All DP algorithms in this package reduce *sufficient statistics* (fold Gram
+stacks, histogram stacks, score moments, bootstrap partials), so the data itself
+never crosses ranks; messages are KB..MB and the design minimises collective
+COUNT (one packed buffer per phase), the right trade on point-to-point xGMI.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+
+class LocalComm:
+    rank = 0
+    world_size = 1
+
+    def all_reduce_(self, t):
+        return t
+
+    def all_gather(self, t):
+        return [t]
+
+    def broadcast_(self, t, src=0):
+        return t
+
+    def barrier(self):
+        pass
+
+
+class TorchComm:
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+
+    def all_reduce_(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_gather(self, t):
+        out = [torch.empty_like(t) for _ in range(self.world_size)]
+        self.dist.all_gather(out, t.contiguous(), group=self.group)
+        return out
+
+    def broadcast_(self, t, src=0):
+        self.dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def barrier(self):
+        if self.dist.get_backend(self.group) == "nccl":
+            # RCCL barrier via a tiny all-reduce on the current device (avoids
+            # device-guessing warnings)
+            x = torch.zeros(1, device=torch.cuda.current_device())
+            self.dist.all_reduce(x, group=self.group)
+            torch.cuda.synchronize()
+        else:
+            self.dist.barrier(group=self.group)
+
+
+class _SimWorld:
+    def __init__(self, n):
+        self.n = n
+        self.barrier = threading.Barrier(n)
+        self.slots = [None] * n
+        self.lock = threading.Lock()
+
+
+class ThreadSimComm:
+    """Rank ``rank`` of an in-process simulated world (use :func:`run_simulated`)."""
+
+    def __init__(self, world: _SimWorld, rank: int):
+        self.w = world
+        self.rank = rank
+        self.world_size = world.n
+
+    def all_reduce_(self, t):
+        self.w.slots[self.rank] = t.detach().clone()
+        self.w.barrier.wait()
+        acc = self.w.slots[0].clone()
+        for r in range(1, self.world_size):    # fixed rank order -> deterministic
+            acc += self.w.slots[r]
+        self.w.barrier.wait()
+        t.copy_(acc)
+        return t
+
+    def all_gather(self, t):
+        self.w.slots[self.rank] = t.detach().clone()
+        self.w.barrier.wait()
+        out = [s.clone() for s in self.w.slots]
+        self.w.barrier.wait()
+        return out
+
+    def broadcast_(self, t, src=0):
+        if self.rank == src:
+            self.w.slots[src] = t.detach().clone()
+        self.w.barrier.wait()
+        t.copy_(self.w.slots[src])
+        self.w.barrier.wait()
+        return t
+
+    def barrier(self):
+        self.w.barrier.wait()
+
+
+def run_simulated(world_size: int, fn):
+    """Run ``fn(comm)`` on ``world_size`` threads; returns the per-rank results."""
+    world = _SimWorld(world_size)
+    results = [None] * world_size
+    errors = []
+
+    def worker(r):
+        try:
+            results[r] = fn(ThreadSimComm(world, r))
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+            world.barrier.abort()
+
+    ts = [threading.Thread(target=worker, args=(r,)) for r in range(world_size)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errors:
+        raise errors[0]
+    return results
+
+
+def from_env():
+    """TorchComm if launched under torch.distributed.run (WORLD_SIZE>1), else LocalComm."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            dist.init_process_group(backend=backend)
+        return TorchComm()
+    return LocalComm()

@@ -83,9 +83,10 @@ def cd_solve(C, g, a, vp, xv, ab, dem, thr, ju, cint=None, gint=None, xmz=None, 
     active = state if state is not None else np.zeros(p, dtype=bool)
     npass = 0
     b0_delta = 0.0
+    rsq_delta = 0.0
 
     def one_pass(idx_list):
-        nonlocal gint, b0_delta
+        nonlocal gint, b0_delta, rsq_delta
         dlx = 0.0
         pos = 0
         idx_list = np.asarray(idx_list)
@@ -108,6 +109,7 @@ def cd_solve(C, g, a, vp, xv, ab, dem, thr, ju, cint=None, gint=None, xmz=None, 
             active[j] = True
             d = anew - ak
             a[j] = anew
+            rsq_delta += d * (2.0 * g[j] - d * xv[j])   # glmnet's incremental R^2
             dlx = max(dlx, xv[j] * d * d)
             g[:] -= C[:, j] * d
             if cint is not None:
@@ -132,6 +134,7 @@ def cd_solve(C, g, a, vp, xv, ab, dem, thr, ju, cint=None, gint=None, xmz=None, 
             dlx = one_pass(np.flatnonzero(active))
             if dlx < thr:
                 break
+    cd_solve.last_rsq_delta = rsq_delta
     return npass, gint, b0_delta, active
 
 
@@ -182,6 +185,7 @@ def _elnet_core(C, g, xv, xm, xs, ym, ys, ju, alpha, penalty_factor, lambdas, nl
     alf = flmin ** (1.0 / (nlam - 1)) if ulam is None else 1.0
     betas, lams, devs = [], [], []
     alm = 0.0
+    rsq = 0.0
     npass_tot = 0
     active = np.zeros(p, dtype=bool)
     for m, spec in _lambda_seq_iter(nlam, flmin, ulam):
@@ -195,7 +199,7 @@ def _elnet_core(C, g, xv, xm, xs, ym, ys, ju, alpha, penalty_factor, lambdas, nl
         npass, _, _, active = cd_solve(C, g, a, vp, xv, alm * alpha, alm * (1 - alpha), thresh, ju,
                                        maxit=maxit - npass_tot, state=active)
         npass_tot += npass
-        rsq = _rsq(C, g, a)   # 1 - RSS/TSS on the standardised scale
+        rsq += cd_solve.last_rsq_delta   # 1 - RSS/TSS on the standardised scale
         betas.append(a.copy())
         lams.append(alm)
         devs.append(rsq)

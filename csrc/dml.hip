@@ -1,0 +1,124 @@
+// Fused cross-fit residual pass for partially-linear DML with linear nuisances.
+//
+// For every row i of held-out segment k:
+//   yr_i = y_i - (cy[k][0] + x_i . cy[k][1:]) ,  wr_i = w_i - (cw[k][0] + x_i . cw[k][1:])
+// and the orthogonal-score moments {S_wy, S_ww, S_yyww, S_yw3, S_w4, n, S_yy} are
+// accumulated in fp64 -- the residual vectors are never written to HBM. The panel
+// is read exactly once (bandwidth-bound: one column-major stream per feature,
+// coalesced across the 256 rows of a block). Coefficients for all folds are staged
+// in LDS. y/w are reconstructed from their hi+lo bf16 columns on bf16 panels.
+#include "common.hpp"
+
+using namespace ate;
+
+template <typename T>
+__device__ __forceinline__ double ld_col(const T* X, int64_t ld, int c, int64_t i) {
+  return (double)X[(int64_t)c * ld + i];
+}
+template <>
+__device__ __forceinline__ double ld_col<bf16_t>(const bf16_t* X, int64_t ld, int c, int64_t i) {
+  return (double)bf16_to_f32(X[(int64_t)c * ld + i]);
+}
+
+struct Seg { int64_t r0, r1; };
+
+template <typename T, int RPT>
+__global__ __launch_bounds__(256) void dml_resid_kernel(
+    const T* __restrict__ X, int64_t ld, const int* __restrict__ xcols, int p,
+    const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef /*[nseg][2][p+1]*/,
+    int y0, int y1, int w0, int w1, int vcol, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double sh[];
+  double* cy = sh;                    // [p+1]
+  double* cw = sh + (p + 1);          // [p+1]
+  int* xc = (int*)(sh + 2 * (p + 1)); // [p]
+  __shared__ double red[16 * 7];
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int j = threadIdx.x; j < p; j += blockDim.x) xc[j] = xcols[j];
+  // grid: blockIdx.y = segment; blocks stride over that segment's rows
+  const int k = blockIdx.y;
+  for (int j = threadIdx.x; j <= p; j += blockDim.x) {
+    cy[j] = coef[((int64_t)k * 2 + 0) * (p + 1) + j];
+    cw[j] = coef[((int64_t)k * 2 + 1) * (p + 1) + j];
+  }
+  __syncthreads();
+  const Seg sg = segs[k];
+  for (int64_t base = sg.r0 + (int64_t)blockIdx.x * 256 * RPT; base < sg.r1;
+       base += (int64_t)gridDim.x * 256 * RPT) {
+    double py[RPT], pw[RPT];
+    int64_t ii[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      ii[r] = base + r * 256 + threadIdx.x;
+      py[r] = cy[0];
+      pw[r] = cw[0];
+    }
+    for (int j = 0; j < p; ++j) {
+      const double by = cy[1 + j], bw = cw[1 + j];
+      const int c = xc[j];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        double x = ii[r] < sg.r1 ? ld_col(X, ld, c, ii[r]) : 0.0;
+        py[r] += by * x;
+        pw[r] += bw * x;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (ii[r] >= sg.r1) continue;
+      if (ld_col(X, ld, vcol, ii[r]) == 0.0) continue;
+      double y = ld_col(X, ld, y0, ii[r]) + (y1 >= 0 ? ld_col(X, ld, y1, ii[r]) : 0.0);
+      double w = ld_col(X, ld, w0, ii[r]) + (w1 >= 0 ? ld_col(X, ld, w1, ii[r]) : 0.0);
+      double yr = y - py[r], wr = w - pw[r], w2 = wr * wr;
+      v[0] += wr * yr; v[1] += w2; v[2] += yr * yr * w2; v[3] += yr * w2 * wr; v[4] += w2 * w2;
+      v[5] += 1.0; v[6] += yr * yr;
+    }
+  }
+  block_sum<7>(v, red);
+  if (threadIdx.x == 0) {
+    double* out = partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 7;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) out[q] = v[q];
+  }
+}
+
+__global__ void sum7_kernel(const double* __restrict__ partial, int nb, double* __restrict__ out) {
+  int q = threadIdx.x;
+  if (q >= 7) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * 7 + q];
+  out[q] = s;
+}
+
+template <typename T>
+static int dml_resid_t(const void* X, int64_t ld, const void* xcols, int p, const void* segs,
+                       int nseg, const void* coef, int y0, int y1, int w0, int w1, int vcol,
+                       int nbx, void* partial, void* moments, hipStream_t s) {
+  size_t sh = (size_t)2 * (p + 1) * sizeof(double) + (size_t)p * sizeof(int);
+  dim3 grid(nbx, nseg);
+  hipLaunchKernelGGL((dml_resid_kernel<T, 4>), grid, dim3(256), sh, s, (const T*)X, ld,
+                     (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
+                     w0, w1, vcol, (double*)partial);
+  ATE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(64), 0, s, (const double*)partial, nbx * nseg,
+                     (double*)moments);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// dtype 1 f32, 2 f64, 3 bf16. partial: [nseg*nbx*7]
+ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t ld, const void* xcols, int p,
+                                  const void* segs, int nseg, const void* coef, int y0, int y1,
+                                  int w0, int w1, int vcol, int nbx, void* partial, void* moments,
+                                  void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1)
+    return dml_resid_t<float>(X, ld, xcols, p, segs, nseg, coef, y0, y1, w0, w1, vcol, nbx,
+                              partial, moments, s);
+  if (dtype == 2)
+    return dml_resid_t<double>(X, ld, xcols, p, segs, nseg, coef, y0, y1, w0, w1, vcol, nbx,
+                               partial, moments, s);
+  if (dtype == 3)
+    return dml_resid_t<bf16_t>(X, ld, xcols, p, segs, nseg, coef, y0, y1, w0, w1, vcol, nbx,
+                               partial, moments, s);
+  return -1;
+}

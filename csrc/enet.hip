@@ -1,0 +1,403 @@
+// K08 enet_cd_gram + K09 cv_loss (gaussian): glmnet-equivalent LASSO / elastic-net
+// paths and cv.glmnet selection computed entirely from per-fold Gram matrices (K01).
+// Reference call sites: ate_functions.R:101,123,304,305 (cv.glmnet gaussian).
+//
+//  prepare:  for each training set s (a subset of fold segments) sum the raw
+//            augmented fold Grams and standardise (glmnet `standard`: population
+//            SD, centred): C_s = D^-1 (G/n - m m') D^-1, g_{s,y} = D^-1 (G_xy/n - m ym)/ys.
+//  path:     ONE WAVE per problem (training set, response). The gradient g, the
+//            coefficients a, xv, vp live in registers, lane l owning coordinates
+//            l, l+64, ...; a pass walks coordinates in order and uses a ballot to
+//            jump to the next coordinate that can move (nonzero, or |u| > vp*lambda),
+//            re-evaluated after every update -- exactly glmnet's sequential semantics
+//            (full pass, then active-set passes until max xv*d^2 < thresh). Gram rows
+//            are read from L2 (the Gram stack is a few MB).
+//  cv loss:  held-out MSE of every (fold problem, lambda) from the held-out fold's
+//            Gram: sum (y - a0 - x b)^2 = y'y - 2 a0 S_y - 2 b'X'y + n a0^2 + 2 a0 b'S_x
+//            + b'X'X b -- no pass over the data.
+//  select:   cvm, cvsd, lambda.min, lambda.1se with glmnet's rules.
+#include "common.hpp"
+
+using namespace ate;
+
+// ------------------------------------------------------------------ prepare
+// G: [nseg][P][P] raw Gram stack (panel columns). masks: [ntrain][nseg] (1 = in training set).
+// xcols[p], ones_col, ycols[ny]. Outputs per training set s:
+//   C[s][p][p], g[s][ny][p], xm[s][p], xs[s][p] (1 where constant), ju[s][p],
+//   ym[s][ny], ys[s][ny], nobs[s]
+__global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int P,
+                                    const unsigned char* __restrict__ masks, int ntrain,
+                                    const int* __restrict__ xcols, int p, int ones_col,
+                                    const int* __restrict__ ycols, int ny, double* __restrict__ C,
+                                    double* __restrict__ g, double* __restrict__ xm,
+                                    double* __restrict__ xs, unsigned char* __restrict__ ju,
+                                    double* __restrict__ ym, double* __restrict__ ys,
+                                    double* __restrict__ nobs) {
+  const int s = blockIdx.y;
+  const unsigned char* mk = masks + (int64_t)s * nseg;
+  auto gsum = [&](int a, int b) {
+    double acc = 0.0;
+    for (int q = 0; q < nseg; ++q)
+      if (mk[q]) acc += G[((int64_t)q * P + a) * P + b];
+    return acc;
+  };
+  const double n = gsum(ones_col, ones_col);
+  // each block recomputes the (cheap) means/sds it needs
+  const int64_t total = (int64_t)p * p + (int64_t)ny * p + p + ny;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < (int64_t)p * p) {
+      int j = (int)(e / p), k = (int)(e % p);
+      double mj = gsum(ones_col, xcols[j]) / n, mk2 = gsum(ones_col, xcols[k]) / n;
+      double vj = gsum(xcols[j], xcols[j]) / n - mj * mj;
+      double vk = gsum(xcols[k], xcols[k]) / n - mk2 * mk2;
+      double sj = vj > 0 ? sqrt(vj) : 1.0, sk = vk > 0 ? sqrt(vk) : 1.0;
+      double cjk = (gsum(xcols[j], xcols[k]) / n - mj * mk2) / (sj * sk);
+      if (!(vj > 0) || !(vk > 0)) cjk = (j == k) ? 1.0 : 0.0;
+      C[((int64_t)s * p + j) * p + k] = cjk;
+    } else if (e < (int64_t)p * p + (int64_t)ny * p) {
+      int64_t r = e - (int64_t)p * p;
+      int y = (int)(r / p), j = (int)(r % p);
+      double mj = gsum(ones_col, xcols[j]) / n;
+      double vj = gsum(xcols[j], xcols[j]) / n - mj * mj;
+      double my = gsum(ones_col, ycols[y]) / n;
+      double vy = gsum(ycols[y], ycols[y]) / n - my * my;
+      double sj = vj > 0 ? sqrt(vj) : 1.0, sy = vy > 0 ? sqrt(vy) : 1.0;
+      double gj = vj > 0 ? (gsum(xcols[j], ycols[y]) / n - mj * my) / (sj * sy) : 0.0;
+      g[((int64_t)s * ny + y) * p + j] = gj;
+    } else if (e < (int64_t)p * p + (int64_t)ny * p + p) {
+      int j = (int)(e - (int64_t)p * p - (int64_t)ny * p);
+      double mj = gsum(ones_col, xcols[j]) / n;
+      double vj = gsum(xcols[j], xcols[j]) / n - mj * mj;
+      xm[(int64_t)s * p + j] = mj;
+      xs[(int64_t)s * p + j] = vj > 0 ? sqrt(vj) : 1.0;
+      ju[(int64_t)s * p + j] = vj > 0 ? 1 : 0;
+      if (j == 0) nobs[s] = n;
+    } else {
+      int y = (int)(e - (int64_t)p * p - (int64_t)ny * p - p);
+      double my = gsum(ones_col, ycols[y]) / n;
+      double vy = gsum(ycols[y], ycols[y]) / n - my * my;
+      ym[(int64_t)s * ny + y] = my;
+      ys[(int64_t)s * ny + y] = vy > 0 ? sqrt(vy) : 1.0;
+    }
+  }
+}
+
+ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, int ntrain,
+                             const void* xcols, int p, int ones_col, const void* ycols, int ny,
+                             void* C, void* g, void* xm, void* xs, void* ju, void* ym, void* ys,
+                             void* nobs, void* stream) {
+  int64_t total = (int64_t)p * p + (int64_t)ny * p + p + ny;
+  dim3 grid(grid_for(total, 256, 512), ntrain);
+  hipLaunchKernelGGL(enet_prepare_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
+                     (const int*)xcols, p, ones_col, (const int*)ycols, ny, (double*)C, (double*)g,
+                     (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
+                     (double*)nobs);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ path (one wave / problem)
+struct EnetProblem {
+  int train;        // training set index (C, xm, xs, ju)
+  int y;            // response index within the training set's g/ym/ys
+  int ulam_src;     // -1: computed path; else problem whose (original-scale) lambdas to use
+  int nlam_req;
+};
+
+constexpr double BIGL = 9.9e35;
+
+template <int T>
+__global__ __launch_bounds__(64) void enet_path_kernel(
+    const double* __restrict__ C, const double* __restrict__ gin, int p, int ny,
+    const unsigned char* __restrict__ ju_s, const double* __restrict__ ys_s,
+    const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
+    double alpha, double flmin, double thr, int maxit,
+    double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
+    int* __restrict__ nlam_out, int* __restrict__ npass_out, int L) {
+  const int q = blockIdx.x;
+  if (q >= nprob) return;
+  const EnetProblem pr = probs[q];
+  if (pr.ulam_src < -1) return;          // placeholder slot (source path already computed)
+  const int lane = threadIdx.x;
+  const double* Cq = C + (int64_t)pr.train * p * p;
+  const double ysq = ys_s[(int64_t)pr.train * ny + pr.y];
+  double g[T], a[T], vp[T];
+  bool ju[T], act[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    int k = t * 64 + lane;
+    bool in = k < p;
+    g[t] = in ? gin[((int64_t)pr.train * ny + pr.y) * p + k] : 0.0;
+    a[t] = 0.0;
+    vp[t] = in ? vp_in[k] : 0.0;
+    ju[t] = in && ju_s[(int64_t)pr.train * p + k];
+    act[t] = false;
+  }
+  const int nlam = pr.ulam_src >= 0 ? nlam_out[pr.ulam_src] : pr.nlam_req;
+  const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
+  double alm = 0.0, rsq = 0.0, rsq_prev = 0.0;
+  int npass = 0, m_out = 0;
+  for (int m = 0; m < nlam; ++m) {
+    if (pr.ulam_src >= 0) {
+      alm = lams[(int64_t)pr.ulam_src * L + m] / ysq;
+    } else if (m == 0) {
+      alm = BIGL;
+    } else if (m == 1) {
+      double mx = 0.0;
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+        if (ju[t] && vp[t] > 0.0) mx = fmax(mx, fabs(g[t]) / vp[t]);
+      mx = wave_max(mx);
+      alm = alf * mx / fmax(alpha, 1e-3);
+    } else {
+      alm *= alf;
+    }
+    const double ab = alm * alpha, dem = alm * (1.0 - alpha);
+    // ---- coordinate descent at this lambda
+    auto pass = [&](bool full) -> double {
+      double dlx = 0.0;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        int last = -1;
+        while (true) {
+          double u = g[t] + a[t];           // xv = 1 (standardised gaussian)
+          bool cand = ju[t] && (full || act[t]) && lane > last &&
+                      (a[t] != 0.0 || fabs(u) > vp[t] * ab);
+          uint64_t msk = __ballot(cand);
+          if (!msk) break;
+          int jl = __ffsll((unsigned long long)msk) - 1;
+          last = jl;
+          double gj = __shfl(g[t], jl), aj = __shfl(a[t], jl), vpj = __shfl(vp[t], jl);
+          double uj = gj + aj;
+          double v = fabs(uj) - vpj * ab;
+          double an = v > 0.0 ? copysign(v, uj) / (1.0 + vpj * dem) : 0.0;
+          if (an == aj) continue;
+          double d = an - aj;
+          rsq += d * (2.0 * gj - d);
+          dlx = fmax(dlx, d * d);
+          if (lane == jl) { a[t] = an; act[t] = true; }
+          const double* row = Cq + (int64_t)(t * 64 + jl) * p;
+#pragma unroll
+          for (int t2 = 0; t2 < T; ++t2) {
+            int k = t2 * 64 + lane;
+            if (k < p) g[t2] -= row[k] * d;
+          }
+        }
+      }
+      return dlx;
+    };
+    while (npass < maxit) {
+      ++npass;
+      double dlx = pass(true);
+      if (dlx < thr) break;
+      while (npass < maxit) {
+        ++npass;
+        dlx = pass(false);
+        if (dlx < thr) break;
+      }
+    }
+    // ---- record (standardised coefficients, original-scale lambda)
+    double* ap = apath + ((int64_t)q * L + m) * p;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      int k = t * 64 + lane;
+      if (k < p) ap[k] = a[t];
+    }
+    if (lane == 0) {
+      lams[(int64_t)q * L + m] = alm * ysq;
+      rsqs[(int64_t)q * L + m] = rsq;
+    }
+    m_out = m + 1;
+    if (pr.ulam_src < 0 && m >= 4 && m > 0) {
+      if (rsq - rsq_prev < 1e-5 * rsq || rsq > 0.999) break;
+    }
+    rsq_prev = rsq;
+  }
+  if (lane == 0) {
+    if (pr.ulam_src < 0 && m_out >= 3) {
+      double l1 = lams[(int64_t)q * L + 1], l2 = lams[(int64_t)q * L + 2];
+      lams[(int64_t)q * L] = exp(2.0 * log(l1) - log(l2));
+    }
+    nlam_out[q] = m_out;
+    npass_out[q] = npass;
+  }
+}
+
+ATE_API int ate_enet_path(const void* C, const void* g, int p, int ny, const void* ju,
+                          const void* ys, const void* vp, const void* probs, int nprob,
+                          double alpha, double flmin, double thr, int maxit, void* apath,
+                          void* lams, void* rsqs, void* nlam_out, void* npass_out, int L,
+                          void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+#define LAUNCH_T(TT)                                                                          \
+  hipLaunchKernelGGL(enet_path_kernel<TT>, dim3(nprob), dim3(64), 0, s, (const double*)C,     \
+                     (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,    \
+                     (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,  \
+                     maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,    \
+                     (int*)npass_out, L)
+  if (p <= 64) LAUNCH_T(1);
+  else if (p <= 128) LAUNCH_T(2);
+  else if (p <= 256) LAUNCH_T(4);
+  else if (p <= 512) LAUNCH_T(8);
+  else return -2;
+#undef LAUNCH_T
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ coefficients (original scale)
+// coef[q][m][0] = intercept, coef[q][m][1+j] = beta_j = a_j * ys / xs_j (0 if !ju)
+__global__ void enet_coef_kernel(const double* __restrict__ apath, const EnetProblem* __restrict__ probs,
+                                 int nprob, int p, int ny, int L, const int* __restrict__ nlam_out,
+                                 const double* __restrict__ xm, const double* __restrict__ xs,
+                                 const unsigned char* __restrict__ ju, const double* __restrict__ ym,
+                                 const double* __restrict__ ys, double* __restrict__ coef) {
+  const int q = blockIdx.y, m = blockIdx.x;
+  if (q >= nprob || m >= L) return;
+  const EnetProblem pr = probs[q];
+  double* out = coef + ((int64_t)q * L + m) * (p + 1);
+  if (m >= nlam_out[q]) {
+    for (int j = threadIdx.x; j <= p; j += blockDim.x) out[j] = NAN;
+    return;
+  }
+  const double* a = apath + ((int64_t)q * L + m) * p;
+  const double ysq = ys[(int64_t)pr.train * ny + pr.y], ymq = ym[(int64_t)pr.train * ny + pr.y];
+  __shared__ double smem[16];
+  double acc[1] = {0.0};
+  for (int j = threadIdx.x; j < p; j += blockDim.x) {
+    int64_t sj = (int64_t)pr.train * p + j;
+    double b = ju[sj] ? a[j] * ysq / xs[sj] : 0.0;
+    out[1 + j] = b;
+    acc[0] += b * xm[sj];
+  }
+  block_sum<1>(acc, smem);
+  if (threadIdx.x == 0) out[0] = ymq - acc[0];
+}
+
+ATE_API int ate_enet_coef(const void* apath, const void* probs, int nprob, int p, int ny, int L,
+                          const void* nlam_out, const void* xm, const void* xs, const void* ju,
+                          const void* ym, const void* ys, void* coef, void* stream) {
+  hipLaunchKernelGGL(enet_coef_kernel, dim3(L, nprob), dim3(128), 0, (hipStream_t)stream,
+                     (const double*)apath, (const EnetProblem*)probs, nprob, p, ny, L,
+                     (const int*)nlam_out, (const double*)xm, (const double*)xs,
+                     (const unsigned char*)ju, (const double*)ym, (const double*)ys,
+                     (double*)coef);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ K09 CV loss from held-out Gram
+// For fold problem q (trained without segment hold[q]) and every lambda m:
+// cvraw[q][m] = SSE / n_hold using the raw held-out Gram G[hold] (panel columns).
+__global__ void enet_cvloss_gauss_kernel(const double* __restrict__ G, int P, const int* __restrict__ hold,
+                                         const int* __restrict__ xcols, int p, int ones_col,
+                                         const int* __restrict__ ycol_of_prob,
+                                         const double* __restrict__ coef, const int* __restrict__ nlam_out,
+                                         int L, double* __restrict__ cvraw) {
+  const int q = blockIdx.y, m = blockIdx.x;
+  if (m >= nlam_out[q]) { if (threadIdx.x == 0) cvraw[(int64_t)q * L + m] = NAN; return; }
+  const double* Gh = G + (int64_t)hold[q] * P * P;
+  const double* cf = coef + ((int64_t)q * L + m) * (p + 1);
+  const int yc = ycol_of_prob[q];
+  const double a0 = cf[0];
+  __shared__ double smem[16 * 3];
+  // quad = b' Gxx b, lin = b' (Gxy - a0 Sx)
+  double v[3] = {0.0, 0.0, 0.0};
+  for (int64_t e = threadIdx.x; e < (int64_t)p * p; e += blockDim.x) {
+    int j = (int)(e / p), k = (int)(e % p);
+    double bj = cf[1 + j], bk = cf[1 + k];
+    if (bj != 0.0 && bk != 0.0) v[0] += bj * bk * Gh[(int64_t)xcols[j] * P + xcols[k]];
+  }
+  for (int j = threadIdx.x; j < p; j += blockDim.x) {
+    double bj = cf[1 + j];
+    if (bj != 0.0) {
+      v[1] += bj * Gh[(int64_t)xcols[j] * P + yc];
+      v[2] += bj * Gh[(int64_t)xcols[j] * P + ones_col];
+    }
+  }
+  block_sum<3>(v, smem);
+  if (threadIdx.x == 0) {
+    double n = Gh[(int64_t)ones_col * P + ones_col];
+    double yy = Gh[(int64_t)yc * P + yc], sy = Gh[(int64_t)ones_col * P + yc];
+    double sse = yy - 2.0 * a0 * sy - 2.0 * v[1] + n * a0 * a0 + 2.0 * a0 * v[2] + v[0];
+    cvraw[(int64_t)q * L + m] = sse / n;
+  }
+}
+
+ATE_API int ate_enet_cvloss_gauss(const void* G, int P, const void* hold, const void* xcols, int p,
+                                  int ones_col, const void* ycol_of_prob, const void* coef,
+                                  const void* nlam_out, int L, int nprob, void* cvraw, void* stream) {
+  hipLaunchKernelGGL(enet_cvloss_gauss_kernel, dim3(L, nprob), dim3(256), 0, (hipStream_t)stream,
+                     (const double*)G, P, (const int*)hold, (const int*)xcols, p, ones_col,
+                     (const int*)ycol_of_prob, (const double*)coef, (const int*)nlam_out, L,
+                     (double*)cvraw);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ selection (cv.glmnet rules)
+// For full problem f with K fold problems fold_probs[f*K + k] and fold sizes nfold[f*K+k]:
+// cvm = weighted mean, cvsd = sqrt(weighted var/(K-1)); idx_min = first (largest lambda)
+// attaining min cvm; idx_1se = first with cvm <= cvm[min] + cvsd[min].
+__global__ void cv_select_kernel(const double* __restrict__ cvraw, const int* __restrict__ fold_probs,
+                                 const double* __restrict__ nfold, int K, int nfull,
+                                 const int* __restrict__ nlam_full, int L, double* __restrict__ cvm,
+                                 double* __restrict__ cvsd, int* __restrict__ sel) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfull) return;
+  const int nl = nlam_full[f];
+  double wsum = 0.0;
+  for (int k = 0; k < K; ++k) wsum += nfold[f * K + k];
+  int imin = 0;
+  double best = INFINITY;
+  for (int m = 0; m < nl; ++m) {
+    double mu = 0.0;
+    for (int k = 0; k < K; ++k) mu += nfold[f * K + k] * cvraw[(int64_t)fold_probs[f * K + k] * L + m];
+    mu /= wsum;
+    double var = 0.0;
+    for (int k = 0; k < K; ++k) {
+      double d = cvraw[(int64_t)fold_probs[f * K + k] * L + m] - mu;
+      var += nfold[f * K + k] * d * d;
+    }
+    double sd = sqrt(var / wsum / (double)(K - 1));
+    cvm[(int64_t)f * L + m] = mu;
+    cvsd[(int64_t)f * L + m] = sd;
+    if (mu < best) { best = mu; imin = m; }
+  }
+  // lambda.min = max(lambda[cvm <= min(cvm)]) -> first index attaining the min
+  int i1 = imin;
+  double thr1 = cvm[(int64_t)f * L + imin] + cvsd[(int64_t)f * L + imin];
+  for (int m = 0; m < nl; ++m)
+    if (cvm[(int64_t)f * L + m] <= thr1) { i1 = m; break; }
+  sel[2 * f] = imin;
+  sel[2 * f + 1] = i1;
+}
+
+ATE_API int ate_cv_select(const void* cvraw, const void* fold_probs, const void* nfold, int K,
+                          int nfull, const void* nlam_full, int L, void* cvm, void* cvsd, void* sel,
+                          void* stream) {
+  hipLaunchKernelGGL(cv_select_kernel, dim3((nfull + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+                     (const double*)cvraw, (const int*)fold_probs, (const double*)nfold, K, nfull,
+                     (const int*)nlam_full, L, (double*)cvm, (double*)cvsd, (int*)sel);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// gather the selected coefficient vector for each full problem: out[f][p+1]
+__global__ void enet_pick_kernel(const double* __restrict__ coef, const int* __restrict__ sel,
+                                 int which, int p, int L, int nfull, double* __restrict__ out) {
+  const int f = blockIdx.x;
+  const int m = sel[2 * f + which];
+  for (int j = threadIdx.x; j <= p; j += blockDim.x)
+    out[(int64_t)f * (p + 1) + j] = coef[((int64_t)f * L + m) * (p + 1) + j];
+}
+
+ATE_API int ate_enet_pick(const void* coef, const void* sel, int which, int p, int L, int nfull,
+                          void* out, void* stream) {
+  hipLaunchKernelGGL(enet_pick_kernel, dim3(nfull), dim3(128), 0, (hipStream_t)stream,
+                     (const double*)coef, (const int*)sel, which, p, L, nfull, (double*)out);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}

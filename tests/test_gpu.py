@@ -1,0 +1,209 @@
+"""GPU numerics tests: every HIP kernel against a plain float64 PyTorch/numpy
+reference of the same op, and every device estimator against the float64 CPU
+reference path (T-ref). Run on the MI355X box: ``pytest -m gpu``."""
+import numpy as np
+import pytest
+import torch
+
+from ate_replication_causalml_amd import _native
+from ate_replication_causalml_amd.ops import gram as gram_op
+from ate_replication_causalml_amd.ops import stats as S
+from ate_replication_causalml_amd.ops.linalg import chol_solve, logistic_irls, predict
+from ate_replication_causalml_amd.ops.panel import build_panel
+from ate_replication_causalml_amd.reference import estimators as E
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    assert a.ate == pytest.approx(b.ate, abs=tol, rel=tol), (a, b)
+    if not np.isnan(b.se):
+        assert a.se == pytest.approx(b.se, abs=tol, rel=tol), (a, b)
+
+
+def test_native_library_loaded(gpu):
+    _native.hip()
+    assert any("libatehip.so" in p for p in _native.loaded_libraries())
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32", "f64"])
+def test_gram_kernel_vs_fp64(gpu, dtype):
+    rs = np.random.RandomState(0)
+    n, p = 3001, 150          # P pads to 256 (bf16: 2x2 tiles incl. an off-diagonal tile)
+    X = rs.randn(n, p) * np.linspace(0.5, 2, p) + np.linspace(-1, 1, p)
+    folds = rs.randint(0, 3, n)
+    pan = build_panel(X, rs.rand(n), rs.randint(0, 2, n), folds=folds, dtype=dtype, device=gpu)
+    G = gram_op.gram(pan).cpu()
+    ref = gram_op.gram_reference(pan)
+    scale = ref.abs().max()
+    tol = {"bf16": 2e-6, "f32": 2e-6, "f64": 1e-13}[dtype]
+    assert ((G - ref).abs().max() / scale) < tol
+    assert torch.allclose(G, G.transpose(1, 2))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_weighted_gram_kernel(gpu, dtype):
+    rs = np.random.RandomState(1)
+    X = rs.randn(1000, 20)
+    pan = build_panel(X, None, rs.rand(1000), dtype=dtype, device=gpu)
+    w = pan.gather_rows(torch.as_tensor(rs.rand(1000) + 0.1, device=gpu).to(pan.dtype))
+    G = gram_op.gram(pan, w).cpu()
+    ref = gram_op.gram_reference(pan, w)
+    tol = 2e-6 if dtype == "f32" else 1e-13
+    assert ((G - ref).abs().max() / ref.abs().max()) < tol
+
+
+def test_chol_solve_kernel_vs_cpu(gpu):
+    rs = np.random.RandomState(2)
+    X = rs.randn(500, 6)
+    X[:, 4] = X[:, 0] - 2 * X[:, 3]
+    y = rs.randn(500)
+    pan = build_panel(X, None, y, dtype="f64", device=gpu)
+    G = gram_op.gram(pan)[0]
+    cols = [pan.cols["one"], *pan.xcols]
+    r = chol_solve(G, cols, pan.cols["Y"])
+    rc = chol_solve(G.cpu(), cols, pan.cols["Y"])
+    b, bc = r.beta.cpu().numpy(), rc.beta.numpy()
+    assert np.array_equal(np.isnan(b), np.isnan(bc)) and np.isnan(b[5])
+    assert np.allclose(np.nan_to_num(b), np.nan_to_num(bc), rtol=1e-10)
+    assert np.allclose(np.nan_to_num(r.invdiag.cpu().numpy()), np.nan_to_num(rc.invdiag.numpy()),
+                       rtol=1e-10)
+    assert np.allclose(r.aux.cpu().numpy()[:2], rc.aux.numpy()[:2], rtol=1e-9)
+
+
+def test_irls_kernel_vs_cpu(gpu):
+    rs = np.random.RandomState(3)
+    X = rs.randn(4000, 8)
+    y = (rs.rand(4000) < 1 / (1 + np.exp(-(X[:, 0] - 0.5 * X[:, 1])))).astype(float)
+    pan = build_panel(X, y, None, dtype="f64", device=gpu, extra_cols=("z",))
+    cols = [pan.cols["one"], *pan.xcols]
+    fit = logistic_irls(pan, cols, pan.cols["W"], pan.cols["z"])
+    from ate_replication_causalml_amd.reference.linear import glm_logit
+    ref = glm_logit(X, y)
+    assert np.allclose(fit.beta.cpu().numpy(), ref.coef, rtol=1e-8, atol=1e-10)
+    assert int(fit.state[2].item()) == ref.iters and fit.state[3].item() == 1.0
+    mu = pan.scatter_rows(fit.mu).cpu().numpy()
+    assert np.allclose(mu, ref.fitted, atol=1e-10)
+    eta = predict(pan, cols, fit.beta, link="logit")
+    assert np.allclose(pan.scatter_rows(eta).cpu().numpy(), ref.fitted, atol=1e-10)
+
+
+def test_score_kernels_vs_cpu(gpu):
+    rs = np.random.RandomState(4)
+    n = 20000
+    w = (rs.rand(n) < 0.3).astype(float)
+    y = (rs.rand(n) < 0.4).astype(float)
+    p = np.clip(rs.rand(n), 0.05, 0.95)
+    p[:3] = [0.0, 1.0, 0.0]
+    mu0, mu1 = rs.rand(n), rs.rand(n)
+    t = lambda a: torch.as_tensor(a, device=gpu)
+    r, m = S.naive(t(y), t(w))
+    rc, mc = S.naive(torch.as_tensor(y), torch.as_tensor(w))
+    assert torch.allclose(r.cpu(), rc, rtol=1e-12)
+    pg = S.clip_propensity_(t(p.copy()))
+    pc = E.clip_propensity(p)
+    assert np.allclose(pg.cpu().numpy(), pc)
+    ra, _ = S.aipw(t(w), t(y), pg, t(mu0), t(mu1))
+    tau = E.aipw_point(w, y, pc, mu0, mu1)
+    se = E.aipw_sandwich_se(w, y, pc, mu0, mu1, tau)
+    assert np.allclose(ra.cpu().numpy(), [tau, se], rtol=1e-10)
+    yr, wr = rs.randn(n), rs.randn(n)
+    mg = S.dml_moments(t(yr), t(wr))
+    mcpu = S.dml_moments(torch.as_tensor(yr), torch.as_tensor(wr))
+    assert torch.allclose(mg.cpu(), mcpu, rtol=1e-11)
+    for mode in ("plr", "lm"):
+        assert torch.allclose(S.dml_finalize(mg, mode).cpu(), S.dml_finalize(mcpu, mode), rtol=1e-11)
+
+
+def test_bootstrap_kernel_matches_philox_reference(gpu):
+    rs = np.random.RandomState(5)
+    e1 = rs.randn(3000)
+    e1[7] = np.nan
+    e2 = rs.randn(3000)
+    tg = S.bootstrap_multinomial(torch.as_tensor(e1, device=gpu), torch.as_tensor(e2, device=gpu),
+                                 64, seed=1991)
+    tc = S.bootstrap_multinomial(torch.as_tensor(e1), torch.as_tensor(e2), 64, seed=1991)
+    assert np.allclose(tg.cpu().numpy(), tc.numpy(), rtol=1e-11)   # same Philox draws
+
+
+def test_enet_cv_kernels_vs_cpu(gpu):
+    from ate_replication_causalml_amd.ops.enet import cv_enet_gaussian
+    from ate_replication_causalml_amd.parallel import rng
+    rs = np.random.RandomState(6)
+    n, p = 3000, 70
+    X = rs.randn(n, p)
+    y = X[:, :4] @ [1.0, -1.0, 0.5, 0.25] + rs.randn(n)
+    fid = rng.fold_ids(n, 10, 1)
+    pan = build_panel(X, None, y, folds=fid, dtype="f64", device=gpu)
+    G = gram_op.gram(pan)
+    pf = np.ones(p)
+    pf[-1] = 0
+    rg = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf)
+    rc = cv_enet_gaussian(G.cpu(), pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf)
+    nl = int(rc.nlam[0])
+    assert int(rg.nlam[0]) == nl
+    assert np.allclose(rg.lambdas[0, :nl].cpu().numpy(), rc.lambdas[0, :nl].numpy(), rtol=1e-12)
+    assert np.allclose(rg.coef_path[0, :nl].cpu().numpy(), rc.coef_path[0, :nl].numpy(),
+                       atol=1e-6)
+    assert torch.equal(rg.sel.cpu().long(), rc.sel.long())
+    assert np.allclose(rg.cvm[0, :nl].cpu().numpy(), rc.cvm[0, :nl].numpy(), rtol=1e-6)
+
+
+def test_device_estimators_vs_reference(gpu, tutorial):
+    from ate_replication_causalml_amd.estimators import lasso as DL
+    from ate_replication_causalml_amd.estimators import linear as D
+    _, m, _ = tutorial
+    Y, W, X = m.Y, m.W, m.X
+    _close(D.naive(Y, W, device=gpu), E.naive(Y, W), 1e-12)
+    _close(D.ols(Y, W, X, device=gpu), E.ols(Y, W, X), 1e-9)
+    p = E.propensity_logistic(W, X)
+    assert np.abs(D.propensity_logistic(W, X, device=gpu).cpu().numpy() - p).max() < 1e-9
+    for compat in ("reference", "textbook"):
+        _close(D.ipw(Y, W, X, p, compat=compat, device=gpu), E.ipw(Y, W, X, p, compat=compat), 1e-8)
+    _close(D.ipw_wls(Y, W, p, device=gpu), E.ipw_wls(Y, W, p), 1e-9)
+    _close(D.aipw_glm(Y, W, X, device=gpu), E.aipw_glm(Y, W, X), 1e-8)
+    _close(D.aipw_glm(Y, W, X, bootstrap_se=True, B=100, device=gpu),
+           E.aipw_glm(Y, W, X, bootstrap_se=True, B=100), 1e-8)
+    _close(DL.lasso_single(Y, W, X, device=gpu), E.lasso_single(Y, W, X), 1e-6)
+    _close(DL.lasso_usual(Y, W, X, device=gpu), E.lasso_usual(Y, W, X), 1e-6)
+    _close(DL.dml_plr_lasso(Y, W, X, device=gpu), E.dml_plr_lasso(Y, W, X), 1e-6)
+
+
+def test_belloni_gpu_vs_reference(gpu, tutorial):
+    from ate_replication_causalml_amd.estimators import lasso as DL
+    _, m, _ = tutorial
+    a = DL.belloni(m.Y, m.W, m.X, device=gpu)
+    b = E.belloni(m.Y, m.W, m.X)
+    _close(a, b, 1e-6)
+
+
+def test_device_dgp_matches_host(gpu):
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    pg = synthetic_panel(5000, p=30, folds=5, seed=9, dtype="f32", device=gpu)
+    pc = synthetic_panel(5000, p=30, folds=5, seed=9, dtype="f64", device="cpu")
+    a = pg.data[:pc.P].double().cpu()[:, : pc.ld]
+    b = pc.data[:, : pg.ld]
+    assert pg.ld == pc.ld
+    diff = (a[: b.shape[0]] - b).abs()
+    # continuous columns agree to fp32 Box-Muller accuracy; binary thresholds may flip
+    # on a handful of draws sitting exactly at the threshold
+    assert (diff > 1e-3).float().mean() < 1e-4
+
+
+def test_dml_bf16_vs_f64_panel(gpu):
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    pb = synthetic_panel(200000, p=60, folds=5, seed=2, dtype="bf16", device=gpu)
+    p64 = synthetic_panel(200000, p=60, folds=5, seed=2, dtype="f64", device=gpu)
+    rb, _, _ = dml_crossfit_panel(pb, 5)
+    r64, _, _ = dml_crossfit_panel(p64, 5)
+    rb, r64 = rb.cpu().numpy(), r64.cpu().numpy()
+    # bf16 storage quantises the continuous covariates (rel 2^-9); the ATE moves by far
+    # less than its standard error
+    assert abs(rb[0] - r64[0]) < 0.05 * r64[1]
+    assert abs(rb[1] - r64[1]) < 0.02 * r64[1]
+
+
+def test_smoke_entry(gpu):
+    import __graft_entry__
+    __graft_entry__.smoke()

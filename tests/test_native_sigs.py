@@ -1,0 +1,41 @@
+"""The ctypes signature table must match every ``ATE_API`` declaration in csrc/,
+and the HIP library must build for gfx950 (cross-compiled here, no GPU needed)."""
+import re
+from pathlib import Path
+
+from ate_replication_causalml_amd import _native
+
+ROOT = Path(__file__).resolve().parent.parent
+TYPE = {"int": "i", "int64_t": "l", "uint64_t": "u", "double": "d"}
+
+
+def _decls():
+    out = {}
+    for f in (ROOT / "csrc").glob("*.hip"):
+        src = f.read_text()
+        for m in re.finditer(r"ATE_API\s+int\s+(\w+)\s*\(([^)]*)\)", src):
+            args = [a.strip() for a in m.group(2).split(",") if a.strip()]
+            sig = ""
+            for a in args:
+                if "*" in a:
+                    sig += "p"
+                else:
+                    t = a.rsplit(" ", 1)[0].replace("const", "").strip()
+                    sig += TYPE[t]
+            out[m.group(1)] = sig
+    return out
+
+
+def test_signature_table_matches_sources():
+    decls = _decls()
+    for name, sig in _native._SIGS.items():
+        assert name in decls, f"{name} not exported by csrc"
+        assert decls[name] == sig, f"{name}: table {sig} != source {decls[name]}"
+    missing = set(decls) - set(_native._SIGS)
+    assert not missing, f"exports without a ctypes signature: {missing}"
+
+
+def test_hip_library_builds():
+    from ate_replication_causalml_amd import _build
+    lib = _build.build_hip()
+    assert lib.exists() and lib.stat().st_size > 10000
