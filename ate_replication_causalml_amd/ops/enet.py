@@ -104,10 +104,19 @@ def cv_enet_gaussian(G: torch.Tensor, panel, xcols, ycols, full_sets=None, penal
             for y in range(ny):
                 fold_index[f * ny + y, k] = (f * K + k) * ny + y
                 nfold[f * ny + y, k] = nreal[fold_hold[f * K + k]]
+    # group fold problems by training set (the path kernel places consecutive problems
+    # on the same XCD, so problems sharing a Gram share an L2)
+    perm = np.argsort([fp[0] for fp in fold_probs], kind="stable")
+    inv = np.empty_like(perm)
+    inv[perm] = np.arange(len(perm))
+    fold_probs = [fold_probs[i] for i in perm]
+    fold_ycol = [fold_ycol[i] for i in perm]
+    fold_holds = [fold_holds[i] for i in perm]
+    fold_index = inv[fold_index].astype(np.int32)
     if G.is_cuda:
         return _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, panel.cols["one"], full_probs,
                        fold_probs, fold_ycol, fold_holds, fold_index, nfold, alpha,
-                       lambda_min_ratio, thresh, maxit, L, full_keys)
+                       lambda_min_ratio, thresh, maxit, L, full_keys, panel.dtype)
     return _cv_cpu(G, masks, xcols, ycols, p, ny, vp, panel.cols["one"], full_probs, fold_probs,
                    fold_ycol, fold_holds, fold_index, nfold, alpha, lambda_min_ratio, thresh, maxit,
                    L, full_keys)
@@ -122,7 +131,8 @@ def _probs_tensor(probs, dev):
 
 
 def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_probs, fold_ycol,
-            fold_holds, fold_index, nfold, alpha, flmin, thresh, maxit, L, full_keys):
+            fold_holds, fold_index, nfold, alpha, flmin, thresh, maxit, L, full_keys,
+            panel_dtype):
     dev = G.device
     s = _stream()
     f64 = dict(dtype=torch.float64, device=dev)
@@ -130,7 +140,8 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     masks_t = torch.from_numpy(masks).to(dev)
     xc = torch.tensor(xcols, dtype=torch.int32, device=dev)
     yc = torch.tensor(ycols, dtype=torch.int32, device=dev)
-    C = torch.empty((nt, p, p), **f64)
+    c_f32 = int(panel_dtype != torch.float64)
+    C = torch.empty((nt, p, p), dtype=torch.float32 if c_f32 else torch.float64, device=dev)
     g = torch.empty((nt, ny, p), **f64)
     xm = torch.empty((nt, p), **f64)
     xs = torch.empty((nt, p), **f64)
@@ -139,7 +150,7 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     ys = torch.empty((nt, ny), **f64)
     nobs = torch.empty(nt, **f64)
     _native.call("ate_enet_prepare", G.data_ptr(), nseg, P, masks_t.data_ptr(), nt, xc.data_ptr(),
-                 p, one, yc.data_ptr(), ny, C.data_ptr(), g.data_ptr(), xm.data_ptr(),
+                 p, one, yc.data_ptr(), ny, C.data_ptr(), c_f32, g.data_ptr(), xm.data_ptr(),
                  xs.data_ptr(), ju.data_ptr(), ym.data_ptr(), ys.data_ptr(), nobs.data_ptr(), s)
     vp_t = torch.tensor(vp, **f64)
     outs = {}
@@ -165,7 +176,7 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
             probs2 = [(0, 0, -2, 0)] * nf + list(probs)
             pr = _probs_tensor(probs2, dev)
             nq = len(probs2)
-        _native.call("ate_enet_path", C.data_ptr(), g.data_ptr(), p, ny, ju.data_ptr(),
+        _native.call("ate_enet_path", C.data_ptr(), c_f32, g.data_ptr(), p, ny, ju.data_ptr(),
                      ys.data_ptr(), vp_t.data_ptr(), pr.data_ptr(), nq, alpha, flmin, thresh,
                      maxit, apath.data_ptr(), lams.data_ptr(), rsq.data_ptr(), nlam.data_ptr(),
                      npass.data_ptr(), L, s)

@@ -25,10 +25,11 @@ using namespace ate;
 // xcols[p], ones_col, ycols[ny]. Outputs per training set s:
 //   C[s][p][p], g[s][ny][p], xm[s][p], xs[s][p] (1 where constant), ju[s][p],
 //   ym[s][ny], ys[s][ny], nobs[s]
+template <typename CT>
 __global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int P,
                                     const unsigned char* __restrict__ masks, int ntrain,
                                     const int* __restrict__ xcols, int p, int ones_col,
-                                    const int* __restrict__ ycols, int ny, double* __restrict__ C,
+                                    const int* __restrict__ ycols, int ny, CT* __restrict__ C,
                                     double* __restrict__ g, double* __restrict__ xm,
                                     double* __restrict__ xs, unsigned char* __restrict__ ju,
                                     double* __restrict__ ym, double* __restrict__ ys,
@@ -54,7 +55,7 @@ __global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int 
       double sj = vj > 0 ? sqrt(vj) : 1.0, sk = vk > 0 ? sqrt(vk) : 1.0;
       double cjk = (gsum(xcols[j], xcols[k]) / n - mj * mk2) / (sj * sk);
       if (!(vj > 0) || !(vk > 0)) cjk = (j == k) ? 1.0 : 0.0;
-      C[((int64_t)s * p + j) * p + k] = cjk;
+      C[((int64_t)s * p + j) * p + k] = (CT)cjk;
     } else if (e < (int64_t)p * p + (int64_t)ny * p) {
       int64_t r = e - (int64_t)p * p;
       int y = (int)(r / p), j = (int)(r % p);
@@ -85,15 +86,22 @@ __global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int 
 
 ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, int ntrain,
                              const void* xcols, int p, int ones_col, const void* ycols, int ny,
-                             void* C, void* g, void* xm, void* xs, void* ju, void* ym, void* ys,
-                             void* nobs, void* stream) {
+                             void* C, int c_f32, void* g, void* xm, void* xs, void* ju, void* ym,
+                             void* ys, void* nobs, void* stream) {
   int64_t total = (int64_t)p * p + (int64_t)ny * p + p + ny;
   dim3 grid(grid_for(total, 256, 512), ntrain);
-  hipLaunchKernelGGL(enet_prepare_kernel, grid, dim3(256), 0, (hipStream_t)stream,
-                     (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
-                     (const int*)xcols, p, ones_col, (const int*)ycols, ny, (double*)C, (double*)g,
-                     (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
-                     (double*)nobs);
+  if (c_f32)
+    hipLaunchKernelGGL(enet_prepare_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
+                       (const int*)xcols, p, ones_col, (const int*)ycols, ny, (float*)C, (double*)g,
+                       (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
+                       (double*)nobs);
+  else
+    hipLaunchKernelGGL(enet_prepare_kernel<double>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
+                       (const int*)xcols, p, ones_col, (const int*)ycols, ny, (double*)C, (double*)g,
+                       (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
+                       (double*)nobs);
   ATE_CHECK_LAUNCH();
   return 0;
 }
@@ -102,26 +110,41 @@ ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, 
 struct EnetProblem {
   int train;        // training set index (C, xm, xs, ju)
   int y;            // response index within the training set's g/ym/ys
-  int ulam_src;     // -1: computed path; else problem whose (original-scale) lambdas to use
+  int ulam_src;     // -1: computed path; >=0: problem whose (original-scale) lambdas to use;
+                    // < -1: placeholder slot (skipped)
   int nlam_req;
 };
 
 constexpr double BIGL = 9.9e35;
 
-template <int T>
-__global__ __launch_bounds__(64) void enet_path_kernel(
-    const double* __restrict__ C, const double* __restrict__ gin, int p, int ny,
+// Pass structure (glmnet elnet1): coordinates are visited in index order; a coordinate
+// is processed iff it is nonzero or |u| > vp*lambda (u = g + a). The coordinates that
+// are NONZERO when a pass starts are certain to be processed, in order, so their Gram
+// rows are streamed ahead of use through a double-buffered register ring of D rows
+// (fp32 rows for bf16/fp32 panels; the g/a state stays fp64). Coordinates that newly
+// cross the threshold (rare) take a slow path with a direct row load.
+template <int T, typename CT, int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void enet_path_kernel(
+    const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
     const unsigned char* __restrict__ ju_s, const double* __restrict__ ys_s,
     const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
     int* __restrict__ nlam_out, int* __restrict__ npass_out, int L) {
-  const int q = blockIdx.x;
+  __shared__ short slist[T * 64];
+  // XCD-aware placement: consecutive problem ids (sorted by training set on the host)
+  // land on the same XCD, so problems sharing a Gram share that XCD's L2.
+  int q;
+  {
+    int bid = blockIdx.x, nwg = gridDim.x;
+    int xcd = bid & 7, qq = nwg >> 3, r = nwg & 7;
+    q = ((xcd < r) ? xcd * (qq + 1) : r * (qq + 1) + (xcd - r) * qq) + (bid >> 3);
+  }
   if (q >= nprob) return;
   const EnetProblem pr = probs[q];
-  if (pr.ulam_src < -1) return;          // placeholder slot (source path already computed)
+  if (pr.ulam_src < -1) return;
   const int lane = threadIdx.x;
-  const double* Cq = C + (int64_t)pr.train * p * p;
+  const CT* Cq = C + (int64_t)pr.train * p * p;
   const double ysq = ys_s[(int64_t)pr.train * ny + pr.y];
   double g[T], a[T], vp[T];
   bool ju[T], act[T];
@@ -139,6 +162,100 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
   const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
   double alm = 0.0, rsq = 0.0, rsq_prev = 0.0;
   int npass = 0, m_out = 0;
+  double ab = 0.0, dem = 0.0, dlx = 0.0;
+
+  auto load_row = [&](CT (&R)[T], int j) {
+    const CT* row = Cq + (int64_t)j * p;
+#pragma unroll
+    for (int t2 = 0; t2 < T; ++t2) {
+      int k = t2 * 64 + lane;
+      R[t2] = k < p ? row[k] : CT(0);
+    }
+  };
+  // coordinate update of j (uniform) given its Gram row in registers
+  auto update = [&](int j, const CT (&R)[T]) {
+    const int tj = j >> 6, jl = j & 63;
+    double gsel = 0.0, asel = 0.0, vsel = 0.0;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+      if (t == tj) { gsel = g[t]; asel = a[t]; vsel = vp[t]; }
+    const double gj = __shfl(gsel, jl), aj = __shfl(asel, jl), vpj = __shfl(vsel, jl);
+    const double uj = gj + aj;
+    const double v = fabs(uj) - vpj * ab;
+    const double an = v > 0.0 ? copysign(v, uj) / (1.0 + vpj * dem) : 0.0;
+    if (an == aj) return;
+    const double d = an - aj;
+    rsq += d * (2.0 * gj - d);
+    dlx = fmax(dlx, d * d);
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+      if (t == tj && lane == jl) { a[t] = an; act[t] = true; }
+#pragma unroll
+    for (int t2 = 0; t2 < T; ++t2) g[t2] -= (double)R[t2] * d;
+  };
+  // process, in order, every coordinate in [lo, hi) with a == 0 that crosses the threshold.
+  // The block index is dynamic, so per-block state is gathered with static selects
+  // (keeps g/a/vp in registers; a runtime-indexed register array would go to scratch).
+  auto scan_new = [&](bool full, int lo, int hi) {
+    int tb = lo >> 6;
+    int last = lo - tb * 64 - 1;
+    while (tb < T && tb * 64 < hi) {
+      double gt = 0.0, at = 0.0, vt = 0.0;
+      bool jt = false, actt = false;
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+        if (t == tb) { gt = g[t]; at = a[t]; vt = vp[t]; jt = ju[t]; actt = act[t]; }
+      const int k = tb * 64 + lane;
+      bool cand = jt && (full || actt) && at == 0.0 && lane > last && k < hi && fabs(gt) > vt * ab;
+      uint64_t msk = __ballot(cand);
+      if (!msk) { ++tb; last = -1; continue; }
+      int jl = __ffsll((unsigned long long)msk) - 1;
+      last = jl;
+      CT R[T];
+      load_row(R, tb * 64 + jl);
+      update(tb * 64 + jl, R);
+    }
+  };
+  auto pass = [&](bool full) -> double {
+    dlx = 0.0;
+    int S = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      bool sure = ju[t] && (full || act[t]) && a[t] != 0.0;
+      uint64_t m = __ballot(sure);
+      int rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (sure) slist[S + rank] = (short)(t * 64 + lane);
+      S += __popcll(m);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): list visible to the whole wave
+    int pos = 0;
+    CT RA[D][T], RB[D][T];
+    auto fill = [&](CT (&R)[D][T], int c0) {
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+        if (c0 + i < S) load_row(R[i], slist[c0 + i]);
+    };
+    auto drain = [&](CT (&R)[D][T], int c0) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        if (c0 + i >= S) break;
+        const int tgt = slist[c0 + i];
+        if (tgt > pos) scan_new(full, pos, tgt);
+        update(tgt, R[i]);
+        pos = tgt + 1;
+      }
+    };
+    fill(RA, 0);
+    for (int c0 = 0; c0 < S; c0 += 2 * D) {
+      fill(RB, c0 + D);
+      drain(RA, c0);
+      fill(RA, c0 + 2 * D);
+      drain(RB, c0 + D);
+    }
+    if (pos < p) scan_new(full, pos, p);
+    return dlx;
+  };
+
   for (int m = 0; m < nlam; ++m) {
     if (pr.ulam_src >= 0) {
       alm = lams[(int64_t)pr.ulam_src * L + m] / ysq;
@@ -154,51 +271,18 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
     } else {
       alm *= alf;
     }
-    const double ab = alm * alpha, dem = alm * (1.0 - alpha);
-    // ---- coordinate descent at this lambda
-    auto pass = [&](bool full) -> double {
-      double dlx = 0.0;
-#pragma unroll
-      for (int t = 0; t < T; ++t) {
-        int last = -1;
-        while (true) {
-          double u = g[t] + a[t];           // xv = 1 (standardised gaussian)
-          bool cand = ju[t] && (full || act[t]) && lane > last &&
-                      (a[t] != 0.0 || fabs(u) > vp[t] * ab);
-          uint64_t msk = __ballot(cand);
-          if (!msk) break;
-          int jl = __ffsll((unsigned long long)msk) - 1;
-          last = jl;
-          double gj = __shfl(g[t], jl), aj = __shfl(a[t], jl), vpj = __shfl(vp[t], jl);
-          double uj = gj + aj;
-          double v = fabs(uj) - vpj * ab;
-          double an = v > 0.0 ? copysign(v, uj) / (1.0 + vpj * dem) : 0.0;
-          if (an == aj) continue;
-          double d = an - aj;
-          rsq += d * (2.0 * gj - d);
-          dlx = fmax(dlx, d * d);
-          if (lane == jl) { a[t] = an; act[t] = true; }
-          const double* row = Cq + (int64_t)(t * 64 + jl) * p;
-#pragma unroll
-          for (int t2 = 0; t2 < T; ++t2) {
-            int k = t2 * 64 + lane;
-            if (k < p) g[t2] -= row[k] * d;
-          }
-        }
-      }
-      return dlx;
-    };
+    ab = alm * alpha;
+    dem = alm * (1.0 - alpha);
     while (npass < maxit) {
       ++npass;
-      double dlx = pass(true);
-      if (dlx < thr) break;
+      double dl = pass(true);
+      if (dl < thr) break;
       while (npass < maxit) {
         ++npass;
-        dlx = pass(false);
-        if (dlx < thr) break;
+        dl = pass(false);
+        if (dl < thr) break;
       }
     }
-    // ---- record (standardised coefficients, original-scale lambda)
     double* ap = apath + ((int64_t)q * L + m) * p;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -225,23 +309,33 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
   }
 }
 
-ATE_API int ate_enet_path(const void* C, const void* g, int p, int ny, const void* ju,
+ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny, const void* ju,
                           const void* ys, const void* vp, const void* probs, int nprob,
                           double alpha, double flmin, double thr, int maxit, void* apath,
                           void* lams, void* rsqs, void* nlam_out, void* npass_out, int L,
                           void* stream) {
   hipStream_t s = (hipStream_t)stream;
-#define LAUNCH_T(TT)                                                                          \
-  hipLaunchKernelGGL(enet_path_kernel<TT>, dim3(nprob), dim3(64), 0, s, (const double*)C,     \
-                     (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,    \
-                     (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,  \
-                     maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,    \
+  // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nprob)
+  const int nwg = (nprob + 7) / 8 * 8;
+#define LAUNCH_T(TT, CTT, DD)                                                                   \
+  hipLaunchKernelGGL((enet_path_kernel<TT, CTT, DD>), dim3(nwg), dim3(64), 0, s, (const CTT*)C, \
+                     (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,      \
+                     (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,    \
+                     maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,      \
                      (int*)npass_out, L)
-  if (p <= 64) LAUNCH_T(1);
-  else if (p <= 128) LAUNCH_T(2);
-  else if (p <= 256) LAUNCH_T(4);
-  else if (p <= 512) LAUNCH_T(8);
-  else return -2;
+  if (c_f32) {
+    if (p <= 64) LAUNCH_T(1, float, 8);
+    else if (p <= 128) LAUNCH_T(2, float, 8);
+    else if (p <= 256) LAUNCH_T(4, float, 8);
+    else if (p <= 512) LAUNCH_T(8, float, 6);
+    else return -2;
+  } else {
+    if (p <= 64) LAUNCH_T(1, double, 8);
+    else if (p <= 128) LAUNCH_T(2, double, 8);
+    else if (p <= 256) LAUNCH_T(4, double, 4);
+    else if (p <= 512) LAUNCH_T(8, double, 4);
+    else return -2;
+  }
 #undef LAUNCH_T
   ATE_CHECK_LAUNCH();
   return 0;
