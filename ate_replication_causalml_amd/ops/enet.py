@@ -141,7 +141,8 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     xc = torch.tensor(xcols, dtype=torch.int32, device=dev)
     yc = torch.tensor(ycols, dtype=torch.int32, device=dev)
     c_f32 = int(panel_dtype != torch.float64)
-    C = torch.empty((nt, p, p), dtype=torch.float32 if c_f32 else torch.float64, device=dev)
+    ldc = (p + 63) // 64 * 64   # zero-padded row stride (16-B aligned row segments)
+    C = torch.zeros((nt, p, ldc), dtype=torch.float32 if c_f32 else torch.float64, device=dev)
     g = torch.empty((nt, ny, p), **f64)
     xm = torch.empty((nt, p), **f64)
     xs = torch.empty((nt, p), **f64)

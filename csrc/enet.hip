@@ -28,7 +28,7 @@ using namespace ate;
 template <typename CT>
 __global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int P,
                                     const unsigned char* __restrict__ masks, int ntrain,
-                                    const int* __restrict__ xcols, int p, int ones_col,
+                                    const int* __restrict__ xcols, int p, int ldc, int ones_col,
                                     const int* __restrict__ ycols, int ny, CT* __restrict__ C,
                                     double* __restrict__ g, double* __restrict__ xm,
                                     double* __restrict__ xs, unsigned char* __restrict__ ju,
@@ -55,7 +55,7 @@ __global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int 
       double sj = vj > 0 ? sqrt(vj) : 1.0, sk = vk > 0 ? sqrt(vk) : 1.0;
       double cjk = (gsum(xcols[j], xcols[k]) / n - mj * mk2) / (sj * sk);
       if (!(vj > 0) || !(vk > 0)) cjk = (j == k) ? 1.0 : 0.0;
-      C[((int64_t)s * p + j) * p + k] = (CT)cjk;
+      C[((int64_t)s * p + j) * ldc + k] = (CT)cjk;
     } else if (e < (int64_t)p * p + (int64_t)ny * p) {
       int64_t r = e - (int64_t)p * p;
       int y = (int)(r / p), j = (int)(r % p);
@@ -90,16 +90,17 @@ ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, 
                              void* ys, void* nobs, void* stream) {
   int64_t total = (int64_t)p * p + (int64_t)ny * p + p + ny;
   dim3 grid(grid_for(total, 256, 512), ntrain);
+  const int ldc = (p + 63) / 64 * 64;   // padded row stride (C buffer must be zeroed)
   if (c_f32)
     hipLaunchKernelGGL(enet_prepare_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream,
                        (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
-                       (const int*)xcols, p, ones_col, (const int*)ycols, ny, (float*)C, (double*)g,
+                       (const int*)xcols, p, ldc, ones_col, (const int*)ycols, ny, (float*)C, (double*)g,
                        (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
                        (double*)nobs);
   else
     hipLaunchKernelGGL(enet_prepare_kernel<double>, grid, dim3(256), 0, (hipStream_t)stream,
                        (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
-                       (const int*)xcols, p, ones_col, (const int*)ycols, ny, (double*)C, (double*)g,
+                       (const int*)xcols, p, ldc, ones_col, (const int*)ycols, ny, (double*)C, (double*)g,
                        (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
                        (double*)nobs);
   ATE_CHECK_LAUNCH();
@@ -116,22 +117,49 @@ struct EnetProblem {
 };
 
 constexpr double BIGL = 9.9e35;
+constexpr int PMAX = 512;
 
-// Pass structure (glmnet elnet1): coordinates are visited in index order; a coordinate
-// is processed iff it is nonzero or |u| > vp*lambda (u = g + a). The coordinates that
-// are NONZERO when a pass starts are certain to be processed, in order, so their Gram
-// rows are streamed ahead of use through a double-buffered register ring of D rows
-// (fp32 rows for bf16/fp32 panels; the g/a state stays fp64). Coordinates that newly
-// cross the threshold (rare) take a slow path with a direct row load.
-template <int T, typename CT, int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void enet_path_kernel(
+template <typename CT> struct VecT;
+template <> struct VecT<float> { typedef float4 type; };
+template <> struct VecT<double> { typedef double2 type; };
+__device__ __forceinline__ float vdot(float4 a, float4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+__device__ __forceinline__ double vdot(double2 a, double2 b) { return a.x * b.x + a.y * b.y; }
+
+__device__ __forceinline__ double readlane_d(double v, int i) {
+  int lo = __builtin_amdgcn_readlane(__double2loint(v), i);
+  int hi = __builtin_amdgcn_readlane(__double2hiint(v), i);
+  return __hiloint2double(hi, lo);
+}
+
+// Blocked covariance-mode coordinate descent, ONE WAVE per problem.
+//
+// glmnet's pass visits coordinates j = 0..p-1 in order and processes j iff it is nonzero
+// or |u_j| > vp_j*lambda (u = g + a). We walk the coordinates in blocks of 64:
+//   * gradient / coefficients / flags of all p coordinates live in LDS (fp64);
+//   * inside block t the recurrence only involves the 64x64 diagonal Gram block, staged
+//     in LDS: lane l keeps g of coordinate t*64+l in a register, the next coordinate to
+//     process is found with a ballot re-evaluated after every update (so zero coordinates
+//     are tested against the current gradient exactly as in the sequential pass), and an
+//     update costs one LDS read + one FMA per lane;
+//   * after block t its deltas are propagated to every other block with bulk, coalesced
+//     row-segment loads  g[t2*64+l] -= sum_i C[t2*64+l][t*64+i] d_i  -- no serial memory
+//     latency on the coordinate chain.
+// Same sequence of coordinate updates as glmnet's pass; only the order of floating-point
+// additions into far gradients differs.
+template <typename CT>
+__global__ __launch_bounds__(64) void enet_path_kernel(
     const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
     const unsigned char* __restrict__ ju_s, const double* __restrict__ ys_s,
     const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
     int* __restrict__ nlam_out, int* __restrict__ npass_out, int L) {
-  __shared__ short slist[T * 64];
+  __shared__ double sg[PMAX], sa[PMAX], svp[PMAX];
+  __shared__ int sflag[PMAX];       // bit0 ju, bit1 active
+  __shared__ CT sC[64 * 64];
+  __shared__ __attribute__((aligned(16))) CT sd[64];
   // XCD-aware placement: consecutive problem ids (sorted by training set on the host)
   // land on the same XCD, so problems sharing a Gram share that XCD's L2.
   int q;
@@ -144,115 +172,83 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const EnetProblem pr = probs[q];
   if (pr.ulam_src < -1) return;
   const int lane = threadIdx.x;
-  const CT* Cq = C + (int64_t)pr.train * p * p;
+  const int T = (p + 63) >> 6;
+  const int ldc = T * 64;
+  const CT* Cq = C + (int64_t)pr.train * p * ldc;
   const double ysq = ys_s[(int64_t)pr.train * ny + pr.y];
-  double g[T], a[T], vp[T];
-  bool ju[T], act[T];
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    int k = t * 64 + lane;
+  for (int k = lane; k < T * 64; k += 64) {
     bool in = k < p;
-    g[t] = in ? gin[((int64_t)pr.train * ny + pr.y) * p + k] : 0.0;
-    a[t] = 0.0;
-    vp[t] = in ? vp_in[k] : 0.0;
-    ju[t] = in && ju_s[(int64_t)pr.train * p + k];
-    act[t] = false;
+    sg[k] = in ? gin[((int64_t)pr.train * ny + pr.y) * p + k] : 0.0;
+    sa[k] = 0.0;
+    svp[k] = in ? vp_in[k] : 0.0;
+    sflag[k] = (in && ju_s[(int64_t)pr.train * p + k]) ? 1 : 0;
   }
+  __syncthreads();
   const int nlam = pr.ulam_src >= 0 ? nlam_out[pr.ulam_src] : pr.nlam_req;
   const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
   double alm = 0.0, rsq = 0.0, rsq_prev = 0.0;
   int npass = 0, m_out = 0;
-  double ab = 0.0, dem = 0.0, dlx = 0.0;
+  double ab = 0.0, dem = 0.0;
 
-  auto load_row = [&](CT (&R)[T], int j) {
-    const CT* row = Cq + (int64_t)j * p;
-#pragma unroll
-    for (int t2 = 0; t2 < T; ++t2) {
-      int k = t2 * 64 + lane;
-      R[t2] = k < p ? row[k] : CT(0);
-    }
-  };
-  // coordinate update of j (uniform) given its Gram row in registers
-  auto update = [&](int j, const CT (&R)[T]) {
-    const int tj = j >> 6, jl = j & 63;
-    double gsel = 0.0, asel = 0.0, vsel = 0.0;
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-      if (t == tj) { gsel = g[t]; asel = a[t]; vsel = vp[t]; }
-    const double gj = __shfl(gsel, jl), aj = __shfl(asel, jl), vpj = __shfl(vsel, jl);
-    const double uj = gj + aj;
-    const double v = fabs(uj) - vpj * ab;
-    const double an = v > 0.0 ? copysign(v, uj) / (1.0 + vpj * dem) : 0.0;
-    if (an == aj) return;
-    const double d = an - aj;
-    rsq += d * (2.0 * gj - d);
-    dlx = fmax(dlx, d * d);
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-      if (t == tj && lane == jl) { a[t] = an; act[t] = true; }
-#pragma unroll
-    for (int t2 = 0; t2 < T; ++t2) g[t2] -= (double)R[t2] * d;
-  };
-  // process, in order, every coordinate in [lo, hi) with a == 0 that crosses the threshold.
-  // The block index is dynamic, so per-block state is gathered with static selects
-  // (keeps g/a/vp in registers; a runtime-indexed register array would go to scratch).
-  auto scan_new = [&](bool full, int lo, int hi) {
-    int tb = lo >> 6;
-    int last = lo - tb * 64 - 1;
-    while (tb < T && tb * 64 < hi) {
-      double gt = 0.0, at = 0.0, vt = 0.0;
-      bool jt = false, actt = false;
-#pragma unroll
-      for (int t = 0; t < T; ++t)
-        if (t == tb) { gt = g[t]; at = a[t]; vt = vp[t]; jt = ju[t]; actt = act[t]; }
-      const int k = tb * 64 + lane;
-      bool cand = jt && (full || actt) && at == 0.0 && lane > last && k < hi && fabs(gt) > vt * ab;
-      uint64_t msk = __ballot(cand);
-      if (!msk) { ++tb; last = -1; continue; }
-      int jl = __ffsll((unsigned long long)msk) - 1;
-      last = jl;
-      CT R[T];
-      load_row(R, tb * 64 + jl);
-      update(tb * 64 + jl, R);
-    }
-  };
   auto pass = [&](bool full) -> double {
-    dlx = 0.0;
-    int S = 0;
-#pragma unroll
+    double dlx = 0.0;
     for (int t = 0; t < T; ++t) {
-      bool sure = ju[t] && (full || act[t]) && a[t] != 0.0;
-      uint64_t m = __ballot(sure);
-      int rank = __popcll(m & ((1ull << lane) - 1ull));
-      if (sure) slist[S + rank] = (short)(t * 64 + lane);
-      S += __popcll(m);
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): list visible to the whole wave
-    int pos = 0;
-    CT RA[D][T], RB[D][T];
-    auto fill = [&](CT (&R)[D][T], int c0) {
-#pragma unroll
-      for (int i = 0; i < D; ++i)
-        if (c0 + i < S) load_row(R[i], slist[c0 + i]);
-    };
-    auto drain = [&](CT (&R)[D][T], int c0) {
-#pragma unroll
-      for (int i = 0; i < D; ++i) {
-        if (c0 + i >= S) break;
-        const int tgt = slist[c0 + i];
-        if (tgt > pos) scan_new(full, pos, tgt);
-        update(tgt, R[i]);
-        pos = tgt + 1;
+      const int k = t * 64 + lane;
+      double gt = sg[k], at = sa[k];
+      const double vpt = svp[k];
+      int fl = sflag[k];
+      const bool elig = (fl & 1) && (full || (fl & 2));
+      if (!__ballot(elig && (at != 0.0 || fabs(gt + at) > vpt * ab))) continue;
+      // stage the diagonal Gram block: sC[i*64 + l] = C[t*64+i][t*64+l]
+      for (int i = 0; i < 64; ++i) {
+        int r = t * 64 + i;
+        sC[i * 64 + lane] = r < p ? Cq[(int64_t)r * ldc + k] : CT(0);
       }
-    };
-    fill(RA, 0);
-    for (int c0 = 0; c0 < S; c0 += 2 * D) {
-      fill(RB, c0 + D);
-      drain(RA, c0);
-      fill(RA, c0 + 2 * D);
-      drain(RB, c0 + D);
+      __syncthreads();
+      double dblk = 0.0;
+      int last = -1;
+      while (true) {
+        const bool cand = elig && lane > last && (at != 0.0 || fabs(gt + at) > vpt * ab);
+        const uint64_t msk = __ballot(cand);
+        if (!msk) break;
+        const int i = __ffsll((unsigned long long)msk) - 1;
+        last = i;
+        const double cil = (double)sC[i * 64 + lane];
+        const double gi = readlane_d(gt, i), ai = readlane_d(at, i), vpi = readlane_d(vpt, i);
+        const double u = gi + ai;
+        const double v = fabs(u) - vpi * ab;
+        const double an = v > 0.0 ? copysign(v, u) / (1.0 + vpi * dem) : 0.0;
+        if (an == ai) continue;
+        const double d = an - ai;
+        rsq += d * (2.0 * gi - d);
+        dlx = fmax(dlx, d * d);
+        if (lane == i) { at = an; fl |= 2; dblk = d; }
+        gt -= cil * d;
+      }
+      sg[k] = gt;
+      sa[k] = at;
+      sflag[k] = fl;
+      if (!__ballot(dblk != 0.0)) { __syncthreads(); continue; }
+      sd[lane] = (CT)dblk;
+      __syncthreads();
+      // propagate: g[t2*64+l] -= sum_i C[t2*64+l][t*64+i] * d_i  for t2 != t
+      for (int t2 = 0; t2 < T; ++t2) {
+        if (t2 == t) continue;
+        const int k2 = t2 * 64 + lane;
+        if (k2 < p) {
+          // 64 contiguous (16-B aligned, zero-padded) entries of row k2, 16 B per load
+          typedef typename VecT<CT>::type V;
+          constexpr int W = sizeof(V) / sizeof(CT);
+          const V* row = reinterpret_cast<const V*>(Cq + (int64_t)k2 * ldc + t * 64);
+          const V* dv = reinterpret_cast<const V*>(sd);
+          CT acc = 0;
+#pragma unroll
+          for (int c = 0; c < 64 / W; ++c) acc += vdot(row[c], dv[c]);
+          sg[k2] -= (double)acc;
+        }
+      }
+      __syncthreads();
     }
-    if (pos < p) scan_new(full, pos, p);
     return dlx;
   };
 
@@ -263,9 +259,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       alm = BIGL;
     } else if (m == 1) {
       double mx = 0.0;
-#pragma unroll
-      for (int t = 0; t < T; ++t)
-        if (ju[t] && vp[t] > 0.0) mx = fmax(mx, fabs(g[t]) / vp[t]);
+      for (int k = lane; k < p; k += 64)
+        if ((sflag[k] & 1) && svp[k] > 0.0) mx = fmax(mx, fabs(sg[k]) / svp[k]);
       mx = wave_max(mx);
       alm = alf * mx / fmax(alpha, 1e-3);
     } else {
@@ -284,11 +279,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     double* ap = apath + ((int64_t)q * L + m) * p;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      int k = t * 64 + lane;
-      if (k < p) ap[k] = a[t];
-    }
+    for (int k = lane; k < p; k += 64) ap[k] = sa[k];
     if (lane == 0) {
       lams[(int64_t)q * L + m] = alm * ysq;
       rsqs[(int64_t)q * L + m] = rsq;
@@ -314,29 +305,19 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
                           double alpha, double flmin, double thr, int maxit, void* apath,
                           void* lams, void* rsqs, void* nlam_out, void* npass_out, int L,
                           void* stream) {
+  if (p > PMAX) return -2;
   hipStream_t s = (hipStream_t)stream;
-  // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nprob)
+  // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nwg)
   const int nwg = (nprob + 7) / 8 * 8;
-#define LAUNCH_T(TT, CTT, DD)                                                                   \
-  hipLaunchKernelGGL((enet_path_kernel<TT, CTT, DD>), dim3(nwg), dim3(64), 0, s, (const CTT*)C, \
-                     (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,      \
-                     (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,    \
-                     maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,      \
+#define LAUNCH_C(CTT)                                                                          \
+  hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(64), 0, s, (const CTT*)C,        \
+                     (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
+                     (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
+                     maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
                      (int*)npass_out, L)
-  if (c_f32) {
-    if (p <= 64) LAUNCH_T(1, float, 8);
-    else if (p <= 128) LAUNCH_T(2, float, 8);
-    else if (p <= 256) LAUNCH_T(4, float, 8);
-    else if (p <= 512) LAUNCH_T(8, float, 6);
-    else return -2;
-  } else {
-    if (p <= 64) LAUNCH_T(1, double, 8);
-    else if (p <= 128) LAUNCH_T(2, double, 8);
-    else if (p <= 256) LAUNCH_T(4, double, 4);
-    else if (p <= 512) LAUNCH_T(8, double, 4);
-    else return -2;
-  }
-#undef LAUNCH_T
+  if (c_f32) LAUNCH_C(float);
+  else LAUNCH_C(double);
+#undef LAUNCH_C
   ATE_CHECK_LAUNCH();
   return 0;
 }
