@@ -142,7 +142,9 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
     dev = pan.device
     xc = torch.tensor(pan.xcols, dtype=torch.int32, device=dev)
     segs = torch.tensor(np.asarray(pan.seg_bounds[:K], dtype=np.int64), device=dev)
-    nbx = 256
+    bf = pan.dtype == torch.bfloat16
+    # bf16: 2048 rows per block; enough blocks per fold to fill 256 CUs several times
+    nbx = 512 if bf else 256
     part = torch.empty(K * nbx * 7, dtype=torch.float64, device=dev)
     mom = torch.empty(7, dtype=torch.float64, device=dev)
     bf = pan.dtype == torch.bfloat16

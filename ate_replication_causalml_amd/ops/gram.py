@@ -15,6 +15,7 @@ from .. import _native
 from .panel import DevicePanel
 
 BF16_TILE, BF16_K = 128, 64
+BF16_TILE_BIG = 256
 SMALL_TILE, SMALL_K = 64, 16
 TARGET_WG = 2048   # workgroups per launch (>= 8 per CU on 256 CUs)
 
@@ -30,16 +31,20 @@ class GramPlan:
         bf16 = panel.dtype == torch.bfloat16
         if bf16 and weighted:
             raise ValueError("weighted Gram needs an fp32/fp64 panel")
-        T = BF16_TILE if bf16 else SMALL_TILE
-        K = BF16_K if bf16 else SMALL_K
         P = panel.P
+        if bf16:
+            T = BF16_TILE_BIG if P % BF16_TILE_BIG == 0 else BF16_TILE
+        else:
+            T = SMALL_TILE
+        K = BF16_K if bf16 else SMALL_K
         if P % T:
             raise ValueError(f"panel P={P} must be a multiple of {T}")
         nt = P // T
         tiles = [(a, b) for a in range(nt) for b in range(a, nt)]
         ntiles = len(tiles)
         rows_total = int((panel.seg_bounds[:, 1] - panel.seg_bounds[:, 0]).sum())
-        nchunk_target = max(1, TARGET_WG // ntiles)
+        target = 768 if T == BF16_TILE_BIG else TARGET_WG   # 256-tile: 1 WG (128 KB LDS) / CU
+        nchunk_target = max(1, target // ntiles)
         ch_rows = max(K, (rows_total // nchunk_target) // K * K)
         chunks = []
         seg_chunk0 = [0]
@@ -84,7 +89,7 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     G = pl.G if out is None else out
     s = _stream()
     if X.dtype == torch.bfloat16:
-        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.tiles.data_ptr(),
+        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.T, pl.tiles.data_ptr(),
                      pl.ntiles, pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(),
                      panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
     else:

@@ -105,6 +105,73 @@ static int dml_resid_t(const void* X, int64_t ld, const void* xcols, int p, cons
   return 0;
 }
 
+// bf16 panels: each thread owns 8 CONSECUTIVE rows, so every column read is one 16-byte
+// load (a wave reads 1 KB contiguous per column -- Guideline 13); dot products in fp32
+// (bf16 values are exact in fp32; coefficients rounded to fp32), moments in fp64.
+__global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
+    const bf16_t* __restrict__ X, int64_t ld, const int* __restrict__ xcols, int p,
+    const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+    int y0, int y1, int w0, int w1, int vcol, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float shf[];
+  float* cy = shf;                 // [p+1]
+  float* cw = shf + (p + 1);       // [p+1]
+  int* xc = (int*)(shf + 2 * (p + 1));
+  __shared__ double red[16 * 7];
+  const int k = blockIdx.y;
+  for (int j = threadIdx.x; j < p; j += blockDim.x) xc[j] = xcols[j];
+  for (int j = threadIdx.x; j <= p; j += blockDim.x) {
+    cy[j] = (float)coef[((int64_t)k * 2 + 0) * (p + 1) + j];
+    cw[j] = (float)coef[((int64_t)k * 2 + 1) * (p + 1) + j];
+  }
+  __syncthreads();
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  const Seg sg = segs[k];
+  auto ld8 = [&](int c, int64_t i, float (&o)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(X + (int64_t)c * ld + i);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[2 * q] = __uint_as_float(w[q] << 16);
+      o[2 * q + 1] = __uint_as_float(w[q] & 0xFFFF0000u);
+    }
+  };
+  for (int64_t i = sg.r0 + ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8; i < sg.r1;
+       i += (int64_t)gridDim.x * 256 * 8) {
+    float py[8], pw[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) { py[r] = cy[0]; pw[r] = cw[0]; }
+#pragma unroll 4
+    for (int j = 0; j < p; ++j) {
+      float x[8];
+      ld8(xc[j], i, x);
+      const float by = cy[1 + j], bw = cw[1 + j];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) { py[r] += by * x[r]; pw[r] += bw * x[r]; }
+    }
+    float vv[8], ya[8], yb[8], wa[8], wb[8];
+    ld8(vcol, i, vv);
+    ld8(y0, i, ya);
+    ld8(w0, i, wa);
+    if (y1 >= 0) ld8(y1, i, yb); else { for (int r = 0; r < 8; ++r) yb[r] = 0.f; }
+    if (w1 >= 0) ld8(w1, i, wb); else { for (int r = 0; r < 8; ++r) wb[r] = 0.f; }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (vv[r] == 0.f) continue;
+      const double yr = ((double)ya[r] + (double)yb[r]) - (double)py[r];
+      const double wr = ((double)wa[r] + (double)wb[r]) - (double)pw[r];
+      const double w2 = wr * wr;
+      v[0] += wr * yr; v[1] += w2; v[2] += yr * yr * w2; v[3] += yr * w2 * wr; v[4] += w2 * w2;
+      v[5] += 1.0; v[6] += yr * yr;
+    }
+  }
+  block_sum<7>(v, red);
+  if (threadIdx.x == 0) {
+    double* out = partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 7;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) out[q] = v[q];
+  }
+}
+
 // dtype 1 f32, 2 f64, 3 bf16. partial: [nseg*nbx*7]
 ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t ld, const void* xcols, int p,
                                   const void* segs, int nseg, const void* coef, int y0, int y1,
@@ -117,8 +184,17 @@ ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t ld, const vo
   if (dtype == 2)
     return dml_resid_t<double>(X, ld, xcols, p, segs, nseg, coef, y0, y1, w0, w1, vcol, nbx,
                                partial, moments, s);
-  if (dtype == 3)
-    return dml_resid_t<bf16_t>(X, ld, xcols, p, segs, nseg, coef, y0, y1, w0, w1, vcol, nbx,
-                               partial, moments, s);
+  if (dtype == 3) {
+    size_t sh = (size_t)2 * (p + 1) * sizeof(float) + (size_t)p * sizeof(int);
+    dim3 grid(nbx, nseg);
+    hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), sh, s, (const bf16_t*)X, ld,
+                       (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
+                       w0, w1, vcol, (double*)partial);
+    ATE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(64), 0, s, (const double*)partial, nbx * nseg,
+                       (double*)moments);
+    ATE_CHECK_LAUNCH();
+    return 0;
+  }
   return -1;
 }

@@ -149,19 +149,22 @@ __device__ __forceinline__ double readlane_d(double v, int i) {
 // Same sequence of coordinate updates as glmnet's pass; only the order of floating-point
 // additions into far gradients differs.
 template <typename CT>
-__global__ __launch_bounds__(64) void enet_path_kernel(
+__global__ __launch_bounds__(256) void enet_path_kernel(
     const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
     const unsigned char* __restrict__ ju_s, const double* __restrict__ ys_s,
     const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
     int* __restrict__ nlam_out, int* __restrict__ npass_out, int L) {
+  // 4 waves per problem: wave 0 runs the sequential in-block recurrence; all 4 waves
+  // stage the diagonal Gram block and share the bulk propagation (memory-level
+  // parallelism: a pass streams the whole Gram once).
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX];
   __shared__ int sflag[PMAX];       // bit0 ju, bit1 active
   __shared__ CT sC[64 * 64];
   __shared__ __attribute__((aligned(16))) CT sd[64];
-  // XCD-aware placement: consecutive problem ids (sorted by training set on the host)
-  // land on the same XCD, so problems sharing a Gram share that XCD's L2.
+  __shared__ double sdl;
+  __shared__ int sany;
   int q;
   {
     int bid = blockIdx.x, nwg = gridDim.x;
@@ -171,12 +174,12 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
   if (q >= nprob) return;
   const EnetProblem pr = probs[q];
   if (pr.ulam_src < -1) return;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int T = (p + 63) >> 6;
   const int ldc = T * 64;
   const CT* Cq = C + (int64_t)pr.train * p * ldc;
   const double ysq = ys_s[(int64_t)pr.train * ny + pr.y];
-  for (int k = lane; k < T * 64; k += 64) {
+  for (int k = tid; k < T * 64; k += 256) {
     bool in = k < p;
     sg[k] = in ? gin[((int64_t)pr.train * ny + pr.y) * p + k] : 0.0;
     sa[k] = 0.0;
@@ -191,65 +194,75 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
   double ab = 0.0, dem = 0.0;
 
   auto pass = [&](bool full) -> double {
-    double dlx = 0.0;
+    double dlx = 0.0;   // meaningful in wave 0
     for (int t = 0; t < T; ++t) {
       const int k = t * 64 + lane;
       double gt = sg[k], at = sa[k];
       const double vpt = svp[k];
       int fl = sflag[k];
       const bool elig = (fl & 1) && (full || (fl & 2));
+      // identical in every wave (same LDS values) -> uniform across the workgroup
       if (!__ballot(elig && (at != 0.0 || fabs(gt + at) > vpt * ab))) continue;
-      // stage the diagonal Gram block: sC[i*64 + l] = C[t*64+i][t*64+l]
-      for (int i = 0; i < 64; ++i) {
-        int r = t * 64 + i;
+      // stage the diagonal Gram block: sC[i*64 + l] = C[t*64+i][t*64+l] (16 rows per wave)
+#pragma unroll 4
+      for (int ii = 0; ii < 16; ++ii) {
+        int i = wid * 16 + ii, r = t * 64 + i;
         sC[i * 64 + lane] = r < p ? Cq[(int64_t)r * ldc + k] : CT(0);
       }
       __syncthreads();
-      double dblk = 0.0;
-      int last = -1;
-      while (true) {
-        const bool cand = elig && lane > last && (at != 0.0 || fabs(gt + at) > vpt * ab);
-        const uint64_t msk = __ballot(cand);
-        if (!msk) break;
-        const int i = __ffsll((unsigned long long)msk) - 1;
-        last = i;
-        const double cil = (double)sC[i * 64 + lane];
-        const double gi = readlane_d(gt, i), ai = readlane_d(at, i), vpi = readlane_d(vpt, i);
-        const double u = gi + ai;
-        const double v = fabs(u) - vpi * ab;
-        const double an = v > 0.0 ? copysign(v, u) / (1.0 + vpi * dem) : 0.0;
-        if (an == ai) continue;
-        const double d = an - ai;
-        rsq += d * (2.0 * gi - d);
-        dlx = fmax(dlx, d * d);
-        if (lane == i) { at = an; fl |= 2; dblk = d; }
-        gt -= cil * d;
+      if (wid == 0) {
+        double dblk = 0.0;
+        int last = -1;
+        while (true) {
+          const bool cand = elig && lane > last && (at != 0.0 || fabs(gt + at) > vpt * ab);
+          const uint64_t msk = __ballot(cand);
+          if (!msk) break;
+          const int i = __ffsll((unsigned long long)msk) - 1;
+          last = i;
+          const double cil = (double)sC[i * 64 + lane];
+          const double gi = readlane_d(gt, i), ai = readlane_d(at, i), vpi = readlane_d(vpt, i);
+          const double u = gi + ai;
+          const double v = fabs(u) - vpi * ab;
+          const double an = v > 0.0 ? copysign(v, u) / (1.0 + vpi * dem) : 0.0;
+          if (an == ai) continue;
+          const double d = an - ai;
+          rsq += d * (2.0 * gi - d);
+          dlx = fmax(dlx, d * d);
+          if (lane == i) { at = an; fl |= 2; dblk = d; }
+          gt -= cil * d;
+        }
+        sg[k] = gt;
+        sa[k] = at;
+        sflag[k] = fl;
+        sd[lane] = (CT)dblk;
+        const bool any = __ballot(dblk != 0.0) != 0;
+        if (lane == 0) sany = any ? 1 : 0;
       }
-      sg[k] = gt;
-      sa[k] = at;
-      sflag[k] = fl;
-      if (!__ballot(dblk != 0.0)) { __syncthreads(); continue; }
-      sd[lane] = (CT)dblk;
       __syncthreads();
-      // propagate: g[t2*64+l] -= sum_i C[t2*64+l][t*64+i] * d_i  for t2 != t
-      for (int t2 = 0; t2 < T; ++t2) {
-        if (t2 == t) continue;
-        const int k2 = t2 * 64 + lane;
-        if (k2 < p) {
-          // 64 contiguous (16-B aligned, zero-padded) entries of row k2, 16 B per load
-          typedef typename VecT<CT>::type V;
-          constexpr int W = sizeof(V) / sizeof(CT);
-          const V* row = reinterpret_cast<const V*>(Cq + (int64_t)k2 * ldc + t * 64);
-          const V* dv = reinterpret_cast<const V*>(sd);
-          CT acc = 0;
+      if (sany) {
+        // propagate: g[t2*64+l] -= sum_i C[t2*64+l][t*64+i] * d_i  for t2 != t
+        typedef typename VecT<CT>::type V;
+        constexpr int W = sizeof(V) / sizeof(CT);
+        const V* dv = reinterpret_cast<const V*>(sd);
+        for (int t2 = wid; t2 < T; t2 += 4) {
+          if (t2 == t) continue;
+          const int k2 = t2 * 64 + lane;
+          if (k2 < p) {
+            const V* row = reinterpret_cast<const V*>(Cq + (int64_t)k2 * ldc + t * 64);
+            CT acc = 0;
 #pragma unroll
-          for (int c = 0; c < 64 / W; ++c) acc += vdot(row[c], dv[c]);
-          sg[k2] -= (double)acc;
+            for (int c = 0; c < 64 / W; ++c) acc += vdot(row[c], dv[c]);
+            sg[k2] -= (double)acc;
+          }
         }
       }
       __syncthreads();
     }
-    return dlx;
+    if (tid == 0) sdl = dlx;
+    __syncthreads();
+    double r = sdl;
+    __syncthreads();
+    return r;
   };
 
   for (int m = 0; m < nlam; ++m) {
@@ -261,7 +274,7 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
       double mx = 0.0;
       for (int k = lane; k < p; k += 64)
         if ((sflag[k] & 1) && svp[k] > 0.0) mx = fmax(mx, fabs(sg[k]) / svp[k]);
-      mx = wave_max(mx);
+      mx = wave_max(mx);      // every wave computes the same value
       alm = alf * mx / fmax(alpha, 1e-3);
     } else {
       alm *= alf;
@@ -279,18 +292,23 @@ __global__ __launch_bounds__(64) void enet_path_kernel(
       }
     }
     double* ap = apath + ((int64_t)q * L + m) * p;
-    for (int k = lane; k < p; k += 64) ap[k] = sa[k];
-    if (lane == 0) {
+    for (int k = tid; k < p; k += 256) ap[k] = sa[k];
+    if (tid == 0) {
       lams[(int64_t)q * L + m] = alm * ysq;
       rsqs[(int64_t)q * L + m] = rsq;
     }
     m_out = m + 1;
+    // rsq is tracked by wave 0: share it so every wave takes the same early-stop branch
+    if (tid == 0) sdl = rsq;
+    __syncthreads();
+    const double rsq_all = sdl;
+    __syncthreads();
     if (pr.ulam_src < 0 && m >= 4 && m > 0) {
-      if (rsq - rsq_prev < 1e-5 * rsq || rsq > 0.999) break;
+      if (rsq_all - rsq_prev < 1e-5 * rsq_all || rsq_all > 0.999) break;
     }
-    rsq_prev = rsq;
+    rsq_prev = rsq_all;
   }
-  if (lane == 0) {
+  if (tid == 0) {
     if (pr.ulam_src < 0 && m_out >= 3) {
       double l1 = lams[(int64_t)q * L + 1], l2 = lams[(int64_t)q * L + 2];
       lams[(int64_t)q * L] = exp(2.0 * log(l1) - log(l2));
@@ -310,7 +328,7 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
   // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nwg)
   const int nwg = (nprob + 7) / 8 * 8;
 #define LAUNCH_C(CTT)                                                                          \
-  hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(64), 0, s, (const CTT*)C,        \
+  hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(256), 0, s, (const CTT*)C,       \
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \

@@ -120,6 +120,97 @@ __global__ __launch_bounds__(256) void gram_bf16_kernel(
       }
 }
 
+// ------------------------------------------------------------------ bf16 256x256, LDS-DMA staged
+// 512 threads = 8 waves as 2 (rows) x 4 (cols); each wave owns a 128x64 output block
+// (8x4 tiles of mfma_f32_16x16x32_bf16 -> 128 accumulator registers). Per 64-row
+// K-step the A and B panels (256 columns x 64 rows x bf16 = 32 KB each) are copied
+// global -> LDS with global_load_lds_dwordx4 (no VGPR round trip), double buffered so
+// the copy of step s+1 overlaps the 64 MFMAs/wave of step s. The LDS image is written
+// lane-linearly, so the per-column XOR swizzle of the 16-byte chunks is applied on the
+// SOURCE address (chunk (l&7)^(col&7) lands at position l&7) and undone on the read.
+constexpr int GT = 256;
+constexpr int GK = 64;
+
+__device__ __forceinline__ void glds16(const void* src, bf16_t* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void gram_bf16_256_kernel(
+    const bf16_t* __restrict__ X, int64_t ld, const int2* __restrict__ tiles, int ntiles,
+    const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][GT * GK];   // 128 KB
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = L / ntiles, t = L % ntiles;
+  const Chunk ch = chunks[c];
+  const int2 tl = tiles[t];
+  const bool diag = tl.x == tl.y;
+  const int a0 = tl.x * GT, b0 = tl.y * GT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // each wave issues 4 x 1 KB pieces per panel: piece q covers columns q*8 .. q*8+7
+  auto stage = [&](int st, int64_t i0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = wid * 4 + r;
+      const int col = q * 8 + (lane >> 3);
+      const int cc = (lane & 7) ^ (col & 7);
+      glds16(X + (int64_t)(a0 + col) * ld + i0 + cc * 8, &lds[st][0][q * 8 * GK]);
+      if (!diag) glds16(X + (int64_t)(b0 + col) * ld + i0 + cc * 8, &lds[st][1][q * 8 * GK]);
+    }
+  };
+
+  const int64_t nsteps = (ch.row1 - ch.row0) / GK;
+  if (nsteps > 0) stage(0, ch.row0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  __syncthreads();
+  for (int64_t s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) stage(cur ^ 1, ch.row0 + (s + 1) * GK);
+    const bf16_t* As = lds[cur][0];
+    const bf16_t* Bs = diag ? lds[cur][0] : lds[cur][1];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int cc = kk * 4 + (lane >> 4);
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int col = wr * 128 + m * 16 + (lane & 15);
+        af[m] = *reinterpret_cast<const bf16x8*>(&As[col * GK + ((cc ^ (col & 7)) << 3)]);
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int col = wc * 64 + n * 16 + (lane & 15);
+        bfr[n] = *reinterpret_cast<const bf16x8*>(&Bs[col * GK + ((cc ^ (col & 7)) << 3)]);
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): next stage landed
+    __syncthreads();
+  }
+  float* out = slab + ((int64_t)c * ntiles + t) * (GT * GT);
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 128 + m * 16 + (lane >> 4) * 4 + r;
+        const int col = wc * 64 + n * 16 + (lane & 15);
+        out[row * GT + col] = acc[m][n][r];
+      }
+}
+
 // ------------------------------------------------------------------ fp32 / fp64 64x64
 constexpr int FT = 64;
 constexpr int FK = 16;
@@ -225,18 +316,28 @@ __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2
 
 // ------------------------------------------------------------------ host API
 // chunks/tiles/seg_chunk0 are device arrays prepared by the caller (ops/gram.py).
-ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, const void* tiles, int ntiles,
-                          const void* chunks, int nchunks, const void* seg_chunk0, int nseg,
-                          void* slab, void* G, void* stream) {
-  if (P % BT) return -1;
+// tile = 128 (4 waves, register-staged) or 256 (8 waves, LDS-DMA staged); the caller's
+// tile table and chunk plan must use the same tile size.
+ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile, const void* tiles,
+                          int ntiles, const void* chunks, int nchunks, const void* seg_chunk0,
+                          int nseg, void* slab, void* G, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int nwg = nchunks * ntiles;
-  hipLaunchKernelGGL(gram_bf16_kernel, dim3(nwg), dim3(256), 0, s, (const bf16_t*)X, ld,
-                     (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
+  if (tile == GT) {
+    if (P % GT) return -1;
+    hipLaunchKernelGGL(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
+                       (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
+  } else if (tile == BT) {
+    if (P % BT) return -1;
+    hipLaunchKernelGGL(gram_bf16_kernel, dim3(nwg), dim3(256), 0, s, (const bf16_t*)X, ld,
+                       (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
+  } else {
+    return -1;
+  }
   ATE_CHECK_LAUNCH();
-  int64_t total = (int64_t)nseg * ntiles * BT * BT;
+  int64_t total = (int64_t)nseg * ntiles * tile * tile;
   hipLaunchKernelGGL(gram_reduce_kernel<float>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
-                     (const float*)slab, BT, (const int2*)tiles, ntiles, (const int*)seg_chunk0,
+                     (const float*)slab, tile, (const int2*)tiles, ntiles, (const int*)seg_chunk0,
                      nseg, P, (double*)G, (const int*)nullptr);
   ATE_CHECK_LAUNCH();
   return 0;

@@ -26,10 +26,13 @@ def test_native_library_loaded(gpu):
     assert any("libatehip.so" in p for p in _native.loaded_libraries())
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f32", "f64"])
-def test_gram_kernel_vs_fp64(gpu, dtype):
+@pytest.mark.parametrize("dtype,p", [("bf16", 100), ("bf16", 150), ("bf16", 300), ("f32", 150),
+                                     ("f64", 150)])
+def test_gram_kernel_vs_fp64(gpu, dtype, p):
+    # bf16: p=100 -> P=128 (128-tile kernel), 150 -> P=256 (one 256 tile),
+    # 300 -> P=512 (256-tile kernel incl. an off-diagonal tile)
     rs = np.random.RandomState(0)
-    n, p = 3001, 150          # P pads to 256 (bf16: 2x2 tiles incl. an off-diagonal tile)
+    n = 3001
     X = rs.randn(n, p) * np.linspace(0.5, 2, p) + np.linspace(-1, 1, p)
     folds = rs.randint(0, 3, n)
     pan = build_panel(X, rs.rand(n), rs.randint(0, 2, n), folds=folds, dtype=dtype, device=gpu)
