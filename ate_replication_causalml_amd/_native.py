@@ -45,7 +45,7 @@ _SIGS = {
     "ate_boot_multinomial": "ppluiipp",
     "ate_boot_poisson": "ppluiilipp",
     "ate_enet_prepare": "piipipiipipipppppppp",
-    "ate_enet_path": "pipiippppidddipppppip",
+    "ate_enet_path": "pipiippppidddipppppipp",
     "ate_enet_coef": "ppiiiipppppppp",
     "ate_enet_cvloss_gauss": "pippiipppiipp",
     "ate_cv_select": "pppiipipppp",

@@ -154,45 +154,31 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
                  p, one, yc.data_ptr(), ny, C.data_ptr(), c_f32, g.data_ptr(), xm.data_ptr(),
                  xs.data_ptr(), ju.data_ptr(), ym.data_ptr(), ys.data_ptr(), nobs.data_ptr(), s)
     vp_t = torch.tensor(vp, **f64)
-    outs = {}
-    for tag, probs in (("full", full_probs), ("fold", fold_probs)):
-        nq = len(probs)
-        pr = _probs_tensor(probs, dev)
-        apath = torch.zeros((nq, L, p), **f64)
-        lams = torch.full((nq, L), float("nan"), **f64)
-        rsq = torch.zeros((nq, L), **f64)
-        nlam = torch.zeros(nq, dtype=torch.int32, device=dev)
-        npass = torch.zeros(nq, dtype=torch.int32, device=dev)
-        if tag == "fold":
-            lams_src = outs["full"]["lams"]
-            nlam_src = outs["full"]["nlam"]
-            # the kernel reads the source lambdas from its own lams/nlam buffers at index src:
-            # place the full problems' values in a combined table
-            nf = lams_src.shape[0]
-            lams = torch.cat([lams_src, lams])
-            nlam = torch.cat([nlam_src, nlam])
-            apath = torch.cat([torch.zeros((nf, L, p), **f64), apath])
-            rsq = torch.cat([torch.zeros((nf, L), **f64), rsq])
-            npass = torch.cat([torch.zeros(nf, dtype=torch.int32, device=dev), npass])
-            probs2 = [(0, 0, -2, 0)] * nf + list(probs)
-            pr = _probs_tensor(probs2, dev)
-            nq = len(probs2)
-        _native.call("ate_enet_path", C.data_ptr(), c_f32, g.data_ptr(), p, ny, ju.data_ptr(),
-                     ys.data_ptr(), vp_t.data_ptr(), pr.data_ptr(), nq, alpha, flmin, thresh,
-                     maxit, apath.data_ptr(), lams.data_ptr(), rsq.data_ptr(), nlam.data_ptr(),
-                     npass.data_ptr(), L, s)
-        coef = torch.empty((nq, L, p + 1), **f64)
-        _native.call("ate_enet_coef", apath.data_ptr(), pr.data_ptr(), nq, p, ny, L,
-                     nlam.data_ptr(), xm.data_ptr(), xs.data_ptr(), ju.data_ptr(), ym.data_ptr(),
-                     ys.data_ptr(), coef.data_ptr(), s)
-        outs[tag] = dict(lams=lams, nlam=nlam, coef=coef, npass=npass, probs=pr, nq=nq)
+    # ONE launch: full problems [0, nf) + fold problems [nf, nq); fold problems consume
+    # their source's lambda sequence as it is published (device-side progress flags)
     nf = len(full_probs)
-    fo = outs["fold"]
+    probs_all = list(full_probs) + list(fold_probs)
+    nq = len(probs_all)
+    pr = _probs_tensor(probs_all, dev)
+    apath = torch.zeros((nq, L, p), **f64)
+    lams = torch.full((nq, L), float("nan"), **f64)
+    rsq = torch.zeros((nq, L), **f64)
+    nlam = torch.zeros(nq, dtype=torch.int32, device=dev)
+    npass = torch.zeros(nq, dtype=torch.int32, device=dev)
+    progress = torch.zeros(nq, dtype=torch.int32, device=dev)
+    _native.call("ate_enet_path", C.data_ptr(), c_f32, g.data_ptr(), p, ny, ju.data_ptr(),
+                 ys.data_ptr(), vp_t.data_ptr(), pr.data_ptr(), nq, alpha, flmin, thresh,
+                 maxit, apath.data_ptr(), lams.data_ptr(), rsq.data_ptr(), nlam.data_ptr(),
+                 npass.data_ptr(), L, progress.data_ptr(), s)
+    coef = torch.empty((nq, L, p + 1), **f64)
+    _native.call("ate_enet_coef", apath.data_ptr(), pr.data_ptr(), nq, p, ny, L,
+                 nlam.data_ptr(), xm.data_ptr(), xs.data_ptr(), ju.data_ptr(), ym.data_ptr(),
+                 ys.data_ptr(), coef.data_ptr(), s)
     hold = torch.tensor([0] * nf + list(fold_holds), dtype=torch.int32, device=dev)
     ycol_p = torch.tensor([0] * nf + list(fold_ycol), dtype=torch.int32, device=dev)
-    cvraw = torch.empty((fo["nq"], L), **f64)
+    cvraw = torch.empty((nq, L), **f64)
     _native.call("ate_enet_cvloss_gauss", G.data_ptr(), P, hold.data_ptr(), xc.data_ptr(), p, one,
-                 ycol_p.data_ptr(), fo["coef"].data_ptr(), fo["nlam"].data_ptr(), L, fo["nq"],
+                 ycol_p.data_ptr(), coef.data_ptr(), nlam.data_ptr(), L, nq,
                  cvraw.data_ptr(), s)
     fidx = torch.from_numpy(fold_index + nf).to(dev)
     nfold_t = torch.from_numpy(nfold).to(dev)
@@ -200,17 +186,16 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     cvsd = torch.empty((nf, L), **f64)
     sel = torch.empty((nf, 2), dtype=torch.int32, device=dev)
     K = fold_index.shape[1]
-    fu = outs["full"]
     _native.call("ate_cv_select", cvraw.data_ptr(), fidx.data_ptr(), nfold_t.data_ptr(), K, nf,
-                 fu["nlam"].data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), s)
+                 nlam.data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), s)
     cmin = torch.empty((nf, p + 1), **f64)
     c1se = torch.empty((nf, p + 1), **f64)
-    _native.call("ate_enet_pick", fu["coef"].data_ptr(), sel.data_ptr(), 0, p, L, nf,
+    _native.call("ate_enet_pick", coef.data_ptr(), sel.data_ptr(), 0, p, L, nf,
                  cmin.data_ptr(), s)
-    _native.call("ate_enet_pick", fu["coef"].data_ptr(), sel.data_ptr(), 1, p, L, nf,
+    _native.call("ate_enet_pick", coef.data_ptr(), sel.data_ptr(), 1, p, L, nf,
                  c1se.data_ptr(), s)
-    return EnetCvResult(fu["lams"], fu["nlam"], cvm, cvsd, sel, fu["coef"], cmin, c1se, full_keys,
-                        fu["npass"])
+    return EnetCvResult(lams[:nf], nlam[:nf], cvm, cvsd, sel, coef[:nf], cmin, c1se, full_keys,
+                        npass[:nf])
 
 
 def _cv_cpu(G, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_probs, fold_ycol, fold_holds,

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
-    int* __restrict__ nlam_out, int* __restrict__ npass_out, int L) {
+    int* __restrict__ nlam_out, int* __restrict__ npass_out, int L, int* __restrict__ progress) {
   // 4 waves per problem: wave 0 runs the sequential in-block recurrence; all 4 waves
   // stage the diagonal Gram block and share the bulk propagation (memory-level
   // parallelism: a pass streams the whole Gram once).
@@ -165,6 +165,8 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   __shared__ __attribute__((aligned(16))) CT sd[64];
   __shared__ double sdl;
   __shared__ int sany;
+  __shared__ double slam;
+  __shared__ int savail;
   int q;
   {
     int bid = blockIdx.x, nwg = gridDim.x;
@@ -187,14 +189,15 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     sflag[k] = (in && ju_s[(int64_t)pr.train * p + k]) ? 1 : 0;
   }
   __syncthreads();
-  const int nlam = pr.ulam_src >= 0 ? nlam_out[pr.ulam_src] : pr.nlam_req;
+  const int nlam = pr.ulam_src >= 0 ? L : pr.nlam_req;   // fold paths end with their source
   const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
   double alm = 0.0, rsq = 0.0, rsq_prev = 0.0;
   int npass = 0, m_out = 0;
   double ab = 0.0, dem = 0.0;
 
+  double rsq_l = 0.0;   // per-lane partial R^2 increments (wave 0)
   auto pass = [&](bool full) -> double {
-    double dlx = 0.0;   // meaningful in wave 0
+    double dlx_l = 0.0;   // per-lane max of d^2 (wave 0)
     for (int t = 0; t < T; ++t) {
       const int k = t * 64 + lane;
       double gt = sg[k], at = sa[k];
@@ -211,25 +214,32 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
       }
       __syncthreads();
       if (wid == 0) {
+        const double thr_l = vpt * ab;
+        const double rden = dem == 0.0 ? 1.0 : 1.0 / (1.0 + vpt * dem);
         double dblk = 0.0;
         int last = -1;
         while (true) {
-          const bool cand = elig && lane > last && (at != 0.0 || fabs(gt + at) > vpt * ab);
+          // every lane evaluates its own tentative update; the serial chain is only
+          // ballot -> first lane -> broadcast d -> one FMA per lane
+          const double u = gt + at;
+          const bool cand = elig && lane > last && (at != 0.0 || fabs(u) > thr_l);
           const uint64_t msk = __ballot(cand);
           if (!msk) break;
           const int i = __ffsll((unsigned long long)msk) - 1;
           last = i;
-          const double cil = (double)sC[i * 64 + lane];
-          const double gi = readlane_d(gt, i), ai = readlane_d(at, i), vpi = readlane_d(vpt, i);
-          const double u = gi + ai;
-          const double v = fabs(u) - vpi * ab;
-          const double an = v > 0.0 ? copysign(v, u) / (1.0 + vpi * dem) : 0.0;
-          if (an == ai) continue;
-          const double d = an - ai;
-          rsq += d * (2.0 * gi - d);
-          dlx = fmax(dlx, d * d);
-          if (lane == i) { at = an; fl |= 2; dblk = d; }
-          gt -= cil * d;
+          const double v = fabs(u) - thr_l;
+          const double an = v > 0.0 ? copysign(v, u) * rden : 0.0;
+          const double dl = an - at;
+          const double d = readlane_d(dl, i);
+          if (d == 0.0) continue;
+          if (lane == i) {
+            rsq_l += d * (2.0 * gt - d);
+            dlx_l = fmax(dlx_l, d * d);
+            at = an;
+            fl |= 2;
+            dblk = d;
+          }
+          gt -= (double)sC[i * 64 + lane] * d;   // C[t*64+l][t*64+i] (symmetric block)
         }
         sg[k] = gt;
         sa[k] = at;
@@ -258,6 +268,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
       }
       __syncthreads();
     }
+    const double dlx = wave_max(dlx_l);
     if (tid == 0) sdl = dlx;
     __syncthreads();
     double r = sdl;
@@ -265,9 +276,52 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     return r;
   };
 
-  for (int m = 0; m < nlam; ++m) {
-    if (pr.ulam_src >= 0) {
-      alm = lams[(int64_t)pr.ulam_src * L + m] / ysq;
+  // Fold problems run CONCURRENTLY with the full-data problem that defines their
+  // lambda sequence: the full problem publishes lambda m (agent-scope release of
+  // progress[q] = m+1 after lams[] is stored), the fold problem polls that counter
+  // (relaxed, bounded spin) and acquires before reading it. All problems of a launch are
+  // co-resident (one 256-thread workgroup per problem, grid <= #CUs), so this never
+  // deadlocks; a timed-out spin ends the fold path (npass_out = -1 flags it).
+  auto publish = [&](int v) {   // thread 0 only
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(progress + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  const bool is_fold = pr.ulam_src >= 0;
+  bool timed_out = false;
+  for (int m = 0; m < (is_fold ? L : nlam); ++m) {
+    if (is_fold) {
+      if (tid == 0) {
+        int v = 0;
+        for (long spin = 0;; ++spin) {
+          v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v > m) break;
+          if (spin > (1l << 26)) { v = -1; break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int avail = 0;
+        double lv = 0.0;
+        if (v < 0) {
+          timed_out = true;
+        } else if (v >= (1 << 30)) {
+          int nl = __hip_atomic_load(nlam_out + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          avail = m < nl;
+        } else {
+          avail = 1;
+        }
+        if (avail) lv = __hip_atomic_load(lams + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        savail = avail;
+        slam = lv;
+      }
+      __syncthreads();
+      const int avail = savail;
+      alm = slam / ysq;
+      __syncthreads();
+      if (!avail) break;
     } else if (m == 0) {
       alm = BIGL;
     } else if (m == 1) {
@@ -293,28 +347,30 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     }
     double* ap = apath + ((int64_t)q * L + m) * p;
     for (int k = tid; k < p; k += 256) ap[k] = sa[k];
-    if (tid == 0) {
-      lams[(int64_t)q * L + m] = alm * ysq;
-      rsqs[(int64_t)q * L + m] = rsq;
-    }
-    m_out = m + 1;
-    // rsq is tracked by wave 0: share it so every wave takes the same early-stop branch
+    // R^2 increments live in wave 0's lanes: reduce and share so every wave takes the
+    // same early-stop branch
+    rsq = wave_sum(rsq_l);
     if (tid == 0) sdl = rsq;
     __syncthreads();
     const double rsq_all = sdl;
     __syncthreads();
+    if (tid == 0) {
+      lams[(int64_t)q * L + m] = alm * ysq;
+      rsqs[(int64_t)q * L + m] = rsq_all;
+      if (!is_fold && m == 2)   // glmnet reports lambda_0 extrapolated from lambda_1, lambda_2
+        lams[(int64_t)q * L] = exp(2.0 * log(lams[(int64_t)q * L + 1]) - log(alm * ysq));
+      if (!is_fold && m >= 2) publish(m + 1);
+    }
+    m_out = m + 1;
     if (pr.ulam_src < 0 && m >= 4 && m > 0) {
       if (rsq_all - rsq_prev < 1e-5 * rsq_all || rsq_all > 0.999) break;
     }
     rsq_prev = rsq_all;
   }
   if (tid == 0) {
-    if (pr.ulam_src < 0 && m_out >= 3) {
-      double l1 = lams[(int64_t)q * L + 1], l2 = lams[(int64_t)q * L + 2];
-      lams[(int64_t)q * L] = exp(2.0 * log(l1) - log(l2));
-    }
     nlam_out[q] = m_out;
-    npass_out[q] = npass;
+    npass_out[q] = timed_out ? -1 : npass;
+    if (!is_fold) publish(1 << 30);
   }
 }
 
@@ -322,8 +378,9 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
                           const void* ys, const void* vp, const void* probs, int nprob,
                           double alpha, double flmin, double thr, int maxit, void* apath,
                           void* lams, void* rsqs, void* nlam_out, void* npass_out, int L,
-                          void* stream) {
+                          void* progress, void* stream) {
   if (p > PMAX) return -2;
+  if (nprob > 256) return -3;   // co-residency of fold problems and their sources
   hipStream_t s = (hipStream_t)stream;
   // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nwg)
   const int nwg = (nprob + 7) / 8 * 8;
@@ -332,7 +389,7 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
-                     (int*)npass_out, L)
+                     (int*)npass_out, L, (int*)progress)
   if (c_f32) LAUNCH_C(float);
   else LAUNCH_C(double);
 #undef LAUNCH_C
