@@ -81,12 +81,19 @@ __global__ __launch_bounds__(256) void dml_resid_kernel(
   }
 }
 
-__global__ void sum7_kernel(const double* __restrict__ partial, int nb, double* __restrict__ out) {
-  int q = threadIdx.x;
-  if (q >= 7) return;
-  double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += partial[(int64_t)b * 7 + q];
-  out[q] = s;
+// one block of 256 threads: thread i sums partials i, i+256, ... (fixed order), then a
+// fixed-shape block reduction -> deterministic for a given launch geometry
+__global__ __launch_bounds__(256) void sum7_kernel(const double* __restrict__ partial, int nb,
+                                                   double* __restrict__ out) {
+  __shared__ double red[16 * 7];
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int b = threadIdx.x; b < nb; b += 256)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) v[q] += partial[(int64_t)b * 7 + q];
+  block_sum<7>(v, red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) out[q] = v[q];
 }
 
 template <typename T>
@@ -99,7 +106,7 @@ static int dml_resid_t(const void* X, int64_t ld, const void* xcols, int p, cons
                      (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
                      w0, w1, vcol, (double*)partial);
   ATE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(64), 0, s, (const double*)partial, nbx * nseg,
+  hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
                      (double*)moments);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -191,7 +198,7 @@ ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t ld, const vo
                        (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
                        w0, w1, vcol, (double*)partial);
     ATE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(64), 0, s, (const double*)partial, nbx * nseg,
+    hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
                        (double*)moments);
     ATE_CHECK_LAUNCH();
     return 0;

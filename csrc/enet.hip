@@ -148,6 +148,14 @@ __device__ __forceinline__ double readlane_d(double v, int i) {
 //     latency on the coordinate chain.
 // Same sequence of coordinate updates as glmnet's pass; only the order of floating-point
 // additions into far gradients differs.
+// PULL formulation. Each coordinate's cumulative change is kept in Dcum; each block t keeps
+// a snapshot Dsnap_t of Dcum taken when its gradient was last brought up to date. Before
+// block t is processed, one bandwidth-bound pass over its 64 Gram rows applies every
+// pending change:   g_t -= C[t rows, :] (Dcum - Dsnap_t)
+// (4 waves split the columns; partial sums reduced through LDS), and the same loads
+// deposit the 64x64 diagonal block in LDS for the sequential in-block recurrence (wave 0).
+// Active passes skip blocks without active coordinates (no pull needed: nothing in them
+// can move); full passes pull every block, so every KKT check uses the current gradient.
 template <typename CT>
 __global__ __launch_bounds__(256) void enet_path_kernel(
     const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
@@ -156,13 +164,13 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
     int* __restrict__ nlam_out, int* __restrict__ npass_out, int L, int* __restrict__ progress) {
-  // 4 waves per problem: wave 0 runs the sequential in-block recurrence; all 4 waves
-  // stage the diagonal Gram block and share the bulk propagation (memory-level
-  // parallelism: a pass streams the whole Gram once).
-  __shared__ double sg[PMAX], sa[PMAX], svp[PMAX];
-  __shared__ int sflag[PMAX];       // bit0 ju, bit1 active
-  __shared__ CT sC[64 * 64];
-  __shared__ __attribute__((aligned(16))) CT sd[64];
+  constexpr int TMAX = PMAX / 64;
+  __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
+  __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
+  __shared__ int sflag[PMAX];             // bit0 ju, bit1 active
+  __shared__ float sC[64 * 64];           // diagonal block, sC[i*64 + l] = C[t*64+l][t*64+i]
+  __shared__ double spart[4][64];
+  __shared__ __attribute__((aligned(16))) CT sdelta[PMAX];
   __shared__ double sdl;
   __shared__ int sany;
   __shared__ double slam;
@@ -179,6 +187,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int T = (p + 63) >> 6;
   const int ldc = T * 64;
+  const int cw = ldc / 4;                  // columns per wave in the pull (multiple of 16)
   const CT* Cq = C + (int64_t)pr.train * p * ldc;
   const double ysq = ys_s[(int64_t)pr.train * ny + pr.y];
   for (int k = tid; k < T * 64; k += 256) {
@@ -186,41 +195,73 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     sg[k] = in ? gin[((int64_t)pr.train * ny + pr.y) * p + k] : 0.0;
     sa[k] = 0.0;
     svp[k] = in ? vp_in[k] : 0.0;
+    sdc[k] = 0.0;
     sflag[k] = (in && ju_s[(int64_t)pr.train * p + k]) ? 1 : 0;
   }
+  for (int e = tid; e < TMAX * PMAX; e += 256) (&sds[0][0])[e] = 0.0;
   __syncthreads();
-  const int nlam = pr.ulam_src >= 0 ? L : pr.nlam_req;   // fold paths end with their source
+  const int nlam = pr.ulam_src >= 0 ? L : pr.nlam_req;
   const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
   double alm = 0.0, rsq = 0.0, rsq_prev = 0.0;
   int npass = 0, m_out = 0;
   double ab = 0.0, dem = 0.0;
+  double rsq_l = 0.0;
+  typedef typename VecT<CT>::type V;
+  constexpr int W = sizeof(V) / sizeof(CT);
 
-  double rsq_l = 0.0;   // per-lane partial R^2 increments (wave 0)
+  // bring block t's gradient up to date (all 256 threads); stage its diagonal block
+  auto pull = [&](int t) {
+    for (int j = tid; j < ldc; j += 256) sdelta[j] = (CT)(sdc[j] - sds[t][j]);
+    __syncthreads();
+    const int r = t * 64 + lane;
+    const int c0 = wid * cw;
+    CT acc = 0;
+    const V* dv = reinterpret_cast<const V*>(sdelta + c0);
+    if (r < p) {
+      const V* row = reinterpret_cast<const V*>(Cq + (int64_t)r * ldc + c0);
+#pragma unroll 4
+      for (int c = 0; c < cw / W; ++c) {
+        const V v = row[c];
+        acc += vdot(v, dv[c]);
+        const int j0 = c0 + c * W;
+        if ((j0 >> 6) == t) {
+          const CT* ve = reinterpret_cast<const CT*>(&v);
+#pragma unroll
+          for (int e = 0; e < W; ++e) sC[((j0 + e) & 63) * 64 + lane] = (float)ve[e];
+        }
+      }
+    } else {
+      // padding rows of the last block: zero diagonal entries so the recurrence ignores them
+      for (int j = c0; j < c0 + cw; ++j)
+        if ((j >> 6) == t) sC[(j & 63) * 64 + lane] = 0.f;
+    }
+    spart[wid][lane] = (double)acc;
+    __syncthreads();
+    if (tid < 64) {
+      const int k = t * 64 + tid;
+      sg[k] -= spart[0][tid] + spart[1][tid] + spart[2][tid] + spart[3][tid];
+    }
+    for (int j = tid; j < ldc; j += 256) sds[t][j] = sdc[j];
+    __syncthreads();
+  };
+
   auto pass = [&](bool full) -> double {
-    double dlx_l = 0.0;   // per-lane max of d^2 (wave 0)
+    double dlx_l = 0.0;
     for (int t = 0; t < T; ++t) {
       const int k = t * 64 + lane;
-      double gt = sg[k], at = sa[k];
-      const double vpt = svp[k];
-      int fl = sflag[k];
-      const bool elig = (fl & 1) && (full || (fl & 2));
-      // identical in every wave (same LDS values) -> uniform across the workgroup
-      if (!__ballot(elig && (at != 0.0 || fabs(gt + at) > vpt * ab))) continue;
-      // stage the diagonal Gram block: sC[i*64 + l] = C[t*64+i][t*64+l] (16 rows per wave)
-#pragma unroll 4
-      for (int ii = 0; ii < 16; ++ii) {
-        int i = wid * 16 + ii, r = t * 64 + i;
-        sC[i * 64 + lane] = r < p ? Cq[(int64_t)r * ldc + k] : CT(0);
-      }
-      __syncthreads();
+      // active pass: a block without active coordinates cannot change (skip, no pull)
+      if (!full && !__ballot((sflag[k] & 3) == 3)) continue;
+      pull(t);
       if (wid == 0) {
+        double gt = sg[k], at = sa[k];
+        const double vpt = svp[k];
+        int fl = sflag[k];
+        const bool elig = (fl & 1) && (full || (fl & 2));
         const double thr_l = vpt * ab;
         const double rden = dem == 0.0 ? 1.0 : 1.0 / (1.0 + vpt * dem);
         double dblk = 0.0;
         int last = -1;
         while (true) {
-          // every lane evaluates its own tentative update; the serial chain is only
-          // ballot -> first lane -> broadcast d -> one FMA per lane
           const double u = gt + at;
           const bool cand = elig && lane > last && (at != 0.0 || fabs(u) > thr_l);
           const uint64_t msk = __ballot(cand);
@@ -239,32 +280,13 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
             fl |= 2;
             dblk = d;
           }
-          gt -= (double)sC[i * 64 + lane] * d;   // C[t*64+l][t*64+i] (symmetric block)
+          gt -= (double)sC[i * 64 + lane] * d;
         }
         sg[k] = gt;
         sa[k] = at;
         sflag[k] = fl;
-        sd[lane] = (CT)dblk;
-        const bool any = __ballot(dblk != 0.0) != 0;
-        if (lane == 0) sany = any ? 1 : 0;
-      }
-      __syncthreads();
-      if (sany) {
-        // propagate: g[t2*64+l] -= sum_i C[t2*64+l][t*64+i] * d_i  for t2 != t
-        typedef typename VecT<CT>::type V;
-        constexpr int W = sizeof(V) / sizeof(CT);
-        const V* dv = reinterpret_cast<const V*>(sd);
-        for (int t2 = wid; t2 < T; t2 += 4) {
-          if (t2 == t) continue;
-          const int k2 = t2 * 64 + lane;
-          if (k2 < p) {
-            const V* row = reinterpret_cast<const V*>(Cq + (int64_t)k2 * ldc + t * 64);
-            CT acc = 0;
-#pragma unroll
-            for (int c = 0; c < 64 / W; ++c) acc += vdot(row[c], dv[c]);
-            sg[k2] -= (double)acc;
-          }
-        }
+        sdc[k] += dblk;
+        sds[t][k] += dblk;       // own changes are already in g_t
       }
       __syncthreads();
     }
@@ -276,21 +298,20 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     return r;
   };
 
-  // Fold problems run CONCURRENTLY with the full-data problem that defines their
-  // lambda sequence: the full problem publishes lambda m (agent-scope release of
-  // progress[q] = m+1 after lams[] is stored), the fold problem polls that counter
-  // (relaxed, bounded spin) and acquires before reading it. All problems of a launch are
-  // co-resident (one 256-thread workgroup per problem, grid <= #CUs), so this never
-  // deadlocks; a timed-out spin ends the fold path (npass_out = -1 flags it).
-  auto publish = [&](int v) {   // thread 0 only
+  auto publish = [&](int v) {   // thread 0 only: agent-scope release of progress[q]
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(progress + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
+  // Fold problems run CONCURRENTLY with the full-data problem that defines their lambda
+  // sequence: it publishes lambda m (release of progress[q] = m+1 after lams[] is
+  // stored), the fold problem polls that counter (relaxed, bounded spin) and acquires
+  // before reading. All problems of a launch are co-resident (one workgroup per problem,
+  // grid <= #CUs); a timed-out spin ends the fold path (npass_out = -1 flags it).
   const bool is_fold = pr.ulam_src >= 0;
   bool timed_out = false;
-  for (int m = 0; m < (is_fold ? L : nlam); ++m) {
+  for (int m = 0; m < nlam; ++m) {
     if (is_fold) {
       if (tid == 0) {
         int v = 0;
@@ -325,6 +346,8 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     } else if (m == 0) {
       alm = BIGL;
     } else if (m == 1) {
+      // lambda_max needs the exact current gradient of every coordinate
+      for (int t = 0; t < T; ++t) pull(t);
       double mx = 0.0;
       for (int k = lane; k < p; k += 64)
         if ((sflag[k] & 1) && svp[k] > 0.0) mx = fmax(mx, fabs(sg[k]) / svp[k]);
@@ -347,8 +370,6 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     }
     double* ap = apath + ((int64_t)q * L + m) * p;
     for (int k = tid; k < p; k += 256) ap[k] = sa[k];
-    // R^2 increments live in wave 0's lanes: reduce and share so every wave takes the
-    // same early-stop branch
     rsq = wave_sum(rsq_l);
     if (tid == 0) sdl = rsq;
     __syncthreads();
