@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     const V* dv = reinterpret_cast<const V*>(sdelta + c0);
     if (r < p) {
       const V* row = reinterpret_cast<const V*>(Cq + (int64_t)r * ldc + c0);
-#pragma unroll 4
+#pragma unroll 16
       for (int c = 0; c < cw / W; ++c) {
         const V v = row[c];
         acc += vdot(v, dv[c]);
