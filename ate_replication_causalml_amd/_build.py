@@ -25,6 +25,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-ffp-contract=fast", "-Wno-unused-result"]
+NO_CONTRACT = {"forest.hip", "gbdt.hip"}
 CPU_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-march=x86-64-v2"]
 
 
@@ -57,7 +58,11 @@ def build_hip(verbose: bool = False) -> Path:
         o = BUILD / (s.stem + ".hip.o")
         objs.append(o)
         if _stale(o, [s, *hdrs, Path(__file__)]):
-            jobs.append([HIPCC, *HIP_FLAGS, "-I", str(CSRC), "-c", str(s), "-o", str(o)])
+            flags = list(HIP_FLAGS)
+            if s.name in NO_CONTRACT:
+                # bit-exact parity with the host reference: no FMA contraction
+                flags = [f for f in flags if not f.startswith("-ffp-contract")] + ["-ffp-contract=off"]
+            jobs.append([HIPCC, *flags, "-I", str(CSRC), "-c", str(s), "-o", str(o)])
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         list(ex.map(_run, jobs))
     lib = LIBDIR / "libatehip.so"

@@ -52,7 +52,12 @@ _SIGS = {
     "ate_enet_pick": "ppiiiipp",
     "ate_dml_resid_moments": "iplpipipiiiiiippp",
     "ate_dgp_fill": "ipllllu" + "iip",
+    "ate_forest_fit": "pppppi" + "ppppppppp",
+    "ate_forest_predict": "ppiii" + "pppppppp",
+    "ate_forest_scratch_bytes": "ii",
+    "ate_bin_matrix": "plipppp",
 }
+_RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}
 
 
@@ -61,7 +66,7 @@ def _load(path: Path, sigs: dict):
     for name, sig in sigs.items():
         if hasattr(lib, name):
             f = getattr(lib, name)
-            f.restype = c_int
+            f.restype = _RESTYPE.get(name, c_int)
             f.argtypes = [_CT[ch] for ch in sig]
     return lib
 

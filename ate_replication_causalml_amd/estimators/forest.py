@@ -1,0 +1,78 @@
+"""Device forest estimators: E8 doubly robust with RF propensity, E12/E13 the
+reference's two-half "double ML" with RF learners, E15 causal forest (grf) ATE.
+
+Forests grow on the GPU (csrc/forest.hip) when a GPU is present; ``backend="cpu"``
+runs the host C++ twin (bit-identical trees). Nuisance GLMs and score reductions use
+the device kernels of estimators/linear.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..models import forest as F
+from ..reference import estimators as R
+from ..result import AteResult
+from . import linear as D
+from .common import as_np, resolve_device
+
+
+def _backend(device):
+    dev = resolve_device(device)
+    return "gpu" if dev.type == "cuda" else "cpu"
+
+
+def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, forest_seed=12325,
+            compat="reference", method="Doubly Robust with Random Forest PS", device=None,
+            dtype="f64"):
+    """E8 ``doubly_robust`` (ate_functions.R:149-207): logistic outcome model (with the
+    mutate_ quirk Q6 under compat="reference"), randomForest OOB propensity clipped (Q9)."""
+    dev = resolve_device(device)
+    Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
+    mu0, mu1 = D.outcome_mu(Yn, Wn, Xn, counterfactual_quirk=(compat == "reference"),
+                            device=dev, dtype=dtype)
+    rf = F.rf_classifier(Xn, Wn, num_trees=num_trees, seed=forest_seed, backend=_backend(dev))
+    p_raw = rf.oob_proba()
+    p = torch.as_tensor(p_raw, device=dev)
+    from ..ops import stats as S
+    S.clip_propensity_(p)
+    return D.aipw_from_nuisances(method, Yn, Wn, p, mu0, mu1, bootstrap_se, B, seed, compat, dev,
+                                 n_oob_nan=int(np.isnan(p_raw).sum()))
+
+
+def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, device=None):
+    """One half of ``double_ml`` (ate_functions.R:332-369): RF classifier for W on idx1,
+    for Y on idx2, both predicted on all rows (in-sample for the training half, Q14)."""
+    be = _backend(device)
+    Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
+    edges = F.bin_edges(Xn)
+    rf1 = F.fit_forest(Xn[idx1], F.KIND_CLASS, y=Wn[idx1], ntree=num_trees, seed=seed,
+                       backend=be, edges=edges)
+    rf2 = F.fit_forest(Xn[idx2], F.KIND_CLASS, y=Yn[idx2], ntree=num_trees, seed=seed + 1,
+                       backend=be, edges=edges)
+    ew = rf1.predict_proba(Xn)
+    ey = rf2.predict_proba(Xn)
+    return R.resid_on_resid(Yn - ey, Wn - ew)
+
+
+def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning", device=None):
+    """E13 ``double_ml`` (ate_functions.R:372-389): positional halves, swapped, averaged
+    tau and averaged SE (Q14)."""
+    n = len(as_np(Y))
+    h = n // 2
+    idx1, idx2 = np.arange(h), np.arange(h, n)
+    t1, s1 = chernozhukov(Y, W, X, idx1, idx2, num_trees, seed, device)
+    t2, s2 = chernozhukov(Y, W, X, idx2, idx1, num_trees, seed + 2, device)
+    return AteResult.make(method, (t1 + t2) / 2, (s1 + s2) / 2)
+
+
+def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest(GRF)",
+                      device=None, nuisance_trees=None):
+    """E15 (ate_replication.Rmd:250-272): grf causal forest; published row = AIPW
+    ``estimate_average_effect``; diagnostics carry the "incorrect" mean-CATE ATE and
+    sqrt(mean(var)) the reference prints (ate_replication.md:294)."""
+    cf = F.causal_forest(as_np(X), as_np(Y), as_np(W), num_trees=num_trees, seed=seed,
+                         nuisance_trees=nuisance_trees, backend=_backend(device))
+    est, se = F.average_treatment_effect(cf)
+    return AteResult.make(method, est, se, ate_bad=float(np.nanmean(cf.tau_oob)),
+                          se_bad=float(np.sqrt(np.nanmean(cf.var_oob))))

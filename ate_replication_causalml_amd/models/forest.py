@@ -1,0 +1,316 @@
+"""Forest nuisance learners on the binned-histogram engine.
+
+* ``rf_classifier`` — randomForest semantics used by ``doubly_robust`` and
+  ``chernozhukov`` (``ate_functions.R:169-174,340-357``): bootstrap, mtry =
+  floor(sqrt(p)), nodesize 1, Gini, majority-vote leaves, ``predict(type="prob")`` =
+  vote share, OOB votes when predicting the training rows.
+* ``regression_forest`` / ``causal_forest`` — grf semantics
+  (``ate_replication.Rmd:250-265``): little bags of 2 trees on half-samples, honesty,
+  min.node.size 5, alpha 0.05, mtry = min(ceil(sqrt(p)+20), p) drawn ~ Poisson,
+  causal splits on gradient pseudo-outcomes, leaf sufficient statistics (forest
+  weights without N^2 storage), OOB predictions and little-bag variance.
+
+Backends: ``"gpu"`` (csrc/forest.hip, one workgroup per tree) and ``"cpu"``
+(csrc/cpu/forest_cpu.cpp, OpenMP). Both implement the spec in
+csrc/forest_common.hpp and grow bit-identical trees from the same Philox streams.
+Continuous covariates are quantile-binned to <= 256 bins (exact for <= 256 distinct
+values); splits are at bin boundaries.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+
+MAX_BINS = 256
+
+
+class ForestParams(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("sampling", ctypes.c_int), ("ntree", ctypes.c_int),
+                ("mtry", ctypes.c_int), ("min_node", ctypes.c_int), ("honesty", ctypes.c_int),
+                ("group", ctypes.c_int), ("mtry_poisson", ctypes.c_int),
+                ("alpha", ctypes.c_double), ("sample_fraction", ctypes.c_double),
+                ("pois0", ctypes.c_double), ("seed", ctypes.c_uint64), ("p", ctypes.c_int),
+                ("n", ctypes.c_int)]
+
+
+KIND_CLASS, KIND_REG, KIND_CAUSAL = 0, 1, 2
+FIX = float(2 ** 32)
+
+
+def to_fix(v) -> np.ndarray:
+    """2^-32 fixed point, round half away from zero (forest_common.hpp::to_fix)."""
+    s = np.asarray(v, dtype=np.float64) * FIX
+    return np.where(s >= 0, np.floor(s + 0.5), np.ceil(s - 0.5)).astype(np.int64)
+
+
+def from_fix(v) -> np.ndarray:
+    return np.asarray(v, dtype=np.float64) / FIX
+
+
+# ------------------------------------------------------------------ K11 binning
+def bin_edges(X: np.ndarray, max_bins: int = MAX_BINS):
+    """Per-feature sorted edges (<= max_bins-1): midpoints between distinct values when
+    there are at most max_bins of them, else distinct quantiles."""
+    X = np.asarray(X, dtype=np.float64)
+    p = X.shape[1]
+    edges = np.full((p, MAX_BINS - 1), np.inf)
+    ne = np.zeros(p, dtype=np.int32)
+    for j in range(p):
+        u = np.unique(X[:, j])
+        if len(u) <= max_bins:
+            e = (u[:-1] + u[1:]) / 2.0
+        else:
+            qs = np.quantile(X[:, j], np.arange(1, max_bins) / max_bins, method="lower")
+            e = np.unique(qs)
+            e = e[e < u[-1]]
+        edges[j, :len(e)] = e
+        ne[j] = len(e)
+    return edges, ne
+
+
+def bin_matrix(X, edges, ne, device=None) -> torch.Tensor:
+    """uint8 [p][n] column-major bins: bin(x) = #{edges < x}."""
+    Xn = X if isinstance(X, torch.Tensor) else torch.as_tensor(np.asarray(X, dtype=np.float64))
+    n, p = Xn.shape
+    dev = torch.device("cpu") if device is None else torch.device(device)
+    if dev.type == "cuda":
+        Xc = Xn.to(dev, torch.float64).t().contiguous()
+        out = torch.empty((p, n), dtype=torch.uint8, device=dev)
+        e = torch.as_tensor(edges, device=dev, dtype=torch.float64).contiguous()
+        nt = torch.as_tensor(ne, device=dev, dtype=torch.int32)
+        _native.call("ate_bin_matrix", Xc.data_ptr(), n, p, e.data_ptr(), nt.data_ptr(),
+                     out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        return out
+    Xh = Xn.double().cpu().numpy()
+    out = np.empty((p, n), dtype=np.uint8)
+    for j in range(p):
+        out[j] = np.searchsorted(edges[j, :ne[j]], Xh[:, j], side="left")
+    return torch.from_numpy(out)
+
+
+# ------------------------------------------------------------------ forest object
+def _nthreads():
+    return int(os.environ.get("ATE_CPU_THREADS", os.cpu_count() or 1))
+
+
+@dataclass
+class Forest:
+    params: ForestParams
+    backend: str
+    cap: int
+    feat: object
+    thr: object
+    left: object
+    val: object
+    nnodes: object
+    inbag: object
+    est: object
+    edges: np.ndarray
+    nedges: np.ndarray
+    Xb_train: object = None
+
+    @property
+    def device(self):
+        return torch.device("cuda", torch.cuda.current_device()) if self.backend == "gpu" \
+            else torch.device("cpu")
+
+    def _bins(self, X):
+        if X is None:
+            return self.Xb_train
+        return bin_matrix(X, self.edges, self.nedges, self.device if self.backend == "gpu" else None)
+
+    def predict_raw(self, X=None, oob=False) -> np.ndarray:
+        """kind 0/1: [n] predictions; kind 2: [n, 4] (tau, var, trees used, groups used)."""
+        Xb = self._bins(X)
+        n2 = Xb.shape[1]
+        if oob and n2 != self.params.n:
+            raise ValueError("OOB prediction requires the training rows")
+        width = 4 if self.params.kind == KIND_CAUSAL else 1
+        if self.backend == "gpu":
+            out = torch.empty(n2 * width, dtype=torch.float64, device=self.device)
+            _native.call("ate_forest_predict", ctypes.addressof(self.params), Xb.data_ptr(), n2,
+                         int(oob), self.cap, self.feat.data_ptr(), self.thr.data_ptr(),
+                         self.left.data_ptr(), self.val.data_ptr(), self.inbag.data_ptr(),
+                         0 if self.est is None else self.est.data_ptr(), out.data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+            res = out.cpu().numpy()
+        else:
+            res = np.empty(n2 * width)
+            Xbn = np.ascontiguousarray(Xb.numpy() if isinstance(Xb, torch.Tensor) else Xb)
+            lib = _native.cpu()
+            rc = lib.atecpu_forest_predict(
+                ctypes.byref(self.params), _ptr(Xbn), ctypes.c_int(n2), ctypes.c_int(int(oob)),
+                ctypes.c_int(self.cap), _ptr(self.feat), _ptr(self.thr), _ptr(self.left),
+                _ptr(self.val), _ptr(self.inbag), _ptr(self.est) if self.est is not None else None,
+                _ptr(res), ctypes.c_int(_nthreads()))
+            if rc != 0:
+                raise RuntimeError("atecpu_forest_predict failed")
+        return res.reshape(n2, width) if width > 1 else res
+
+    # randomForest-style accessors
+    def oob_proba(self):
+        return self.predict_raw(None, oob=True)
+
+    def predict_proba(self, X):
+        return self.predict_raw(X, oob=False)
+
+    def tree_arrays(self):
+        """(feat, thr, left, val, nnodes) as numpy (for parity tests)."""
+        f = lambda a: a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+        return f(self.feat), f(self.thr), f(self.left), f(self.val), f(self.nnodes)
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min_node=1,
+               sampling=0, honesty=False, group=1, mtry_poisson=False, alpha=0.0,
+               sample_fraction=0.5, seed=1, backend=None, edges=None) -> Forest:
+    """Grow a forest. X: (n, p) float; kind 0 needs y in {0,1}; kind 1 needs r1 (response);
+    kind 2 needs r1 = W~ and r2 = Y~ (centred treatment / outcome)."""
+    X = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
+    n, p = X.shape
+    if backend is None:
+        backend = "gpu" if torch.cuda.is_available() else "cpu"
+    if mtry is None:
+        mtry = max(1, int(math.floor(math.sqrt(p))))
+    fp = ForestParams(kind=kind, sampling=sampling, ntree=ntree, mtry=min(mtry, p),
+                      min_node=min_node, honesty=int(honesty), group=max(1, group),
+                      mtry_poisson=int(mtry_poisson), alpha=alpha,
+                      sample_fraction=sample_fraction, pois0=math.exp(-min(mtry, p)),
+                      seed=seed, p=p, n=n)
+    if edges is None:
+        edges, ne = bin_edges(X)
+    else:
+        edges, ne = edges
+    cap = 2 * n + 1
+    ycls = None if y is None else np.asarray(y).astype(np.uint8)
+    r1f = None if r1 is None else to_fix(r1)
+    r2f = None if r2 is None else to_fix(r2)
+    need_est = sampling == 1
+    if backend == "gpu":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        Xb = bin_matrix(X, edges, ne, dev)
+        t = lambda a, dt: None if a is None else torch.as_tensor(a, device=dev, dtype=dt)
+        yt, r1t, r2t = t(ycls, torch.uint8), t(r1f, torch.int64), t(r2f, torch.int64)
+        feat = torch.empty(ntree * cap, dtype=torch.int32, device=dev)
+        thr = torch.empty_like(feat)
+        left = torch.empty_like(feat)
+        val = torch.zeros(ntree * cap, dtype=torch.float64, device=dev)
+        nnodes = torch.empty(ntree, dtype=torch.int32, device=dev)
+        inbag = torch.empty(ntree * n, dtype=torch.uint8, device=dev)
+        est = torch.zeros(ntree * cap * 5, dtype=torch.int64, device=dev) if need_est else None
+        sb = _native.hip().ate_forest_scratch_bytes(n, ntree)
+        scratch = torch.empty(sb, dtype=torch.uint8, device=dev)
+        p_ = lambda a: 0 if a is None else a.data_ptr()
+        _native.call("ate_forest_fit", ctypes.addressof(fp), Xb.data_ptr(), p_(yt), p_(r1t),
+                     p_(r2t), cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(),
+                     val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
+                     scratch.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        del scratch
+        return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xb)
+    Xb = bin_matrix(X, edges, ne, None)
+    Xbn = np.ascontiguousarray(Xb.numpy())
+    feat = np.empty(ntree * cap, dtype=np.int32)
+    thr = np.empty_like(feat)
+    left = np.empty_like(feat)
+    val = np.zeros(ntree * cap)
+    nnodes = np.empty(ntree, dtype=np.int32)
+    inbag = np.empty(ntree * n, dtype=np.uint8)
+    est = np.zeros(ntree * cap * 5, dtype=np.int64) if need_est else None
+    lib = _native.cpu()
+    rc = lib.atecpu_forest_fit(ctypes.byref(fp), _ptr(Xbn), _ptr(ycls), _ptr(r1f), _ptr(r2f),
+                               ctypes.c_int(cap), _ptr(feat), _ptr(thr), _ptr(left), _ptr(val),
+                               _ptr(nnodes), _ptr(inbag), _ptr(est), ctypes.c_int(_nthreads()))
+    if rc != 0:
+        raise RuntimeError("atecpu_forest_fit failed")
+    return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xbn)
+
+
+# ------------------------------------------------------------------ public learners
+def rf_classifier(X, y, num_trees=500, mtry=None, nodesize=1, seed=1, backend=None) -> Forest:
+    """randomForest(factor(y) ~ X, ntree, type="classification") (ate_functions.R:169)."""
+    return fit_forest(X, KIND_CLASS, y=y, ntree=num_trees, mtry=mtry, min_node=nodesize,
+                      seed=seed, backend=backend)
+
+
+def rf_regressor(X, y, num_trees=500, mtry=None, nodesize=5, seed=1, backend=None) -> Forest:
+    """Breiman regression forest (bootstrap, variance-reduction splits)."""
+    p = np.asarray(X).shape[1]
+    return fit_forest(X, KIND_REG, r1=y, ntree=num_trees,
+                      mtry=mtry or max(1, p // 3), min_node=nodesize, seed=seed, backend=backend)
+
+
+def grf_mtry(p):
+    return min(int(math.ceil(math.sqrt(p) + 20)), p)
+
+
+def regression_forest(X, y, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
+                      sample_fraction=0.5, group=2, seed=1, backend=None) -> Forest:
+    """grf::regression_forest defaults; OOB predictions via ``oob_predict``."""
+    p = np.asarray(X).shape[1]
+    return fit_forest(X, KIND_REG, r1=y, ntree=num_trees, mtry=grf_mtry(p), min_node=min_node,
+                      sampling=1, honesty=honesty, group=group, mtry_poisson=True, alpha=alpha,
+                      sample_fraction=sample_fraction, seed=seed, backend=backend)
+
+
+@dataclass
+class CausalForestFit:
+    forest: Forest
+    y_hat: np.ndarray
+    w_hat: np.ndarray
+    tau_oob: np.ndarray
+    var_oob: np.ndarray
+    Y: np.ndarray
+    W: np.ndarray
+
+
+def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
+                  sample_fraction=0.5, group=2, seed=12345, nuisance_trees=None,
+                  backend=None) -> CausalForestFit:
+    """grf::causal_forest(X, Y, W, num.trees, honesty=TRUE, seed) (ate_replication.Rmd:250-255):
+    OOB regression forests for Y.hat and W.hat, then causal trees on the centred
+    (W - W.hat, Y - Y.hat)."""
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    W = np.asarray(W, dtype=np.float64)
+    nt = nuisance_trees or max(50, num_trees // 4)
+    edges = bin_edges(X)
+    fy = regression_forest(X, Y, nt, honesty, min_node, alpha, sample_fraction, group,
+                           seed + 1, backend)
+    fw = regression_forest(X, W, nt, honesty, min_node, alpha, sample_fraction, group,
+                           seed + 2, backend)
+    y_hat = fy.predict_raw(None, oob=True)
+    w_hat = fw.predict_raw(None, oob=True)
+    y_hat = np.where(np.isnan(y_hat), Y.mean(), y_hat)
+    w_hat = np.where(np.isnan(w_hat), W.mean(), w_hat)
+    p = X.shape[1]
+    fc = fit_forest(X, KIND_CAUSAL, r1=W - w_hat, r2=Y - y_hat, ntree=num_trees, mtry=grf_mtry(p),
+                    min_node=min_node, sampling=1, honesty=honesty, group=group, mtry_poisson=True,
+                    alpha=alpha, sample_fraction=sample_fraction, seed=seed, backend=backend,
+                    edges=edges)
+    out = fc.predict_raw(None, oob=True)
+    return CausalForestFit(fc, y_hat, w_hat, out[:, 0], out[:, 1], Y, W)
+
+
+def average_treatment_effect(cf: CausalForestFit):
+    """grf ``estimate_average_effect`` / ``average_treatment_effect`` (AIPW):
+    Gamma_i = tau_i + (W_i - W.hat_i)/(W.hat_i (1 - W.hat_i)) * (Y~_i - tau_i W~_i);
+    estimate = mean(Gamma), std.err = sd(Gamma)/sqrt(n)."""
+    w_res = cf.W - cf.w_hat
+    y_res = cf.Y - cf.y_hat
+    tau = np.where(np.isnan(cf.tau_oob), np.nanmean(cf.tau_oob), cf.tau_oob)
+    what = np.clip(cf.w_hat, 1e-6, 1 - 1e-6)
+    gamma = tau + w_res / (what * (1 - what)) * (y_res - tau * w_res)
+    n = len(gamma)
+    return float(gamma.mean()), float(gamma.std(ddof=1) / math.sqrt(n))

@@ -274,10 +274,13 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
 # ---------------------------------------------------------------- E12/E13 DML (compat)
 def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123):
     """One DML half (ate_functions.R:332-369, Q14/Q15)."""
-    from .forest import rf_classifier_fit
+    from ..models import forest as F
     Y, W, X = _arr(Y), _arr(W), _arr(X)
-    rf1 = rf_classifier_fit(X[idx1], W[idx1], num_trees=num_trees, seed=seed)
-    rf2 = rf_classifier_fit(X[idx2], Y[idx2], num_trees=num_trees, seed=seed + 1)
+    edges = F.bin_edges(X)
+    rf1 = F.fit_forest(X[idx1], F.KIND_CLASS, y=W[idx1], ntree=num_trees, seed=seed,
+                       backend="cpu", edges=edges)
+    rf2 = F.fit_forest(X[idx2], F.KIND_CLASS, y=Y[idx2], ntree=num_trees, seed=seed + 1,
+                       backend="cpu", edges=edges)
     ew = rf1.predict_proba(X)
     ey = rf2.predict_proba(X)
     return resid_on_resid(Y - ey, W - ew)
@@ -300,6 +303,18 @@ def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning"
     t1, s1 = chernozhukov(Y, W, X, idx1, idx2, num_trees, seed)
     t2, s2 = chernozhukov(Y, W, X, idx2, idx1, num_trees, seed + 2)
     return AteResult.make(method, (t1 + t2) / 2, (s1 + s2) / 2)
+
+
+# ---------------------------------------------------------------- E15 causal forest
+def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest(GRF)",
+                      nuisance_trees=None):
+    """grf causal forest + AIPW ATE (ate_replication.Rmd:250-272) on the host engine."""
+    from ..models import forest as F
+    cf = F.causal_forest(_arr(X), _arr(Y), _arr(W), num_trees=num_trees, seed=seed,
+                         nuisance_trees=nuisance_trees, backend="cpu")
+    est, se = F.average_treatment_effect(cf)
+    return AteResult.make(method, est, se, ate_bad=float(np.nanmean(cf.tau_oob)),
+                          se_bad=float(np.sqrt(np.nanmean(cf.var_oob))))
 
 
 # ---------------------------------------------------------------- K-fold DML (north star)

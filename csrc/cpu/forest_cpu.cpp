@@ -1,0 +1,363 @@
+// Host C++ reference of the forest engine (spec: csrc/forest_common.hpp).
+// One tree per OpenMP task; every tree is grown level by level exactly as the gfx950
+// kernel does (csrc/forest.hip), so the two produce bit-identical trees.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "../forest_common.hpp"
+
+using namespace atef;
+
+#define ATECPU_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+struct Out {
+  int cap;
+  int32_t* feat;
+  int32_t* thr;
+  int32_t* left;
+  double* val;
+  int32_t* nnodes;
+  uint8_t* inbag;   // [ntree][n]
+  int64_t* est;     // [ntree*cap][5] (grf): cnt, S1, S2, S11, S12 (fixed point)
+};
+
+struct Rng { int lo, hi, id; };
+
+// sample selection (grf): rows of `pop` (ascending) chosen by Algorithm S on `stream`
+static std::vector<int> select_rows(const ForestParams& fp, const std::vector<int>& pop,
+                                    int64_t k, uint32_t stream) {
+  std::vector<int> out;
+  out.reserve(k);
+  int64_t N = (int64_t)pop.size();
+  for (int64_t i = 0; i < N && (int64_t)out.size() < k; ++i)
+    if (select_next(fp.seed, stream, (uint64_t)i, N - i, k - (int64_t)out.size()))
+      out.push_back(pop[i]);
+  return out;
+}
+
+static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const uint8_t* ycls,
+                      const int64_t* r1, const int64_t* r2, const Out& o) {
+  const int n = fp.n, p = fp.p;
+  std::vector<int32_t> w(n, 0);
+  std::vector<int> est_rows;
+  uint8_t* inb = o.inbag + (int64_t)t * n;
+  if (fp.sampling == 0) {
+    for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)t, (uint64_t)j, (uint32_t)n)]++;
+    for (int i = 0; i < n; ++i) inb[i] = w[i] > 0;
+  } else {
+    const int g = t / fp.group;
+    std::vector<int> all(n);
+    std::iota(all.begin(), all.end(), 0);
+    std::vector<int> H = select_rows(fp, all, n / 2, (uint32_t)g);
+    std::memset(inb, 0, n);
+    for (int i : H) inb[i] = 1;
+    double f = fp.sample_fraction * fp.group;
+    if (f > 1.0) f = 1.0;
+    std::vector<int> S = f >= 1.0 ? H : select_rows(fp, H, (int64_t)std::floor(H.size() * f),
+                                                   0x10000u + (uint32_t)t);
+    std::vector<int> J1 = S;
+    if (fp.honesty) {
+      J1 = select_rows(fp, S, (int64_t)(S.size() / 2), 0x20000u + (uint32_t)t);
+      std::vector<uint8_t> in1(n, 0);
+      for (int i : J1) in1[i] = 1;
+      for (int i : S)
+        if (!in1[i]) est_rows.push_back(i);
+    } else {
+      est_rows = S;
+    }
+    for (int i : J1) w[i] = 1;
+  }
+  std::vector<int> idx;
+  for (int i = 0; i < n; ++i)
+    if (w[i] > 0) idx.push_back(i);
+  const int m = (int)idx.size();
+  const int64_t base = (int64_t)t * o.cap;
+  int32_t* feat = o.feat + base;
+  int32_t* thr = o.thr + base;
+  int32_t* left = o.left + base;
+  double* val = o.val + base;
+  std::vector<Rng> cur{{0, m, 0}};
+  int next_id = 1;
+  std::vector<int> tmp(m);
+  std::vector<int64_t> rho(n);
+  std::vector<int> perm(p);
+  int64_t h0[NBINS], h1[NBINS], hs[NBINS], ht[NBINS];
+  for (int depth = 0; !cur.empty(); ++depth) {
+    std::vector<Rng> nxt;
+    for (const Rng& nd : cur) {
+      const int v = nd.id;
+      // ---- node statistics (exact integers)
+      int64_t nw = 0, n1 = 0, s1 = 0, sw = 0, sy = 0, sww = 0, swy = 0;
+      for (int q = nd.lo; q < nd.hi; ++q) {
+        int i = idx[q];
+        nw += w[i];
+        if (fp.kind == 0) n1 += (int64_t)w[i] * ycls[i];
+        else if (fp.kind == 1) s1 += (int64_t)w[i] * r1[i];
+        else {
+          sw += r1[i];
+          sy += r2[i];
+          sww += to_fix(from_fix(r1[i]) * from_fix(r1[i]));
+          swy += to_fix(from_fix(r1[i]) * from_fix(r2[i]));
+        }
+      }
+      const double dn = (double)nw;
+      bool terminal = nw <= fp.min_node || depth >= MAX_DEPTH - 1;
+      if (fp.kind == 0 && (n1 == 0 || n1 == nw)) terminal = true;
+      CausalNode cn{0, 0, 0, 0};
+      if (fp.kind == 2) {
+        cn = causal_node(dn, sw, sy, sww, swy);
+        if (!(cn.varw > 0.0)) terminal = true;
+      }
+      int bf = -1, bb = -1;
+      int64_t bnl_rows = 0;
+      if (!terminal) {
+        if (fp.kind == 2)
+          for (int q = nd.lo; q < nd.hi; ++q) {
+            int i = idx[q];
+            rho[i] = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
+          }
+        double parent;
+        int64_t stot = 0;
+        if (fp.kind == 0) {
+          double a = (double)(nw - n1), b = (double)n1;
+          parent = (a * a + b * b) / dn;
+        } else {
+          if (fp.kind == 1) stot = s1;
+          else
+            for (int q = nd.lo; q < nd.hi; ++q) stot += rho[idx[q]];
+          double sd = from_fix(stot);
+          parent = (sd * sd) / dn;
+        }
+        const int minc = min_child(fp, dn);
+        const int nf = draw_num_features(fp, t, v);
+        std::iota(perm.begin(), perm.end(), 0);
+        for (int k = 0; k < nf; ++k) {
+          uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, k), (uint32_t)(p - k));
+          std::swap(perm[k], perm[k + r]);
+        }
+        double best = -INFINITY;
+        for (int k = 0; k < nf; ++k) {
+          const int f = perm[k];
+          const uint8_t* xf = Xb + (int64_t)f * n;
+          std::memset(h0, 0, sizeof h0);
+          std::memset(h1, 0, sizeof h1);
+          std::memset(hs, 0, sizeof hs);
+          std::memset(ht, 0, sizeof ht);
+          for (int q = nd.lo; q < nd.hi; ++q) {
+            int i = idx[q];
+            int b = xf[i];
+            if (fp.kind == 0) {
+              h0[b] += (int64_t)w[i] * (1 - ycls[i]);
+              h1[b] += (int64_t)w[i] * ycls[i];
+            } else if (fp.kind == 1) {
+              h0[b] += w[i];
+              hs[b] += (int64_t)w[i] * r1[i];
+            } else {
+              h0[b] += 1;
+              hs[b] += rho[i];
+              ht[b] += from_fix(r1[i]) > cn.wbar ? 1 : 0;
+            }
+          }
+          int64_t c0 = 0, c1 = 0, cs = 0, ct = 0;
+          int64_t ntreat = 0;
+          if (fp.kind == 2)
+            for (int b = 0; b < NBINS; ++b) ntreat += ht[b];
+          for (int b = 0; b < NBINS - 1; ++b) {
+            c0 += h0[b];
+            c1 += h1[b];
+            cs += hs[b];
+            ct += ht[b];
+            int64_t nl = fp.kind == 0 ? c0 + c1 : c0;
+            int64_t nr = nw - nl;
+            if (nl < minc || nr < minc) continue;
+            double crit;
+            if (fp.kind == 0) {
+              crit = gini_crit((double)c0, (double)c1, (double)(nw - n1 - c0), (double)(n1 - c1));
+            } else {
+              if (fp.kind == 2) {
+                int64_t tr = ntreat - ct;
+                if (ct < 1 || nl - ct < 1 || tr < 1 || nr - tr < 1) continue;
+              }
+              crit = mse_crit(from_fix(cs), (double)nl, from_fix(stot - cs), (double)nr);
+            }
+            if (crit > best) {
+              best = crit;
+              bf = f;
+              bb = b;
+            }
+          }
+        }
+        if (!(bf >= 0 && best > parent + 1e-12 * std::max(1.0, std::fabs(parent)))) bf = -1;
+      }
+      if (bf < 0) {
+        feat[v] = -1;
+        thr[v] = -1;
+        left[v] = -1;
+        if (fp.kind == 0) {
+          int vote;
+          if (2 * n1 > nw) vote = 1;
+          else if (2 * n1 < nw) vote = 0;
+          else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, 4095)) & 1u);
+          val[v] = vote;
+        } else if (fp.kind == 1) {
+          val[v] = from_fix(s1) / dn;
+        } else {
+          val[v] = 0.0;
+        }
+        continue;
+      }
+      // ---- stable partition of [lo, hi) by bin <= bb
+      const uint8_t* xf = Xb + (int64_t)bf * n;
+      int nl = 0;
+      for (int q = nd.lo; q < nd.hi; ++q)
+        if (xf[idx[q]] <= bb) tmp[nd.lo + nl++] = idx[q];
+      int nr = 0;
+      for (int q = nd.lo; q < nd.hi; ++q)
+        if (xf[idx[q]] > bb) tmp[nd.lo + nl + nr++] = idx[q];
+      for (int q = nd.lo; q < nd.hi; ++q) idx[q] = tmp[q];
+      (void)bnl_rows;
+      feat[v] = bf;
+      thr[v] = bb;
+      left[v] = next_id;
+      val[v] = 0.0;
+      nxt.push_back({nd.lo, nd.lo + nl, next_id});
+      nxt.push_back({nd.lo + nl, nd.hi, next_id + 1});
+      next_id += 2;
+    }
+    cur.swap(nxt);
+  }
+  o.nnodes[t] = next_id;
+  // ---- grf: estimation statistics of every node from the J2 (honest) rows
+  if (fp.sampling == 1 && o.est) {
+    int64_t* est = o.est + base * 5;
+    std::memset(est, 0, sizeof(int64_t) * 5 * next_id);
+    for (int i : est_rows) {
+      int v = 0;
+      while (true) {
+        int64_t* e = est + (int64_t)v * 5;
+        e[0] += 1;
+        if (fp.kind == 1) {
+          e[1] += r1[i];
+        } else {
+          e[1] += r1[i];
+          e[2] += r2[i];
+          e[3] += to_fix(from_fix(r1[i]) * from_fix(r1[i]));
+          e[4] += to_fix(from_fix(r1[i]) * from_fix(r2[i]));
+        }
+        if (feat[v] < 0) break;
+        v = Xb[(int64_t)feat[v] * n + i] <= thr[v] ? left[v] : left[v] + 1;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+ATECPU_API int atecpu_forest_fit(const ForestParams* fpp, const uint8_t* Xb, const uint8_t* ycls,
+                                 const int64_t* r1, const int64_t* r2, int cap, int32_t* feat,
+                                 int32_t* thr, int32_t* left, double* val, int32_t* nnodes,
+                                 uint8_t* inbag, int64_t* est, int nthreads) {
+  const ForestParams fp = *fpp;
+  if (fp.p >= 4094 || fp.n <= 0) return -1;
+  Out o{cap, feat, thr, left, val, nnodes, inbag, est};
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int t = 0; t < fp.ntree; ++t) grow_tree(fp, t, Xb, ycls, r1, r2, o);
+  return 0;
+}
+
+// Forest predictions on a binned matrix Xb [p][n2].
+//  oob: use tree t for row i only if inbag[t][i] == 0 (requires n2 == fp.n).
+//  out (kind 0): [n2] vote share (NaN if no tree used); (kind 1): [n2] mean of tree
+//  predictions; (kind 2): [n2][4] = tau, var (little bags), trees used, groups used.
+// Regression/causal grf trees predict from the deepest node on the path with J2 rows.
+ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb, int n2, int oob,
+                                     int cap, const int32_t* feat, const int32_t* thr,
+                                     const int32_t* left, const double* val,
+                                     const uint8_t* inbag, const int64_t* est, double* out,
+                                     int nthreads) {
+  const ForestParams fp = *fpp;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int i = 0; i < n2; ++i) {
+    // returns the node whose statistics predict for row i in tree t (-1 if tree unused)
+    auto leaf_of = [&](int t) -> int64_t {
+      if (oob && inbag[(int64_t)t * fp.n + i]) return -1;
+      const int64_t base = (int64_t)t * cap;
+      int v = 0, last_ok = 0;
+      while (true) {
+        if (fp.sampling == 1 && est && est[(base + v) * 5] > 0) last_ok = v;
+        if (feat[base + v] < 0) break;
+        v = Xb[(int64_t)feat[base + v] * n2 + i] <= thr[base + v] ? left[base + v] : left[base + v] + 1;
+      }
+      return base + (fp.sampling == 1 && est ? last_ok : v);
+    };
+    if (fp.kind != 2) {
+      double acc = 0;
+      int used = 0;
+      for (int t = 0; t < fp.ntree; ++t) {
+        const int64_t nd = leaf_of(t);
+        if (nd < 0) continue;
+        ++used;
+        if (fp.kind == 0 || fp.sampling == 0) acc += val[nd];
+        else acc += from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
+      }
+      out[i] = used > 0 ? acc / used : NAN;
+      continue;
+    }
+    // kind 2: forest-weighted leaf moments -> tau; little-bag variance of the linearised
+    // score psi = (w - Wbar)(y - Ybar - tau (w - Wbar)) over groups, divided by H^2
+    double a1 = 0, aw = 0, ay = 0, aww = 0, awy = 0;
+    for (int t = 0; t < fp.ntree; ++t) {
+      const int64_t nd = leaf_of(t);
+      if (nd < 0) continue;
+      const int64_t* e = est + nd * 5;
+      const double c = (double)e[0];
+      a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
+      aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
+    }
+    double tau = NAN, var = NAN;
+    int ng = 0;
+    if (a1 > 0) {
+      const double wb = aw / a1, yb = ay / a1;
+      const double H = aww / a1 - wb * wb;
+      if (H > 0) {
+        tau = (awy / a1 - wb * yb) / H;
+        double gs = 0, gss = 0, within = 0;
+        int nwithin = 0;
+        for (int g0 = 0; g0 < fp.ntree; g0 += fp.group) {
+          double ps = 0, pss = 0;
+          int nb = 0;
+          for (int t = g0; t < g0 + fp.group && t < fp.ntree; ++t) {
+            const int64_t nd = leaf_of(t);
+            if (nd < 0) continue;
+            const int64_t* e = est + nd * 5;
+            const double c = (double)e[0];
+            const double w_ = from_fix(e[1]) / c, y_ = from_fix(e[2]) / c;
+            const double ww = from_fix(e[3]) / c, wy = from_fix(e[4]) / c;
+            const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
+            ps += psi; pss += psi * psi; ++nb;
+          }
+          if (nb == 0) continue;
+          const double pg = ps / nb;
+          gs += pg; gss += pg * pg; ++ng;
+          if (nb >= 2) { within += pss / nb - pg * pg; ++nwithin; }
+        }
+        if (ng >= 2) {
+          const double mean = gs / ng;
+          const double between = gss / ng - mean * mean;
+          const double wc = nwithin > 0 ? within / nwithin / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
+          var = std::fmax(between - wc, 0.0) / (H * H);
+        }
+      }
+    }
+    out[4 * i + 0] = tau;
+    out[4 * i + 1] = var;
+    out[4 * i + 2] = a1;
+    out[4 * i + 3] = ng;
+  }
+  return 0;
+}

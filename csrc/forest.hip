@@ -1,0 +1,578 @@
+// K10-K15 forest engine on gfx950 (spec and CPU twin: forest_common.hpp, cpu/forest_cpu.cpp).
+//
+// K10 bootstrap_counts / grf half-sampling, K11 (binning is done by bin_kernel below),
+// K12 hist_build (LDS int64 histograms, ds_add_u64), K13 split_search (wave prefix scan +
+// argmax with (feature slot, bin) tie-break), K14 partition (stable ballot compaction),
+// K15 forest_predict (row x tree traversal, OOB masks), K16/K17 causal pseudo-outcomes
+// and leaf sufficient statistics.
+//
+// Decomposition: ONE 256-thread workgroup grows ONE tree level by level (trees are
+// independent: tree parallelism across CUs). Within a level the 4 waves take nodes
+// round-robin; a node's decision is made by one wave. Child ids are assigned after the
+// level by a scan in list order, so node numbering equals the CPU reference.
+#include "common.hpp"
+#include "forest_common.hpp"
+
+using namespace atef;
+
+constexpr int PMAX_F = 512;   // max features for the per-wave permutation buffer
+
+namespace {
+
+struct Rng3 { int lo, hi, id; };
+
+__device__ __forceinline__ int64_t wsum64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+struct Scratch {
+  int32_t* w;       // [n] weights of growing rows
+  int32_t* idx;     // [n]
+  int32_t* tmp;     // [n]
+  int64_t* rho;     // [n] causal pseudo-outcomes (fixed point)
+  Rng3* cur;        // [n+1]
+  Rng3* nxt;        // [n+1]
+  int4* dec;        // [n+1] per level node: (split flag, feat, bin, left rows)
+  int32_t* est_rows;// [n]
+};
+
+__device__ Scratch scratch_for(char* base, int n, int t) {
+  // per-tree region; layout must match forest_scratch_bytes()
+  const int64_t nn = n + 1;
+  const int64_t bytes = nn * (4 + 4 + 4 + 8 + 12 + 12 + 16 + 4) + 64;
+  char* p = base + (int64_t)t * ((bytes + 255) / 256 * 256);
+  Scratch s;
+  s.rho = (int64_t*)p;            p += nn * 8;
+  s.dec = (int4*)p;               p += nn * 16;
+  s.w = (int32_t*)p;              p += nn * 4;
+  s.idx = (int32_t*)p;            p += nn * 4;
+  s.tmp = (int32_t*)p;            p += nn * 4;
+  s.cur = (Rng3*)p;               p += nn * 12;
+  s.nxt = (Rng3*)p;               p += nn * 12;
+  s.est_rows = (int32_t*)p;
+  return s;
+}
+
+}  // namespace
+
+ATE_API int64_t ate_forest_scratch_bytes(int n, int ntree) {
+  const int64_t nn = n + 1;
+  const int64_t bytes = nn * (4 + 4 + 4 + 8 + 12 + 12 + 16 + 4) + 64;
+  return (bytes + 255) / 256 * 256 * (int64_t)ntree;
+}
+
+// block-wide exclusive scan of one int per thread (256 threads); returns total via *tot
+__device__ int block_scan_excl(int v, int* sh /*>= 8*/, int* tot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  int off = 0;
+  for (int k = 0; k < wid; ++k) off += sh[k];
+  int total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  *tot = total;
+  return off + x - v;
+}
+
+__global__ __launch_bounds__(256) void forest_grow_kernel(
+    ForestParams fp, const uint8_t* __restrict__ Xb, const uint8_t* __restrict__ ycls,
+    const int64_t* __restrict__ r1, const int64_t* __restrict__ r2, int cap,
+    int32_t* __restrict__ feat_o, int32_t* __restrict__ thr_o, int32_t* __restrict__ left_o,
+    double* __restrict__ val_o, int32_t* __restrict__ nnodes, uint8_t* __restrict__ inbag,
+    int64_t* __restrict__ est_o, char* __restrict__ scratch_base) {
+  // LDS: per wave histogram (256 bins x 4 int64 = 8 KB) + feature permutation
+  __shared__ int64_t hist[4][4][NBINS];
+  __shared__ int16_t perm[4][PMAX_F];
+  __shared__ int shi[8];
+  __shared__ int sncur, snext_id, sm, sestn;
+  const int t = blockIdx.x;
+  const int n = fp.n, p = fp.p;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  Scratch S = scratch_for(scratch_base, n, t);
+  uint8_t* inb = inbag + (int64_t)t * n;
+  // ------------------------------------------------------------ sampling (K10)
+  for (int i = tid; i < n; i += 256) S.w[i] = 0;
+  __syncthreads();
+  if (fp.sampling == 0) {
+    for (int j = tid; j < n; j += 256)
+      atomicAdd(&S.w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)t, (uint64_t)j, (uint32_t)n)], 1);
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) inb[i] = S.w[i] > 0;
+    if (tid == 0) sestn = 0;
+  } else if (tid == 0) {
+    // Algorithm S (sequential by definition): group half-sample H, tree subsample S,
+    // honesty split J1 (grow) / J2 (estimate). tmp holds H, then S; est_rows holds J2.
+    const int g = t / fp.group;
+    int nh = 0;
+    const int64_t kh = n / 2;
+    for (int i = 0; i < n && nh < kh; ++i)
+      if (select_next(fp.seed, (uint32_t)g, (uint64_t)i, (int64_t)(n - i), kh - nh)) S.tmp[nh++] = i;
+    for (int i = 0; i < n; ++i) inb[i] = 0;
+    for (int q = 0; q < nh; ++q) inb[S.tmp[q]] = 1;
+    double f = fp.sample_fraction * fp.group;
+    if (f > 1.0) f = 1.0;
+    int ns = nh;
+    if (f < 1.0) {
+      const int64_t ks = (int64_t)floor(nh * f);
+      int c = 0;
+      for (int q = 0; q < nh && c < ks; ++q)
+        if (select_next(fp.seed, 0x10000u + (uint32_t)t, (uint64_t)q, (int64_t)(nh - q), ks - c))
+          S.tmp[c++] = S.tmp[q];
+      ns = c;
+    }
+    int ne = 0;
+    if (fp.honesty) {
+      const int64_t k1 = ns / 2;
+      int c = 0;
+      for (int q = 0; q < ns; ++q) {
+        const int i = S.tmp[q];
+        if (c < k1 && select_next(fp.seed, 0x20000u + (uint32_t)t, (uint64_t)q, (int64_t)(ns - q), k1 - c)) {
+          S.w[i] = 1;
+          ++c;
+        } else {
+          S.est_rows[ne++] = i;
+        }
+      }
+    } else {
+      for (int q = 0; q < ns; ++q) {
+        S.w[S.tmp[q]] = 1;
+        S.est_rows[ne++] = S.tmp[q];
+      }
+    }
+    sestn = ne;
+  }
+  __syncthreads();
+  // ------------------------------------------------------------ in-bag rows, ascending
+  int m = 0;
+  for (int base = 0; base < n; base += 256) {
+    const int i = base + tid;
+    const int f = (i < n && S.w[i] > 0) ? 1 : 0;
+    int tot;
+    const int pos = block_scan_excl(f, shi, &tot);
+    if (f) S.idx[m + pos] = i;
+    m += tot;
+  }
+  const int64_t obase = (int64_t)t * cap;
+  int32_t* feat = feat_o + obase;
+  int32_t* thr = thr_o + obase;
+  int32_t* left = left_o + obase;
+  double* val = val_o + obase;
+  if (tid == 0) {
+    S.cur[0] = {0, m, 0};
+    sncur = 1;
+    snext_id = 1;
+  }
+  __syncthreads();
+  // ------------------------------------------------------------ levels
+  for (int depth = 0;; ++depth) {
+    const int ncur = sncur;
+    if (ncur == 0) break;
+    // ---- decisions: one wave per node
+    for (int j = wid; j < ncur; j += 4) {
+      const Rng3 nd = S.cur[j];
+      const int v = nd.id;
+      int64_t nw = 0, n1 = 0, s1 = 0, sw = 0, sy = 0, sww = 0, swy = 0;
+      for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+        const int i = S.idx[q];
+        const int64_t wi = S.w[i];
+        nw += wi;
+        if (fp.kind == 0) n1 += wi * ycls[i];
+        else if (fp.kind == 1) s1 += wi * r1[i];
+        else {
+          sw += r1[i];
+          sy += r2[i];
+          sww += to_fix(__dmul_rn(from_fix(r1[i]), from_fix(r1[i])));
+          swy += to_fix(__dmul_rn(from_fix(r1[i]), from_fix(r2[i])));
+        }
+      }
+      nw = wsum64(nw); n1 = wsum64(n1); s1 = wsum64(s1);
+      sw = wsum64(sw); sy = wsum64(sy); sww = wsum64(sww); swy = wsum64(swy);
+      const double dn = (double)nw;
+      bool terminal = nw <= fp.min_node || depth >= MAX_DEPTH - 1;
+      if (fp.kind == 0 && (n1 == 0 || n1 == nw)) terminal = true;
+      CausalNode cn{0, 0, 0, 0};
+      if (fp.kind == 2) {
+        cn = causal_node(dn, sw, sy, sww, swy);
+        if (!(cn.varw > 0.0)) terminal = true;
+      }
+      int bf = -1, bb = -1;
+      if (!terminal) {
+        int64_t stot = 0;
+        if (fp.kind == 2) {
+          for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+            const int i = S.idx[q];
+            const int64_t rv = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
+            S.rho[i] = rv;
+            stot += rv;
+          }
+          stot = wsum64(stot);
+        } else if (fp.kind == 1) {
+          stot = s1;
+        }
+        double parent;
+        if (fp.kind == 0) {
+          const double a = (double)(nw - n1), b = (double)n1;
+          parent = __ddiv_rn(__dadd_rn(__dmul_rn(a, a), __dmul_rn(b, b)), dn);
+        } else {
+          const double sd = from_fix(stot);
+          parent = __ddiv_rn(__dmul_rn(sd, sd), dn);
+        }
+        const int minc = min_child(fp, dn);
+        const int nf = draw_num_features(fp, t, v);
+        if (lane == 0) {
+          for (int k = 0; k < p; ++k) perm[wid][k] = (int16_t)k;
+          for (int k = 0; k < nf; ++k) {
+            const uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, k), (uint32_t)(p - k));
+            const int16_t tmpv = perm[wid][k];
+            perm[wid][k] = perm[wid][k + r];
+            perm[wid][k + r] = tmpv;
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        double best = -INFINITY;
+        int64_t ntreat = 0;
+        for (int k = 0; k < nf; ++k) {
+          const int f = perm[wid][k];
+          const uint8_t* xf = Xb + (int64_t)f * n;
+          for (int b = lane; b < NBINS; b += 64) {
+            hist[wid][0][b] = 0; hist[wid][1][b] = 0; hist[wid][2][b] = 0; hist[wid][3][b] = 0;
+          }
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+            const int i = S.idx[q];
+            const int b = xf[i];
+            if (fp.kind == 0) {
+              const int64_t wi = S.w[i];
+              if (ycls[i]) atomicAdd((unsigned long long*)&hist[wid][1][b], (unsigned long long)wi);
+              else atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
+            } else if (fp.kind == 1) {
+              const int64_t wi = S.w[i];
+              atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
+              atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)(wi * r1[i]));
+            } else {
+              atomicAdd((unsigned long long*)&hist[wid][0][b], 1ull);
+              atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)S.rho[i]);
+              if (from_fix(r1[i]) > cn.wbar) atomicAdd((unsigned long long*)&hist[wid][3][b], 1ull);
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          // wave prefix scan: lane owns bins 4*lane .. 4*lane+3
+          int64_t c0[4], c1[4], cs[4], ct[4];
+          int64_t a0 = 0, a1 = 0, as = 0, at_ = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int b = 4 * lane + e;
+            a0 += hist[wid][0][b]; a1 += hist[wid][1][b]; as += hist[wid][2][b]; at_ += hist[wid][3][b];
+            c0[e] = a0; c1[e] = a1; cs[e] = as; ct[e] = at_;
+          }
+          int64_t x0 = a0, x1 = a1, xs = as, xt = at_;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y0 = __shfl_up(x0, o, 64), y1 = __shfl_up(x1, o, 64);
+            const int64_t ys_ = __shfl_up(xs, o, 64), yt = __shfl_up(xt, o, 64);
+            if (lane >= o) { x0 += y0; x1 += y1; xs += ys_; xt += yt; }
+          }
+          const int64_t p0 = x0 - a0, p1 = x1 - a1, ps = xs - as, pt = xt - at_;   // exclusive
+          if (fp.kind == 2) ntreat = __shfl(xt, 63, 64);
+          double lbest = -INFINITY;
+          int lbin = NBINS;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int b = 4 * lane + e;
+            if (b >= NBINS - 1) continue;
+            const int64_t L0 = p0 + c0[e], L1 = p1 + c1[e], LS = ps + cs[e], LT = pt + ct[e];
+            const int64_t nl = fp.kind == 0 ? L0 + L1 : L0;
+            const int64_t nr = nw - nl;
+            if (nl < minc || nr < minc) continue;
+            double crit;
+            if (fp.kind == 0) {
+              crit = gini_crit((double)L0, (double)L1, (double)(nw - n1 - L0), (double)(n1 - L1));
+            } else {
+              if (fp.kind == 2) {
+                const int64_t tr = ntreat - LT;
+                if (LT < 1 || nl - LT < 1 || tr < 1 || nr - tr < 1) continue;
+              }
+              crit = mse_crit(from_fix(LS), (double)nl, from_fix(stot - LS), (double)nr);
+            }
+            if (crit > lbest) { lbest = crit; lbin = b; }
+          }
+          // wave argmax: max crit, then lowest bin
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            const double oc = __shfl_xor(lbest, o, 64);
+            const int ob = __shfl_xor(lbin, o, 64);
+            if (oc > lbest || (oc == lbest && ob < lbin)) { lbest = oc; lbin = ob; }
+          }
+          if (lbin < NBINS && lbest > best) { best = lbest; bf = f; bb = lbin; }
+        }
+        if (!(bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent)))) bf = -1;
+      }
+      // ---- record the decision (lane 0)
+      if (lane == 0) {
+        int nl_rows = 0;
+        if (bf >= 0) {
+          feat[v] = bf;
+          thr[v] = bb;
+          val[v] = 0.0;
+        } else {
+          feat[v] = -1;
+          thr[v] = -1;
+          left[v] = -1;
+          if (fp.kind == 0) {
+            int vote;
+            if (2 * n1 > nw) vote = 1;
+            else if (2 * n1 < nw) vote = 0;
+            else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, 4095)) & 1u);
+            val[v] = vote;
+          } else if (fp.kind == 1) {
+            val[v] = from_fix(s1) / dn;
+          } else {
+            val[v] = 0.0;
+          }
+        }
+        S.dec[j] = make_int4(bf >= 0 ? 1 : 0, bf, bb, nl_rows);
+      }
+    }
+    __syncthreads();
+    // ---- child ids in level order (block scan over split flags)
+    int id_base = snext_id;
+    int nsplit_total = 0;
+    for (int base = 0; base < ncur; base += 256) {
+      const int j = base + tid;
+      const int f = j < ncur ? S.dec[j].x : 0;
+      int tot;
+      const int pos = block_scan_excl(f, shi, &tot);
+      if (f) {
+        const int v = S.cur[j].id;
+        left[v] = id_base + 2 * (nsplit_total + pos);
+        S.dec[j].w = nsplit_total + pos;   // split rank
+      }
+      nsplit_total += tot;
+    }
+    __syncthreads();
+    // ---- stable partition of each split node (one wave per node) + next level list
+    for (int j = wid; j < ncur; j += 4) {
+      const int4 d = S.dec[j];
+      if (!d.x) continue;
+      const Rng3 nd = S.cur[j];
+      const uint8_t* xf = Xb + (int64_t)d.y * n;
+      int cnt_l = 0;
+      for (int q0 = nd.lo; q0 < nd.hi; q0 += 64) {
+        const int q = q0 + lane;
+        const bool gl = q < nd.hi && xf[S.idx[q]] <= d.z;
+        const uint64_t bl = __ballot(gl);
+        if (gl) S.tmp[nd.lo + cnt_l + __popcll(bl & ((1ull << lane) - 1ull))] = S.idx[q];
+        cnt_l += __popcll(bl);
+      }
+      int cnt_r = 0;
+      for (int q0 = nd.lo; q0 < nd.hi; q0 += 64) {
+        const int q = q0 + lane;
+        const bool gr = q < nd.hi && xf[S.idx[q]] > d.z;
+        const uint64_t br = __ballot(gr);
+        if (gr) S.tmp[nd.lo + cnt_l + cnt_r + __popcll(br & ((1ull << lane) - 1ull))] = S.idx[q];
+        cnt_r += __popcll(br);
+      }
+      for (int q = nd.lo + lane; q < nd.hi; q += 64) S.idx[q] = S.tmp[q];
+      if (lane == 0) {
+        const int r = d.w;
+        const int lid = id_base + 2 * r;
+        S.nxt[2 * r] = {nd.lo, nd.lo + cnt_l, lid};
+        S.nxt[2 * r + 1] = {nd.lo + cnt_l, nd.hi, lid + 1};
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      sncur = 2 * nsplit_total;
+      snext_id = id_base + 2 * nsplit_total;
+    }
+    // swap lists
+    Rng3* tswap = S.cur; S.cur = S.nxt; S.nxt = tswap;
+    __syncthreads();
+  }
+  const int nn = snext_id;
+  if (tid == 0) nnodes[t] = nn;
+  // ------------------------------------------------------------ grf leaf statistics (J2)
+  if (fp.sampling == 1 && est_o) {
+    int64_t* est = est_o + obase * 5;
+    for (int e = tid; e < nn * 5; e += 256) est[e] = 0;
+    __syncthreads();
+    const int ne = sestn;
+    for (int q = tid; q < ne; q += 256) {
+      const int i = S.est_rows[q];
+      int v = 0;
+      while (true) {
+        int64_t* e = est + (int64_t)v * 5;
+        atomicAdd((unsigned long long*)&e[0], 1ull);
+        if (fp.kind == 1) {
+          atomicAdd((unsigned long long*)&e[1], (unsigned long long)r1[i]);
+        } else {
+          atomicAdd((unsigned long long*)&e[1], (unsigned long long)r1[i]);
+          atomicAdd((unsigned long long*)&e[2], (unsigned long long)r2[i]);
+          atomicAdd((unsigned long long*)&e[3],
+                    (unsigned long long)to_fix(__dmul_rn(from_fix(r1[i]), from_fix(r1[i]))));
+          atomicAdd((unsigned long long*)&e[4],
+                    (unsigned long long)to_fix(__dmul_rn(from_fix(r1[i]), from_fix(r2[i]))));
+        }
+        if (feat[v] < 0) break;
+        v = Xb[(int64_t)feat[v] * n + i] <= thr[v] ? left[v] : left[v] + 1;
+      }
+    }
+  }
+}
+
+ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, const void* r1,
+                           const void* r2, int cap, void* feat, void* thr, void* left, void* val,
+                           void* nnodes, void* inbag, void* est, void* scratch, void* stream) {
+  const ForestParams fp = *(const ForestParams*)fpp;
+  if (fp.p > PMAX_F || fp.n <= 0) return -1;
+  hipLaunchKernelGGL(forest_grow_kernel, dim3(fp.ntree), dim3(256), 0, (hipStream_t)stream, fp,
+                     (const uint8_t*)Xb, (const uint8_t*)ycls, (const int64_t*)r1,
+                     (const int64_t*)r2, cap, (int32_t*)feat, (int32_t*)thr, (int32_t*)left,
+                     (double*)val, (int32_t*)nnodes, (uint8_t*)inbag, (int64_t*)est,
+                     (char*)scratch);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------ K15 prediction
+// One thread per row, all trees (tree arrays are L2-resident). Same formulas and
+// summation order as the CPU twin (atecpu_forest_predict).
+__device__ __forceinline__ int64_t leaf_of(const ForestParams& fp, const uint8_t* Xb, int n2,
+                                           int i, int t, int oob, int cap, const int32_t* feat,
+                                           const int32_t* thr, const int32_t* left,
+                                           const uint8_t* inbag, const int64_t* est) {
+  if (oob && inbag[(int64_t)t * fp.n + i]) return -1;
+  const int64_t base = (int64_t)t * cap;
+  int v = 0, last_ok = 0;
+  while (true) {
+    if (fp.sampling == 1 && est && est[(base + v) * 5] > 0) last_ok = v;
+    const int f = feat[base + v];
+    if (f < 0) break;
+    v = Xb[(int64_t)f * n2 + i] <= thr[base + v] ? left[base + v] : left[base + v] + 1;
+  }
+  return base + ((fp.sampling == 1 && est) ? last_ok : v);
+}
+
+__global__ __launch_bounds__(256) void forest_predict_kernel(
+    ForestParams fp, const uint8_t* __restrict__ Xb, int n2, int oob, int cap,
+    const int32_t* __restrict__ feat, const int32_t* __restrict__ thr,
+    const int32_t* __restrict__ left, const double* __restrict__ val,
+    const uint8_t* __restrict__ inbag, const int64_t* __restrict__ est, double* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n2) return;
+  if (fp.kind != 2) {
+    double acc = 0;
+    int used = 0;
+    for (int t = 0; t < fp.ntree; ++t) {
+      const int64_t nd = leaf_of(fp, Xb, n2, i, t, oob, cap, feat, thr, left, inbag, est);
+      if (nd < 0) continue;
+      ++used;
+      if (fp.kind == 0 || fp.sampling == 0) acc += val[nd];
+      else acc += from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
+    }
+    out[i] = used > 0 ? acc / used : NAN;
+    return;
+  }
+  double a1 = 0, aw = 0, ay = 0, aww = 0, awy = 0;
+  for (int t = 0; t < fp.ntree; ++t) {
+    const int64_t nd = leaf_of(fp, Xb, n2, i, t, oob, cap, feat, thr, left, inbag, est);
+    if (nd < 0) continue;
+    const int64_t* e = est + nd * 5;
+    const double c = (double)e[0];
+    a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
+    aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
+  }
+  double tau = NAN, var = NAN;
+  int ng = 0;
+  if (a1 > 0) {
+    const double wb = aw / a1, yb = ay / a1;
+    const double H = aww / a1 - wb * wb;
+    if (H > 0) {
+      tau = (awy / a1 - wb * yb) / H;
+      double gs = 0, gss = 0, within = 0;
+      int nwithin = 0;
+      for (int g0 = 0; g0 < fp.ntree; g0 += fp.group) {
+        double ps = 0, pss = 0;
+        int nb = 0;
+        for (int t = g0; t < g0 + fp.group && t < fp.ntree; ++t) {
+          const int64_t nd = leaf_of(fp, Xb, n2, i, t, oob, cap, feat, thr, left, inbag, est);
+          if (nd < 0) continue;
+          const int64_t* e = est + nd * 5;
+          const double c = (double)e[0];
+          const double w_ = from_fix(e[1]) / c, y_ = from_fix(e[2]) / c;
+          const double ww = from_fix(e[3]) / c, wy = from_fix(e[4]) / c;
+          const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
+          ps += psi; pss += psi * psi; ++nb;
+        }
+        if (nb == 0) continue;
+        const double pg = ps / nb;
+        gs += pg; gss += pg * pg; ++ng;
+        if (nb >= 2) { within += pss / nb - pg * pg; ++nwithin; }
+      }
+      if (ng >= 2) {
+        const double mean = gs / ng;
+        const double between = gss / ng - mean * mean;
+        const double wc = nwithin > 0 ? within / nwithin / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
+        var = fmax(between - wc, 0.0) / (H * H);
+      }
+    }
+  }
+  out[4 * i + 0] = tau;
+  out[4 * i + 1] = var;
+  out[4 * i + 2] = a1;
+  out[4 * i + 3] = ng;
+}
+
+ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob, int cap,
+                               const void* feat, const void* thr, const void* left,
+                               const void* val, const void* inbag, const void* est, void* out,
+                               void* stream) {
+  const ForestParams fp = *(const ForestParams*)fpp;
+  hipLaunchKernelGGL(forest_predict_kernel, dim3((n2 + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, fp, (const uint8_t*)Xb, n2, oob, cap,
+                     (const int32_t*)feat, (const int32_t*)thr, (const int32_t*)left,
+                     (const double*)val, (const uint8_t*)inbag, (const int64_t*)est,
+                     (double*)out);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------ K11 binning
+// bin(x) = #{edges < x} with per-feature sorted edges (<= 255), binary search in LDS.
+// X: [p][n] column-major (float64), edges: [p][255] (unused slots = +inf), out uint8 [p][n].
+__global__ __launch_bounds__(256) void bin_kernel(const double* __restrict__ X, int64_t n, int p,
+                                                  const double* __restrict__ edges,
+                                                  const int* __restrict__ nedges,
+                                                  uint8_t* __restrict__ out) {
+  __shared__ double e[255];
+  const int f = blockIdx.y;
+  const int ne = nedges[f];
+  for (int k = threadIdx.x; k < 255; k += 256) e[k] = edges[(int64_t)f * 255 + k];
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double x = X[(int64_t)f * n + i];
+    int lo = 0, hi = ne;   // first edge >= x
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (e[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    out[(int64_t)f * n + i] = (uint8_t)lo;
+  }
+}
+
+ATE_API int ate_bin_matrix(const void* X, int64_t n, int p, const void* edges, const void* nedges,
+                           void* out, void* stream) {
+  dim3 grid(ate::grid_for(n, 256, 512), p);
+  hipLaunchKernelGGL(bin_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const double*)X, n, p,
+                     (const double*)edges, (const int*)nedges, (uint8_t*)out);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}

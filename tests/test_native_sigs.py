@@ -13,7 +13,7 @@ def _decls():
     out = {}
     for f in (ROOT / "csrc").glob("*.hip"):
         src = f.read_text()
-        for m in re.finditer(r"ATE_API\s+int\s+(\w+)\s*\(([^)]*)\)", src):
+        for m in re.finditer(r"ATE_API\s+(?:int|int64_t)\s+(\w+)\s*\(([^)]*)\)", src):
             args = [a.strip() for a in m.group(2).split(",") if a.strip()]
             sig = ""
             for a in args:
