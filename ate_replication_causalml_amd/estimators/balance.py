@@ -1,0 +1,211 @@
+"""Device approximate residual balancing (E14; ate_functions.R:393-405 ->
+balanceHD::residualBalance.ate).
+
+Both arms share ONE fold-segmented panel (segments 0..K-1 = treated folds,
+K..2K-1 = control folds), so
+
+* the per-arm ``cv.glmnet(alpha=0.9)`` fits are two "full sets" of a single
+  ``cv_enet_gaussian`` call on one Gram stack (K01 + K08/K09);
+* the balancing QPs of both arms run in lock-step through one interior-point
+  loop whose O(n) work per iteration is ONE weighted Gram launch over the whole
+  panel (segment-summed per arm) plus two GEMVs; the (2p+1)-dim Schur systems
+  are batched over the arms.
+
+Matches reference/balance.py (same algorithm, both solved to ~1e-10).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops.enet import cv_enet_gaussian
+from ..ops.gram import gram
+from ..ops.panel import build_panel
+from ..parallel import rng
+from ..reference.balance import scale_columns
+from ..result import AteResult
+from .common import as_np, resolve_device
+
+
+def _arm_masks(pan, K):
+    valid = pan.valid() != 0
+    m = torch.zeros(2, pan.ld, dtype=torch.bool, device=pan.device)
+    for a in range(2):
+        for s in range(a * K, (a + 1) * K):
+            r0, r1 = pan.seg_bounds[s]
+            m[a, r0:r1] = valid[r0:r1]
+    return m
+
+
+def _schur(Garm, xc, one, Dd, W, p):
+    """Batched K = B D^-1 B' + diag(1/W, 0) from the per-arm weighted Gram [2,P,P]."""
+    Smm = Garm[:, xc][:, :, xc]
+    Sm1 = Garm[:, xc, one]
+    S11 = Garm[:, one, one]
+    A = Garm.shape[0]
+    K = torch.zeros(A, 2 * p + 1, 2 * p + 1, dtype=Garm.dtype, device=Garm.device)
+    K[:, :p, :p] = Smm
+    K[:, p:2 * p, p:2 * p] = Smm
+    K[:, :p, p:2 * p] = -Smm
+    K[:, p:2 * p, :p] = -Smm
+    K[:, :p, 2 * p] = Sm1
+    K[:, 2 * p, :p] = Sm1
+    K[:, p:2 * p, 2 * p] = -Sm1
+    K[:, 2 * p, p:2 * p] = -Sm1
+    K[:, 2 * p, 2 * p] = S11
+    K[:, :2 * p, :2 * p] += (1.0 / Dd)[:, None, None]
+    K[:, range(2 * p), range(2 * p)] += 1.0 / W
+    return K
+
+
+def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
+    """Balancing weights for every arm a (rows ``masks[a]``) toward ``target`` [p].
+    Returns gamma [ld] (each row carries its own arm's weight) and iteration counts."""
+    dev, dt = pan.device, torch.float64
+    X = pan.data if pan.data.dtype == dt else pan.data.double()
+    xc = torch.tensor(pan.xcols, device=dev)
+    one = pan.cols["one"]
+    Mt = X[pan.xcols]                                   # [p, ld]
+    p = Mt.shape[0]
+    A = masks.shape[0]
+    mf = masks.to(dt)                                   # [A, ld]
+    live = masks.any(0)
+    lf = live.to(dt)
+    nA = mf.sum(1)
+    m = target.to(dev, dt)
+    h = torch.cat([m, -m])
+    seg_arm = torch.full((pan.nseg,), -1, dtype=torch.long)
+    for a in range(A):
+        for s in range(pan.nseg):
+            r0, r1 = pan.seg_bounds[s]
+            if r1 > r0 and bool(masks[a, r0:r1].any()):
+                seg_arm[s] = a
+
+    def per_arm_T(v):            # M_a' v over each arm's rows -> [A, p]
+        return (Mt @ (mf * v).T).T
+
+    def rows_from(V):            # row i of arm a: M_i . V[a] -> [ld]
+        return ((V @ Mt) * mf).sum(0)
+
+    def arm_sum(v):
+        return (mf * v).sum(1)
+
+    def Gx(gam, delta):
+        mg = per_arm_T(gam)
+        return torch.cat([mg - delta[:, None], -mg - delta[:, None]], 1)
+
+    c_g, c_d = 2 * (1 - zeta), 2 * zeta
+    gam = lf * (mf / nA[:, None]).sum(0) + (1 - lf)    # padding rows: 1 (masked everywhere)
+    delta = (per_arm_T(gam) - m).abs().amax(1) + 1.0
+    y = torch.zeros(A, dtype=dt, device=dev)
+    s = h[None] - Gx(gam, delta)
+    z = torch.ones(A, 2 * p, dtype=dt, device=dev)
+    t = torch.ones(pan.ld, dtype=dt, device=dev)
+    ncomp = 2 * p + nA
+    done = torch.zeros(A, dtype=torch.bool, device=dev)
+    iters = np.zeros(A, dtype=int)
+
+    def solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, r_sz, r_gt):
+        v = (z * r_g - r_sz) / s                                   # [A, 2p]
+        rhs_g = lf * (-r_d_g - rows_from(v[:, :p] - v[:, p:]) - r_gt / gam)
+        rhs_d = -r_d_d + v.sum(1)
+        wts = lf / Dg
+        Gs = gram(pan, w=wts.to(pan.data.dtype))                  # [nseg, P, P]
+        Garm = torch.zeros(A, Gs.shape[1], Gs.shape[2], dtype=dt, device=dev)
+        Garm.index_add_(0, seg_arm.clamp(min=0).to(dev), Gs * (seg_arm >= 0).to(dev, dt)[:, None, None])
+        K = _schur(Garm, xc, one, Dd, W, p)
+        u_g = rhs_g / Dg
+        u_d = rhs_d / Dd
+        mg = per_arm_T(u_g)
+        rk = torch.cat([mg - u_d[:, None], -mg - u_d[:, None], (arm_sum(u_g) + r_p)[:, None]], 1)
+        L, info = torch.linalg.cholesky_ex(K)
+        sol = torch.cholesky_solve(rk[:, :, None], L)[:, :, 0]
+        uu, dy = sol[:, :2 * p], sol[:, 2 * p]
+        dxg = lf * (rhs_g - rows_from(uu[:, :p] - uu[:, p:]) - (mf * dy[:, None]).sum(0)) / Dg
+        dxd = (rhs_d + uu.sum(1)) / Dd
+        dz = uu + v
+        mdx = per_arm_T(dxg)
+        ds = -r_g - torch.cat([mdx - dxd[:, None], -mdx - dxd[:, None]], 1)
+        dtt = lf * (-r_gt - t * dxg) / gam
+        return dxg, dxd, dy, dz, ds, dtt
+
+    def step(vr, dv, vs, dvs):
+        """Per-arm max step keeping row vectors (masked) and arm vectors positive."""
+        inf = torch.full_like(vr, float("inf"))
+        rr = torch.where(dv < 0, -vr / dv, inf)
+        ra = torch.stack([torch.where(masks[a], rr, inf).amin() for a in range(A)])
+        rs = torch.where(dvs < 0, -vs / dvs, torch.full_like(vs, float("inf"))).amin(1)
+        return torch.minimum(torch.minimum(ra, rs), torch.ones_like(ra))
+
+    for it in range(1, maxit + 1):
+        r_d_g = lf * (c_g * gam + rows_from(z[:, :p] - z[:, p:]) + (mf * y[:, None]).sum(0) - t)
+        r_d_d = c_d * delta - z.sum(1)
+        r_p = arm_sum(gam) - 1.0
+        r_g = Gx(gam, delta) + s - h[None]
+        mu = ((s * z).sum(1) + arm_sum(gam * t)) / ncomp
+        scale = torch.clamp(torch.maximum(arm_sum(gam.abs()) * 0 + delta.abs(),
+                                          torch.ones_like(delta)), min=1.0)
+        rdmax = torch.stack([torch.where(masks[a], r_d_g.abs(), torch.zeros_like(r_d_g)).amax()
+                             for a in range(A)])
+        conv = (mu < tol / nA) & (r_p.abs() < tol) & (r_g.abs().amax(1) < tol * scale) \
+            & (rdmax < tol * scale) & (r_d_d.abs() < tol * scale)
+        done_h = (done | conv).cpu().numpy()
+        iters[~done_h] = it
+        done = done | conv
+        if bool(done_h.all()):
+            break
+        Dg = c_g + t / gam
+        Dd = torch.full((A,), c_d, dtype=dt, device=dev)
+        W = z / s
+        dxg, dxd, dy, dz, ds, dtt = solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, s * z, lf * gam * t)
+        a_aff = torch.minimum(step(gam, dxg, torch.cat([s, z], 1), torch.cat([ds, dz], 1)),
+                              step(t, dtt, s, ds))
+        af = (mf * a_aff[:, None]).sum(0)
+        mu_aff = (((s + a_aff[:, None] * ds) * (z + a_aff[:, None] * dz)).sum(1)
+                  + arm_sum((gam + af * dxg) * (t + af * dtt))) / ncomp
+        sigma = (mu_aff / mu) ** 3
+        sm = (mf * (sigma * mu)[:, None]).sum(0)
+        r_sz = s * z + ds * dz - (sigma * mu)[:, None]
+        r_gt = lf * (gam * t + dxg * dtt - sm)
+        dxg, dxd, dy, dz, ds, dtt = solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, r_sz, r_gt)
+        a = torch.minimum(step(gam, dxg, torch.cat([s, z], 1), torch.cat([ds, dz], 1)),
+                          step(t, dtt, s, ds))
+        a = torch.where(done, torch.zeros_like(a), torch.clamp(0.99 * a, max=1.0))
+        af = (mf * a[:, None]).sum(0)
+        gam = gam + af * dxg
+        t = t + af * dtt
+        delta = delta + a * dxd
+        y = y + a * dy
+        z = z + a[:, None] * dz
+        s = s + a[:, None] * ds
+    return gam * lf, iters
+
+
+def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 11), nfolds=10,
+                     scale_x=True, method="residual_balancing", device=None, dtype="f64"):
+    """E14 on the device; matches reference.balance.residual_balance_ate."""
+    dev = resolve_device(device)
+    Yn, Wn = as_np(Y), as_np(W)
+    Xs = scale_columns(as_np(X))[0] if scale_x else as_np(X)
+    target = torch.as_tensor(Xs.mean(0))
+    arm = (Wn == 1)
+    seg = np.empty(len(Yn), dtype=np.int64)
+    seg[arm] = rng.fold_ids(int(arm.sum()), nfolds, seed, fold_streams[0])
+    seg[~arm] = nfolds + rng.fold_ids(int((~arm).sum()), nfolds, seed, fold_streams[1])
+    pan = build_panel(Xs, None, Yn, folds=seg, dtype=dtype, device=dev)
+    G = gram(pan).clone()
+    K = nfolds
+    cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
+                          full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha)
+    masks = _arm_masks(pan, K)
+    gam, iters = ipm_balance_panel(pan, masks, target, zeta)
+    b = cv.coef_1se.to(torch.float64)                      # [2, p+1]: arm 1, arm 0
+    Xd = pan.data.double()
+    fit = b[:, :1] + b[:, 1:] @ Xd[pan.xcols]              # [2, ld]
+    resid = Xd[pan.cols["Y"]][None] - fit
+    mf = masks.double()
+    mu = b[:, 0] + b[:, 1:] @ target.to(dev, torch.float64) + (mf * gam * resid).sum(1)
+    var = (mf * gam ** 2 * resid ** 2).sum(1)
+    mu, var = mu.cpu().numpy(), var.cpu().numpy()
+    return AteResult.make(method, mu[0] - mu[1], float(np.sqrt(var.sum())), mu1=float(mu[0]),
+                          mu0=float(mu[1]), ipm_iters=tuple(int(i) for i in iters))

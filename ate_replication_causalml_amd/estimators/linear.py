@@ -53,6 +53,21 @@ def propensity_logistic(W, X, device=None, dtype="f64", return_panel_order=False
     return pan.scatter_rows(fit.mu)
 
 
+def propensity_lasso(W, X, seed=1991, nfolds=10, fold_stream=7, device=None, dtype="f64"):
+    """E7 ``prop_score_lasso`` (ate_functions.R:133-146): binomial cv.glmnet, predicted
+    response at lambda.1se (Q5); folds = Philox fold ids (stream 7) as the reference."""
+    from ..ops.lognet import cv_lognet
+    from ..parallel import rng
+    dev = resolve_device(device)
+    Wn = as_np(W)
+    fid = rng.fold_ids(len(Wn), nfolds, seed, fold_stream)
+    pan = build_panel(as_np(X), None, Wn, folds=fid, dtype=dtype, device=dev)
+    cv = cv_lognet(pan, pan.xcols, pan.cols["Y"])
+    cols = [pan.cols["one"], *pan.xcols]
+    mu = predict(pan, cols, cv.coef_1se.to(dev, torch.float64).contiguous(), link="logit")
+    return pan.scatter_rows(mu)
+
+
 def ipw(Y, W, X, p, method="Propensity_Weighting", compat="reference", device=None, dtype="f64"):
     """E3 ``prop_score_weight`` (ate_functions.R:44-63) with the full-frame projection
     design under compat="reference" (Q25; see reference.estimators.ipw_design)."""

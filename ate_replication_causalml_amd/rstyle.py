@@ -1,0 +1,120 @@
+"""R-compatible entry points: the reference's function names and calling convention
+(``dataset`` data frame + column names, returning a one-row
+``data.frame(Method, ATE, lower_ci, upper_ci)``), so driver code ports line by line.
+
+Each maps onto ``api`` (see its docstring for the name table). ``covariates``
+defaults to every column except the treatment and outcome, as the reference's
+global ``covariates`` vector (ate_replication.Rmd:57) does for its data frame.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import api
+from .config import BalanceConfig, RunConfig
+
+
+def _split(dataset, treatment_var, outcome_var, covariates=None):
+    cov = list(covariates) if covariates is not None else \
+        [c for c in dataset.columns if c not in (treatment_var, outcome_var)]
+    X = dataset[cov].to_numpy(dtype=np.float64)
+    W = dataset[treatment_var].to_numpy(dtype=np.float64)
+    Y = dataset[outcome_var].to_numpy(dtype=np.float64) if outcome_var else None
+    return Y, W, X
+
+
+def _df(r):
+    import pandas as pd
+    return pd.DataFrame([{"Method": r.method, "ATE": r.ate, "lower_ci": r.lower_ci,
+                          "upper_ci": r.upper_ci}])
+
+
+def naive_ate(dataset, treatment_var, outcome_var, method="naive", run=None):
+    Y, W, _ = _split(dataset, treatment_var, outcome_var)
+    return _df(api.ate_naive(Y, W, method=method, run=run))
+
+
+def ate_condmean_ols(dataset, treatment_var, outcome_var, method="Direct Method",
+                     covariates=None, run=None):
+    return _df(api.ate_ols(*_split(dataset, treatment_var, outcome_var, covariates), method=method,
+                           run=run))
+
+
+def prop_score_weight(dataset, p, treatment_var, outcome_var, method="Propensity_Weighting",
+                      covariates=None, run=None):
+    Y, W, X = _split(dataset, treatment_var, outcome_var, covariates)
+    return _df(api.ate_ipw(Y, W, X, np.asarray(p, dtype=np.float64), method=method, run=run))
+
+
+def prop_score_ols(dataset, p, treatment_var, outcome_var, method="Propensity_Regression",
+                   run=None):
+    Y, W, _ = _split(dataset, treatment_var, outcome_var)
+    return _df(api.ate_ipw_wls(Y, W, np.asarray(p, dtype=np.float64), method=method, run=run))
+
+
+def ate_condmean_lasso(dataset, treatment_var, outcome_var, method="Single-equation LASSO",
+                       covariates=None, run=None):
+    return _df(api.ate_lasso_single(*_split(dataset, treatment_var, outcome_var, covariates),
+                                    method=method, run=run))
+
+
+def ate_lasso(dataset, treatment_var, outcome_var, method="Usual LASSO", covariates=None,
+              run=None):
+    return _df(api.ate_lasso(*_split(dataset, treatment_var, outcome_var, covariates),
+                             method=method, run=run))
+
+
+def prop_score_lasso(dataset, treatment_var, covariates=None, run=None):
+    """Returns the (n, 1) matrix of predicted propensities (R: ``p_lasso[,1]``)."""
+    cov = list(covariates) if covariates is not None else \
+        [c for c in dataset.columns if c not in (treatment_var, "Y")]
+    X = dataset[cov].to_numpy(dtype=np.float64)
+    W = dataset[treatment_var].to_numpy(dtype=np.float64)
+    return api.propensity_lasso(W, X, run=run)[:, None]
+
+
+def doubly_robust(dataset, treatment_var, outcome_var, num_trees=100, bootstrap_se=False,
+                  method="Doubly Robust with Random Forest PS", covariates=None, run=None):
+    return _df(api.ate_aipw_rf(*_split(dataset, treatment_var, outcome_var, covariates),
+                               num_trees=num_trees, bootstrap_se=bootstrap_se, method=method,
+                               run=run))
+
+
+def doubly_robust_glm(dataset, treatment_var, outcome_var, bootstrap_se=False,
+                      method="Doubly Robust with logistic regression PS", covariates=None,
+                      run=None):
+    return _df(api.ate_aipw_glm(*_split(dataset, treatment_var, outcome_var, covariates),
+                                bootstrap_se=bootstrap_se, method=method, run=run))
+
+
+def belloni(dataset, treatment_var, outcome_var, method="Belloni et.al", covariates=None,
+            run=None):
+    return _df(api.ate_belloni(*_split(dataset, treatment_var, outcome_var, covariates),
+                               method=method, run=run))
+
+
+def double_ml(dataset, treatment_var, outcome_var, num_trees=100,
+              method="Double Machine Learning", covariates=None, run=None, **kw):
+    # the driver passes num_tree= (R partial matching, ate_replication.Rmd:232)
+    num_trees = kw.pop("num_tree", num_trees)
+    return _df(api.ate_double_ml(*_split(dataset, treatment_var, outcome_var, covariates),
+                                 num_trees=num_trees, method=method, run=run))
+
+
+def residual_balance_ATE(dataset, treatment_var, outcome_var, optimizer="quadprog",
+                         method="residual_balancing", covariates=None, run=None):
+    """``optimizer`` is accepted for compatibility; the QP is solved exactly by the IPM."""
+    return _df(api.ate_residual_balance(*_split(dataset, treatment_var, outcome_var, covariates),
+                                        BalanceConfig(), method=method, run=run))
+
+
+def causal_forest_ate(dataset, treatment_var, outcome_var, num_trees=2000, seed=12345,
+                      covariates=None, run=None):
+    return _df(api.ate_causal_forest(*_split(dataset, treatment_var, outcome_var, covariates),
+                                     num_trees=num_trees, seed=seed, run=run))
+
+
+__all__ = ["naive_ate", "ate_condmean_ols", "prop_score_weight", "prop_score_ols",
+           "ate_condmean_lasso", "ate_lasso", "prop_score_lasso", "doubly_robust",
+           "doubly_robust_glm", "belloni", "double_ml", "residual_balance_ATE",
+           "causal_forest_ate", "RunConfig"]

@@ -104,3 +104,12 @@ def test_synthetic_panel_cpu_matches_host_dgp():
     got = pan.scatter_rows(torch.stack([pan.col(f"x{j}") for j in range(25)], 1))
     assert np.allclose(got.numpy(), X)
     assert np.allclose(pan.scatter_rows(pan.col("W")).numpy(), W)
+
+
+def test_propensity_lasso_device_orchestration(tutorial):
+    from ate_replication_causalml_amd.estimators import linear as D
+    from ate_replication_causalml_amd.reference import estimators as E
+    _, m, _ = tutorial
+    a = E.propensity_lasso(m.W, m.X)
+    b = D.propensity_lasso(m.W, m.X, device="cpu").numpy()
+    np.testing.assert_allclose(b, a, atol=1e-10)
