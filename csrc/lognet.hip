@@ -7,10 +7,13 @@
 // Call site: ``prop_score_lasso`` (ate_functions.R:133-146, E7).
 //
 // Layout: ONE workgroup (4 waves) per problem (full fit or one CV fold fit).
-//   * per IRLS step, the working-weighted Gram of Z = [1, Xs] is accumulated from row
-//     chunks staged in LDS (one row per thread, standardisation fused into the load);
-//     each thread owns TPT (a, b) tasks (C_ab = sum v Z_a Z_b, or g_a = sum r Z_a) and
-//     keeps their partial sums in registers for the whole pass;
+//   * per IRLS step ONE pass over the training rows builds C = Z' diag(v) Z for
+//     Z = [1, Xs, r/v]: the Gram, the intercept cross terms and the gradient (last
+//     column: sum v z (r/v) = sum r z) in one register-blocked product. Rows are staged
+//     in LDS (one row per thread, 16 loads in flight, standardisation fused); each
+//     thread owns a 4x4 block of C for one row group, row groups are combined in a
+//     fixed order. The deviance of the current fit falls out of the same pass, and is
+//     the deviance of lambda_{m-1}'s converged fit at lambda_m's first step;
 //   * wave 0 then runs the exact glmnet coordinate sweep over that Gram: every lane
 //     evaluates its own coordinate's update speculatively; a ballot picks the next
 //     coordinate that changes, readlane broadcasts its delta, and all lanes update the
@@ -37,10 +40,13 @@ __device__ __forceinline__ double rl_d(double v, int i) {
 
 template <int PM>
 struct Cfg {
-  static constexpr int Q = PM + 1;                        // Z columns: 1, x_1..x_p
-  static constexpr int RB = PM <= 32 ? 128 : 32;          // staged rows per chunk
-  static constexpr int NTASK = Q * (Q + 1) / 2 + Q;
-  static constexpr int TPT = (NTASK + NT - 1) / NT;
+  static constexpr int Q = PM + 1;                        // Gram stride: 1, x_1..x_p
+  static constexpr int QA = PM + 2;                       // + r/v column (gradient)
+  static constexpr int NB = (QA + 3) / 4;                 // 4-wide column blocks
+  static constexpr int QP = NB * 4;                       // LDS row stride (doubles)
+  static constexpr int NPAIR = NB * (NB + 1) / 2;
+  static constexpr int TPT = (NPAIR + NT - 1) / NT;       // block pairs per thread
+  static constexpr int RB = PM <= 32 ? 256 : 64;          // staged rows per chunk
   static constexpr int NCH = (PM + 63) / 64;
 };
 
@@ -61,20 +67,19 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     double* __restrict__ a0_out, double* __restrict__ beta_out, double* __restrict__ lam_out,
     double* __restrict__ dev_out, int* __restrict__ nlam_out, int* __restrict__ npass_out) {
   using C = Cfg<PM>;
-  constexpr int Q = C::Q, RB = C::RB, TPT = C::TPT, NCH = C::NCH;
+  constexpr int Q = C::Q, QP = C::QP, RB = C::RB, TPT = C::TPT, NCH = C::NCH;
   __shared__ double sC[Q * Q];
   __shared__ double sg[Q];
-  __shared__ double sZ[RB * Q];
-  __shared__ double sVZ[RB * Q];
-  __shared__ double sR[RB];
+  __shared__ __attribute__((aligned(16))) double sZ[RB * QP];   // staged rows / reduce scratch
+  __shared__ double sV[RB];
   __shared__ double sxm[PM], sxs[PM];
   __shared__ double sb[Q];                    // sb[0] = intercept (standardised scale)
-  __shared__ int sju[PM];
+  __shared__ int sju[PM], sxc[PM];
   __shared__ int64_t sr0[MAXSEG];
   __shared__ int spre[MAXSEG + 1];
   __shared__ double red[16 * 2];
-  __shared__ double sctl[4];                  // broadcast doubles (alm, ...)
-  __shared__ int sictl[4];                    // broadcast ints (continue flags)
+  __shared__ double sctl[4];
+  __shared__ int sictl[4];
 
   const int prob = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -92,20 +97,21 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     spre[k] = acc;
     sictl[0] = k;
   }
+  for (int j = tid; j < p; j += NT) sxc[j] = xcols[j];
   __syncthreads();
   const int nts = sictl[0];
   const int ntr = spre[nts];
   const double w = 1.0 / (double)ntr;
   auto vrow = [&](int v) -> int64_t {
     int k = 0;
-    while (spre[k + 1] <= v) ++k;
+    while (k + 1 < nts && spre[k + 1] <= v) ++k;
     return sr0[k] + (v - spre[k]);
   };
   const T* Yc = X + (int64_t)ycol * ld;
 
-  // ---- standardisation (population SD with weights 1/n) and the null model
+  // ---- standardisation (population SD, weights 1/n) and the null model
   for (int j = wid; j < p; j += NT / 64) {
-    const T* xc = X + (int64_t)xcols[j] * ld;
+    const T* xc = X + (int64_t)sxc[j] * ld;
     double s1 = 0.0, s2 = 0.0;
     for (int v = lane; v < ntr; v += 64) {
       double x = ld_x(xc, vrow(v));
@@ -135,41 +141,35 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   const double dev0 = -2.0 * (q0 * log(q0c) + (1.0 - q0) * log(1.0 - q0c));
   if (tid == 0) sb[0] = log(q0 / (1.0 - q0));
 
-  // ---- task decode: task t < Q(Q+1)/2 -> (a <= b) Gram entry; else gradient of column a
-  int ta[TPT], tb[TPT];
+  // ---- Gram task layout (runtime p): column blocks of 4 over [1, z_1..z_p, r/v]
+  const int qa = p + 2, nb = (qa + 3) / 4, npair = nb * (nb + 1) / 2;
+  const int ngrp = npair >= NT ? 1 : NT / npair;
+  const int grp = ngrp == 1 ? 0 : tid / npair;
+  int pa[TPT], pb[TPT];
 #pragma unroll
   for (int q = 0; q < TPT; ++q) {
-    int t = tid + q * NT;
-    ta[q] = -1;
-    tb[q] = -1;
-    const int ng = Q * (Q + 1) / 2;
-    if (t < ng) {
+    const int t = ngrp == 1 ? tid + q * NT : (q == 0 && grp < ngrp ? tid % npair : npair);
+    pa[q] = pb[q] = -1;
+    if (t < npair) {
       int a = 0, rem = t;
-      while (rem >= Q - a) { rem -= Q - a; ++a; }
-      ta[q] = a;
-      tb[q] = a + rem;
-    } else if (t < ng + Q) {
-      ta[q] = t - ng;
-      tb[q] = -2;
+      while (rem >= nb - a) { rem -= nb - a; ++a; }
+      pa[q] = a;
+      pb[q] = a + rem;
     }
   }
+
   // ---- wave-0 coordinate state (lane l owns features l + 64c)
   double ga[NCH], aa[NCH], xva[NCH], vpa[NCH], cia[NCH];
   int jua[NCH], act[NCH];
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int j = lane + 64 * c;
     aa[c] = 0.0;
     act[c] = 0;
     vpa[c] = j < p ? vp_in[j] : 0.0;
-    jua[c] = 0;
-    ga[c] = xva[c] = cia[c] = 0.0;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int j = lane + 64 * c;
     jua[c] = j < p ? sju[j] : 0;
+    ga[c] = xva[c] = cia[c] = 0.0;
   }
 
   const bool have_ulam = ulam != nullptr;
@@ -178,93 +178,134 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   const double shr = thresh * dev0;
   double alm = 0.0, dev_prev = 0.0;
   int npass_tot = 0, nlam_eff = 0;
-  const int ldb = p;
-  double* bo = beta_out + (int64_t)prob * L * ldb;
+  double* bo = beta_out + (int64_t)prob * L * p;
 
-  // accumulate C = Z' diag(v) Z, g = Z' r at the current coefficients
-  auto accumulate = [&]() {
-    double acc[TPT];
+  // One pass over the training rows at the current coefficients:
+  //   C = Z' diag(v) Z with Z = [1, z, r/v]  ->  Gram, intercept cross terms, gradient;
+  //   deviance of the current fit (returned, valid in every thread).
+  auto accumulate = [&]() -> double {
+    double acc[TPT][16];
 #pragma unroll
-    for (int q = 0; q < TPT; ++q) acc[q] = 0.0;
+    for (int q = 0; q < TPT; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[q][e] = 0.0;
+    double devl = 0.0;
     for (int base = 0; base < ntr; base += RB) {
-      if (tid < RB) {
-        double* z = sZ + tid * Q;
-        double* vz = sVZ + tid * Q;
-        if (base + tid < ntr) {
-          const int64_t row = vrow(base + tid);
+      for (int t = tid; t < RB; t += NT) {
+        double* z = sZ + t * QP;
+        if (base + t < ntr) {
+          const int64_t row = vrow(base + t);
           double eta = sb[0];
-          z[0] = 1.0;
-          for (int j = 0; j < p; ++j) {
-            double xv = sju[j] ? (ld_x(X + (int64_t)xcols[j] * ld, row) - sxm[j]) / sxs[j] : 0.0;
-            z[1 + j] = xv;
-            eta += xv * sb[1 + j];
+          for (int jb = 0; jb < p; jb += 16) {
+            double xr[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              xr[u] = jb + u < p ? ld_x(X + (int64_t)sxc[jb + u] * ld, row) : 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int j = jb + u;
+              if (j < p) {
+                const double zv = sju[j] ? (xr[u] - sxm[j]) / sxs[j] : 0.0;
+                z[1 + j] = zv;
+                eta += zv * sb[1 + j];
+              }
+            }
           }
           const double q = clampq(eta);
           const double vv = w * q * (1.0 - q);
-          sR[tid] = w * (ld_x(Yc, row) - q);
-          for (int j = 0; j <= p; ++j) vz[j] = vv * z[j];
+          const double y = ld_x(Yc, row);
+          z[0] = 1.0;
+          z[p + 1] = (w * (y - q)) / vv;
+          for (int j = p + 2; j < QP; ++j) z[j] = 0.0;
+          sV[t] = vv;
+          devl += y * log(q) + (1.0 - y) * log(1.0 - q);
         } else {
-          for (int j = 0; j <= p; ++j) z[j] = vz[j] = 0.0;
-          sR[tid] = 0.0;
+          for (int j = 0; j < QP; ++j) z[j] = 0.0;
+          sV[t] = 0.0;
         }
       }
       __syncthreads();
-      for (int r = 0; r < RB; ++r) {
+      const int nr = min(RB, ntr - base);
+      for (int r = grp; r < nr; r += ngrp) {
+        const double v = sV[r];
+        const double* zr = sZ + r * QP;
 #pragma unroll
         for (int q = 0; q < TPT; ++q) {
-          if (ta[q] >= 0 && ta[q] <= p) {
-            if (tb[q] >= 0) {
-              if (tb[q] <= p) acc[q] += sVZ[r * Q + ta[q]] * sZ[r * Q + tb[q]];
-            } else {
-              acc[q] += sR[r] * sZ[r * Q + ta[q]];
-            }
+          if (pa[q] >= 0) {
+            const double4 za = *reinterpret_cast<const double4*>(zr + 4 * pa[q]);
+            const double4 zb = *reinterpret_cast<const double4*>(zr + 4 * pb[q]);
+            const double va[4] = {v * za.x, v * za.y, v * za.z, v * za.w};
+            const double vb[4] = {zb.x, zb.y, zb.z, zb.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[q][i * 4 + j] += va[i] * vb[j];
           }
         }
       }
       __syncthreads();
     }
+    // combine row groups (fixed order) and scatter into sC / sg
+    auto emit = [&](int pair, int e, double val) {
+      int A = 0, rem = pair;
+      while (rem >= nb - A) { rem -= nb - A; ++A; }
+      const int B = A + rem;
+      const int a = 4 * A + (e >> 2), b = 4 * B + (e & 3);
+      // a <= b only: inside a diagonal block (a,b) and (b,a) round differently
+      if (a > b || b > p + 1) return;
+      if (b <= p) {
+        sC[a * Q + b] = val;
+        sC[b * Q + a] = val;
+      } else if (a <= p) {
+        sg[a] = val;
+      }
+    };
+    if (ngrp == 1) {
 #pragma unroll
-    for (int q = 0; q < TPT; ++q) {
-      if (ta[q] >= 0 && ta[q] <= p) {
-        if (tb[q] >= 0) {
-          if (tb[q] <= p) {
-            sC[ta[q] * Q + tb[q]] = acc[q];
-            sC[tb[q] * Q + ta[q]] = acc[q];
-          }
-        } else {
-          sg[ta[q]] = acc[q];
+      for (int q = 0; q < TPT; ++q)
+        if (pa[q] >= 0) {
+          const int pair = tid + q * NT;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) emit(pair, e, acc[q][e]);
         }
+    } else {
+      if (grp < ngrp && pa[0] >= 0)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sZ[(grp * npair + tid % npair) * 16 + e] = acc[0][e];
+      __syncthreads();
+      for (int t = tid; t < npair * 16; t += NT) {
+        double sum = 0.0;
+        for (int gq = 0; gq < ngrp; ++gq) sum += sZ[(gq * npair) * 16 + t];
+        emit(t >> 4, t & 15, sum);
       }
     }
+    double dv[1] = {devl};
+    ate::block_sum<1>(dv, red);
+    if (tid == 0) sctl[2] = -2.0 * w * dv[0];
     __syncthreads();
+    return sctl[2];
   };
 
-  auto deviance = [&]() -> double {
-    double acc[1] = {0.0};
-    for (int v = tid; v < ntr; v += NT) {
-      const int64_t row = vrow(v);
-      double eta = sb[0];
-      for (int j = 0; j < p; ++j)
-        if (sb[1 + j] != 0.0)
-          eta += (ld_x(X + (int64_t)xcols[j] * ld, row) - sxm[j]) / sxs[j] * sb[1 + j];
-      const double q = clampq(eta);
-      const double y = ld_x(Yc, row);
-      acc[0] += y * log(q) + (1.0 - y) * log(1.0 - q);
-    }
-    ate::block_sum<1>(acc, red);
-    return -2.0 * w * acc[0];   // valid in thread 0
-  };
-
-  for (int m = 0; m < nlam; ++m) {
-    int kind = have_ulam ? 0 : (m == 0 ? 1 : (m == 1 ? 2 : 3));
+  bool stopped = false;
+  for (int m = 0; m < nlam && !stopped; ++m) {
+    const int kind = have_ulam ? 0 : (m == 0 ? 1 : (m == 1 ? 2 : 3));
     if (kind == 0) alm = ulam[m];
     else if (kind == 1) alm = BIG;
     else if (kind == 3) alm *= alf;
     for (int outer = 0; outer < 1000; ++outer) {
-      accumulate();
+      const double dev_cur = accumulate();
+      if (outer == 0 && m > 0) {
+        // deviance at the converged fit of lambda_{m-1}; glmnet's early path stop
+        const double dr = 1.0 - dev_cur / dev0;
+        if (tid == 0) dev_out[(int64_t)prob * L + m - 1] = dr;
+        if (!have_ulam && m - 1 >= MNLAM - 1 && (dr - dev_prev < FDEV * dr || dr > DEVMAX)) {
+          stopped = true;
+          break;
+        }
+        dev_prev = dr;
+      }
       int stop = 0;
       if (wid == 0) {
-        // load the working gradient / Gram diagonal for this IRLS step
         double gint = sg[0];
         const double xmz = sC[0];
 #pragma unroll
@@ -331,12 +372,10 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
         while (npass < mleft) {
           ++npass;
           if (one_pass(true) < shr) break;
-          bool conv = false;
           while (npass < mleft) {
             ++npass;
-            if (one_pass(false) < shr) { conv = true; break; }
+            if (one_pass(false) < shr) break;
           }
-          (void)conv;
         }
         npass_tot += npass;
         const double b0n = b0s + b0d;
@@ -362,31 +401,26 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
       __syncthreads();
       if (stop) break;
     }
-    const double dev = deviance();
+    if (stopped) break;
     if (tid == 0) {
-      const double dr = 1.0 - dev / dev0;
       a0_out[(int64_t)prob * L + m] = sb[0];
       lam_out[(int64_t)prob * L + m] = alm;
-      dev_out[(int64_t)prob * L + m] = dr;
-      int brk = 0;
-      if (!have_ulam && m >= MNLAM - 1 && m > 0)
-        if (dr - dev_prev < FDEV * dr || dr > DEVMAX) brk = 1;
-      dev_prev = dr;
-      sictl[2] = brk;
     }
-    for (int j = tid; j < p; j += NT) bo[(int64_t)m * ldb + j] = sb[1 + j];
-    __syncthreads();
+    for (int j = tid; j < p; j += NT) bo[(int64_t)m * p + j] = sb[1 + j];
     nlam_eff = m + 1;
-    if (sictl[2]) break;
     __syncthreads();
+  }
+  if (!stopped) {
+    const double dev_cur = accumulate();
+    if (tid == 0) dev_out[(int64_t)prob * L + nlam_eff - 1] = 1.0 - dev_cur / dev0;
   }
   __syncthreads();
   // ---- back to the original scale; lambda_0 extrapolated as glmnet does
   for (int m = 0; m < nlam_eff; ++m) {
     double part[1] = {0.0};
     for (int j = tid; j < p; j += NT) {
-      double bj = sju[j] ? bo[(int64_t)m * ldb + j] / sxs[j] : 0.0;
-      bo[(int64_t)m * ldb + j] = bj;
+      double bj = sju[j] ? bo[(int64_t)m * p + j] / sxs[j] : 0.0;
+      bo[(int64_t)m * p + j] = bj;
       part[0] += bj * sxm[j];
     }
     ate::block_sum<1>(part, red);
