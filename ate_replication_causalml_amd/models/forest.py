@@ -115,6 +115,7 @@ class Forest:
     edges: np.ndarray
     nedges: np.ndarray
     Xb_train: object = None
+    packed: object = None        # GPU: int2 per node (see csrc/forest.hip forest_pack_kernel)
 
     @property
     def device(self):
@@ -134,12 +135,26 @@ class Forest:
             raise ValueError("OOB prediction requires the training rows")
         width = 4 if self.params.kind == KIND_CAUSAL else 1
         if self.backend == "gpu":
-            out = torch.empty(n2 * width, dtype=torch.float64, device=self.device)
+            dev = self.device
+            s = torch.cuda.current_stream().cuda_stream
+            if self.packed is None:
+                self.packed = torch.zeros(self.params.ntree * self.cap * 2, dtype=torch.int32,
+                                          device=dev)
+                _native.call("ate_forest_pack", ctypes.addressof(self.params), self.cap,
+                             self.feat.data_ptr(), self.thr.data_ptr(), self.left.data_ptr(),
+                             self.nnodes.data_ptr(),
+                             0 if self.est is None else self.est.data_ptr(),
+                             self.packed.data_ptr(), s)
+            g = max(1, self.params.group) if self.params.kind == KIND_CAUSAL else 1
+            # leaf-index scratch capped at ~1 GiB: trees per chunk, a multiple of the group
+            tchunk = max(g, min(self.params.ntree, (1 << 28) // max(n2, 1)) // g * g)
+            leaves = torch.empty(tchunk * n2, dtype=torch.int32, device=dev)
+            state = torch.zeros(10 * n2, dtype=torch.float64, device=dev)
+            out = torch.empty(n2 * width, dtype=torch.float64, device=dev)
             _native.call("ate_forest_predict", ctypes.addressof(self.params), Xb.data_ptr(), n2,
-                         int(oob), self.cap, self.feat.data_ptr(), self.thr.data_ptr(),
-                         self.left.data_ptr(), self.val.data_ptr(), self.inbag.data_ptr(),
-                         0 if self.est is None else self.est.data_ptr(), out.data_ptr(),
-                         torch.cuda.current_stream().cuda_stream)
+                         int(oob), self.cap, self.packed.data_ptr(), self.val.data_ptr(),
+                         self.inbag.data_ptr(), 0 if self.est is None else self.est.data_ptr(),
+                         leaves.data_ptr(), tchunk, state.data_ptr(), out.data_ptr(), s)
             res = out.cpu().numpy()
         else:
             res = np.empty(n2 * width)

@@ -462,34 +462,57 @@ ATE_API int ate_enet_coef(const void* apath, const void* probs, int nprob, int p
 // ------------------------------------------------------------------ K09 CV loss from held-out Gram
 // For fold problem q (trained without segment hold[q]) and every lambda m:
 // cvraw[q][m] = SSE / n_hold using the raw held-out Gram G[hold] (panel columns).
-__global__ void enet_cvloss_gauss_kernel(const double* __restrict__ G, int P, const int* __restrict__ hold,
-                                         const int* __restrict__ xcols, int p, int ones_col,
-                                         const int* __restrict__ ycol_of_prob,
-                                         const double* __restrict__ coef, const int* __restrict__ nlam_out,
-                                         int L, double* __restrict__ cvraw) {
+// The nonzero coefficients are compacted first (ordered ballot scan), so the quadratic
+// form costs nnz^2 instead of p^2 — LASSO paths are sparse over most lambdas.
+__global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
+    const double* __restrict__ G, int P, const int* __restrict__ hold,
+    const int* __restrict__ xcols, int p, int ones_col, const int* __restrict__ ycol_of_prob,
+    const double* __restrict__ coef, const int* __restrict__ nlam_out, int L,
+    double* __restrict__ cvraw) {
   const int q = blockIdx.y, m = blockIdx.x;
   if (m >= nlam_out[q]) { if (threadIdx.x == 0) cvraw[(int64_t)q * L + m] = NAN; return; }
   const double* Gh = G + (int64_t)hold[q] * P * P;
   const double* cf = coef + ((int64_t)q * L + m) * (p + 1);
   const int yc = ycol_of_prob[q];
   const double a0 = cf[0];
+  __shared__ int sc[PMAX];        // panel column of the i-th nonzero
+  __shared__ double sb[PMAX];
+  __shared__ int wcnt[4];
+  __shared__ int snnz;
   __shared__ double smem[16 * 3];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) snnz = 0;
+  __syncthreads();
+  for (int base = 0; base < p; base += 256) {
+    const int j = base + tid;
+    const double bj = j < p ? cf[1 + j] : 0.0;
+    const bool nz = bj != 0.0;
+    const uint64_t bal = __ballot(nz);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[wid] = __popcll(bal);
+    __syncthreads();
+    int off = snnz;
+    for (int w = 0; w < wid; ++w) off += wcnt[w];
+    if (nz) { sc[off + pre] = xcols[j]; sb[off + pre] = bj; }
+    __syncthreads();
+    if (tid == 0) snnz += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+  }
+  const int nnz = snnz;
   // quad = b' Gxx b, lin = b' (Gxy - a0 Sx)
   double v[3] = {0.0, 0.0, 0.0};
-  for (int64_t e = threadIdx.x; e < (int64_t)p * p; e += blockDim.x) {
-    int j = (int)(e / p), k = (int)(e % p);
-    double bj = cf[1 + j], bk = cf[1 + k];
-    if (bj != 0.0 && bk != 0.0) v[0] += bj * bk * Gh[(int64_t)xcols[j] * P + xcols[k]];
+  for (int a = wid; a < nnz; a += 4) {
+    const double* Gr = Gh + (int64_t)sc[a] * P;
+    double r = 0.0;
+    for (int b = lane; b < nnz; b += 64) r += sb[b] * Gr[sc[b]];
+    v[0] += sb[a] * r;
   }
-  for (int j = threadIdx.x; j < p; j += blockDim.x) {
-    double bj = cf[1 + j];
-    if (bj != 0.0) {
-      v[1] += bj * Gh[(int64_t)xcols[j] * P + yc];
-      v[2] += bj * Gh[(int64_t)xcols[j] * P + ones_col];
-    }
+  for (int a = tid; a < nnz; a += 256) {
+    v[1] += sb[a] * Gh[(int64_t)sc[a] * P + yc];
+    v[2] += sb[a] * Gh[(int64_t)sc[a] * P + ones_col];
   }
   block_sum<3>(v, smem);
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     double n = Gh[(int64_t)ones_col * P + ones_col];
     double yy = Gh[(int64_t)yc * P + yc], sy = Gh[(int64_t)ones_col * P + yc];
     double sse = yy - 2.0 * a0 * sy - 2.0 * v[1] + n * a0 * a0 + 2.0 * a0 * v[2] + v[0];

@@ -445,82 +445,156 @@ ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, co
 // ------------------------------------------------------------ K15 prediction
 // One thread per row, all trees (tree arrays are L2-resident). Same formulas and
 // summation order as the CPU twin (atecpu_forest_predict).
-__device__ __forceinline__ int64_t leaf_of(const ForestParams& fp, const uint8_t* Xb, int n2,
-                                           int i, int t, int oob, int cap, const int32_t* feat,
-                                           const int32_t* thr, const int32_t* left,
-                                           const uint8_t* inbag, const int64_t* est) {
-  if (oob && inbag[(int64_t)t * fp.n + i]) return -1;
-  const int64_t base = (int64_t)t * cap;
-  int v = 0, last_ok = 0;
-  while (true) {
-    if (fp.sampling == 1 && est && est[(base + v) * 5] > 0) last_ok = v;
-    const int f = feat[base + v];
-    if (f < 0) break;
-    v = Xb[(int64_t)f * n2 + i] <= thr[base + v] ? left[base + v] : left[base + v] + 1;
+// ---------------------------------------------------------------- K15/K17 prediction
+// Node packing: one 8-byte load per tree level. code = (feat+1) << 9 | estok << 8 | thr,
+// code >> 9 == 0 marks a leaf; estok = honest estimation count of the node > 0.
+__global__ __launch_bounds__(256) void forest_pack_kernel(ForestParams fp, int cap,
+                                                          const int32_t* __restrict__ feat,
+                                                          const int32_t* __restrict__ thr,
+                                                          const int32_t* __restrict__ left,
+                                                          const int32_t* __restrict__ nnodes,
+                                                          const int64_t* __restrict__ est,
+                                                          int2* __restrict__ packed) {
+  const int64_t total = (int64_t)fp.ntree * cap;
+  for (int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x; k < total;
+       k += (int64_t)gridDim.x * 256) {
+    const int t = (int)(k / cap), v = (int)(k % cap);
+    if (v >= nnodes[t]) continue;
+    const int f = feat[k];
+    const int estok = (fp.sampling == 1 && est) ? (est[k * 5] > 0) : 1;
+    const int code = f < 0 ? (estok << 8) : (((f + 1) << 9) | (estok << 8) | (thr[k] & 255));
+    packed[k] = make_int2(f < 0 ? 0 : left[k], code);
   }
-  return base + ((fp.sampling == 1 && est) ? last_ok : v);
 }
 
-__global__ __launch_bounds__(256) void forest_predict_kernel(
-    ForestParams fp, const uint8_t* __restrict__ Xb, int n2, int oob, int cap,
-    const int32_t* __restrict__ feat, const int32_t* __restrict__ thr,
-    const int32_t* __restrict__ left, const double* __restrict__ val,
-    const uint8_t* __restrict__ inbag, const int64_t* __restrict__ est, double* __restrict__ out) {
+// leaves[tt][i] = leaf (node id within tree t0+tt) reached by row i, -1 if excluded (OOB)
+__global__ __launch_bounds__(256) void forest_leaf_kernel(ForestParams fp,
+                                                          const uint8_t* __restrict__ Xb, int n2,
+                                                          int oob, int cap, int t0,
+                                                          const int2* __restrict__ packed,
+                                                          const uint8_t* __restrict__ inbag,
+                                                          int32_t* __restrict__ leaves) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int t = t0 + blockIdx.y;
+  if (i >= n2) return;
+  int32_t* out = leaves + (int64_t)blockIdx.y * n2 + i;
+  if (oob && inbag[(int64_t)t * fp.n + i]) { *out = -1; return; }
+  const int2* tree = packed + (int64_t)t * cap;
+  const bool honest = fp.sampling == 1;
+  int v = 0, last_ok = 0;
+  while (true) {
+    const int2 nd = tree[v];
+    if (honest && ((nd.y >> 8) & 1)) last_ok = v;
+    const int f1 = nd.y >> 9;
+    if (f1 == 0) break;
+    v = Xb[(int64_t)(f1 - 1) * n2 + i] <= (nd.y & 255) ? nd.x : nd.x + 1;
+  }
+  *out = honest ? last_ok : v;
+}
+
+// kind 0/1: running (sum, count) per row over trees in ascending order
+__global__ __launch_bounds__(256) void forest_vote_kernel(ForestParams fp, int n2, int cap, int t0,
+                                                          int nt, const int32_t* __restrict__ leaves,
+                                                          const double* __restrict__ val,
+                                                          const int64_t* __restrict__ est,
+                                                          double* __restrict__ state) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n2) return;
-  if (fp.kind != 2) {
-    double acc = 0;
-    int used = 0;
-    for (int t = 0; t < fp.ntree; ++t) {
-      const int64_t nd = leaf_of(fp, Xb, n2, i, t, oob, cap, feat, thr, left, inbag, est);
-      if (nd < 0) continue;
-      ++used;
-      if (fp.kind == 0 || fp.sampling == 0) acc += val[nd];
-      else acc += from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
-    }
-    out[i] = used > 0 ? acc / used : NAN;
-    return;
+  double acc = state[i], used = state[n2 + i];
+  const bool leafmean = fp.kind == 0 || fp.sampling == 0;
+#pragma unroll 4
+  for (int tt = 0; tt < nt; ++tt) {
+    const int lf = leaves[(int64_t)tt * n2 + i];
+    if (lf < 0) continue;
+    const int64_t nd = (int64_t)(t0 + tt) * cap + lf;
+    used += 1.0;
+    acc += leafmean ? val[nd] : from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
   }
-  double a1 = 0, aw = 0, ay = 0, aww = 0, awy = 0;
-  for (int t = 0; t < fp.ntree; ++t) {
-    const int64_t nd = leaf_of(fp, Xb, n2, i, t, oob, cap, feat, thr, left, inbag, est);
-    if (nd < 0) continue;
-    const int64_t* e = est + nd * 5;
+  state[i] = acc;
+  state[n2 + i] = used;
+}
+
+// kind 2, pass 1: forest-weighted leaf moments (1, W, Y, WW, WY)
+__global__ __launch_bounds__(256) void forest_cate1_kernel(int n2, int cap, int t0, int nt,
+                                                           const int32_t* __restrict__ leaves,
+                                                           const int64_t* __restrict__ est,
+                                                           double* __restrict__ st) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n2) return;
+  double a1 = st[i], aw = st[n2 + i], ay = st[2 * n2 + i], aww = st[3 * n2 + i],
+         awy = st[4 * n2 + i];
+  for (int tt = 0; tt < nt; ++tt) {
+    const int lf = leaves[(int64_t)tt * n2 + i];
+    if (lf < 0) continue;
+    const int64_t* e = est + ((int64_t)(t0 + tt) * cap + lf) * 5;
     const double c = (double)e[0];
     a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
     aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
   }
+  st[i] = a1; st[n2 + i] = aw; st[2 * n2 + i] = ay; st[3 * n2 + i] = aww; st[4 * n2 + i] = awy;
+}
+
+// kind 2, pass 2: little-bag groups of the linearised score psi at the full-forest tau
+// (chunks hold whole groups). st[5..9]: gs, gss, within, nwithin, ng.
+__global__ __launch_bounds__(256) void forest_cate2_kernel(ForestParams fp, int n2, int cap, int t0,
+                                                           int nt, const int32_t* __restrict__ leaves,
+                                                           const int64_t* __restrict__ est,
+                                                           double* __restrict__ st) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n2) return;
+  const double a1 = st[i];
+  if (!(a1 > 0)) return;
+  const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
+  const double H = st[3 * n2 + i] / a1 - wb * wb;
+  if (!(H > 0)) return;
+  const double tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
+  double gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
+  double nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
+  for (int g0 = 0; g0 < nt; g0 += fp.group) {
+    double ps = 0, pss = 0;
+    int nb = 0;
+    for (int tt = g0; tt < g0 + fp.group && tt < nt; ++tt) {
+      const int lf = leaves[(int64_t)tt * n2 + i];
+      if (lf < 0) continue;
+      const int64_t* e = est + ((int64_t)(t0 + tt) * cap + lf) * 5;
+      const double c = (double)e[0];
+      const double w_ = from_fix(e[1]) / c, y_ = from_fix(e[2]) / c;
+      const double ww = from_fix(e[3]) / c, wy = from_fix(e[4]) / c;
+      const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
+      ps += psi; pss += psi * psi; ++nb;
+    }
+    if (nb == 0) continue;
+    const double pg = ps / nb;
+    gs += pg; gss += pg * pg; ng += 1.0;
+    if (nb >= 2) { within += pss / nb - pg * pg; nwithin += 1.0; }
+  }
+  st[5 * n2 + i] = gs; st[6 * n2 + i] = gss; st[7 * n2 + i] = within;
+  st[8 * n2 + i] = nwithin; st[9 * n2 + i] = ng;
+}
+
+__global__ __launch_bounds__(256) void forest_final_kernel(ForestParams fp, int n2,
+                                                           const double* __restrict__ st,
+                                                           double* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n2) return;
+  if (fp.kind != 2) {
+    out[i] = st[n2 + i] > 0 ? st[i] / st[n2 + i] : NAN;
+    return;
+  }
+  const double a1 = st[i];
   double tau = NAN, var = NAN;
-  int ng = 0;
+  const double ng = st[9 * n2 + i];
   if (a1 > 0) {
-    const double wb = aw / a1, yb = ay / a1;
-    const double H = aww / a1 - wb * wb;
+    const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
+    const double H = st[3 * n2 + i] / a1 - wb * wb;
     if (H > 0) {
-      tau = (awy / a1 - wb * yb) / H;
-      double gs = 0, gss = 0, within = 0;
-      int nwithin = 0;
-      for (int g0 = 0; g0 < fp.ntree; g0 += fp.group) {
-        double ps = 0, pss = 0;
-        int nb = 0;
-        for (int t = g0; t < g0 + fp.group && t < fp.ntree; ++t) {
-          const int64_t nd = leaf_of(fp, Xb, n2, i, t, oob, cap, feat, thr, left, inbag, est);
-          if (nd < 0) continue;
-          const int64_t* e = est + nd * 5;
-          const double c = (double)e[0];
-          const double w_ = from_fix(e[1]) / c, y_ = from_fix(e[2]) / c;
-          const double ww = from_fix(e[3]) / c, wy = from_fix(e[4]) / c;
-          const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
-          ps += psi; pss += psi * psi; ++nb;
-        }
-        if (nb == 0) continue;
-        const double pg = ps / nb;
-        gs += pg; gss += pg * pg; ++ng;
-        if (nb >= 2) { within += pss / nb - pg * pg; ++nwithin; }
-      }
+      tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
       if (ng >= 2) {
-        const double mean = gs / ng;
-        const double between = gss / ng - mean * mean;
-        const double wc = nwithin > 0 ? within / nwithin / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
+        const double mean = st[5 * n2 + i] / ng;
+        const double between = st[6 * n2 + i] / ng - mean * mean;
+        const double nw = st[8 * n2 + i];
+        const double wc = nw > 0 ? st[7 * n2 + i] / nw / (double)(fp.group > 1 ? fp.group - 1 : 1)
+                                 : 0.0;
         var = fmax(between - wc, 0.0) / (H * H);
       }
     }
@@ -531,16 +605,50 @@ __global__ __launch_bounds__(256) void forest_predict_kernel(
   out[4 * i + 3] = ng;
 }
 
+ATE_API int ate_forest_pack(const void* fpp, int cap, const void* feat, const void* thr,
+                            const void* left, const void* nnodes, const void* est, void* packed,
+                            void* stream) {
+  const ForestParams fp = *(const ForestParams*)fpp;
+  hipLaunchKernelGGL(forest_pack_kernel, dim3(ate::grid_for((int64_t)fp.ntree * cap, 256, 4096)),
+                     dim3(256), 0, (hipStream_t)stream, fp, cap, (const int32_t*)feat,
+                     (const int32_t*)thr, (const int32_t*)left, (const int32_t*)nnodes,
+                     (const int64_t*)est, (int2*)packed);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// state: zeroed [10][n2] fp64 scratch; leaves: [tchunk][n2] int32 scratch, tchunk a
+// multiple of the little-bag group size. Trees are visited in ascending order, so the
+// sums match the host engine's sequential loop.
 ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob, int cap,
-                               const void* feat, const void* thr, const void* left,
-                               const void* val, const void* inbag, const void* est, void* out,
+                               const void* packed, const void* val, const void* inbag,
+                               const void* est, void* leaves, int tchunk, void* state, void* out,
                                void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
-  hipLaunchKernelGGL(forest_predict_kernel, dim3((n2 + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, fp, (const uint8_t*)Xb, n2, oob, cap,
-                     (const int32_t*)feat, (const int32_t*)thr, (const int32_t*)left,
-                     (const double*)val, (const uint8_t*)inbag, (const int64_t*)est,
-                     (double*)out);
+  hipStream_t st = (hipStream_t)stream;
+  if (tchunk < 1 || (fp.kind == 2 && tchunk % fp.group)) return -1;
+  const int rb = (n2 + 255) / 256;
+  const int passes = fp.kind == 2 ? 2 : 1;
+  for (int pass = 0; pass < passes; ++pass) {
+    for (int t0 = 0; t0 < fp.ntree; t0 += tchunk) {
+      const int nt = min(tchunk, fp.ntree - t0);
+      hipLaunchKernelGGL(forest_leaf_kernel, dim3(rb, nt), dim3(256), 0, st, fp,
+                         (const uint8_t*)Xb, n2, oob, cap, t0, (const int2*)packed,
+                         (const uint8_t*)inbag, (int32_t*)leaves);
+      if (fp.kind != 2)
+        hipLaunchKernelGGL(forest_vote_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
+                           (const int32_t*)leaves, (const double*)val, (const int64_t*)est,
+                           (double*)state);
+      else if (pass == 0)
+        hipLaunchKernelGGL(forest_cate1_kernel, dim3(rb), dim3(256), 0, st, n2, cap, t0, nt,
+                           (const int32_t*)leaves, (const int64_t*)est, (double*)state);
+      else
+        hipLaunchKernelGGL(forest_cate2_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
+                           (const int32_t*)leaves, (const int64_t*)est, (double*)state);
+    }
+  }
+  hipLaunchKernelGGL(forest_final_kernel, dim3(rb), dim3(256), 0, st, fp, n2,
+                     (const double*)state, (double*)out);
   ATE_CHECK_LAUNCH();
   return 0;
 }
