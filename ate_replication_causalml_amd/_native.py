@@ -59,6 +59,8 @@ _SIGS = {
     "ate_forest_pack": "pippppppp",
     "ate_forest_scratch_bytes": "ii",
     "ate_bin_matrix": "plipppp",
+    "ate_panel_xtv": "iplpipplipp",
+    "ate_panel_xv": "iplpipiplpp",
 }
 _RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}

@@ -18,6 +18,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..ops import gemv
 from ..ops.enet import cv_enet_gaussian
 from ..ops.gram import gram
 from ..ops.panel import build_panel
@@ -62,11 +63,9 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
     """Balancing weights for every arm a (rows ``masks[a]``) toward ``target`` [p].
     Returns gamma [ld] (each row carries its own arm's weight) and iteration counts."""
     dev, dt = pan.device, torch.float64
-    X = pan.data if pan.data.dtype == dt else pan.data.double()
     xc = torch.tensor(pan.xcols, device=dev)
     one = pan.cols["one"]
-    Mt = X[pan.xcols]                                   # [p, ld]
-    p = Mt.shape[0]
+    p = len(pan.xcols)
     A = masks.shape[0]
     mf = masks.to(dt)                                   # [A, ld]
     live = masks.any(0)
@@ -81,11 +80,15 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
             if r1 > r0 and bool(masks[a, r0:r1].any()):
                 seg_arm[s] = a
 
+    grp = torch.full((pan.ld,), -1, dtype=torch.int8, device=dev)
+    for a in range(A):
+        grp[masks[a]] = a
+
     def per_arm_T(v):            # M_a' v over each arm's rows -> [A, p]
-        return (Mt @ (mf * v).T).T
+        return gemv.xtv(pan, pan.xcols, v, grp, A)
 
     def rows_from(V):            # row i of arm a: M_i . V[a] -> [ld]
-        return ((V @ Mt) * mf).sum(0)
+        return gemv.xv(pan, pan.xcols, V, grp)
 
     def arm_sum(v):
         return (mf * v).sum(1)
