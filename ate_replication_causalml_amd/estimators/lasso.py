@@ -22,30 +22,43 @@ from ..result import AteResult
 from .common import as_np, read_result, resolve_device
 
 
-def _lasso_w_coef(Y, W, X, pf_w, seed, nfolds, fold_stream, device, dtype):
+def _fold_ids(n, K, seed, stream, dist):
+    return dist.fold_ids(K, seed, stream) if dist is not None else rng.fold_ids(n, K, seed, stream)
+
+
+def _sharded_gram(pan, dist):
+    """Per-segment Gram stack, all-reduced over row shards; + global segment counts."""
+    G = gram(pan)
+    if dist is None:
+        return G, None
+    dist.sum_(G)
+    return G, global_seg_counts(pan, dist.comm)
+
+
+def _lasso_w_coef(Y, W, X, pf_w, seed, nfolds, fold_stream, device, dtype, dist=None):
     dev = resolve_device(device)
     Xn = np.column_stack([as_np(X), as_np(W)])
     n, pp = Xn.shape
-    fid = rng.fold_ids(n, nfolds, seed, fold_stream)
+    fid = _fold_ids(n, nfolds, seed, fold_stream, dist)
     pan = build_panel(Xn, None, as_np(Y), folds=fid, dtype=dtype, device=dev)
-    G = gram(pan)
+    G, counts = _sharded_gram(pan, dist)
     pf = np.r_[np.ones(pp - 1), pf_w]
-    cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf)
+    cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf, seg_counts=counts)
     return cv
 
 
 def lasso_single(Y, W, X, seed=1991, nfolds=10, fold_stream=5, method="Single-equation LASSO",
-                 device=None, dtype="f64"):
+                 device=None, dtype="f64", dist=None):
     """E5 ``ate_condmean_lasso`` (ate_functions.R:89-108): W unpenalised, coef at lambda.1se."""
-    cv = _lasso_w_coef(Y, W, X, 0.0, seed, nfolds, fold_stream, device, dtype)
+    cv = _lasso_w_coef(Y, W, X, 0.0, seed, nfolds, fold_stream, device, dtype, dist)
     return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
                           lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
 
 
 def lasso_usual(Y, W, X, seed=1991, nfolds=10, fold_stream=6, method="Usual LASSO", device=None,
-                dtype="f64"):
+                dtype="f64", dist=None):
     """E6 ``ate_lasso`` (ate_functions.R:111-130): W penalised."""
-    cv = _lasso_w_coef(Y, W, X, 1.0, seed, nfolds, fold_stream, device, dtype)
+    cv = _lasso_w_coef(Y, W, X, 1.0, seed, nfolds, fold_stream, device, dtype, dist)
     return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
                           lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
 
@@ -57,7 +70,7 @@ def interaction_expand(x: torch.Tensor) -> torch.Tensor:
 
 
 def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni et.al",
-            device=None, dtype="f64"):
+            device=None, dtype="f64", dist=None):
     """E11 ``belloni`` (ate_functions.R:286-328) with quirks Q10-Q13."""
     dev = resolve_device(device)
     Yn, Wn = as_np(Y), as_np(W)
@@ -65,10 +78,11 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
     n, q = xint.shape
     fits = []
     for target, stream in ((Wn, 8), (Yn, 9)):
-        fid = rng.fold_ids(n, nfolds, seed, stream)
+        fid = _fold_ids(n, nfolds, seed, stream, dist)
         pan = build_panel(xint, None, target, folds=fid, dtype=dtype, device=dev)
-        G = gram(pan)
-        fits.append((pan, G, cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]])))
+        G, counts = _sharded_gram(pan, dist)
+        fits.append((pan, G, cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
+                                              seg_counts=counts)))
     (_, _, cw), (_, _, cy) = fits
     s = float(cw.lambdas[0, int(cw.sel[0, 0])])
     lw = cw.lambdas[0, :int(cw.nlam[0])].cpu().numpy()
@@ -93,27 +107,45 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
     # post-selection OLS: y ~ 1 + x_int[:, cols] + W
     pan = build_panel(np.column_stack([xint[:, cols], Wn]), None, Yn, dtype=dtype, device=dev)
     G = gram(pan)[0]
+    if dist is not None:
+        dist.sum_(G)
     dcols = [pan.cols["one"], *pan.xcols]
     r = chol_solve(G, dcols, pan.cols["Y"])
-    se = torch.sqrt(r.aux[1] / (pan.n - r.aux[0]) * r.invdiag[-1])
+    n_all = dist.n_total if dist is not None else pan.n
+    se = torch.sqrt(r.aux[1] / (n_all - r.aux[0]) * r.invdiag[-1])
     return read_result(torch.stack([r.beta[-1], se]), method, n_selected=len(cols),
                        rank=int(r.aux[0]))
 
 
 # ---------------------------------------------------------------- K-fold DML (PLR)
-def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None):
+def global_seg_counts(pan, comm):
+    """Rows per segment summed over ranks (host ints; one tiny all-reduce)."""
+    c = torch.as_tensor(np.asarray(pan.seg_nreal, dtype=np.float64))
+    if comm is not None and comm.world_size > 1:
+        dev = pan.device
+        t = c.to(dev)
+        comm.all_reduce_(t)
+        c = t.cpu()
+    return c.numpy()
+
+
+def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, seg_counts=None):
     """DML-PLR on a fold-segmented panel (segment k = fold k). Returns (res[2], moments[7], cv).
 
     comm: optional parallel.comm.Communicator — each rank holds a row shard of every
-    fold; the fold Gram stack and the score moments are all-reduced (C01, C06)."""
+    fold; the fold Gram stack and the score moments are all-reduced (C01, C06).
+    seg_counts: global rows per fold (computed with one all-reduce when omitted)."""
     if G is None:
         G = gram(pan)
-    if comm is not None and comm.world_size > 1:
+    dist = comm is not None and comm.world_size > 1
+    if dist:
         comm.all_reduce_(G)
+        if seg_counts is None:
+            seg_counts = global_seg_counts(pan, comm)
     K = folds
     full_sets = [[s for s in range(K) if s != k] for k in range(K)]
     ycols = [pan.cols["Y"], pan.cols["W"]]
-    cv = cv_enet_gaussian(G, pan, pan.xcols, ycols, full_sets=full_sets)
+    cv = cv_enet_gaussian(G, pan, pan.xcols, ycols, full_sets=full_sets, seg_counts=seg_counts)
     coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1).contiguous()
     mom = dml_residual_moments(pan, coef)
     if comm is not None and comm.world_size > 1:
@@ -159,12 +191,13 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
 
 
 def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cross-fit (LASSO)",
-                  device=None, dtype="f64"):
+                  device=None, dtype="f64", dist=None):
     """K-fold cross-fit partially-linear DML with CV-LASSO nuisances E[Y|X], E[W|X]
     (inner CV over the other K-1 folds). Matches reference.estimators.dml_plr_lasso."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
-    fid = rng.fold_ids(len(Yn), folds, seed, stream=0)
+    fid = _fold_ids(len(Yn), folds, seed, 0, dist)
     pan = build_panel(Xn, Wn, Yn, folds=fid, dtype=dtype, device=dev)
-    res, mom, _ = dml_crossfit_panel(pan, folds, lambda_rule)
-    return read_result(res, method, n=len(Yn))
+    res, mom, _ = dml_crossfit_panel(pan, folds, lambda_rule,
+                                     comm=dist.comm if dist is not None else None)
+    return read_result(res, method, n=dist.n_total if dist is not None else len(Yn))

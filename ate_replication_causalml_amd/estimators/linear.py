@@ -6,6 +6,10 @@ Semantics follow ``ate_functions.R`` exactly (see reference/estimators.py for th
 float64 CPU oracle and SURVEY.md §2.7); each function takes ``(Y, W, X)``.
 Default precision is the fp64 parity panel (fp64 MFMA Gram), the right choice at
 tutorial scale (N ~ 1e4, p = 21); ``dtype="f32"`` uses fp32 MFMA.
+
+``dist=parallel.dist.DistContext(...)``: (Y, W, X) are this rank's row shard; group
+moments, Gram matrices, IRLS statistics and score moments are all-reduced, and the
+bootstrap replicates are sharded across ranks (all-gather of the estimates, C07).
 """
 from __future__ import annotations
 
@@ -20,34 +24,42 @@ from ..result import AteResult
 from .common import as_np, read_result, resolve_device
 
 
-def naive(Y, W, method="naive", device=None):
+def _n(pan, dist):
+    return dist.n_total if dist is not None else pan.n
+
+
+def naive(Y, W, method="naive", device=None, dist=None):
     """E1 ``naive_ate`` (ate_functions.R:3-21)."""
     dev = resolve_device(device)
     y = torch.as_tensor(as_np(Y), device=dev)
     w = torch.as_tensor(as_np(W), device=dev)
     res, mom = S.naive(y, w)
+    if dist is not None:
+        res = S._naive_finalize(dist.sum_(mom.clone()).cpu())
     return read_result(res, method)
 
 
-def ols(Y, W, X, method="Direct Method", device=None, dtype="f64"):
+def ols(Y, W, X, method="Direct Method", device=None, dtype="f64", dist=None):
     """E2 ``ate_condmean_ols`` (ate_functions.R:25-39): lm(Y ~ covariates + W)."""
     dev = resolve_device(device)
     pan = build_panel(as_np(X), as_np(W), as_np(Y), dtype=dtype, device=dev)
     G = gram(pan)[0]
+    if dist is not None:
+        dist.sum_(G)
     cols = [pan.cols["one"], *pan.xcols, pan.cols["W"]]
     r = chol_solve(G, cols, pan.cols["Y"])
-    out = torch.stack([r.beta[-1], torch.sqrt(r.aux[1] / (pan.n - r.aux[0]) * r.invdiag[-1]),
+    out = torch.stack([r.beta[-1], torch.sqrt(r.aux[1] / (_n(pan, dist) - r.aux[0]) * r.invdiag[-1]),
                        r.aux[0]])
     v = out.cpu().numpy()
     return AteResult.make(method, v[0], v[1], rank=int(v[2]))
 
 
-def propensity_logistic(W, X, device=None, dtype="f64", return_panel_order=False):
+def propensity_logistic(W, X, device=None, dtype="f64", return_panel_order=False, dist=None):
     """E16: glm(W ~ covariates, binomial) fitted values (ate_replication.Rmd:165-168)."""
     dev = resolve_device(device)
     pan = build_panel(as_np(X), as_np(W), None, dtype=dtype, device=dev, extra_cols=("z",))
     cols = [pan.cols["one"], *pan.xcols]
-    fit = logistic_irls(pan, cols, pan.cols["W"], pan.cols["z"])
+    fit = logistic_irls(pan, cols, pan.cols["W"], pan.cols["z"], dist=dist)
     if return_panel_order:
         return fit.mu, pan
     return pan.scatter_rows(fit.mu)
@@ -68,7 +80,8 @@ def propensity_lasso(W, X, seed=1991, nfolds=10, fold_stream=7, device=None, dty
     return pan.scatter_rows(mu)
 
 
-def ipw(Y, W, X, p, method="Propensity_Weighting", compat="reference", device=None, dtype="f64"):
+def ipw(Y, W, X, p, method="Propensity_Weighting", compat="reference", device=None, dtype="f64",
+        dist=None):
     """E3 ``prop_score_weight`` (ate_functions.R:44-63) with the full-frame projection
     design under compat="reference" (Q25; see reference.estimators.ipw_design)."""
     dev = resolve_device(device)
@@ -84,15 +97,17 @@ def ipw(Y, W, X, p, method="Propensity_Weighting", compat="reference", device=No
     d = frame * ps[:, None]
     pan = build_panel(d.cpu().numpy(), None, tau.cpu().numpy(), dtype=dtype, device=dev)
     G = gram(pan)[0]
+    if dist is not None:
+        dist.sum_(G)
     cols = [pan.cols["one"], *pan.xcols]
     r = chol_solve(G, cols, pan.cols["Y"])
-    n = pan.n
+    n = _n(pan, dist)
     ate = G[pan.cols["one"], pan.cols["Y"]] / n
     se = torch.sqrt(r.aux[1] / n) / np.sqrt(n)
     return read_result(torch.stack([ate, se]), method)
 
 
-def ipw_wls(Y, W, p, method="Propensity_Regression", device=None, dtype="f64"):
+def ipw_wls(Y, W, p, method="Propensity_Regression", device=None, dtype="f64", dist=None):
     """E4 ``prop_score_ols`` (ate_functions.R:67-86): WLS of Y on W, weights W/p+(1-W)/(1-p)."""
     dev = resolve_device(device)
     Wn, pn = as_np(W), as_np(p)
@@ -100,20 +115,22 @@ def ipw_wls(Y, W, p, method="Propensity_Regression", device=None, dtype="f64"):
     pan = build_panel(Wn[:, None], None, as_np(Y), dtype=dtype, device=dev)
     wt = pan.gather_rows(torch.as_tensor(wts, device=dev).to(pan.dtype))
     G = gram(pan, wt)[0]
+    if dist is not None:
+        dist.sum_(G)
     cols = [pan.cols["one"], pan.xcols[0]]
     r = chol_solve(G, cols, pan.cols["Y"])
-    se = torch.sqrt(r.aux[1] / (pan.n - r.aux[0]) * r.invdiag[1])
+    se = torch.sqrt(r.aux[1] / (_n(pan, dist) - r.aux[0]) * r.invdiag[1])
     return read_result(torch.stack([r.beta[1], se]), method)
 
 
-def outcome_mu(Y, W, X, counterfactual_quirk, device=None, dtype="f64"):
+def outcome_mu(Y, W, X, counterfactual_quirk, device=None, dtype="f64", dist=None):
     """Outcome GLM Y ~ covariates + W (Q24); mu1/mu0 with W overridden to 1/0, or both
     equal to mu(x, W_obs) under the ``mutate_("W = 1")`` quirk (Q6)."""
     dev = resolve_device(device)
     pan = build_panel(np.column_stack([as_np(X), as_np(W)]), None, as_np(Y), dtype=dtype,
                       device=dev, extra_cols=("z",))
     cols = [pan.cols["one"], *pan.xcols]
-    fit = logistic_irls(pan, cols, pan.cols["Y"], pan.cols["z"])
+    fit = logistic_irls(pan, cols, pan.cols["Y"], pan.cols["z"], dist=dist)
     if counterfactual_quirk:
         mu = pan.scatter_rows(fit.mu)
         return mu, mu.clone()
@@ -126,22 +143,47 @@ def outcome_mu(Y, W, X, counterfactual_quirk, device=None, dtype="f64"):
 
 
 def aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se=False, B=1000, seed=1991,
-                        compat="reference", device=None, **diag):
+                        compat="reference", device=None, dist=None, **diag):
     dev = resolve_device(device)
     y = torch.as_tensor(as_np(Y), device=dev)
     w = torch.as_tensor(as_np(W), device=dev)
     p = p.to(dev).double()
-    res, _ = S.aipw(w, y, p, mu0.to(dev), mu1.to(dev), compat=compat)
+    res, mom = S.aipw(w, y, p, mu0.to(dev), mu1.to(dev), compat=compat)
+    if dist is not None:
+        res = S._aipw_finalize(dist.sum_(mom.clone()))
     if bootstrap_se:
         e1, e2 = S.aipw_terms(w, y, p, mu0.to(dev), mu1.to(dev), compat)
-        taus = S.bootstrap_multinomial(e1.contiguous(), e2.contiguous(), B, seed)
+        if dist is None:
+            taus = S.bootstrap_multinomial(e1.contiguous(), e2.contiguous(), B, seed)
+        else:
+            taus = bootstrap_sharded(e1, e2, B, seed, dist)
         res = torch.stack([res[0], taus.std(unbiased=True).to(res.device)])
     return read_result(res, method, **diag)
 
 
+def bootstrap_sharded(e1, e2, B, seed, dist):
+    """E10 with the B replicates split across ranks (C07): the score terms are
+    all-gathered (N doubles x2), rank r evaluates replicates [b0, b0+B_r) with the same
+    global-index Philox draws as one device, then the estimates are all-gathered."""
+    from ..parallel.dist import shard_range
+    e1f = dist.gather_rows(e1.double().contiguous())
+    e2f = dist.gather_rows(e2.double().contiguous())
+    b0, nb = shard_range(B, dist.rank, dist.world)
+    mine = S.bootstrap_multinomial(e1f.contiguous(), e2f.contiguous(), nb, seed, b0=b0) \
+        if nb else torch.empty(0, dtype=torch.float64, device=e1.device)
+    mb = shard_range(B, 0, dist.world)[1]
+    buf = torch.zeros(mb, dtype=torch.float64, device=e1.device)
+    buf[:nb] = mine.to(buf.device)
+    parts = dist.comm.all_gather(buf) if dist.world > 1 else [buf]
+    return torch.cat([pp[:shard_range(B, r, dist.world)[1]] for r, pp in enumerate(parts)])
+
+
 def aipw_glm(Y, W, X, bootstrap_se=False, B=1000, seed=1991, compat="reference",
-             method="Doubly Robust with logistic regression PS", device=None, dtype="f64"):
+             method="Doubly Robust with logistic regression PS", device=None, dtype="f64",
+             dist=None):
     """E9 ``doubly_robust_glm`` (ate_functions.R:211-264)."""
-    mu0, mu1 = outcome_mu(Y, W, X, counterfactual_quirk=False, device=device, dtype=dtype)
-    p = propensity_logistic(W, X, device=device, dtype=dtype)
-    return aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se, B, seed, compat, device)
+    mu0, mu1 = outcome_mu(Y, W, X, counterfactual_quirk=False, device=device, dtype=dtype,
+                          dist=dist)
+    p = propensity_logistic(W, X, device=device, dtype=dtype, dist=dist)
+    return aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se, B, seed, compat, device,
+                               dist=dist)

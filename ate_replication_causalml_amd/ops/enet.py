@@ -47,11 +47,12 @@ def _rescale_vp(vp, p):
 
 def cv_enet_gaussian(G: torch.Tensor, panel, xcols, ycols, full_sets=None, penalty_factor=None,
                      alpha=1.0, nlambda=100, lambda_min_ratio=None, thresh=1e-7,
-                     maxit=100000) -> EnetCvResult:
+                     maxit=100000, seg_counts=None) -> EnetCvResult:
     """Cross-validated gaussian elastic net from the segment Gram stack ``G`` [nseg,P,P].
 
     full_sets: list of lists of segment ids (default: one set with all segments).
-    Problems are ordered (full set f, y index) for the result arrays."""
+    seg_counts: rows per segment (default: the panel's; pass the GLOBAL counts when G
+    was all-reduced over row shards). Problems are ordered (full set f, y index)."""
     nseg = G.shape[0]
     P = G.shape[1]
     p = len(xcols)
@@ -79,7 +80,7 @@ def cv_enet_gaussian(G: torch.Tensor, panel, xcols, ycols, full_sets=None, penal
     masks = np.zeros((len(tsets), nseg), dtype=np.uint8)
     for i, ts in enumerate(tsets):
         masks[i, list(ts)] = 1
-    nreal = np.asarray(panel.seg_nreal, dtype=np.float64)
+    nreal = np.asarray(panel.seg_nreal if seg_counts is None else seg_counts, dtype=np.float64)
     n_full = [nreal[list(fs)].sum() for fs in full_sets]
     if lambda_min_ratio is None:
         lambda_min_ratio = 1e-4 if min(n_full) > p else 1e-2

@@ -120,15 +120,19 @@ class IrlsResult:
 
 
 def logistic_irls(panel: DevicePanel, cols, ycol: int, zcol: int, maxit: int = 25,
-                  eps: float = 1e-8) -> IrlsResult:
+                  eps: float = 1e-8, dist=None) -> IrlsResult:
     """``glm(y ~ X[cols], binomial)`` by IRLS (glm.fit semantics: mustart=(y+.5)/2,
     |dev-dev_old|/(|dev|+0.1) < eps, maxit 25). GPU: fixed-budget launch sequence with
-    a device convergence flag (no host sync; capturable in a hipGraph)."""
+    a device convergence flag (no host sync; capturable in a hipGraph).
+
+    ``dist`` (parallel.dist.DistContext): the panel is this rank's row shard; each
+    iteration all-reduces the weighted Gram and the deviance partials (C01/C02), so
+    every rank takes the same Newton step and the same convergence decision."""
     dev = panel.device
     cols_t = torch.tensor(cols, dtype=torch.int32, device=dev)
     k = len(cols)
     if not panel.data.is_cuda:
-        return _irls_cpu(panel, cols, ycol, zcol, maxit, eps)
+        return _irls_cpu(panel, cols, ycol, zcol, maxit, eps, dist)
     nb = 1024
     eta = torch.empty(panel.ld, dtype=torch.float64, device=dev)
     mu = torch.empty_like(eta)
@@ -143,6 +147,8 @@ def logistic_irls(panel: DevicePanel, cols, ycol: int, zcol: int, maxit: int = 2
     _native.call("ate_irls_update", dc, X.data_ptr(), panel.ld, panel.ld, cols_t.data_ptr(),
                  ws.beta.data_ptr(), k, ycol, panel.cols["one"], zcol, 1, eta.data_ptr(),
                  mu.data_ptr(), w.data_ptr(), devp.data_ptr(), nb, done.data_ptr(), s)
+    if dist is not None:
+        dist.sum_(devp)
     _native.call("ate_irls_check", devp.data_ptr(), nb, 1, eps, maxit, state.data_ptr(),
                  done.data_ptr(), s)
     Gsum = torch.empty((panel.P, panel.P), dtype=torch.float64, device=dev) if panel.nseg > 1 else None
@@ -153,10 +159,14 @@ def logistic_irls(panel: DevicePanel, cols, ycol: int, zcol: int, maxit: int = 2
             G = Gsum
         else:
             G = G[0]
+        if dist is not None:
+            dist.sum_(G)
         chol_solve(G, cols_t, zcol, done=done, ws=ws)
         _native.call("ate_irls_update", dc, X.data_ptr(), panel.ld, panel.ld, cols_t.data_ptr(),
                      ws.beta.data_ptr(), k, ycol, panel.cols["one"], zcol, 0, eta.data_ptr(),
                      mu.data_ptr(), w.data_ptr(), devp.data_ptr(), nb, done.data_ptr(), s)
+        if dist is not None:
+            dist.sum_(devp)
         _native.call("ate_irls_check", devp.data_ptr(), nb, 0, eps, maxit, state.data_ptr(),
                      done.data_ptr(), s)
     return IrlsResult(ws.beta, mu, eta, state, done)
@@ -169,14 +179,16 @@ def _binom_dev(y, mu):
     return 2.0 * np.sum(t1 + t2)
 
 
-def _irls_cpu(panel, cols, ycol, zcol, maxit, eps):
+def _irls_cpu(panel, cols, ycol, zcol, maxit, eps, dist=None):
+    red = (lambda a: dist.sum_(torch.as_tensor(a, dtype=torch.float64)).numpy()) \
+        if dist is not None else (lambda a: np.asarray(a, dtype=np.float64))
     X = panel.data.double().cpu().numpy()
     v = X[panel.cols["one"]] != 0
     A = X[cols][:, v]
     y = X[ycol, v]
     mu = (y + 0.5) / 2
     eta = np.log(mu / (1 - mu))
-    dev_old = _binom_dev(y, mu)
+    dev_old = float(red([_binom_dev(y, mu)])[0])
     beta = np.zeros(len(cols))
     it = 0
     conv = False
@@ -189,11 +201,12 @@ def _irls_cpu(panel, cols, ycol, zcol, maxit, eps):
         Gfull[:len(cols), :] = G
         Gfull[len(cols), :len(cols)] = G[:, len(cols)]
         Gfull[len(cols), len(cols)] = (me * z) @ z
+        Gfull = red(Gfull)
         r = _chol_solve_cpu(torch.from_numpy(Gfull), np.arange(len(cols)), len(cols), None, LM_TOL)
         beta = r.beta.numpy()
         eta = np.nan_to_num(beta) @ A
         mu = np.clip(1 / (1 + np.exp(-eta)), e10, 1 - e10)
-        dev = _binom_dev(y, mu)
+        dev = float(red([_binom_dev(y, mu)])[0])
         if abs(dev - dev_old) / (abs(dev) + 0.1) < eps:
             conv = True
             break

@@ -28,6 +28,12 @@ class LocalComm:
     def all_reduce_(self, t):
         return t
 
+    def all_reduce_max_(self, t):
+        return t
+
+    def all_reduce_min_(self, t):
+        return t
+
     def all_gather(self, t):
         return [t]
 
@@ -48,6 +54,14 @@ class TorchComm:
 
     def all_reduce_(self, t):
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_reduce_max_(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def all_reduce_min_(self, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
         return t
 
     def all_gather(self, t):
@@ -86,15 +100,24 @@ class ThreadSimComm:
         self.rank = rank
         self.world_size = world.n
 
-    def all_reduce_(self, t):
+    def _reduce(self, t, op):
         self.w.slots[self.rank] = t.detach().clone()
         self.w.barrier.wait()
         acc = self.w.slots[0].clone()
         for r in range(1, self.world_size):    # fixed rank order -> deterministic
-            acc += self.w.slots[r]
+            acc = op(acc, self.w.slots[r])
         self.w.barrier.wait()
         t.copy_(acc)
         return t
+
+    def all_reduce_(self, t):
+        return self._reduce(t, lambda a, b: a + b)
+
+    def all_reduce_max_(self, t):
+        return self._reduce(t, torch.maximum)
+
+    def all_reduce_min_(self, t):
+        return self._reduce(t, torch.minimum)
 
     def all_gather(self, t):
         self.w.slots[self.rank] = t.detach().clone()

@@ -53,7 +53,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from ate_replication_causalml_amd.parallel import comm as C
     from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
-    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel, global_seg_counts
 
     comm = C.from_env()
     world, rank = comm.world_size, comm.rank
@@ -70,8 +70,10 @@ def main():
         if device.type == "cuda":
             torch.cuda.synchronize()
 
+    seg_counts = global_seg_counts(pan, comm)   # fold sizes: data layout, fixed across steps
+
     def step():
-        res, _, _ = dml_crossfit_panel(pan, args.folds, "min", comm=comm)
+        res, _, _ = dml_crossfit_panel(pan, args.folds, "min", comm=comm, seg_counts=seg_counts)
         return res
 
     for _ in range(args.warmup):

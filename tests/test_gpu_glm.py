@@ -53,3 +53,25 @@ def test_residual_balance_gpu(gpu, tutorial):
     b = residual_balance(m.Y, m.W, m.X, device=gpu)
     assert b.ate == pytest.approx(a.ate, abs=1e-8)
     assert b.se == pytest.approx(a.se, rel=1e-6)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_panel_gemv_kernels(gpu, dtype):
+    from ate_replication_causalml_amd.ops import gemv
+    r = np.random.default_rng(1)
+    n, p = 5000, 17
+    X = r.normal(size=(n, p))
+    pan = build_panel(X, None, r.normal(size=n), dtype=dtype, device=gpu)
+    grp = torch.full((pan.ld,), -1, dtype=torch.int8, device=gpu)
+    grp[: pan.n] = torch.as_tensor(r.integers(0, 2, pan.n), dtype=torch.int8, device=gpu)
+    v = torch.as_tensor(r.normal(size=pan.ld), device=gpu)
+    M = pan.data[pan.xcols].double().cpu()
+    g = grp.cpu().long()
+    ref = torch.stack([M @ torch.where(g == a, v.cpu(), torch.zeros_like(v.cpu())) for a in range(2)])
+    out = gemv.xtv(pan, pan.xcols, v, grp, 2).cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-10, atol=1e-9)
+    V = torch.as_tensor(r.normal(size=(2, p)), device=gpu)
+    full = V.cpu() @ M
+    ref2 = torch.where(g >= 0, full.gather(0, g.clamp(min=0)[None])[0], torch.zeros(pan.ld,
+                                                                                     dtype=torch.float64))
+    torch.testing.assert_close(gemv.xv(pan, pan.xcols, V, grp).cpu(), ref2, rtol=1e-10, atol=1e-9)
