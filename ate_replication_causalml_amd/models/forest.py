@@ -37,7 +37,7 @@ class ForestParams(ctypes.Structure):
                 ("group", ctypes.c_int), ("mtry_poisson", ctypes.c_int),
                 ("alpha", ctypes.c_double), ("sample_fraction", ctypes.c_double),
                 ("pois0", ctypes.c_double), ("seed", ctypes.c_uint64), ("p", ctypes.c_int),
-                ("n", ctypes.c_int)]
+                ("n", ctypes.c_int), ("t0", ctypes.c_int)]
 
 
 KIND_CLASS, KIND_REG, KIND_CAUSAL = 0, 1, 2
@@ -130,6 +130,17 @@ class Forest:
     def predict_raw(self, X=None, oob=False) -> np.ndarray:
         """kind 0/1: [n] predictions; kind 2: [n, 4] (tau, var, trees used, groups used)."""
         Xb = self._bins(X)
+        state = self.new_state(Xb.shape[1])
+        return self.predict_state(Xb, oob, state, phases=7)
+
+    def new_state(self, n2):
+        if self.backend == "gpu":
+            return torch.zeros(10 * n2, dtype=torch.float64, device=self.device)
+        return np.zeros(10 * n2)
+
+    def predict_state(self, Xb, oob, state, phases):
+        """Run prediction phases (1: per-tree sums, 2: little-bag group sums, 4: finalise)
+        on accumulator ``state`` ([10, n2]); returns the predictions when phase 4 ran."""
         n2 = Xb.shape[1]
         if oob and n2 != self.params.n:
             raise ValueError("OOB prediction requires the training rows")
@@ -149,12 +160,13 @@ class Forest:
             # leaf-index scratch capped at ~1 GiB: trees per chunk, a multiple of the group
             tchunk = max(g, min(self.params.ntree, (1 << 28) // max(n2, 1)) // g * g)
             leaves = torch.empty(tchunk * n2, dtype=torch.int32, device=dev)
-            state = torch.zeros(10 * n2, dtype=torch.float64, device=dev)
             out = torch.empty(n2 * width, dtype=torch.float64, device=dev)
             _native.call("ate_forest_predict", ctypes.addressof(self.params), Xb.data_ptr(), n2,
                          int(oob), self.cap, self.packed.data_ptr(), self.val.data_ptr(),
                          self.inbag.data_ptr(), 0 if self.est is None else self.est.data_ptr(),
-                         leaves.data_ptr(), tchunk, state.data_ptr(), out.data_ptr(), s)
+                         leaves.data_ptr(), tchunk, state.data_ptr(), out.data_ptr(), phases, s)
+            if not phases & 4:
+                return None
             res = out.cpu().numpy()
         else:
             res = np.empty(n2 * width)
@@ -164,9 +176,11 @@ class Forest:
                 ctypes.byref(self.params), _ptr(Xbn), ctypes.c_int(n2), ctypes.c_int(int(oob)),
                 ctypes.c_int(self.cap), _ptr(self.feat), _ptr(self.thr), _ptr(self.left),
                 _ptr(self.val), _ptr(self.inbag), _ptr(self.est) if self.est is not None else None,
-                _ptr(res), ctypes.c_int(_nthreads()))
+                _ptr(state), ctypes.c_int(phases), _ptr(res), ctypes.c_int(_nthreads()))
             if rc != 0:
                 raise RuntimeError("atecpu_forest_predict failed")
+            if not phases & 4:
+                return None
         return res.reshape(n2, width) if width > 1 else res
 
     # randomForest-style accessors
@@ -190,7 +204,7 @@ def _ptr(a):
 
 def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min_node=1,
                sampling=0, honesty=False, group=1, mtry_poisson=False, alpha=0.0,
-               sample_fraction=0.5, seed=1, backend=None, edges=None) -> Forest:
+               sample_fraction=0.5, seed=1, backend=None, edges=None, tree_offset=0) -> Forest:
     """Grow a forest. X: (n, p) float; kind 0 needs y in {0,1}; kind 1 needs r1 (response);
     kind 2 needs r1 = W~ and r2 = Y~ (centred treatment / outcome)."""
     X = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
@@ -203,7 +217,7 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
                       min_node=min_node, honesty=int(honesty), group=max(1, group),
                       mtry_poisson=int(mtry_poisson), alpha=alpha,
                       sample_fraction=sample_fraction, pois0=math.exp(-min(mtry, p)),
-                      seed=seed, p=p, n=n)
+                      seed=seed, p=p, n=n, t0=tree_offset)
     if edges is None:
         edges, ne = bin_edges(X)
     else:
@@ -292,7 +306,7 @@ class CausalForestFit:
 
 def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
                   sample_fraction=0.5, group=2, seed=12345, nuisance_trees=None,
-                  backend=None) -> CausalForestFit:
+                  backend=None, comm=None) -> CausalForestFit:
     """grf::causal_forest(X, Y, W, num.trees, honesty=TRUE, seed) (ate_replication.Rmd:250-255):
     OOB regression forests for Y.hat and W.hat, then causal trees on the centred
     (W - W.hat, Y - Y.hat)."""
@@ -301,6 +315,22 @@ def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
     W = np.asarray(W, dtype=np.float64)
     nt = nuisance_trees or max(50, num_trees // 4)
     edges = bin_edges(X)
+    p = X.shape[1]
+    grf = dict(mtry=grf_mtry(p), min_node=min_node, sampling=1, honesty=honesty, group=group,
+               mtry_poisson=True, alpha=alpha, sample_fraction=sample_fraction, backend=backend,
+               edges=edges)
+    if comm is not None and comm.world_size > 1:
+        # tree-parallel: every rank grows its share of each forest (C05 all-reduces)
+        fy = fit_forest_sharded(X, KIND_REG, nt, comm, r1=Y, seed=seed + 1, **grf)
+        fw = fit_forest_sharded(X, KIND_REG, nt, comm, r1=W, seed=seed + 2, **grf)
+        y_hat = predict_tree_parallel(fy, comm, oob=True)
+        w_hat = predict_tree_parallel(fw, comm, oob=True)
+        y_hat = np.where(np.isnan(y_hat), Y.mean(), y_hat)
+        w_hat = np.where(np.isnan(w_hat), W.mean(), w_hat)
+        fc = fit_forest_sharded(X, KIND_CAUSAL, num_trees, comm, r1=W - w_hat, r2=Y - y_hat,
+                                seed=seed, **grf)
+        out = predict_tree_parallel(fc, comm, oob=True)
+        return CausalForestFit(fc, y_hat, w_hat, out[:, 0], out[:, 1], Y, W)
     fy = regression_forest(X, Y, nt, honesty, min_node, alpha, sample_fraction, group,
                            seed + 1, backend)
     fw = regression_forest(X, W, nt, honesty, min_node, alpha, sample_fraction, group,
@@ -309,7 +339,6 @@ def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
     w_hat = fw.predict_raw(None, oob=True)
     y_hat = np.where(np.isnan(y_hat), Y.mean(), y_hat)
     w_hat = np.where(np.isnan(w_hat), W.mean(), w_hat)
-    p = X.shape[1]
     fc = fit_forest(X, KIND_CAUSAL, r1=W - w_hat, r2=Y - y_hat, ntree=num_trees, mtry=grf_mtry(p),
                     min_node=min_node, sampling=1, honesty=honesty, group=group, mtry_poisson=True,
                     alpha=alpha, sample_fraction=sample_fraction, seed=seed, backend=backend,
@@ -329,3 +358,41 @@ def average_treatment_effect(cf: CausalForestFit):
     gamma = tau + w_res / (what * (1 - what)) * (y_res - tau * w_res)
     n = len(gamma)
     return float(gamma.mean()), float(gamma.std(ddof=1) / math.sqrt(n))
+
+
+# ------------------------------------------------------------------ tree parallelism (C05)
+def tree_shard(ntree: int, group: int, rank: int, world: int):
+    """(first tree, tree count) of this rank; shards are whole little-bag groups."""
+    from ..parallel.dist import shard_range
+    g = max(1, group)
+    g0, ng = shard_range(-(-ntree // g), rank, world)
+    t0 = g0 * g
+    return t0, max(0, min(ntree, (g0 + ng) * g) - t0)
+
+
+def fit_forest_sharded(X, kind, ntree, comm, group=1, **kw) -> Forest:
+    """Every rank holds all rows (binned panel replicated) and grows its share of the
+    trees; tree t uses the same Philox streams as on a single device (global id)."""
+    t0, cnt = tree_shard(ntree, group, comm.rank, comm.world_size)
+    if cnt < 1:
+        raise ValueError(f"{ntree} trees cannot be sharded over {comm.world_size} ranks "
+                         f"in groups of {group}")
+    return fit_forest(X, kind, ntree=max(cnt, 0), group=group, tree_offset=t0, **kw)
+
+
+def predict_tree_parallel(forest: Forest, comm, X=None, oob=False):
+    """Forest prediction with trees sharded over ranks: all-reduce the per-tree sums
+    (C05), then (causal forests) the little-bag group sums, then finalise locally."""
+    Xb = forest._bins(X)
+    n2 = Xb.shape[1]
+    st = forest.new_state(n2)
+    t = st if isinstance(st, torch.Tensor) else torch.from_numpy(st)
+    forest.predict_state(Xb, oob, st, phases=1)
+    k = 5 if forest.params.kind == KIND_CAUSAL else 2
+    if comm.world_size > 1:
+        comm.all_reduce_(t[:k * n2])
+    if forest.params.kind == KIND_CAUSAL:
+        forest.predict_state(Xb, oob, st, phases=2)
+        if comm.world_size > 1:
+            comm.all_reduce_(t[5 * n2:])
+    return forest.predict_state(Xb, oob, st, phases=4)

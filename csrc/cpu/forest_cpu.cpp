@@ -44,13 +44,14 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
                       const int64_t* r1, const int64_t* r2, const Out& o) {
   const int n = fp.n, p = fp.p;
   std::vector<int32_t> w(n, 0);
+  const int tg = fp.t0 + t;          // global tree id (RNG key)
   std::vector<int> est_rows;
   uint8_t* inb = o.inbag + (int64_t)t * n;
   if (fp.sampling == 0) {
-    for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)t, (uint64_t)j, (uint32_t)n)]++;
+    for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)]++;
     for (int i = 0; i < n; ++i) inb[i] = w[i] > 0;
   } else {
-    const int g = t / fp.group;
+    const int g = tg / fp.group;
     std::vector<int> all(n);
     std::iota(all.begin(), all.end(), 0);
     std::vector<int> H = select_rows(fp, all, n / 2, (uint32_t)g);
@@ -59,10 +60,10 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
     double f = fp.sample_fraction * fp.group;
     if (f > 1.0) f = 1.0;
     std::vector<int> S = f >= 1.0 ? H : select_rows(fp, H, (int64_t)std::floor(H.size() * f),
-                                                   0x10000u + (uint32_t)t);
+                                                   0x10000u + (uint32_t)tg);
     std::vector<int> J1 = S;
     if (fp.honesty) {
-      J1 = select_rows(fp, S, (int64_t)(S.size() / 2), 0x20000u + (uint32_t)t);
+      J1 = select_rows(fp, S, (int64_t)(S.size() / 2), 0x20000u + (uint32_t)tg);
       std::vector<uint8_t> in1(n, 0);
       for (int i : J1) in1[i] = 1;
       for (int i : S)
@@ -134,10 +135,10 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
           parent = (sd * sd) / dn;
         }
         const int minc = min_child(fp, dn);
-        const int nf = draw_num_features(fp, t, v);
+        const int nf = draw_num_features(fp, tg, v);
         std::iota(perm.begin(), perm.end(), 0);
         for (int k = 0; k < nf; ++k) {
-          uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, k), (uint32_t)(p - k));
+          uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, k), (uint32_t)(p - k));
           std::swap(perm[k], perm[k + r]);
         }
         double best = -INFINITY;
@@ -202,7 +203,7 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
           int vote;
           if (2 * n1 > nw) vote = 1;
           else if (2 * n1 < nw) vote = 0;
-          else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, 4095)) & 1u);
+          else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, 4095)) & 1u);
           val[v] = vote;
         } else if (fp.kind == 1) {
           val[v] = from_fix(s1) / dn;
@@ -278,12 +279,14 @@ ATECPU_API int atecpu_forest_fit(const ForestParams* fpp, const uint8_t* Xb, con
 ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb, int n2, int oob,
                                      int cap, const int32_t* feat, const int32_t* thr,
                                      const int32_t* left, const double* val,
-                                     const uint8_t* inbag, const int64_t* est, double* out,
-                                     int nthreads) {
+                                     const uint8_t* inbag, const int64_t* est, double* state,
+                                     int phases, double* out, int nthreads) {
+  // state: [10][n2] accumulators, same protocol as csrc/forest.hip ate_forest_predict
+  // (1 = per-tree sums, 2 = kind-2 little-bag group sums, 4 = finalise).
   const ForestParams fp = *fpp;
 #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
   for (int i = 0; i < n2; ++i) {
-    // returns the node whose statistics predict for row i in tree t (-1 if tree unused)
+    // the node whose statistics predict for row i in tree t (-1 if the tree is excluded)
     auto leaf_of = [&](int t) -> int64_t {
       if (oob && inbag[(int64_t)t * fp.n + i]) return -1;
       const int64_t base = (int64_t)t * cap;
@@ -295,39 +298,44 @@ ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb,
       }
       return base + (fp.sampling == 1 && est ? last_ok : v);
     };
-    if (fp.kind != 2) {
-      double acc = 0;
-      int used = 0;
-      for (int t = 0; t < fp.ntree; ++t) {
-        const int64_t nd = leaf_of(t);
-        if (nd < 0) continue;
-        ++used;
-        if (fp.kind == 0 || fp.sampling == 0) acc += val[nd];
-        else acc += from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
+    double* st = state;
+    if (phases & 1) {
+      if (fp.kind != 2) {
+        double acc = st[i], used = st[n2 + i];
+        for (int t = 0; t < fp.ntree; ++t) {
+          const int64_t nd = leaf_of(t);
+          if (nd < 0) continue;
+          used += 1.0;
+          if (fp.kind == 0 || fp.sampling == 0) acc += val[nd];
+          else acc += from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
+        }
+        st[i] = acc;
+        st[n2 + i] = used;
+      } else {
+        double a1 = st[i], aw = st[n2 + i], ay = st[2 * n2 + i], aww = st[3 * n2 + i],
+               awy = st[4 * n2 + i];
+        for (int t = 0; t < fp.ntree; ++t) {
+          const int64_t nd = leaf_of(t);
+          if (nd < 0) continue;
+          const int64_t* e = est + nd * 5;
+          const double c = (double)e[0];
+          a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
+          aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
+        }
+        st[i] = a1; st[n2 + i] = aw; st[2 * n2 + i] = ay; st[3 * n2 + i] = aww;
+        st[4 * n2 + i] = awy;
       }
-      out[i] = used > 0 ? acc / used : NAN;
-      continue;
     }
-    // kind 2: forest-weighted leaf moments -> tau; little-bag variance of the linearised
-    // score psi = (w - Wbar)(y - Ybar - tau (w - Wbar)) over groups, divided by H^2
-    double a1 = 0, aw = 0, ay = 0, aww = 0, awy = 0;
-    for (int t = 0; t < fp.ntree; ++t) {
-      const int64_t nd = leaf_of(t);
-      if (nd < 0) continue;
-      const int64_t* e = est + nd * 5;
-      const double c = (double)e[0];
-      a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
-      aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
-    }
-    double tau = NAN, var = NAN;
-    int ng = 0;
-    if (a1 > 0) {
-      const double wb = aw / a1, yb = ay / a1;
-      const double H = aww / a1 - wb * wb;
+    if ((phases & 2) && fp.kind == 2 && st[i] > 0) {
+      // little bags: linearised score psi = (w - Wbar)(y - Ybar - tau (w - Wbar)) per
+      // group at the full-forest tau
+      const double a1 = st[i];
+      const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
+      const double H = st[3 * n2 + i] / a1 - wb * wb;
       if (H > 0) {
-        tau = (awy / a1 - wb * yb) / H;
-        double gs = 0, gss = 0, within = 0;
-        int nwithin = 0;
+        const double tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
+        double gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
+        double nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
         for (int g0 = 0; g0 < fp.ntree; g0 += fp.group) {
           double ps = 0, pss = 0;
           int nb = 0;
@@ -343,21 +351,40 @@ ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb,
           }
           if (nb == 0) continue;
           const double pg = ps / nb;
-          gs += pg; gss += pg * pg; ++ng;
-          if (nb >= 2) { within += pss / nb - pg * pg; ++nwithin; }
+          gs += pg; gss += pg * pg; ng += 1.0;
+          if (nb >= 2) { within += pss / nb - pg * pg; nwithin += 1.0; }
         }
-        if (ng >= 2) {
-          const double mean = gs / ng;
-          const double between = gss / ng - mean * mean;
-          const double wc = nwithin > 0 ? within / nwithin / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
-          var = std::fmax(between - wc, 0.0) / (H * H);
-        }
+        st[5 * n2 + i] = gs; st[6 * n2 + i] = gss; st[7 * n2 + i] = within;
+        st[8 * n2 + i] = nwithin; st[9 * n2 + i] = ng;
       }
     }
-    out[4 * i + 0] = tau;
-    out[4 * i + 1] = var;
-    out[4 * i + 2] = a1;
-    out[4 * i + 3] = ng;
+    if (phases & 4) {
+      if (fp.kind != 2) {
+        out[i] = st[n2 + i] > 0 ? st[i] / st[n2 + i] : NAN;
+        continue;
+      }
+      const double a1 = st[i];
+      double tau = NAN, var = NAN;
+      const double ng = st[9 * n2 + i];
+      if (a1 > 0) {
+        const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
+        const double H = st[3 * n2 + i] / a1 - wb * wb;
+        if (H > 0) {
+          tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
+          if (ng >= 2) {
+            const double mean = st[5 * n2 + i] / ng;
+            const double between = st[6 * n2 + i] / ng - mean * mean;
+            const double nw = st[8 * n2 + i];
+            const double wc = nw > 0 ? st[7 * n2 + i] / nw / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
+            var = std::fmax(between - wc, 0.0) / (H * H);
+          }
+        }
+      }
+      out[4 * i + 0] = tau;
+      out[4 * i + 1] = var;
+      out[4 * i + 2] = a1;
+      out[4 * i + 3] = ng;
+    }
   }
   return 0;
 }

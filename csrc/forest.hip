@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   __shared__ int shi[8];
   __shared__ int sncur, snext_id, sm, sestn;
   const int t = blockIdx.x;
+  const int tg = fp.t0 + t;          // global tree id (RNG key)
   const int n = fp.n, p = fp.p;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   Scratch S = scratch_for(scratch_base, n, t);
@@ -103,14 +104,14 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   __syncthreads();
   if (fp.sampling == 0) {
     for (int j = tid; j < n; j += 256)
-      atomicAdd(&S.w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)t, (uint64_t)j, (uint32_t)n)], 1);
+      atomicAdd(&S.w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)], 1);
     __syncthreads();
     for (int i = tid; i < n; i += 256) inb[i] = S.w[i] > 0;
     if (tid == 0) sestn = 0;
   } else if (tid == 0) {
     // Algorithm S (sequential by definition): group half-sample H, tree subsample S,
     // honesty split J1 (grow) / J2 (estimate). tmp holds H, then S; est_rows holds J2.
-    const int g = t / fp.group;
+    const int g = tg / fp.group;
     int nh = 0;
     const int64_t kh = n / 2;
     for (int i = 0; i < n && nh < kh; ++i)
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
       const int64_t ks = (int64_t)floor(nh * f);
       int c = 0;
       for (int q = 0; q < nh && c < ks; ++q)
-        if (select_next(fp.seed, 0x10000u + (uint32_t)t, (uint64_t)q, (int64_t)(nh - q), ks - c))
+        if (select_next(fp.seed, 0x10000u + (uint32_t)tg, (uint64_t)q, (int64_t)(nh - q), ks - c))
           S.tmp[c++] = S.tmp[q];
       ns = c;
     }
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
       int c = 0;
       for (int q = 0; q < ns; ++q) {
         const int i = S.tmp[q];
-        if (c < k1 && select_next(fp.seed, 0x20000u + (uint32_t)t, (uint64_t)q, (int64_t)(ns - q), k1 - c)) {
+        if (c < k1 && select_next(fp.seed, 0x20000u + (uint32_t)tg, (uint64_t)q, (int64_t)(ns - q), k1 - c)) {
           S.w[i] = 1;
           ++c;
         } else {
@@ -226,11 +227,11 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
           parent = __ddiv_rn(__dmul_rn(sd, sd), dn);
         }
         const int minc = min_child(fp, dn);
-        const int nf = draw_num_features(fp, t, v);
+        const int nf = draw_num_features(fp, tg, v);
         if (lane == 0) {
           for (int k = 0; k < p; ++k) perm[wid][k] = (int16_t)k;
           for (int k = 0; k < nf; ++k) {
-            const uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, k), (uint32_t)(p - k));
+            const uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, k), (uint32_t)(p - k));
             const int16_t tmpv = perm[wid][k];
             perm[wid][k] = perm[wid][k + r];
             perm[wid][k + r] = tmpv;
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
             int vote;
             if (2 * n1 > nw) vote = 1;
             else if (2 * n1 < nw) vote = 0;
-            else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)t, node_index(v, 4095)) & 1u);
+            else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, 4095)) & 1u);
             val[v] = vote;
           } else if (fp.kind == 1) {
             val[v] = from_fix(s1) / dn;
@@ -617,19 +618,23 @@ ATE_API int ate_forest_pack(const void* fpp, int cap, const void* feat, const vo
   return 0;
 }
 
-// state: zeroed [10][n2] fp64 scratch; leaves: [tchunk][n2] int32 scratch, tchunk a
-// multiple of the little-bag group size. Trees are visited in ascending order, so the
-// sums match the host engine's sequential loop.
+// state: [10][n2] fp64 accumulators (zeroed by the caller before phase 1); leaves:
+// [tchunk][n2] int32 scratch, tchunk a multiple of the little-bag group size. Trees are
+// visited in ascending order, so the sums match the host engine's sequential loop.
+// phases (bitmask): 1 = per-tree sums (kind 0/1 votes, kind 2 leaf moments),
+// 2 = kind-2 little-bag group sums (needs the COMPLETE phase-1 sums in state),
+// 4 = finalise state -> out. A tree-parallel forest runs 1, all-reduce(state[0:5n2]),
+// 2, all-reduce(state[5n2:10n2]), 4 (models/forest.py::predict_tree_parallel).
 ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob, int cap,
                                const void* packed, const void* val, const void* inbag,
                                const void* est, void* leaves, int tchunk, void* state, void* out,
-                               void* stream) {
+                               int phases, void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
   hipStream_t st = (hipStream_t)stream;
   if (tchunk < 1 || (fp.kind == 2 && tchunk % fp.group)) return -1;
   const int rb = (n2 + 255) / 256;
-  const int passes = fp.kind == 2 ? 2 : 1;
-  for (int pass = 0; pass < passes; ++pass) {
+  for (int pass = 0; pass < 2; ++pass) {
+    if (!(phases & (1 << pass)) || (pass == 1 && fp.kind != 2)) continue;
     for (int t0 = 0; t0 < fp.ntree; t0 += tchunk) {
       const int nt = min(tchunk, fp.ntree - t0);
       hipLaunchKernelGGL(forest_leaf_kernel, dim3(rb, nt), dim3(256), 0, st, fp,
@@ -647,8 +652,9 @@ ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob,
                            (const int32_t*)leaves, (const int64_t*)est, (double*)state);
     }
   }
-  hipLaunchKernelGGL(forest_final_kernel, dim3(rb), dim3(256), 0, st, fp, n2,
-                     (const double*)state, (double*)out);
+  if (phases & 4)
+    hipLaunchKernelGGL(forest_final_kernel, dim3(rb), dim3(256), 0, st, fp, n2,
+                       (const double*)state, (double*)out);
   ATE_CHECK_LAUNCH();
   return 0;
 }

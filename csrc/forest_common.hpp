@@ -58,6 +58,8 @@ struct ForestParams {
   uint64_t seed;
   int p;              // features
   int n;              // rows
+  int t0;             // global index of this forest's first tree (tree-parallel shards):
+                      // every RNG stream / little-bag group is keyed by t0 + t
 };
 
 struct u4 { uint32_t x, y, z, w; };

@@ -81,3 +81,29 @@ def test_lasso_family_sharded_equals_single(tutorial, world):
             assert a.ate == pytest.approx(b.ate, rel=1e-7, abs=1e-10), a.method
             if np.isfinite(b.se):
                 assert a.se == pytest.approx(b.se, rel=1e-7), a.method
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tree_parallel_forests_equal_single(world):
+    """Trees sharded over ranks (C05): identical trees per global tree id; OOB votes and
+    causal-forest tau/variance equal the single-device forest up to summation order."""
+    from ate_replication_causalml_amd.models import forest as F
+    r = np.random.default_rng(0)
+    n = 1500
+    X = r.normal(size=(n, 5))
+    W = (r.uniform(size=n) < 0.4).astype(float)
+    Y = X[:, 0] + (1 + (X[:, 1] > 0)) * W + 0.3 * r.normal(size=n)
+    rf1 = F.rf_classifier(X, W, num_trees=24, seed=5, backend="cpu").oob_proba()
+    cf1 = F.causal_forest(X, Y, W, num_trees=24, nuisance_trees=12, seed=9, backend="cpu")
+
+    def fn(dist):
+        fr = F.fit_forest_sharded(X, F.KIND_CLASS, 24, dist.comm, y=W, seed=5, backend="cpu")
+        p = F.predict_tree_parallel(fr, dist.comm, oob=True)
+        cf = F.causal_forest(X, Y, W, num_trees=24, nuisance_trees=12, seed=9, backend="cpu",
+                             comm=dist.comm)
+        return p, cf
+
+    for p, cf in _run(fn, world, n):
+        np.testing.assert_allclose(p, rf1, rtol=1e-12, atol=1e-12, equal_nan=True)
+        np.testing.assert_allclose(cf.tau_oob, cf1.tau_oob, rtol=1e-9, atol=1e-11, equal_nan=True)
+        np.testing.assert_allclose(cf.var_oob, cf1.var_oob, rtol=1e-7, atol=1e-11, equal_nan=True)
