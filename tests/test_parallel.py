@@ -75,3 +75,53 @@ dist.destroy_process_group()
     got = np.array(json.loads(line.split(" ", 1)[1]))
     ref, _ = _dml(1, 0, LocalComm())
     assert np.allclose(got, ref, rtol=1e-9)
+
+
+def test_gloo_two_process_sharded_estimators():
+    """Real torch.distributed (gloo) ranks: row-sharded AIPW-glm with sharded bootstrap,
+    and a tree-parallel RF OOB propensity, equal to the single-process results."""
+    script = r"""
+import os, sys, json
+sys.path.insert(0, %r)
+import numpy as np, torch, torch.distributed as dist
+dist.init_process_group("gloo")
+from ate_replication_causalml_amd.parallel.comm import TorchComm
+from ate_replication_causalml_amd.parallel.dist import DistContext
+from ate_replication_causalml_amd.data.dgp import make_tutorial_data
+from ate_replication_causalml_amd.data.selection import apply_selection_bias
+from ate_replication_causalml_amd.estimators import linear as D
+from ate_replication_causalml_amd.models import forest as F
+c = TorchComm()
+m, _ = apply_selection_bias(make_tutorial_data(4000, 1991))
+d = DistContext.for_rank(c, len(m.Y))
+r = D.aipw_glm(d.local(m.Y), d.local(m.W), d.local(m.X), bootstrap_se=True, B=30, device="cpu", dist=d)
+fr = F.fit_forest_sharded(m.X, F.KIND_CLASS, 16, c, y=m.W, seed=4, backend="cpu")
+p = F.predict_tree_parallel(fr, c, oob=True)
+if c.rank == 0:
+    print("RESULT", json.dumps([r.ate, r.se, float(np.nansum(p))]))
+dist.destroy_process_group()
+""" % ROOT
+    import json
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
+        f.write(script)
+        path = f.name
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29519", path]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+    finally:
+        os.unlink(path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT")][0].split(" ", 1)[1])
+    from ate_replication_causalml_amd.data.dgp import make_tutorial_data
+    from ate_replication_causalml_amd.data.selection import apply_selection_bias
+    from ate_replication_causalml_amd.estimators import linear as D
+    from ate_replication_causalml_amd.models import forest as F
+    m, _ = apply_selection_bias(make_tutorial_data(4000, 1991))
+    ref = D.aipw_glm(m.Y, m.W, m.X, bootstrap_se=True, B=30, device="cpu")
+    p = F.rf_classifier(m.X, m.W, num_trees=16, seed=4, backend="cpu").oob_proba()
+    assert got[0] == pytest.approx(ref.ate, rel=1e-9)
+    assert got[1] == pytest.approx(ref.se, rel=1e-8)
+    assert got[2] == pytest.approx(float(np.nansum(p)), rel=1e-12)
