@@ -4,7 +4,8 @@ Capability parity with the R replication of Athey & Imbens' causal-ML ATE tutori
 (ate_functions.R + ate_replication.Rmd): 14 estimators, the synthetic/real data
 pipeline, and the large-N K-fold DML cross-fit. See ``api`` for the entry points.
 """
-from .api import (Replication, ate_aipw_glm, ate_aipw_rf, ate_belloni, ate_causal_forest,
+from .api import (Replication, ate_aipw_crossfit, ate_aipw_glm, ate_aipw_rf, ate_belloni, ate_causal_forest,
+                  ate_causal_forest_bootstrap,
                   ate_dml, ate_double_ml, ate_ipw, ate_ipw_wls, ate_lasso, ate_lasso_single,
                   ate_naive, ate_ols, ate_residual_balance, propensity_lasso,
                   propensity_logistic, replicate)

@@ -242,6 +242,30 @@ def ate_causal_forest(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest
                                     device=run.device())
 
 
+def ate_aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, run=None, comm=None,
+                      **kw) -> AteResult:
+    """K-fold cross-fitted AIPW (textbook signs) with rf / glm / gbdt nuisances
+    (BASELINE config 3); ``comm`` shards the forests' trees over ranks."""
+    run = _run(run)
+    with trace("ate_aipw_crossfit", learner=learner, folds=folds):
+        from .estimators.crossfit import aipw_crossfit
+        return aipw_crossfit(Y, W, X, folds=folds, learner=learner, num_trees=num_trees,
+                             seed=run.seed, device=run.device() if not _ref(run) else "cpu",
+                             comm=comm, **kw)
+
+
+def ate_causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, run=None,
+                                comm=None) -> AteResult:
+    """Causal-forest ATE with a B-replicate bootstrap SE sharded over ranks (config 4)."""
+    run = _run(run)
+    with trace("ate_causal_forest_bootstrap", trees=num_trees, B=B):
+        from .estimators.crossfit import causal_forest_bootstrap
+        return causal_forest_bootstrap(Y, W, X, num_trees=num_trees, B=B, seed=seed,
+                                       boot_seed=run.seed,
+                                       device=run.device() if not _ref(run) else "cpu",
+                                       comm=comm)
+
+
 # ------------------------------------------------------------------ driver
 @dataclass
 class Replication:
@@ -327,5 +351,6 @@ __all__ = [
     "ate_naive", "ate_ols", "propensity_logistic", "propensity_lasso", "ate_ipw", "ate_ipw_wls",
     "ate_lasso_single", "ate_lasso", "ate_aipw_rf", "ate_aipw_glm", "ate_belloni",
     "ate_double_ml", "ate_dml", "ate_residual_balance", "ate_causal_forest", "replicate",
+    "ate_aipw_crossfit", "ate_causal_forest_bootstrap",
     "Replication", "AteResult", "RunConfig", "ReplicateConfig", "BalanceConfig",
 ]

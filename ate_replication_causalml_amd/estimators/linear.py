@@ -162,20 +162,30 @@ def aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se=False, B=1000, s
 
 
 def bootstrap_sharded(e1, e2, B, seed, dist):
-    """E10 with the B replicates split across ranks (C07): the score terms are
-    all-gathered (N doubles x2), rank r evaluates replicates [b0, b0+B_r) with the same
-    global-index Philox draws as one device, then the estimates are all-gathered."""
-    from ..parallel.dist import shard_range
+    """E10 with the B replicates split across ranks (C07) for ROW-SHARDED scores: the
+    terms are all-gathered (N doubles x2) and handed to ``bootstrap_replicates``."""
     e1f = dist.gather_rows(e1.double().contiguous())
     e2f = dist.gather_rows(e2.double().contiguous())
-    b0, nb = shard_range(B, dist.rank, dist.world)
-    mine = S.bootstrap_multinomial(e1f.contiguous(), e2f.contiguous(), nb, seed, b0=b0) \
+    return bootstrap_replicates(e1f, e2f, B, seed, dist.comm)
+
+
+def bootstrap_replicates(e1, e2, B, seed, comm=None):
+    """tau_b for b < B with the replicates sharded over ``comm`` (rows replicated on
+    every rank): rank r evaluates [b0, b0+B_r) with the same global-index Philox draws
+    as one device, then the estimates are all-gathered in rank order (C07)."""
+    from ..parallel.dist import shard_range
+    world = comm.world_size if comm is not None else 1
+    rank = comm.rank if comm is not None else 0
+    b0, nb = shard_range(B, rank, world)
+    mine = S.bootstrap_multinomial(e1.contiguous(), e2.contiguous(), nb, seed, b0=b0) \
         if nb else torch.empty(0, dtype=torch.float64, device=e1.device)
-    mb = shard_range(B, 0, dist.world)[1]
+    if world == 1:
+        return mine
+    mb = shard_range(B, 0, world)[1]
     buf = torch.zeros(mb, dtype=torch.float64, device=e1.device)
     buf[:nb] = mine.to(buf.device)
-    parts = dist.comm.all_gather(buf) if dist.world > 1 else [buf]
-    return torch.cat([pp[:shard_range(B, r, dist.world)[1]] for r, pp in enumerate(parts)])
+    parts = comm.all_gather(buf)
+    return torch.cat([pp[:shard_range(B, r, world)[1]] for r, pp in enumerate(parts)])
 
 
 def aipw_glm(Y, W, X, bootstrap_se=False, B=1000, seed=1991, compat="reference",
