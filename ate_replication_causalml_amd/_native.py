@@ -60,6 +60,11 @@ _SIGS = {
     "ate_forest_scratch_bytes": "ii",
     "ate_bin_matrix": "plipppp",
     "ate_panel_xtv": "iplpipplipp",
+    "ate_gbdt_grad": "ippplppp" + "p",
+    "ate_gbdt_hist": "plpplii" + "pp",
+    "ate_gbdt_split": "piiiidlddppppp",
+    "ate_gbdt_partition": "plplippp",
+    "ate_gbdt_apply": "plliipppp" + "p",
     "ate_panel_xv": "iplpipiplpp",
 }
 _RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64}
