@@ -60,6 +60,7 @@ _SIGS = {
     "ate_forest_scratch_bytes": "ii",
     "ate_bin_matrix": "plipppp",
     "ate_panel_xtv": "iplpipplipp",
+    "ate_select_compact": "plppddpppp" + "p",
     "ate_gbdt_grad": "ippplppp" + "p",
     "ate_gbdt_hist": "plpplii" + "pp",
     "ate_gbdt_split": "piiiidlddppppp",

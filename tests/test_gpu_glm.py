@@ -75,3 +75,13 @@ def test_panel_gemv_kernels(gpu, dtype):
     ref2 = torch.where(g >= 0, full.gather(0, g.clamp(min=0)[None])[0], torch.zeros(pan.ld,
                                                                                      dtype=torch.float64))
     torch.testing.assert_close(gemv.xv(pan, pan.xcols, V, grp).cpu(), ref2, rtol=1e-10, atol=1e-9)
+
+
+@pytest.mark.parametrize("compat", ["reference", "textbook"])
+def test_device_selection_matches_host(gpu, compat):
+    from ate_replication_causalml_amd.data.device_selection import keep_indices
+    from ate_replication_causalml_amd.data.dgp import make_tutorial_data
+    d = make_tutorial_data(n=50000, seed=1991)
+    a = keep_indices(d.X, d.W, d.names, compat=compat, device=gpu).cpu().numpy()
+    b = keep_indices(d.X, d.W, d.names, compat=compat, device="cpu").numpy()
+    np.testing.assert_array_equal(a, b)
