@@ -67,7 +67,7 @@ def _gbdt_fit_predict(Xtr, ytr, Xho, dev, seed, gbdt_kw):
 
 
 def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold_stream=11,
-                  clip=1e-3, method=None, device=None, comm=None, gbdt_kw=None) -> AteResult:
+                  clip=0.01, method=None, device=None, comm=None, gbdt_kw=None) -> AteResult:
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
     n = len(Yn)
