@@ -91,7 +91,10 @@ def hip():
     global _hip
     if _hip is None:
         import torch  # noqa: F401  (ensure torch's HIP runtime is loaded first)
-        p = _LIBDIR / "libatehip.so"
+        # ATE_HIP_LIB: an alternative build of the same library (e.g. the cycle-profiling
+        # variant made by tools/enet_profile.py)
+        p = Path(os.environ["ATE_HIP_LIB"]) if os.environ.get("ATE_HIP_LIB") else \
+            _LIBDIR / "libatehip.so"
         if not p.exists():
             raise NativeMissing(
                 f"{p} not found: build it with `python -m ate_replication_causalml_amd._build` "

@@ -119,6 +119,17 @@ struct EnetProblem {
 constexpr double BIGL = 9.9e35;
 constexpr int PMAX = 512;
 
+#ifdef ENET_PROF
+// cycle accounting per problem (debug builds): [0] pull, [1] recurrence, [2] other,
+// [3] block visits, [4] coordinate updates, [5] pending columns pulled, [6] passes
+__device__ unsigned long long enet_prof[256][8];
+#define PROF_T(var) const unsigned long long var = wall_clock64()
+#define PROF_ADD(k, v) do { if (tid == 0) enet_prof[q][k] += (v); } while (0)
+#else
+#define PROF_T(var)
+#define PROF_ADD(k, v) do { } while (0)
+#endif
+
 template <typename CT> struct VecT;
 template <> struct VecT<float> { typedef float4 type; };
 template <> struct VecT<double> { typedef double2 type; };
@@ -168,9 +179,9 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
   __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
   __shared__ int sflag[PMAX];             // bit0 ju, bit1 active
-  __shared__ float sC[64 * 64];           // diagonal block, sC[i*64 + l] = C[t*64+l][t*64+i]
   __shared__ double spart[4][64];
   __shared__ __attribute__((aligned(16))) CT sdelta[PMAX];
+  __shared__ int slist[PMAX];             // compacted pending columns (per-wave quarters)
   __shared__ double sdl;
   __shared__ int sany;
   __shared__ double slam;
@@ -208,32 +219,62 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   double rsq_l = 0.0;
   typedef typename VecT<CT>::type V;
   constexpr int W = sizeof(V) / sizeof(CT);
+  float dg_lo[32], dg_hi[32];
 
-  // bring block t's gradient up to date (all 256 threads); stage its diagonal block
+  // bring block t's gradient up to date (all 256 threads); stage its diagonal block.
+  // Sparse pull: only coordinates changed since block t's snapshot contribute, and by
+  // symmetry coordinate j's contribution is the contiguous row segment C[j][t*64 .. +63].
+  // Each wave compacts the nonzero pending deltas of its quarter of the columns (ordered
+  // ballot) and streams those segments; then it loads 16 rows of the 64x64 diagonal block.
   auto pull = [&](int t) {
-    for (int j = tid; j < ldc; j += 256) sdelta[j] = (CT)(sdc[j] - sds[t][j]);
-    __syncthreads();
-    const int r = t * 64 + lane;
     const int c0 = wid * cw;
+    int cnt = 0;
+    for (int base = c0; base < c0 + cw; base += 64) {
+      const int j = base + lane;
+      const bool inq = j < c0 + cw;       // cw < 64 when p is small
+      const double dj = inq ? sdc[j] - sds[t][j] : 0.0;
+      const bool nz = dj != 0.0;
+      const uint64_t bal = __ballot(nz);
+      const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+      if (nz) { slist[c0 + pos] = j; sdelta[c0 + pos] = (CT)dj; }
+      cnt += __popcll(bal);
+    }
+    const CT* colt = Cq + t * 64 + lane;
     CT acc = 0;
-    const V* dv = reinterpret_cast<const V*>(sdelta + c0);
-    if (r < p) {
-      const V* row = reinterpret_cast<const V*>(Cq + (int64_t)r * ldc + c0);
-#pragma unroll 16
-      for (int c = 0; c < cw / W; ++c) {
-        const V v = row[c];
-        acc += vdot(v, dv[c]);
-        const int j0 = c0 + c * W;
-        if ((j0 >> 6) == t) {
-          const CT* ve = reinterpret_cast<const CT*>(&v);
+    int e = 0;
+    for (; e + 16 <= cnt; e += 16) {
+      CT v[16];
 #pragma unroll
-          for (int e = 0; e < W; ++e) sC[((j0 + e) & 63) * 64 + lane] = (float)ve[e];
+      for (int u = 0; u < 16; ++u) v[u] = colt[(int64_t)slist[c0 + e + u] * ldc];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u] * sdelta[c0 + e + u];
+    }
+    for (; e < cnt; ++e) acc += colt[(int64_t)slist[c0 + e] * ldc] * sdelta[c0 + e];
+#ifdef ENET_PROF
+    if (lane == 0) atomicAdd(&enet_prof[q][5], (unsigned long long)cnt);
+#endif
+    // wave 0 (the recurrence) keeps its lane's row of the 64x64 diagonal block in
+    // registers: dg_lo[i] / dg_hi[i-32] = C[t*64+lane][t*64+i] (uniform-index reads
+    // lower to s_set_gpr_idx, no LDS or memory latency on the update chain)
+    if (wid == 0) {
+      const int r = t * 64 + lane;
+      if (r < p) {
+        const V* rowv = reinterpret_cast<const V*>(Cq + (int64_t)r * ldc + t * 64);
+#pragma unroll
+        for (int c = 0; c < 32 / W; ++c) {
+          const V a = rowv[c], b = rowv[c + 32 / W];
+          const CT* ea = reinterpret_cast<const CT*>(&a);
+          const CT* eb = reinterpret_cast<const CT*>(&b);
+#pragma unroll
+          for (int e2 = 0; e2 < W; ++e2) {
+            dg_lo[c * W + e2] = (float)ea[e2];
+            dg_hi[c * W + e2] = (float)eb[e2];
+          }
         }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 32; ++c) { dg_lo[c] = 0.f; dg_hi[c] = 0.f; }
       }
-    } else {
-      // padding rows of the last block: zero diagonal entries so the recurrence ignores them
-      for (int j = c0; j < c0 + cw; ++j)
-        if ((j >> 6) == t) sC[(j & 63) * 64 + lane] = 0.f;
     }
     spart[wid][lane] = (double)acc;
     __syncthreads();
@@ -251,7 +292,11 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
       const int k = t * 64 + lane;
       // active pass: a block without active coordinates cannot change (skip, no pull)
       if (!full && !__ballot((sflag[k] & 3) == 3)) continue;
+      PROF_T(t0_);
       pull(t);
+      PROF_T(t1_);
+      PROF_ADD(0, t1_ - t0_);
+      PROF_ADD(3, 1);
       if (wid == 0) {
         double gt = sg[k], at = sa[k];
         const double vpt = svp[k];
@@ -259,28 +304,34 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         const bool elig = (fl & 1) && (full || (fl & 2));
         const double thr_l = vpt * ab;
         const double rden = dem == 0.0 ? 1.0 : 1.0 / (1.0 + vpt * dem);
-        double dblk = 0.0;
+        // Each lane changes at most once per visit (lane > last), so its bookkeeping is
+        // deferred: keep the delta and the gradient it was computed from, and fold the
+        // R^2 / convergence / active-flag updates in after the loop. The loop body is
+        // the bare coordinate recurrence (~18 instructions).
+        double dblk = 0.0, gbef = 0.0;
         int last = -1;
         while (true) {
           const double u = gt + at;
-          const bool cand = elig && lane > last && (at != 0.0 || fabs(u) > thr_l);
-          const uint64_t msk = __ballot(cand);
+          const bool cand = elig & (lane > last) & ((at != 0.0) | (fabs(u) > thr_l));
+          const uint64_t msk = __builtin_amdgcn_ballot_w64(cand);
           if (!msk) break;
           const int i = __ffsll((unsigned long long)msk) - 1;
           last = i;
+          const float clo = dg_lo[i & 31], chi = dg_hi[i & 31];   // masked: stays in VGPRs
+          const float ci = i < 32 ? clo : chi;
           const double v = fabs(u) - thr_l;
           const double an = v > 0.0 ? copysign(v, u) * rden : 0.0;
-          const double dl = an - at;
-          const double d = readlane_d(dl, i);
-          if (d == 0.0) continue;
-          if (lane == i) {
-            rsq_l += d * (2.0 * gt - d);
-            dlx_l = fmax(dlx_l, d * d);
-            at = an;
-            fl |= 2;
-            dblk = d;
-          }
-          gt -= (double)sC[i * 64 + lane] * d;
+          const double d = readlane_d(an - at, i);
+          const bool me = lane == i;
+          at = me ? an : at;               // d == 0 -> an == at
+          gbef = me ? gt : gbef;
+          dblk = me ? d : dblk;
+          gt -= (double)ci * d;
+        }
+        if (dblk != 0.0) {
+          rsq_l += dblk * (2.0 * gbef - dblk);
+          dlx_l = fmax(dlx_l, dblk * dblk);
+          fl |= 2;
         }
         sg[k] = gt;
         sa[k] = at;
@@ -289,6 +340,8 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         sds[t][k] += dblk;       // own changes are already in g_t
       }
       __syncthreads();
+      PROF_T(t2_);
+      PROF_ADD(1, t2_ - t1_);
     }
     const double dlx = wave_max(dlx_l);
     if (tid == 0) sdl = dlx;
@@ -394,6 +447,16 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     if (!is_fold) publish(1 << 30);
   }
 }
+
+#ifdef ENET_PROF
+extern "C" __attribute__((visibility("default"))) int ate_enet_prof_read(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(enet_prof), sizeof(enet_prof));
+}
+extern "C" __attribute__((visibility("default"))) int ate_enet_prof_reset() {
+  static unsigned long long z[256][8];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(enet_prof), z, sizeof(z));
+}
+#endif
 
 ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny, const void* ju,
                           const void* ys, const void* vp, const void* probs, int nprob,
