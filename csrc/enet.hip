@@ -182,6 +182,12 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   __shared__ double spart[4][64];
   __shared__ __attribute__((aligned(16))) CT sdelta[PMAX];
   __shared__ int slist[PMAX];             // compacted pending columns (per-wave quarters)
+  __shared__ int slist2[576];             // pipelined pull: waves 1-3, 192 entries each
+  __shared__ __attribute__((aligned(16))) CT sdelta2[576];
+  __shared__ int scl[64];                 // wave 0: changed coordinates of the block
+  __shared__ CT scd[64];
+  __shared__ float sCn[64 * 64];          // next block's diagonal block
+  __shared__ int svis[8], snv, sblk_any[8];
   __shared__ double sdl;
   __shared__ int sany;
   __shared__ double slam;
@@ -286,29 +292,83 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     __syncthreads();
   };
 
+  // Pipelined pass. Wave 0 runs the sequential recurrence of block t (diagonal block in
+  // registers) and then applies block t's own deltas to block tn = next visited block
+  // (contiguous row segments C[k][tn*64..]); meanwhile waves 1-3 pull every OTHER change
+  // pending for block tn (sdc is frozen until the first barrier) and stage tn's diagonal
+  // block in LDS. After the barrier wave 0 publishes block t, completes block tn's
+  // gradient and snapshot, and moves tn's diagonal block into registers.
+  auto pull_rest = [&](int tn) {            // waves 1..3
+    const int my = wid - 1;
+    int cnt = 0;
+    const int base0 = my * 192;             // private slist/sdelta region (<= 3 * 192 = 576)
+    for (int c = my; c < T; c += 3) {
+      const int j = c * 64 + lane;
+      const double dj = sdc[j] - sds[tn][j];
+      const bool nz = dj != 0.0;
+      const uint64_t bal = __ballot(nz);
+      const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+      if (nz) { slist2[base0 + pos] = j; sdelta2[base0 + pos] = (CT)dj; }
+      cnt += __popcll(bal);
+    }
+    const CT* colt = Cq + tn * 64 + lane;
+    CT acc = 0;
+    int e = 0;
+    for (; e + 16 <= cnt; e += 16) {
+      CT v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u] * sdelta2[base0 + e + u];
+    }
+    for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
+    spart[wid][lane] = (double)acc;
+    for (int i = my; i < 64; i += 3) {
+      const int r = tn * 64 + i;
+      sCn[i * 64 + lane] = r < p ? (float)Cq[(int64_t)r * ldc + tn * 64 + lane] : 0.f;
+    }
+  };
+
   auto pass = [&](bool full) -> double {
     double dlx_l = 0.0;
-    for (int t = 0; t < T; ++t) {
+    for (int t = wid; t < T; t += 4) {      // blocks holding an active coordinate
+      const bool a = full || ((sflag[t * 64 + lane] & 3) == 3);
+      const uint64_t b = __builtin_amdgcn_ballot_w64(a);
+      if (lane == 0) sblk_any[t] = b != 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int nv = 0;
+      for (int t = 0; t < T; ++t)
+        if (sblk_any[t]) svis[nv++] = t;
+      snv = nv;
+    }
+    __syncthreads();
+    const int nv = snv;
+    if (nv == 0) return 0.0;
+    PROF_T(tp0_);
+    pull(svis[0]);
+    PROF_T(tp1_);
+    PROF_ADD(0, tp1_ - tp0_);
+    for (int v = 0; v < nv; ++v) {
+      const int t = svis[v];
+      const int tn = v + 1 < nv ? svis[v + 1] : -1;
       const int k = t * 64 + lane;
-      // active pass: a block without active coordinates cannot change (skip, no pull)
-      if (!full && !__ballot((sflag[k] & 3) == 3)) continue;
-      PROF_T(t0_);
-      pull(t);
-      PROF_T(t1_);
-      PROF_ADD(0, t1_ - t0_);
-      PROF_ADD(3, 1);
+      PROF_T(ta_);
+      double gt = 0.0, at = 0.0, dblk = 0.0;
+      int fl = 0;
       if (wid == 0) {
-        double gt = sg[k], at = sa[k];
+        gt = sg[k];
+        at = sa[k];
         const double vpt = svp[k];
-        int fl = sflag[k];
+        fl = sflag[k];
         const bool elig = (fl & 1) && (full || (fl & 2));
         const double thr_l = vpt * ab;
         const double rden = dem == 0.0 ? 1.0 : 1.0 / (1.0 + vpt * dem);
-        // Each lane changes at most once per visit (lane > last), so its bookkeeping is
-        // deferred: keep the delta and the gradient it was computed from, and fold the
-        // R^2 / convergence / active-flag updates in after the loop. The loop body is
-        // the bare coordinate recurrence (~18 instructions).
-        double dblk = 0.0, gbef = 0.0;
+        // Each lane changes at most once per visit (lane > last): its bookkeeping is
+        // deferred (delta + the gradient it was computed from), so the loop body is the
+        // bare coordinate recurrence.
+        double gbef = 0.0;
         int last = -1;
         while (true) {
           const double u = gt + at;
@@ -319,8 +379,8 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
           last = i;
           const float clo = dg_lo[i & 31], chi = dg_hi[i & 31];   // masked: stays in VGPRs
           const float ci = i < 32 ? clo : chi;
-          const double v = fabs(u) - thr_l;
-          const double an = v > 0.0 ? copysign(v, u) * rden : 0.0;
+          const double vv = fabs(u) - thr_l;
+          const double an = vv > 0.0 ? copysign(vv, u) * rden : 0.0;
           const double d = readlane_d(an - at, i);
           const bool me = lane == i;
           at = me ? an : at;               // d == 0 -> an == at
@@ -333,15 +393,53 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
           dlx_l = fmax(dlx_l, dblk * dblk);
           fl |= 2;
         }
+        // block t's own deltas -> block tn (wave-private list, contiguous segments)
+        CT corr = 0;
+        if (tn >= 0) {
+          const bool ch = dblk != 0.0;
+          const uint64_t bal = __builtin_amdgcn_ballot_w64(ch);
+          const int pos = __popcll(bal & ((1ull << lane) - 1ull));
+          if (ch) { scl[pos] = k; scd[pos] = (CT)dblk; }
+          const int nc = __popcll(bal);
+          const CT* colt = Cq + tn * 64 + lane;
+          int e = 0;
+          for (; e + 16 <= nc; e += 16) {
+            CT w[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) w[u] = colt[(int64_t)scl[e + u] * ldc];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) corr += w[u] * scd[e + u];
+          }
+          for (; e < nc; ++e) corr += colt[(int64_t)scl[e] * ldc] * scd[e];
+        }
+        spart[0][lane] = (double)corr;
+      } else if (tn >= 0) {
+        pull_rest(tn);
+      }
+      __syncthreads();
+      PROF_T(tb_);
+      PROF_ADD(1, tb_ - ta_);
+      PROF_ADD(3, 1);
+      if (wid == 0) {
         sg[k] = gt;
         sa[k] = at;
         sflag[k] = fl;
         sdc[k] += dblk;
         sds[t][k] += dblk;       // own changes are already in g_t
+        if (tn >= 0) {
+          const int kn = tn * 64 + lane;
+          sg[kn] -= spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane];
+          for (int j = lane; j < ldc; j += 64) sds[tn][j] = sdc[j];
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            dg_lo[i] = sCn[i * 64 + lane];
+            dg_hi[i] = sCn[(i + 32) * 64 + lane];
+          }
+        }
       }
       __syncthreads();
-      PROF_T(t2_);
-      PROF_ADD(1, t2_ - t1_);
+      PROF_T(tc_);
+      PROF_ADD(0, tc_ - tb_);
     }
     const double dlx = wave_max(dlx_l);
     if (tid == 0) sdl = dlx;
