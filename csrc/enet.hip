@@ -323,9 +323,21 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     }
     for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     spart[wid][lane] = (double)acc;
-    for (int i = my; i < 64; i += 3) {
-      const int r = tn * 64 + i;
-      sCn[i * 64 + lane] = r < p ? (float)Cq[(int64_t)r * ldc + tn * 64 + lane] : 0.f;
+    // tn's diagonal block -> LDS: rows my + 3*ii in two batches of 11 loads in flight
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2) {
+      float dr[11];
+#pragma unroll
+      for (int ii = 0; ii < 11; ++ii) {
+        const int i = my + 3 * (b2 * 11 + ii);
+        const int r = tn * 64 + i;
+        dr[ii] = (i < 64 && r < p) ? (float)Cq[(int64_t)r * ldc + tn * 64 + lane] : 0.f;
+      }
+#pragma unroll
+      for (int ii = 0; ii < 11; ++ii) {
+        const int i = my + 3 * (b2 * 11 + ii);
+        if (i < 64) sCn[i * 64 + lane] = dr[ii];
+      }
     }
   };
 
@@ -413,8 +425,15 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
           for (; e < nc; ++e) corr += colt[(int64_t)scl[e] * ldc] * scd[e];
         }
         spart[0][lane] = (double)corr;
+#ifdef ENET_PROF
+        if (lane == 0) atomicAdd(&enet_prof[q][2], (unsigned long long)(wall_clock64() - ta_));
+#endif
       } else if (tn >= 0) {
         pull_rest(tn);
+#ifdef ENET_PROF
+        if (wid == 1 && lane == 0)
+          atomicAdd(&enet_prof[q][4], (unsigned long long)(wall_clock64() - ta_));
+#endif
       }
       __syncthreads();
       PROF_T(tb_);
