@@ -443,18 +443,24 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         sg[k] = gt;
         sa[k] = at;
         sflag[k] = fl;
-        sdc[k] += dblk;
+        const double dnew = sdc[k] + dblk;
+        sdc[k] = dnew;
         sds[t][k] += dblk;       // own changes are already in g_t
         if (tn >= 0) {
           const int kn = tn * 64 + lane;
           sg[kn] -= spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane];
-          for (int j = lane; j < ldc; j += 64) sds[tn][j] = sdc[j];
+          sds[tn][k] = dnew;     // block t's columns; waves 1-3 copy the others
+
 #pragma unroll
           for (int i = 0; i < 32; ++i) {
             dg_lo[i] = sCn[i * 64 + lane];
             dg_hi[i] = sCn[(i + 32) * 64 + lane];
           }
         }
+      } else if (tn >= 0) {
+        // snapshot of block tn for every column block except t (unchanged since B1)
+        for (int j = (wid - 1) * 64 + lane; j < ldc; j += 192)
+          if ((j >> 6) != t) sds[tn][j] = sdc[j];
       }
       __syncthreads();
       PROF_T(tc_);
