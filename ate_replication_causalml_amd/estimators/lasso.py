@@ -12,6 +12,7 @@ import torch
 
 from .. import _native
 from ..ops import stats as S
+from ..ops.devconst import const
 from ..ops.enet import cv_enet_gaussian
 from ..ops.gram import gram
 from ..ops.linalg import chol_solve
@@ -172,8 +173,8 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
             moms += S.dml_moments(yr[v], wr[v])
         return moms
     dev = pan.device
-    xc = torch.tensor(pan.xcols, dtype=torch.int32, device=dev)
-    segs = torch.tensor(np.asarray(pan.seg_bounds[:K], dtype=np.int64), device=dev)
+    xc = const(pan.xcols, torch.int32, dev)
+    segs = const(np.asarray(pan.seg_bounds[:K], dtype=np.int64), torch.int64, dev)
     bf = pan.dtype == torch.bfloat16
     # bf16: 2048 rows per block; enough blocks per fold to fill 256 CUs several times
     nbx = 512 if bf else 256

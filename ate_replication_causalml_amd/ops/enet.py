@@ -20,6 +20,7 @@ import torch
 
 from .. import _native
 from ..reference import glmnet as ref
+from .devconst import const, const_bytes
 
 
 def _stream():
@@ -127,8 +128,7 @@ _PROB_DT = np.dtype([("train", "<i4"), ("y", "<i4"), ("src", "<i4"), ("nlam", "<
 
 
 def _probs_tensor(probs, dev):
-    a = np.array(probs, dtype=_PROB_DT)
-    return torch.from_numpy(a.view(np.uint8).copy()).to(dev)
+    return const_bytes(np.array(probs, dtype=_PROB_DT), dev)
 
 
 def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_probs, fold_ycol,
@@ -138,9 +138,9 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     s = _stream()
     f64 = dict(dtype=torch.float64, device=dev)
     nt = masks.shape[0]
-    masks_t = torch.from_numpy(masks).to(dev)
-    xc = torch.tensor(xcols, dtype=torch.int32, device=dev)
-    yc = torch.tensor(ycols, dtype=torch.int32, device=dev)
+    masks_t = const(masks, torch.uint8, dev)
+    xc = const(xcols, torch.int32, dev)
+    yc = const(ycols, torch.int32, dev)
     c_f32 = int(panel_dtype != torch.float64)
     ldc = (p + 63) // 64 * 64   # zero-padded row stride (16-B aligned row segments)
     C = torch.zeros((nt, p, ldc), dtype=torch.float32 if c_f32 else torch.float64, device=dev)
@@ -154,7 +154,7 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     _native.call("ate_enet_prepare", G.data_ptr(), nseg, P, masks_t.data_ptr(), nt, xc.data_ptr(),
                  p, one, yc.data_ptr(), ny, C.data_ptr(), c_f32, g.data_ptr(), xm.data_ptr(),
                  xs.data_ptr(), ju.data_ptr(), ym.data_ptr(), ys.data_ptr(), nobs.data_ptr(), s)
-    vp_t = torch.tensor(vp, **f64)
+    vp_t = const(np.asarray(vp, dtype=np.float64), torch.float64, dev)
     # ONE launch: full problems [0, nf) + fold problems [nf, nq); fold problems consume
     # their source's lambda sequence as it is published (device-side progress flags)
     nf = len(full_probs)
@@ -175,14 +175,14 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     _native.call("ate_enet_coef", apath.data_ptr(), pr.data_ptr(), nq, p, ny, L,
                  nlam.data_ptr(), xm.data_ptr(), xs.data_ptr(), ju.data_ptr(), ym.data_ptr(),
                  ys.data_ptr(), coef.data_ptr(), s)
-    hold = torch.tensor([0] * nf + list(fold_holds), dtype=torch.int32, device=dev)
-    ycol_p = torch.tensor([0] * nf + list(fold_ycol), dtype=torch.int32, device=dev)
+    hold = const([0] * nf + list(fold_holds), torch.int32, dev)
+    ycol_p = const([0] * nf + list(fold_ycol), torch.int32, dev)
     cvraw = torch.empty((nq, L), **f64)
     _native.call("ate_enet_cvloss_gauss", G.data_ptr(), P, hold.data_ptr(), xc.data_ptr(), p, one,
                  ycol_p.data_ptr(), coef.data_ptr(), nlam.data_ptr(), L, nq,
                  cvraw.data_ptr(), s)
-    fidx = torch.from_numpy(fold_index + nf).to(dev)
-    nfold_t = torch.from_numpy(nfold).to(dev)
+    fidx = const(fold_index + nf, torch.int32, dev)
+    nfold_t = const(nfold, torch.float64, dev)
     cvm = torch.empty((nf, L), **f64)
     cvsd = torch.empty((nf, L), **f64)
     sel = torch.empty((nf, 2), dtype=torch.int32, device=dev)

@@ -46,7 +46,8 @@ def main():
     # an Amdahl term every rank repeats (use --scaling strong to measure that).
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--seed", type=int, default=1991)
-    ap.add_argument("--graph", type=int, default=0, help="capture the step in a hipGraph")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the step in a hipGraph (default: on for 1 GPU, off with RCCL)")
     args = ap.parse_args()
 
     import torch
@@ -76,14 +77,17 @@ def main():
         res, _, _ = dml_crossfit_panel(pan, args.folds, "min", comm=comm, seg_counts=seg_counts)
         return res
 
+    from ate_replication_causalml_amd.utils.graphs import maybe_graphed
+    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    run, graphed = maybe_graphed(step, use_graph and device.type == "cuda")
     for _ in range(args.warmup):
-        res = step()
+        res = run()
     sync()
     comm.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step()
+        res = run()
     sync()
     comm.barrier()
     sync()
@@ -121,6 +125,7 @@ def main():
             },
             "ate": ate,
             "se": se,
+            "hipgraph": graphed,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
