@@ -282,10 +282,27 @@ class Replication:
         return format_table(self.results)
 
 
+def _result_arrays(r: AteResult) -> dict:
+    import json
+    return {"method": np.array(r.method), "vals": np.array([r.ate, r.se, r.lower_ci, r.upper_ci]),
+            "diag": np.array(json.dumps(r.diagnostics, default=str))}
+
+
+def _result_from(d: dict) -> AteResult:
+    import json
+    v = d["vals"]
+    return AteResult(str(d["method"]), float(v[0]), float(v[1]), float(v[2]), float(v[3]),
+                     json.loads(str(d["diag"])))
+
+
 def replicate(data=None, config: ReplicateConfig | None = None, log_path=None, plot_path=None,
-              verbose=False) -> Replication:
+              verbose=False, checkpoint_dir=None) -> Replication:
     """ate_replication.Rmd end to end: oracle on the RCT sample, selection bias
-    (pt=pc=0.85), then the 13 estimators on df_mod in the driver's order."""
+    (pt=pc=0.85), then the 13 estimators on df_mod in the driver's order.
+
+    ``checkpoint_dir``: every finished row is saved there (utils/checkpoint.py, keyed by
+    the config and a fingerprint of the data); a rerun loads finished rows and computes
+    only the missing ones — identical results, since every random draw is keyed by seed."""
     from .data.dgp import make_tutorial_data
     from .data.selection import apply_selection_bias
     cfg = config or ReplicateConfig()
@@ -296,12 +313,22 @@ def replicate(data=None, config: ReplicateConfig | None = None, log_path=None, p
     Y, W, X = mod.Y, mod.W, mod.X
     want = set(cfg.include) if cfg.include else set(METHODS)
     results, secs = [], {}
+    ck, dkey = None, ""
+    if checkpoint_dir is not None:
+        from .utils.checkpoint import Checkpoint, fingerprint
+        ck = Checkpoint(checkpoint_dir, cfg.to_dict())
+        dkey = fingerprint(Y, W, X, data.Y, data.W)
 
     def add(label, fn):
         if label not in want:
             return None
         t0 = time.perf_counter()
-        r = fn()
+        if ck is not None and ck.has(label, dkey):
+            r = _result_from(ck.load(label, dkey))
+        else:
+            r = fn()
+            if ck is not None:
+                ck.save(label, dkey, **_result_arrays(r))
         secs[label] = time.perf_counter() - t0
         if verbose:
             print(f"{label:45s} {r.ate:9.4f}  ({secs[label]:.2f}s)", flush=True)
@@ -311,19 +338,26 @@ def replicate(data=None, config: ReplicateConfig | None = None, log_path=None, p
     add("oracle", lambda: ate_naive(data.Y, data.W, method="oracle", run=run))
     add("naive", lambda: ate_naive(Y, W, run=run))
     add("Direct Method", lambda: ate_ols(Y, W, X, run=run))
-    p_log = None
-    if want & {"Propensity_Weighting", "Propensity_Regression"}:
-        t0 = time.perf_counter()
-        p_log = propensity_logistic(W, X, run=run)
-        secs["propensity_logistic"] = time.perf_counter() - t0
-    add("Propensity_Weighting", lambda: ate_ipw(Y, W, X, p_log, run=run))
-    add("Propensity_Regression", lambda: ate_ipw_wls(Y, W, p_log, run=run))
-    if "Propensity_Weighting_LASSOPS" in want:
-        t0 = time.perf_counter()
-        p_las = propensity_lasso(W, X, run=run)
-        secs["propensity_lasso"] = time.perf_counter() - t0
-        add("Propensity_Weighting_LASSOPS",
-            lambda: ate_ipw(Y, W, X, p_las, method="Propensity_Weighting_LASSOPS", run=run))
+    cache = {}
+
+    def p_log():
+        if "log" not in cache:
+            t0 = time.perf_counter()
+            cache["log"] = propensity_logistic(W, X, run=run)
+            secs["propensity_logistic"] = time.perf_counter() - t0
+        return cache["log"]
+
+    def p_las():
+        if "las" not in cache:
+            t0 = time.perf_counter()
+            cache["las"] = propensity_lasso(W, X, run=run)
+            secs["propensity_lasso"] = time.perf_counter() - t0
+        return cache["las"]
+
+    add("Propensity_Weighting", lambda: ate_ipw(Y, W, X, p_log(), run=run))
+    add("Propensity_Regression", lambda: ate_ipw_wls(Y, W, p_log(), run=run))
+    add("Propensity_Weighting_LASSOPS",
+        lambda: ate_ipw(Y, W, X, p_las(), method="Propensity_Weighting_LASSOPS", run=run))
     add("Single-equation LASSO", lambda: ate_lasso_single(Y, W, X, run=run))
     add("Usual LASSO", lambda: ate_lasso(Y, W, X, run=run))
     add("Doubly Robust with Random Forest PS",

@@ -24,7 +24,8 @@ def _replicate(a):
                           include=tuple(a.only) if a.only else None,
                           run=RunConfig(backend=a.backend, dtype=a.dtype, compat=a.compat,
                                         seed=a.seed))
-    rep = replicate(data, cfg, log_path=a.log, plot_path=a.plot, verbose=a.verbose)
+    rep = replicate(data, cfg, log_path=a.log, plot_path=a.plot, verbose=a.verbose,
+                    checkpoint_dir=a.checkpoint)
     print(f"rows dropped by selection bias: {rep.n_dropped}  (df_mod n={rep.n_mod})")
     print(rep.table())
     if a.trace:
@@ -72,6 +73,7 @@ def main(argv=None):
     r.add_argument("--log", help="append results as JSONL")
     r.add_argument("--plot", help="write the pointrange plot (png)")
     r.add_argument("--trace", help="append tracing spans as JSONL")
+    r.add_argument("--checkpoint", help="directory for per-row results (resume)")
     r.add_argument("--json", action="store_true")
     r.add_argument("-v", "--verbose", action="store_true")
     r.set_defaults(fn=_replicate)

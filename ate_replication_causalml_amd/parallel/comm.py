@@ -167,6 +167,9 @@ def from_env():
         import torch.distributed as dist
         if not dist.is_initialized():
             backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # RCCL errors (a failed peer, a timed-out collective) abort the process
+            # instead of leaving the other ranks blocked
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
             if backend == "nccl":
                 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
             dist.init_process_group(backend=backend)

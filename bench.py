@@ -80,6 +80,12 @@ def main():
     from ate_replication_causalml_amd.utils.graphs import maybe_graphed
     use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
     run, graphed = maybe_graphed(step, use_graph and device.type == "cuda")
+    import contextlib
+    from ate_replication_causalml_amd.utils.guards import collective_timeout
+    # a dead peer must end the job with a message, not hang the other ranks in RCCL
+    guard = collective_timeout(float(os.environ.get("ATE_COLLECTIVE_TIMEOUT", "900")),
+                               "bench step") if world > 1 else contextlib.nullcontext()
+    guard.__enter__()
     for _ in range(args.warmup):
         res = run()
     sync()
@@ -97,6 +103,7 @@ def main():
         import torch.distributed as dist
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    guard.__exit__(None, None, None)
     ms = elapsed / args.steps * 1e3
     ate, se = [float(v) for v in res.detach().cpu()]
     rows_per_s = n_total / (ms / 1e3)
