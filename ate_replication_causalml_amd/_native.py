@@ -61,14 +61,12 @@ _SIGS = {
     "ate_bin_matrix": "plipppp",
     "ate_panel_xtv": "iplpipplipp",
     "ate_select_compact": "plppddpppp" + "p",
-    "ate_gbdt_grad": "ippplppp" + "p",
-    "ate_gbdt_hist": "plpplii" + "pp",
-    "ate_gbdt_split": "piiiidlddppppp",
-    "ate_gbdt_partition": "plplippp",
+    "ate_gbdt_fit": "ppp",
+    "ate_gbdt_slab_entries": "liii",
     "ate_gbdt_apply": "plliipppp" + "p",
     "ate_panel_xv": "iplpipiplpp",
 }
-_RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64}
+_RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}
 
 

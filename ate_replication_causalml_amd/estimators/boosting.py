@@ -31,17 +31,22 @@ def dml_plr_gbdt(Y, W, X, folds=5, n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
     fid = dist.fold_ids(folds, seed, fold_stream) if dist is not None else \
         rng.fold_ids(n, folds, seed, fold_stream)
     backend = "gpu" if dev.type == "cuda" else "cpu"
-    edges = G.global_bin_edges(Xn, dist)
+    edges = G.global_bin_edges(Xn, dist, device=dev)
+    Xb = G.binned(Xn, edges, dev)          # binned once, shared by all 2K fits
     ey = np.empty(n)
     ew = np.empty(n)
     kw = dict(n_trees=n_trees, depth=depth, lr=lr, lam=lam, min_child=min_child,
-              backend=backend, edges=edges, dist=dist)
+              backend=backend, edges=edges, dist=dist, Xb=Xb)
+
+    def response(m):
+        f = m.scores.cpu().numpy() if isinstance(m.scores, torch.Tensor) else m.scores
+        return 1.0 / (1.0 + np.exp(-f)) if m.loss == "logistic" else f
+
     for k in range(folds):
         ho = fid == k
-        my = G.fit_gbdt(Xn, Yn, loss=_loss(Yn), train=~ho, **kw)
-        mw = G.fit_gbdt(Xn, Wn, loss=_loss(Wn), train=~ho, **kw)
-        ey[ho] = my.predict(Xn[ho], response=True)
-        ew[ho] = mw.predict(Xn[ho], response=True)
+        # held-out predictions = the trainer's running scores of the rows it skipped
+        ey[ho] = response(G.fit_gbdt(None, Yn, loss=_loss(Yn), train=~ho, **kw))[ho]
+        ew[ho] = response(G.fit_gbdt(None, Wn, loss=_loss(Wn), train=~ho, **kw))[ho]
     yr = torch.as_tensor(Yn - ey, device=dev)
     wr = torch.as_tensor(Wn - ew, device=dev)
     mom = S.dml_moments(yr, wr).clone()

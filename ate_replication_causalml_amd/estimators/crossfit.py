@@ -59,11 +59,16 @@ def _glm_fit_predict(Xtr, ytr, Xho, dev):
     return 1.0 / (1.0 + np.exp(-eta))
 
 
-def _gbdt_fit_predict(Xtr, ytr, Xho, dev, seed, gbdt_kw):
+def _gbdt_fit_predict(y, train, ho, Xb, edges, dev, seed, gbdt_kw):
+    """Trees learn from ``train`` rows of the shared binned panel; the held-out
+    predictions are the trainer's final scores of the ``ho`` rows."""
     from ..models import gbdt as G
-    loss = "logistic" if _binary(ytr) else "squared"
-    m = G.fit_gbdt(Xtr, ytr, loss=loss, seed=seed, backend=_backend(dev), **(gbdt_kw or {}))
-    return m.predict(Xho, response=True)
+    loss = "logistic" if _binary(y[train]) else "squared"
+    m = G.fit_gbdt(None, y, loss=loss, train=train, seed=seed, backend=_backend(dev),
+                   edges=edges, Xb=Xb, **(gbdt_kw or {}))
+    f = m.scores.cpu().numpy() if isinstance(m.scores, torch.Tensor) else m.scores
+    f = f[ho]
+    return 1.0 / (1.0 + np.exp(-f)) if loss == "logistic" else f
 
 
 def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold_stream=11,
@@ -76,6 +81,10 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
     mu1 = np.empty(n)
     mu0 = np.empty(n)
     edges = F.bin_edges(Xn) if learner == "rf" else None
+    if learner == "gbdt":
+        from ..models import gbdt as G
+        edges = G.sample_bin_edges(Xn, device=dev)
+        Xb = G.binned(Xn, edges, dev)
     for k in range(folds):
         ho = fid == k
         tr = ~ho
@@ -91,9 +100,9 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
             mu1[ho] = _glm_fit_predict(Xn[t1], Yn[t1], Xho, dev)
             mu0[ho] = _glm_fit_predict(Xn[t0], Yn[t0], Xho, dev)
         elif learner == "gbdt":
-            e[ho] = _gbdt_fit_predict(Xn[tr], Wn[tr], Xho, dev, s, gbdt_kw)
-            mu1[ho] = _gbdt_fit_predict(Xn[t1], Yn[t1], Xho, dev, s + 1, gbdt_kw)
-            mu0[ho] = _gbdt_fit_predict(Xn[t0], Yn[t0], Xho, dev, s + 2, gbdt_kw)
+            e[ho] = _gbdt_fit_predict(Wn, tr, ho, Xb, edges, dev, s, gbdt_kw)
+            mu1[ho] = _gbdt_fit_predict(Yn, t1, ho, Xb, edges, dev, s + 1, gbdt_kw)
+            mu0[ho] = _gbdt_fit_predict(Yn, t0, ho, Xb, edges, dev, s + 2, gbdt_kw)
         else:
             raise ValueError(learner)
     e = np.clip(e, clip, 1 - clip)

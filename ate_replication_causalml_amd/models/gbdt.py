@@ -32,6 +32,7 @@ class GbdtModel:
     depth: int
     edges: tuple
     backend: str
+    scores: object = None  # raw boosting score of every row seen in training (train or not)
 
     @property
     def n_trees(self):
@@ -45,11 +46,13 @@ class GbdtModel:
         return 1.0 / (1.0 + np.exp(-f)) if (response and self.loss == "logistic") else f
 
     def predict_binned(self, Xb):
+        """Xb: column-major [p][n] bins (models/forest.py::bin_matrix)."""
         n = Xb.shape[1]
         if self.backend == "gpu":
+            Xr, ldr = _to_rowmajor(Xb)
             f = torch.full((n,), self.base, dtype=torch.float64, device=Xb.device)
             M = self.feat.shape[1]
-            _native.call("ate_gbdt_apply", Xb.data_ptr(), n, n, self.n_trees, M,
+            _native.call("ate_gbdt_apply", Xr.data_ptr(), ldr, n, self.n_trees, M,
                          self.feat.data_ptr(), self.thr.data_ptr(), self.value.data_ptr(),
                          f.data_ptr(), torch.cuda.current_stream().cuda_stream)
             return f.cpu().numpy()
@@ -59,12 +62,52 @@ class GbdtModel:
         return t.predict_binned(Xn)
 
 
-def global_bin_edges(X_local, dist, rows_per_rank=20000):
+EDGE_SAMPLE = 200_000
+
+
+def sample_bin_edges(X, rows=EDGE_SAMPLE, device=None):
+    """Quantile edges from an evenly strided row sample when n is large (the standard
+    histogram-GBDT construction; exact for features with <= 256 distinct values in it).
+    With a GPU ``device`` the sort runs there (models/forest.py::bin_edges_device, same
+    edges bit for bit)."""
+    X = np.asarray(X, dtype=np.float64)
+    n = X.shape[0]
+    if n > rows:
+        X = X[np.linspace(0, n - 1, num=rows).astype(np.int64)]
+    if device is not None and torch.device(device).type == "cuda":
+        return F.bin_edges_device(torch.as_tensor(X, device=device))
+    return F.bin_edges(X)
+
+
+def binned(X, edges, device):
+    """Binned panel for fit_gbdt(Xb=...): device row-major [n][ldr] (ldr % 32 == 0, the
+    layout of csrc/gbdt.hip) or host column-major [p][n] (the numpy reference's)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda":
+        return _rowmajor_bins(X, edges, dev)
+    Xb = F.bin_matrix(np.asarray(X, dtype=np.float64), edges[0], edges[1], None).numpy()
+    return Xb, Xb.shape[1]
+
+
+def _to_rowmajor(Xb):
+    """[p][n] column-major bins -> [n][ldr] row-major, ldr = p rounded up to 32."""
+    p, n = Xb.shape
+    ldr = -(-p // 32) * 32
+    out = torch.zeros((n, ldr), dtype=torch.uint8, device=Xb.device)
+    out[:, :p] = Xb.t()
+    return out, ldr
+
+
+def _rowmajor_bins(X, edges, dev):
+    return _to_rowmajor(F.bin_matrix(np.asarray(X, dtype=np.float64), edges[0], edges[1], dev))
+
+
+def global_bin_edges(X_local, dist, rows_per_rank=20000, device=None):
     """Bin edges every rank agrees on: an evenly strided sample of each shard is
     all-gathered and binned together."""
     X_local = np.asarray(X_local, dtype=np.float64)
     if dist is None or dist.world == 1:
-        return F.bin_edges(X_local)
+        return sample_bin_edges(X_local, device=device)
     n = X_local.shape[0]
     take = np.linspace(0, n - 1, num=min(n, rows_per_rank)).astype(np.int64) if n else \
         np.zeros(0, dtype=np.int64)
@@ -77,13 +120,21 @@ def global_bin_edges(X_local, dist, rows_per_rank=20000):
 
 
 def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0,
-             min_gain=0.0, train=None, backend=None, edges=None, dist=None, seed=0) -> GbdtModel:
+             min_gain=0.0, train=None, backend=None, edges=None, dist=None, seed=0,
+             Xb=None) -> GbdtModel:
     """X [n, p] float, y [n]; ``train`` (bool [n]) restricts the rows the trees learn
-    from (predictions still cover every row). ``seed`` is reserved for row/column
-    subsampling (not used: full-data boosting is deterministic)."""
-    X = np.asarray(X, dtype=np.float64)
+    from; ``model.scores`` holds the final raw score of EVERY row (so held-out
+    predictions come for free). ``Xb=(binned, ld)`` from ``binned()`` reuses one binned
+    panel across fits (X and edges are then only used for bookkeeping). ``seed`` is
+    reserved for row/column subsampling (not used: full-data boosting is deterministic)."""
     y = np.asarray(y, dtype=np.float64)
-    n, p = X.shape
+    if Xb is None:
+        X = np.asarray(X, dtype=np.float64)
+        n, p = X.shape
+    else:
+        n = len(y)
+        p = Xb[0].shape[0] if isinstance(Xb[0], np.ndarray) or Xb[0].device.type == "cpu" \
+            else len(edges[0])
     if depth < 1 or depth > 6:
         raise ValueError("depth must be in [1, 6] (<= 32 nodes per level histogram)")
     if backend is None:
@@ -92,60 +143,108 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
         edges = global_bin_edges(X, dist)
     train = np.ones(n, dtype=bool) if train is None else np.asarray(train, dtype=bool)
     if backend != "gpu":
-        Xb = F.bin_matrix(X, edges[0], edges[1], None).numpy()
+        if Xb is None:
+            Xbh = F.bin_matrix(X, edges[0], edges[1], None).numpy()
+        elif isinstance(Xb[0], torch.Tensor) and Xb[0].device.type == "cuda":
+            Xbh = Xb[0][:, :p].t().cpu().numpy()          # device row-major panel
+        else:
+            Xbh = np.asarray(Xb[0].cpu() if isinstance(Xb[0], torch.Tensor) else Xb[0])
         red = None
         if dist is not None and dist.world > 1:
             def red(a):
                 t = torch.from_numpy(np.ascontiguousarray(a))
                 return dist.sum_(t).numpy()
-        tr = ref.fit(Xb, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
+        tr = ref.fit(Xbh, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
                      hist_reduce=red)
-        return GbdtModel(tr.feat, tr.thr, tr.value, tr.base, loss, depth, edges, "cpu")
+        return GbdtModel(tr.feat, tr.thr, tr.value, tr.base, loss, depth, edges, "cpu",
+                         tr.predict_binned(Xbh))
     dev = torch.device("cuda", torch.cuda.current_device())
-    s = torch.cuda.current_stream().cuda_stream
-    Xb = F.bin_matrix(X, edges[0], edges[1], dev)
+    Xr, ldr = Xb if Xb is not None else _rowmajor_bins(X, edges, dev)
+    return _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
+                    edges, dist, dev)
+
+
+class FitArgs(ctypes.Structure):
+    """Mirror of csrc/gbdt.hip::GbdtFitArgs."""
+    P = ctypes.c_void_p
+    _fields_ = [("Xr", P), ("ldr", ctypes.c_int64), ("n", ctypes.c_int64),
+                ("n_train", ctypes.c_int64), ("p", ctypes.c_int), ("depth", ctypes.c_int),
+                ("n_trees", ctypes.c_int), ("loss", ctypes.c_int), ("rule", ctypes.c_int),
+                ("W", ctypes.c_int), ("lam", ctypes.c_double), ("min_gain", ctypes.c_double),
+                ("lr", ctypes.c_double), ("min_child", ctypes.c_int64), ("R", ctypes.c_int64),
+                ("y", P), ("f", P), ("idx", P * 2), ("gh", P * 2), ("bkt", P), ("cnt", P),
+                ("base", P), ("btot", P), ("seg", P * 2), ("tot", P), ("feat", P), ("thr", P),
+                ("value", P), ("H", P * 2), ("slab", P), ("slab_cap", ctypes.c_int64),
+                ("cand", P)]
+
+
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64)
+MAXB = 65
+
+
+def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain, edges,
+             dist, dev):
+    n = len(y)
     yt = torch.as_tensor(y, device=dev)
-    trt = torch.as_tensor(train.astype(np.uint8), device=dev)
-    cnt = torch.tensor([float(y[train].sum()), float(train.sum())], dtype=torch.float64,
-                       device=dev)
+    trn = torch.as_tensor(train, device=dev)
+    order = torch.cat([torch.nonzero(trn).flatten(), torch.nonzero(~trn).flatten()])
+    n_train = int(train.sum())
+    cnt = torch.tensor([float(y[train].sum()), float(n_train)], dtype=torch.float64, device=dev)
     if dist is not None:
         dist.sum_(cnt)
     mean = float(cnt[0] / cnt[1])
     base = mean if loss == "squared" else float(np.log(mean / (1 - mean)))
     M = 2 ** (depth + 1) - 1
-    i64 = dict(dtype=torch.int64, device=dev)
     f = torch.full((n,), base, dtype=torch.float64, device=dev)
-    gh = torch.empty(2 * n, **i64)
-    node = torch.empty(n, dtype=torch.int32, device=dev)
-    root = torch.zeros(2, **i64)
-    tot = torch.zeros(2 * M, **i64)
     feat = torch.full((n_trees, M), -2, dtype=torch.int32, device=dev)
     thr = torch.zeros((n_trees, M), dtype=torch.int32, device=dev)
     value = torch.zeros((n_trees, M), dtype=torch.float64, device=dev)
-    H = torch.empty(2 ** (depth - 1) * p * 512, **i64)
-    mc = int(np.rint(min_child * ref.FIX))
-    for t in range(n_trees):
-        root.zero_()
-        _native.call("ate_gbdt_grad", LOSS[loss], f.data_ptr(), yt.data_ptr(), trt.data_ptr(), n,
-                     gh.data_ptr(), node.data_ptr(), root.data_ptr(), s)
-        if dist is not None:
-            dist.sum_(root)
-        tot[:2] = root
-        ft, th, vt = feat[t], thr[t], value[t]
-        for d in range(depth + 1):
-            nn = 2 ** d
-            if d < depth:
-                Hd = H[:nn * p * 512]
-                Hd.zero_()
-                _native.call("ate_gbdt_hist", Xb.data_ptr(), n, node.data_ptr(), gh.data_ptr(), n,
-                             nn, p, Hd.data_ptr(), s)
-                if dist is not None:
-                    dist.sum_(Hd)
-            _native.call("ate_gbdt_split", H.data_ptr(), nn, p, d, depth, lam, mc, min_gain, lr,
-                         tot.data_ptr(), ft.data_ptr(), th.data_ptr(), vt.data_ptr(), s)
-            if d < depth:
-                _native.call("ate_gbdt_partition", Xb.data_ptr(), n, node.data_ptr(), n, d,
-                             ft.data_ptr(), th.data_ptr(), s)
-        _native.call("ate_gbdt_apply", Xb.data_ptr(), n, n, 1, M, ft.data_ptr(), th.data_ptr(),
-                     vt.data_ptr(), f.data_ptr(), s)
-    return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu")
+    if n_train == 0 or n_trees == 0:
+        # a rank may hold no training rows; it still has to join every collective
+        if dist is not None and dist.world > 1 and n_trees:
+            raise ValueError("row-sharded GBDT needs training rows on every rank")
+        return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu", f)
+    i32 = dict(dtype=torch.int32, device=dev)
+    i64 = dict(dtype=torch.int64, device=dev)
+    R = max(1024, -(-n_train // 1024))
+    R = -(-R // 256) * 256
+    W = -(-n_train // R)
+    idx = [order[:n_train].to(torch.int32).contiguous(), torch.empty(n_train, **i32)]
+    gh = [torch.empty(n_train, **i64), torch.empty(n_train, **i64)]
+    bkt = torch.empty(n_train, dtype=torch.uint8, device=dev)
+    cntb = torch.empty(MAXB * W, **i32)
+    baseb = torch.empty(MAXB * W, **i32)
+    btot = torch.empty(MAXB, **i32)
+    seg = [torch.zeros(MAXB + 1, **i32), torch.zeros(MAXB + 1, **i32)]
+    tot = torch.zeros(2 * M, **i64)
+    H = [torch.empty(2 ** (depth - 1) * p * 512, **i64) for _ in range(2)]
+    rule = 0 if dist is None else 1
+    cap = int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule))
+    slab = torch.empty(cap, **i64)
+    cand = torch.empty(32 * (-(-p // 32)) * 4, **i64)
+    P = ctypes.c_void_p
+    a = FitArgs(Xr=Xr.data_ptr(), ldr=ldr, n=n, n_train=n_train, p=p, depth=depth,
+                n_trees=n_trees, loss=LOSS[loss], rule=rule, W=W, lam=lam,
+                min_gain=min_gain, lr=lr, min_child=int(np.rint(min_child * ref.FIX)), R=R,
+                y=yt.data_ptr(), f=f.data_ptr(), bkt=bkt.data_ptr(), cnt=cntb.data_ptr(),
+                base=baseb.data_ptr(), btot=btot.data_ptr(), tot=tot.data_ptr(),
+                feat=feat.data_ptr(), thr=thr.data_ptr(), value=value.data_ptr(),
+                slab=slab.data_ptr(), slab_cap=cap, cand=cand.data_ptr())
+    a.idx = (P * 2)(idx[0].data_ptr(), idx[1].data_ptr())
+    a.gh = (P * 2)(gh[0].data_ptr(), gh[1].data_ptr())
+    a.seg = (P * 2)(seg[0].data_ptr(), seg[1].data_ptr())
+    a.H = (P * 2)(H[0].data_ptr(), H[1].data_ptr())
+    cb = None
+    if dist is not None:
+        bufs = {tot.data_ptr(): tot, H[0].data_ptr(): H[0], H[1].data_ptr(): H[1]}
+
+        def _reduce(ptr, count):
+            try:
+                dist.sum_(bufs[ptr][:count])
+                return 0
+            except Exception:          # noqa: BLE001 - reported as a non-zero status
+                return 1
+        cb = REDUCE_FN(_reduce)
+    _native.call("ate_gbdt_fit", ctypes.addressof(a), ctypes.cast(cb, ctypes.c_void_p) if cb
+                 else None, torch.cuda.current_stream().cuda_stream)
+    return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu", f)

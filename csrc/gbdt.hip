@@ -1,99 +1,315 @@
 // Histogram gradient-boosted trees (extension nuisance learner, BASELINE config 5).
 // Spec and numpy reference: ate_replication_causalml_amd/reference/gbdt.py.
 //
-// * gradients/hessians are int64 fixed point (2^-28): every histogram sum is an exact
-//   integer, so LDS/global atomics in any order, row shards + RCCL all-reduce (C04),
-//   and the host reference all produce the same bits;
-// * level-wise growth, heap-indexed trees; per level: hist (LDS int64 atomics, F
-//   features per workgroup so the row's node id and gradient pair are loaded once per
-//   F features; F = 32 / nodes so the LDS histogram stays <= 128 KB), split search
-//   (one workgroup per node, wave-parallel prefix over 256 bins, deterministic
-//   (gain, feature, bin) tie-break), partition (row -> child id);
-// * compiled with -ffp-contract=off: the split gains round exactly like numpy's.
+// Numerics: gradients/hessians are int64 fixed point (2^-28), so every histogram sum is
+// an exact integer — LDS/global atomics in any order, row shards + RCCL all-reduce (C04),
+// histogram subtraction and the host reference all give the same bits. Split gains are
+// compiled with -ffp-contract=off so they round exactly like numpy's.
+//
+// Data layout (MI355X-first, LightGBM-style):
+// * bins are ROW-major uint8 [n][ldr], ldr % 32 == 0: one 128-B line holds a row's bins
+//   for p <= 128, and a workgroup reading a 16-feature block reads 16 aligned bytes;
+// * training rows are kept in a position array `idx` sorted by tree node (the
+//   "segments"), with the fixed-point gradient pair (packed into one int64) stored in
+//   the same order. After each level's split a three-kernel partition (count / scan /
+//   scatter) moves (idx, gh) into child buckets — 12 B per row, bins never move;
+// * a histogram workgroup = (node segment chunk, 16-feature block): 16 features x 256
+//   bins x (G, H) int64 live in 64 KB of LDS (two workgroups per CU), feature-minor so
+//   the int64 LDS atomics are bank-conflict-free; partial images go to slabs (plain stores) and a reduce kernel
+//   sums each node's slabs into H[node][c][bin][feature] — no global atomics. Only the
+//   SMALLER child of each split parent is histogrammed — the sibling is parent - child
+//   (histogram subtraction), so levels >= 1 touch at most half of the rows;
+// * split search: workgroup = (node, 32-feature block) staged in LDS, thread = (feature,
+//   16-bin segment); a one-wave finalize picks each node's best block candidate;
+// * the whole boosting loop (grad -> per level: hist / [reduce] / derive / split /
+//   partition -> apply) is issued from C++ on one stream; row-sharded fits pass a
+//   host callback that all-reduces each level's histograms (root totals come from the
+//   reduced level-0 histogram).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
 
 constexpr int NT = 256;
+constexpr int NTH = 512;             // histogram workgroup (two per CU: 2 x 64-KB LDS images)
+constexpr int FB = 16;               // features per histogram workgroup
+constexpr int SFB = 32;              // features per split-search workgroup
+constexpr int HS = 257;              // padded bins per (feature, channel) in LDS
+constexpr int MAXB = 65;             // partition buckets: 2 * 32 children + retired
 constexpr double GFIX = 268435456.0;   // 2^28
 
 typedef unsigned long long u64;
 
-// g, h of the loss at the current raw score; rows outside the training set get node -1
-__global__ __launch_bounds__(NT) void gbdt_grad_kernel(int loss, const double* __restrict__ f,
-                                                       const double* __restrict__ y,
-                                                       const uint8_t* __restrict__ train,
-                                                       int64_t n, int64_t* __restrict__ gh,
-                                                       int32_t* __restrict__ node,
-                                                       int64_t* __restrict__ root) {
-  __shared__ int64_t red[2][NT / 64];
-  int64_t sg = 0, sh = 0;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    if (!train[i]) {
-      node[i] = -1;
-      continue;
-    }
-    double g, h;
-    if (loss == 0) {
-      g = f[i] - y[i];
-      h = 1.0;
-    } else {
-      const double s = 1.0 / (1.0 + exp(-f[i]));
-      g = s - y[i];
-      h = fmax(s * (1.0 - s), 1e-16);
-    }
-    const int64_t G = llrint(g * GFIX), H = llrint(h * GFIX);
-    gh[2 * i] = G;
-    gh[2 * i + 1] = H;
-    node[i] = 0;
-    sg += G;
-    sh += H;
-  }
-  sg = ate::wave_sum(sg);
-  sh = ate::wave_sum(sh);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) { red[0][wid] = sg; red[1][wid] = sh; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t a = 0, b = 0;
-    for (int w = 0; w < NT / 64; ++w) { a += red[0][w]; b += red[1][w]; }
-    atomicAdd((u64*)&root[0], (u64)a);
-    atomicAdd((u64*)&root[1], (u64)b);
+// One int64 per row carries the fixed-point pair: squared loss -> G (H is exactly 2^28);
+// logistic -> (int32 G, int32 H) since |g| < 1 and h <= 1/4 (|G| <= 2^28, H <= 2^26).
+__device__ __forceinline__ int64_t gbdt_pack(int loss, int64_t G, int64_t H) {
+  return loss == 0 ? G : (int64_t)(((uint64_t)(uint32_t)H << 32) | (uint32_t)(int32_t)G);
+}
+__device__ __forceinline__ void gbdt_unpack(int loss, int64_t v, u64& g, u64& h) {
+  if (loss == 0) {
+    g = (u64)v;
+    h = (u64)268435456;                                      // 2^28
+  } else {
+    g = (u64)(int64_t)(int32_t)(uint32_t)v;
+    h = (u64)((uint64_t)v >> 32);
   }
 }
 
-// H[((k*p + j)*256 + b)*2 + c] += sum over rows of node k with bin b in feature j
-__global__ __launch_bounds__(NT) void gbdt_hist_kernel(const uint8_t* __restrict__ Xb, int64_t ld,
-                                                       const int32_t* __restrict__ node,
-                                                       const int64_t* __restrict__ gh, int64_t n,
-                                                       int nn, int p, int F, int64_t chunk,
-                                                       int64_t* __restrict__ H) {
-  extern __shared__ u64 sh[];                 // [F][nn][256][2]
-  const int j0 = blockIdx.y * F;
-  const int nf = min(F, p - j0);
-  const int tot = nf * nn * 512;
-  for (int k = threadIdx.x; k < tot; k += NT) sh[k] = 0;
+// g, h of the loss at the current raw score for the training positions [0, n_train)
+// (4 positions per thread, loads batched); level-0 segment = [0, n_train). The root
+// totals are taken from the level-0 histogram (gbdt_root_kernel).
+__global__ __launch_bounds__(NT) void gbdt_grad_kernel(int loss, const double* __restrict__ f,
+                                                       const double* __restrict__ y,
+                                                       const int32_t* __restrict__ idx,
+                                                       int64_t n_train, int64_t* __restrict__ gh,
+                                                       int32_t* __restrict__ seg) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) { seg[0] = 0; seg[1] = (int32_t)n_train; }
+  const int64_t q0 = (blockIdx.x * (int64_t)NT * 4) + threadIdx.x;
+  int32_t ii[4];
+  double fv[4], yv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ii[u] = idx[min(q0 + u * NT, n_train - 1)];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) { fv[u] = f[ii[u]]; yv[u] = y[ii[u]]; }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t q = q0 + u * NT;
+    if (q >= n_train) continue;
+    double g, h;
+    if (loss == 0) {
+      g = fv[u] - yv[u];
+      h = 1.0;
+    } else {
+      const double s = 1.0 / (1.0 + exp(-fv[u]));
+      g = s - yv[u];
+      h = fmax(s * (1.0 - s), 1e-16);
+    }
+    gh[q] = gbdt_pack(loss, llrint(g * GFIX), llrint(h * GFIX));
+  }
+}
+
+// root totals = the level-0 histogram of feature 0 summed over its bins (every training
+// row is in exactly one bin), exact and already reduced over row shards
+__global__ __launch_bounds__(NT) void gbdt_root_kernel(const int64_t* __restrict__ H, int p,
+                                                       int64_t* __restrict__ tot) {
+  __shared__ int64_t red[2][NT / 64];
+  int64_t a = H[(int64_t)threadIdx.x * p], b = H[(int64_t)(256 + threadIdx.x) * p];
+  a = ate::wave_sum(a);
+  b = ate::wave_sum(b);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = a; red[1][wid] = b; }
   __syncthreads();
-  const int64_t r0 = blockIdx.x * chunk, r1 = min(n, r0 + chunk);
-  for (int64_t i = r0 + threadIdx.x; i < r1; i += NT) {
-    const int nd = node[i];
-    if (nd < 0) continue;
-    const u64 g = (u64)gh[2 * i], h = (u64)gh[2 * i + 1];
-    for (int f = 0; f < nf; ++f) {
-      const int b = Xb[(int64_t)(j0 + f) * ld + i];
-      u64* e = sh + (((int64_t)f * nn + nd) * 256 + b) * 2;
-      atomicAdd(e, g);
-      atomicAdd(e + 1, h);
+  if (threadIdx.x == 0) {
+    int64_t sa = 0, sb = 0;
+    for (int w = 0; w < NT / 64; ++w) { sa += red[0][w]; sb += red[1][w]; }
+    tot[0] = sa;
+    tot[1] = sb;
+  }
+}
+
+// Which nodes of level d get a histogram of their own: the root, and for every split
+// parent the child with fewer rows (rule 0, single rank: segment lengths) or with the
+// smaller hessian total (rule 1, row shards: tot[] is identical on every rank, so all
+// ranks histogram the same child). Ties -> left child.
+__device__ __forceinline__ bool gbdt_computed(int k, int d, const int32_t* seg,
+                                              const int64_t* tot, int rule) {
+  if (d == 0) return true;
+  const int sib = k ^ 1;
+  int64_t a, b;
+  if (rule == 0) {
+    a = seg[k + 1] - seg[k];
+    b = seg[sib + 1] - seg[sib];
+  } else {
+    const int hk = (1 << d) - 1;
+    a = tot[2 * (hk + k) + 1];
+    b = tot[2 * (hk + sib) + 1];
+  }
+  return a < b || (a == b && !(k & 1));
+}
+
+// Work plan of a level's histogram: computed nodes are cut into chunks of CH positions;
+// chunk i of node k is global chunk acc[k] + i. Filled by thread 0 into LDS.
+__device__ void gbdt_plan(const int* sseg, const int64_t* tot, int rule, int nn, int d,
+                          int64_t CH, int* acc, int* nch) {
+  int a = 0;
+  for (int k = 0; k < nn; ++k) {
+    const int64_t len = sseg[k + 1] - sseg[k];
+    const int c = (len > 0 && gbdt_computed(k, d, sseg, tot, rule)) ? (int)((len + CH - 1) / CH)
+                                                                     : 0;
+    acc[k] = a;
+    nch[k] = c;
+    a += c;
+  }
+  acc[nn] = a;
+}
+
+constexpr int SLAB = 2 * 256 * FB;   // one workgroup's histogram image, u64 entries
+
+// Partial histograms: workgroup = (chunk of a computed node's segment, 32-feature block),
+// LDS image [c][bin][slot(f)] (feature-minor, see the lane map below: the int64 LDS
+// atomics are bank-conflict-free whatever the bins are). The image goes to slab
+// `logical` with plain 16-B stores; gbdt_hist_reduce_kernel sums a node's slabs.
+// 1-D grid, XCD-remapped so the feature blocks of one chunk share an XCD's L2.
+__global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
+    const uint8_t* __restrict__ Xr, int64_t ldr, const int32_t* __restrict__ idx,
+    const int64_t* __restrict__ gh, const int32_t* __restrict__ seg, const int64_t* tot,
+    int rule, int nn, int p, int d, int64_t CH, int ydim, u64* __restrict__ slab, int mode,
+    int loss) {
+  __shared__ u64 sh[SLAB];
+  __shared__ int sseg[33], sacc[33], snch[32];
+  __shared__ int64_t wk[3];
+  const int G = gridDim.x;
+  const int bid = blockIdx.x;
+  const int logical = (bid & 7) * (G >> 3) + (bid >> 3);   // G % 8 == 0
+  const int chunk = logical / ydim, yb = logical - chunk * ydim;
+  if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gbdt_plan(sseg, tot, rule, nn, d, CH, sacc, snch);
+    wk[0] = -1;
+    for (int k = 0; k < nn; ++k)
+      if (chunk >= sacc[k] && chunk < sacc[k] + snch[k]) {
+        wk[0] = k;
+        wk[1] = sseg[k] + (int64_t)(chunk - sacc[k]) * CH;
+        wk[2] = min((int64_t)sseg[k + 1], wk[1] + CH);
+      }
+  }
+  __syncthreads();
+  if (wk[0] < 0) return;                                    // uniform: spare workgroup
+  const int64_t s = wk[1], e = wk[2];
+  const int j0 = yb * FB, nf = min(FB, p - j0);
+  {
+    ulonglong2* z = reinterpret_cast<ulonglong2*>(sh);
+    for (int t = threadIdx.x; t < SLAB / 2; t += NTH) z[t] = make_ulonglong2(0, 0);
+  }
+  __syncthreads();
+  // lane = (row r16 of 16, word l4 of 4): the lane reads the dword of features
+  // 4*l4..+3 of its row. LDS slot of local feature f: (f & 3) << 2 | f >> 2, so feature
+  // 4*l4 + q sits on bank pair 4*q + l4; row r walks q in the order rotated by r & 3, so
+  // the four rows of every 16-lane LDS group use 16 distinct bank pairs: the int64
+  // atomics are conflict-free whatever the bins are.
+  const int l4 = threadIdx.x & 3, r16 = (threadIdx.x >> 2) & 15, w = threadIdx.x >> 6;
+  const int rot = r16 & 3;
+  const uint32_t* xw = reinterpret_cast<const uint32_t*>(Xr + j0) + l4;   // in the row
+  const int64_t ldw = ldr >> 2;
+  // rows of iteration `base`: base + (u*8 + w)*16 + r16; software pipeline: positions of
+  // iteration i+2 and (g, h, bins) of iteration i+1 are in flight while iteration i's
+  // atomics run. Loads are unconditional (positions past the segment are clamped to its
+  // last row; words past p read row padding), so no branch forces a vmcnt(0) per row.
+  constexpr int U = 8, RPI = U * (NTH / 4);
+  int32_t iiA[U], iiB[U];
+  u64 gA[U], hA[U];
+  uint32_t bA[U];
+  const int64_t last = e - 1;
+  const bool wok = 4 * l4 < nf;
+  auto pos = [&](int64_t base, int u) { return base + (u * (NTH / 64) + w) * 16 + r16; };
+#pragma unroll
+  for (int u = 0; u < U; ++u) iiA[u] = idx[min(pos(s, u), last)];
+#pragma unroll
+  for (int u = 0; u < U; ++u) iiB[u] = idx[min(pos(s + RPI, u), last)];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    gbdt_unpack(loss, gh[min(pos(s, u), last)], gA[u], hA[u]);
+    bA[u] = (mode & 2) ? (uint32_t)iiA[u] * 0x9E3779B1u : xw[(int64_t)iiA[u] * ldw];
+  }
+  u64 dummy = 0;
+  for (int64_t base = s; base < e; base += RPI) {
+    u64 gB[U], hB[U];
+    uint32_t bB[U];
+    int32_t iiC[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      gbdt_unpack(loss, gh[min(pos(base + RPI, u), last)], gB[u], hB[u]);
+      bB[u] = (mode & 2) ? (uint32_t)iiB[u] * 0x9E3779B1u : xw[(int64_t)iiB[u] * ldw];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) iiC[u] = idx[min(pos(base + 2 * RPI, u), last)];
+    if (mode & 1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) dummy += gA[u] * bA[u] + hA[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // padding words and rows past the segment add nothing: their lanes stay idle
+        if (!wok || pos(base, u) > last) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = (k + rot) & 3;
+          const uint32_t bin = (bA[u] >> (8 * q)) & 255;
+          u64* e0 = sh + bin * FB + (q << 2 | l4);
+          atomicAdd(e0, gA[u]);
+          atomicAdd(e0 + 256 * FB, hA[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      iiA[u] = iiB[u];
+      gA[u] = gB[u];
+      hA[u] = hB[u];
+      bA[u] = bB[u];
+      iiB[u] = iiC[u];
     }
   }
+  if (dummy == 0x123456789ull) sh[0] = dummy;
   __syncthreads();
-  for (int k = threadIdx.x; k < tot; k += NT) {
-    const u64 v = sh[k];
-    if (!v) continue;
-    const int c = k & 1, b = (k >> 1) & 255, rest = k >> 9;
-    const int nd = rest % nn, f = rest / nn;
-    atomicAdd((u64*)&H[(((int64_t)nd * p + j0 + f) * 256 + b) * 2 + c], v);
+  if (mode & 4) return;
+  ulonglong2* dst = reinterpret_cast<ulonglong2*>(slab + (int64_t)logical * SLAB);
+  const ulonglong2* src = reinterpret_cast<const ulonglong2*>(sh);
+  for (int t = threadIdx.x; t < SLAB / 2; t += NTH) dst[t] = src[t];
+}
+
+// H[k][c][b][j] (node-major, feature-minor) = sum of node k's slabs; zero for nodes
+// without a histogram of their own (gbdt_derive_kernel fills the larger children).
+__global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
+    const u64* __restrict__ slab, const int32_t* __restrict__ seg, const int64_t* tot, int rule,
+    int nn, int p, int d, int64_t CH, int ydim, int64_t* __restrict__ H) {
+  __shared__ int sseg[33], sacc[33], snch[32];
+  const int k = blockIdx.y;
+  if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) gbdt_plan(sseg, tot, rule, nn, d, CH, sacc, snch);
+  __syncthreads();
+  const int a = sacc[k], c = snch[k];
+  const int64_t per = 512LL * p;
+  int64_t* Hk = H + k * per;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
+    const int cb = (int)(t / p), j = (int)(t - (int64_t)cb * p);
+    const int yb = j / FB, fl = j - yb * FB;
+    const u64* sp = slab + ((int64_t)a * ydim + yb) * SLAB + cb * FB + ((fl & 3) << 2 | fl >> 2);
+    const int64_t stride = (int64_t)ydim * SLAB;
+    u64 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    int i = 0;
+    for (; i + 4 <= c; i += 4) {
+      v0 += sp[i * stride];
+      v1 += sp[(i + 1) * stride];
+      v2 += sp[(i + 2) * stride];
+      v3 += sp[(i + 3) * stride];
+    }
+    for (; i < c; ++i) v0 += sp[i * stride];
+    Hk[t] = (int64_t)(v0 + v1 + v2 + v3);
   }
+}
+
+// larger child = parent - histogrammed child (levels >= 1)
+__global__ __launch_bounds__(NT) void gbdt_derive_kernel(const int64_t* __restrict__ Hp,
+                                                         int64_t* __restrict__ Hc,
+                                                         const int32_t* __restrict__ seg,
+                                                         const int64_t* __restrict__ tot,
+                                                         const int32_t* __restrict__ feat,
+                                                         int rule, int nn, int p, int d) {
+  const int m = blockIdx.y;                                 // parent index at level d-1
+  if (feat[(1 << (d - 1)) - 1 + m] < 0) return;
+  const int small = gbdt_computed(2 * m, d, seg, tot, rule) ? 2 * m : 2 * m + 1;
+  const int big = small ^ 1;
+  const int64_t per = (int64_t)p * 512;
+  const int64_t* P = Hp + m * per;
+  const int64_t* S = Hc + small * per;
+  int64_t* B = Hc + big * per;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT)
+    B[t] = P[t] - S[t];
 }
 
 struct Best {
@@ -107,185 +323,428 @@ __device__ __forceinline__ bool better(double g, int j, int b, const Best& o) {
   return j < o.j || (j == o.j && b < o.b);
 }
 
-// one workgroup per node of level d; writes the split or the leaf value
-__global__ __launch_bounds__(NT) void gbdt_split_kernel(const int64_t* __restrict__ H, int nn, int p,
-                                                        int d, int depth, double lam,
-                                                        int64_t min_child, double min_gain,
-                                                        double lr, int64_t* __restrict__ tot,
-                                                        int32_t* __restrict__ feat,
-                                                        int32_t* __restrict__ thr,
-                                                        double* __restrict__ value) {
-  __shared__ Best wb[NT / 64];
-  __shared__ int64_t wgl[NT / 64], whl[NT / 64];
-  const int k = blockIdx.x;
+constexpr int NTS = 512;   // split search workgroup: 32 features x 16 bin segments
+
+struct Cand {               // best split of one (node, feature block)
+  double gain;
+  int j, b;
+  int64_t gl, hl;
+};
+
+// grid (node, 32-feature block): the block's [c][bin][32] histogram slice is staged in
+// LDS (256-B rows: conflict-free 8-B reads, lane = feature); thread = (feature, 16-bin
+// segment); segment totals are scanned through LDS; each thread scores its 16 split
+// points (ascending bins, strict > keeps the lowest on ties) and the workgroup's best
+// (gain desc, feature asc, bin asc) goes to cand[node][block].
+__global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
+    const int64_t* __restrict__ H, int p, int d, int depth, double lam, int64_t min_child,
+    const int64_t* __restrict__ tot, const int32_t* __restrict__ feat, Cand* __restrict__ cand) {
+  __shared__ int64_t sh[2 * 256 * SFB];
+  __shared__ int64_t segs[2][16][SFB];
+  __shared__ Cand wb[NTS / 64];
+  const int k = blockIdx.x, yb = blockIdx.y, ydim = gridDim.y;
   const int hk = (1 << d) - 1 + k;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (d > 0 && feat[(hk - 1) / 2] < 0) {       // parent is a leaf or absent
-    if (threadIdx.x == 0) feat[hk] = -2;
-    return;
+  if (d >= depth || (d > 0 && feat[(hk - 1) / 2] < 0)) return;
+  const int j0 = yb * SFB, nf = min(SFB, p - j0);
+  const int64_t* Hk = H + (int64_t)k * 512 * p + j0;
+  for (int t = threadIdx.x; t < 512 * SFB; t += NTS) {
+    const int cb = t >> 5, fl = t & 31;
+    const int64_t v = Hk[(int64_t)cb * p + min(fl, nf - 1)];
+    sh[t] = fl < nf ? v : 0;
   }
+  const int f = threadIdx.x & 31, sg = threadIdx.x >> 5;       // 16 segments of 16 bins
+  __syncthreads();
+  int64_t sgs = 0, shs = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    sgs += sh[(sg * 16 + i) * SFB + f];
+    shs += sh[(256 + sg * 16 + i) * SFB + f];
+  }
+  segs[0][sg][f] = sgs;
+  segs[1][sg][f] = shs;
+  __syncthreads();
+  int64_t GL = 0, HL = 0;
+  for (int q = 0; q < sg; ++q) { GL += segs[0][q][f]; HL += segs[1][q][f]; }
   const int64_t G = tot[2 * hk], Hh = tot[2 * hk + 1];
   const double gf = (double)G / GFIX, hf = (double)Hh / GFIX;
-  Best best{-INFINITY, 0x7fffffff, 0x7fffffff};
-  int64_t bgl = 0, bhl = 0;
-  if (d < depth) {
-    const double parent = gf * gf / (hf + lam);
-    for (int j = wid; j < p; j += NT / 64) {
-      const int64_t* hj = H + (((int64_t)k * p + j) * 256) * 2;
-      int64_t cg[4], ch[4];
-      int64_t sg = 0, sh2 = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        sg += hj[(4 * lane + q) * 2];
-        sh2 += hj[(4 * lane + q) * 2 + 1];
-        cg[q] = sg;
-        ch[q] = sh2;
+  const double parent = gf * gf / (hf + lam);
+  Cand lb{-INFINITY, j0 + f, 0x7fffffff, 0, 0};
+  if (f < nf) {
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      GL += sh[(sg * 16 + i) * SFB + f];
+      HL += sh[(256 + sg * 16 + i) * SFB + f];
+      if (HL >= min_child && Hh - HL >= min_child) {
+        const double glf = (double)GL / GFIX, hlf = (double)HL / GFIX;
+        const double grf = gf - glf, hrf = hf - hlf;
+        const double gain = glf * glf / (hlf + lam) + grf * grf / (hrf + lam) - parent;
+        if (gain > lb.gain) lb = {gain, j0 + f, sg * 16 + i, GL, HL};
       }
-      // exclusive scan of the lane totals across the wave
-      int64_t eg = sg, eh = sh2;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t tg = __shfl_up(eg, o, 64), th = __shfl_up(eh, o, 64);
-        if (lane >= o) { eg += tg; eh += th; }
-      }
-      eg -= sg;
-      eh -= sh2;
-      Best lb{-INFINITY, j, 0x7fffffff};
-      int64_t lgl = 0, lhl = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t GL = eg + cg[q], HL = eh + ch[q];
-        if (HL >= min_child && Hh - HL >= min_child) {
-          const double glf = (double)GL / GFIX, hlf = (double)HL / GFIX;
-          const double grf = gf - glf, hrf = hf - hlf;
-          const double gain = glf * glf / (hlf + lam) + grf * grf / (hrf + lam) - parent;
-          if (better(gain, j, 4 * lane + q, lb)) {
-            lb = {gain, j, 4 * lane + q};
-            lgl = GL;
-            lhl = HL;
-          }
-        }
-      }
-      // wave argmax (gain desc, bin asc)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        Best ob;
-        ob.gain = __shfl_xor(lb.gain, o, 64);
-        ob.j = __shfl_xor(lb.j, o, 64);
-        ob.b = __shfl_xor(lb.b, o, 64);
-        const int64_t ogl = __shfl_xor(lgl, o, 64), ohl = __shfl_xor(lhl, o, 64);
-        if (better(ob.gain, ob.j, ob.b, lb)) { lb = ob; lgl = ogl; lhl = ohl; }
-      }
-      if (better(lb.gain, lb.j, lb.b, best)) { best = lb; bgl = lgl; bhl = lhl; }
     }
   }
-  if (lane == 0) { wb[wid] = best; wgl[wid] = bgl; whl[wid] = bhl; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand ob;
+    ob.gain = __shfl_xor(lb.gain, o, 64);
+    ob.j = __shfl_xor(lb.j, o, 64);
+    ob.b = __shfl_xor(lb.b, o, 64);
+    ob.gl = __shfl_xor(lb.gl, o, 64);
+    ob.hl = __shfl_xor(lb.hl, o, 64);
+    if (better(ob.gain, ob.j, ob.b, Best{lb.gain, lb.j, lb.b})) lb = ob;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) wb[wid] = lb;
   __syncthreads();
   if (threadIdx.x == 0) {
-    Best b = wb[0];
-    int64_t gl = wgl[0], hl = whl[0];
-    for (int w = 1; w < NT / 64; ++w)
-      if (better(wb[w].gain, wb[w].j, wb[w].b, b)) { b = wb[w]; gl = wgl[w]; hl = whl[w]; }
-    if (d < depth && b.gain > -INFINITY && b.gain > min_gain) {
-      feat[hk] = b.j;
-      thr[hk] = b.b;
-      tot[2 * (2 * hk + 1)] = gl;
-      tot[2 * (2 * hk + 1) + 1] = hl;
-      tot[2 * (2 * hk + 2)] = G - gl;
-      tot[2 * (2 * hk + 2) + 1] = Hh - hl;
+    Cand b = wb[0];
+    for (int w = 1; w < NTS / 64; ++w)
+      if (better(wb[w].gain, wb[w].j, wb[w].b, Best{b.gain, b.j, b.b})) b = wb[w];
+    cand[(int64_t)k * ydim + yb] = b;
+  }
+}
+
+// one wave per node of level d: best candidate over the feature blocks -> split (and the
+// children's totals) or leaf value; children of leaves / absent nodes are marked -2
+__global__ __launch_bounds__(64) void gbdt_split_final_kernel(
+    const Cand* __restrict__ cand, int ydim, int d, int depth, double min_gain, double lam,
+    double lr, int64_t* __restrict__ tot, int32_t* __restrict__ feat, int32_t* __restrict__ thr,
+    double* __restrict__ value) {
+  const int k = blockIdx.x, lane = threadIdx.x;
+  const int hk = (1 << d) - 1 + k;
+  if (d > 0 && feat[(hk - 1) / 2] < 0) {
+    if (lane == 0) feat[hk] = -2;
+    return;
+  }
+  Cand lb{-INFINITY, 0x7fffffff, 0x7fffffff, 0, 0};
+  if (d < depth)
+    for (int y = lane; y < ydim; y += 64) {
+      const Cand c = cand[(int64_t)k * ydim + y];
+      if (better(c.gain, c.j, c.b, Best{lb.gain, lb.j, lb.b})) lb = c;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Cand ob;
+    ob.gain = __shfl_xor(lb.gain, o, 64);
+    ob.j = __shfl_xor(lb.j, o, 64);
+    ob.b = __shfl_xor(lb.b, o, 64);
+    ob.gl = __shfl_xor(lb.gl, o, 64);
+    ob.hl = __shfl_xor(lb.hl, o, 64);
+    if (better(ob.gain, ob.j, ob.b, Best{lb.gain, lb.j, lb.b})) lb = ob;
+  }
+  if (lane == 0) {
+    const int64_t G = tot[2 * hk], Hh = tot[2 * hk + 1];
+    if (d < depth && lb.gain > -INFINITY && lb.gain > min_gain) {
+      feat[hk] = lb.j;
+      thr[hk] = lb.b;
+      tot[2 * (2 * hk + 1)] = lb.gl;
+      tot[2 * (2 * hk + 1) + 1] = lb.hl;
+      tot[2 * (2 * hk + 2)] = G - lb.gl;
+      tot[2 * (2 * hk + 2) + 1] = Hh - lb.hl;
     } else {
+      const double gf = (double)G / GFIX, hf = (double)Hh / GFIX;
       feat[hk] = -1;
       value[hk] = -lr * gf / (hf + lam);
     }
   }
 }
 
-__global__ __launch_bounds__(NT) void gbdt_partition_kernel(const uint8_t* __restrict__ Xb,
-                                                            int64_t ld, int32_t* __restrict__ node,
-                                                            int64_t n, int d,
-                                                            const int32_t* __restrict__ feat,
-                                                            const int32_t* __restrict__ thr) {
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const int nd = node[i];
-    if (nd < 0) continue;
-    const int hk = (1 << d) - 1 + nd;
-    const int fj = feat[hk];
-    node[i] = fj < 0 ? -1 : 2 * nd + (Xb[(int64_t)fj * ld + i] > thr[hk] ? 1 : 0);
+// ---- partition of the training positions into child buckets after a level's split ----
+// bucket of position q: 2k + (bin > thr) for a row of split node k, 2nn ("retired")
+// for rows of leaves (and rows retired at earlier levels, which sit past seg[nn]).
+__global__ __launch_bounds__(NT) void gbdt_part_count_kernel(
+    const uint8_t* __restrict__ Xr, int64_t ldr, const int32_t* __restrict__ idx,
+    int64_t n_train, const int32_t* __restrict__ seg, int nn, int d,
+    const int32_t* __restrict__ feat, const int32_t* __restrict__ thr, int64_t R, int W,
+    uint8_t* __restrict__ bkt, int32_t* __restrict__ cnt) {
+  __shared__ int sseg[33], sft[32], sth[32], lc[MAXB];
+  if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
+  if (threadIdx.x < nn) {
+    sft[threadIdx.x] = feat[(1 << d) - 1 + threadIdx.x];
+    sth[threadIdx.x] = thr[(1 << d) - 1 + threadIdx.x];
+  }
+  if (threadIdx.x < MAXB) lc[threadIdx.x] = 0;
+  __syncthreads();
+  const int wgi = blockIdx.x;
+  const int64_t q0 = wgi * R, q1 = min(n_train, q0 + R);
+  for (int64_t qb = q0 + threadIdx.x; qb < q1; qb += 4 * NT) {
+    int32_t ii[4];
+    int kk[4];
+    uint8_t bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = min(qb + u * NT, q1 - 1);
+      ii[u] = idx[q];
+      int lo = 0, hi = nn - 1;                              // largest k with seg[k] <= q
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sseg[mid] <= q) lo = mid; else hi = mid - 1;
+      }
+      kk[u] = lo;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bv[u] = Xr[(int64_t)ii[u] * ldr + max(sft[kk[u]], 0)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t q = qb + u * NT;
+      if (q >= q1) continue;
+      int b = 2 * nn;
+      if (q < sseg[nn] && sft[kk[u]] >= 0) b = 2 * kk[u] + (bv[u] > sth[kk[u]] ? 1 : 0);
+      bkt[q] = (uint8_t)b;
+      atomicAdd(&lc[b], 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x <= 2 * nn) cnt[(int64_t)threadIdx.x * W + wgi] = lc[threadIdx.x];
+}
+
+// one workgroup per bucket: exclusive scan of the per-workgroup counts (W <= 4 * NT)
+__global__ __launch_bounds__(NT) void gbdt_part_scan_kernel(const int32_t* __restrict__ cnt,
+                                                            int W, int32_t* __restrict__ base,
+                                                            int32_t* __restrict__ btot) {
+  __shared__ int ws[NT / 64];
+  const int b = blockIdx.x;
+  const int32_t* c = cnt + (int64_t)b * W;
+  int v[4], s = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int w = 4 * threadIdx.x + u;
+    v[u] = w < W ? c[w] : 0;
+    s += v[u];
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) ws[wid] = incl;
+  __syncthreads();
+  int off = 0;
+  for (int w2 = 0; w2 < wid; ++w2) off += ws[w2];
+  int run = off + incl - s;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int w = 4 * threadIdx.x + u;
+    if (w < W) base[(int64_t)b * W + w] = run;
+    run += v[u];
+  }
+  if (threadIdx.x == NT - 1) {
+    int t = 0;
+    for (int w2 = 0; w2 < NT / 64; ++w2) t += ws[w2];
+    btot[b] = t;
   }
 }
 
-// f[i] += value of the leaf row i reaches in the tree (all rows, training or not)
-__global__ __launch_bounds__(NT) void gbdt_apply_kernel(const uint8_t* __restrict__ Xb, int64_t ld,
-                                                        int64_t n, int ntree, int M,
+__global__ __launch_bounds__(NT) void gbdt_part_scatter_kernel(
+    const int32_t* __restrict__ idx, const int64_t* __restrict__ gh,
+    const uint8_t* __restrict__ bkt, int64_t n_train, int nb, int64_t R, int W,
+    const int32_t* __restrict__ base, const int32_t* __restrict__ btot,
+    int32_t* __restrict__ idx2, int64_t* __restrict__ gh2, int32_t* __restrict__ seg2) {
+  __shared__ int off[MAXB], lr[MAXB];
+  if (threadIdx.x == 0) {
+    int a = 0;
+    for (int b = 0; b < nb; ++b) { off[b] = a; a += btot[b]; }
+  }
+  if (threadIdx.x < MAXB) lr[threadIdx.x] = 0;
+  __syncthreads();
+  const int wgi = blockIdx.x;
+  if (wgi == 0 && threadIdx.x < nb) seg2[threadIdx.x] = off[threadIdx.x];
+  if (threadIdx.x < nb) off[threadIdx.x] += base[(int64_t)threadIdx.x * W + wgi];
+  __syncthreads();
+  const int64_t q0 = wgi * R, q1 = min(n_train, q0 + R);
+  for (int64_t q = q0 + threadIdx.x; q < q1; q += NT) {
+    const int b = bkt[q];
+    const int64_t dst = off[b] + atomicAdd(&lr[b], 1);
+    idx2[dst] = idx[q];
+    gh2[dst] = gh[q];
+  }
+}
+
+// f[i] += value of the leaf row i reaches, for trees [0, ntree) (all rows). A workgroup
+// stages RW whole rows in LDS with coalesced 16-B loads (all in flight at once) and the
+// trees (M <= 127 nodes), so a row's walk is LDS-latency only.
+__global__ __launch_bounds__(NT) void gbdt_apply_kernel(const uint8_t* __restrict__ Xr, int64_t ldr,
+                                                        int64_t n, int RW, int ntree, int M,
                                                         const int32_t* __restrict__ feat,
                                                         const int32_t* __restrict__ thr,
                                                         const double* __restrict__ value,
                                                         double* __restrict__ f) {
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    double acc = f[i];
-    for (int t = 0; t < ntree; ++t) {
-      const int32_t* ft = feat + (int64_t)t * M;
-      const int32_t* th = thr + (int64_t)t * M;
-      int k = 0;
-      while (ft[k] >= 0) k = 2 * k + 1 + (Xb[(int64_t)ft[k] * ld + i] > th[k] ? 1 : 0);
-      acc += value[(int64_t)t * M + k];
+  extern __shared__ uint4 srow[];                           // [RW][ldr] bytes
+  __shared__ int sft[127], sth[127];
+  __shared__ double sv[127];
+  const int64_t r0 = blockIdx.x * (int64_t)RW;
+  const int rows = (int)min((int64_t)RW, n - r0);
+  const int v16 = (int)(ldr >> 4);
+  const uint4* src = reinterpret_cast<const uint4*>(Xr + r0 * ldr);
+  for (int t = threadIdx.x; t < rows * v16; t += NT) srow[t] = src[t];
+  const uint8_t* mine = reinterpret_cast<const uint8_t*>(srow) + (int64_t)threadIdx.x * ldr;
+  double acc = threadIdx.x < rows ? f[r0 + threadIdx.x] : 0.0;
+  for (int t = 0; t < ntree; ++t) {
+    __syncthreads();
+    if (threadIdx.x < M) {
+      sft[threadIdx.x] = feat[(int64_t)t * M + threadIdx.x];
+      sth[threadIdx.x] = thr[(int64_t)t * M + threadIdx.x];
+      sv[threadIdx.x] = value[(int64_t)t * M + threadIdx.x];
     }
-    f[i] = acc;
+    __syncthreads();
+    if (threadIdx.x < rows) {
+      int k = 0;
+      while (sft[k] >= 0) k = 2 * k + 1 + (mine[sft[k]] > sth[k] ? 1 : 0);
+      acc += sv[k];
+    }
   }
+  if (threadIdx.x < rows) f[r0 + threadIdx.x] = acc;
+}
+
+static int gbdt_apply_rows(int64_t ldr) {                   // rows staged per workgroup
+  return (int)std::max<int64_t>(16, std::min<int64_t>(NT, 65536 / ldr) / 16 * 16);
+}
+
+static void gbdt_launch_apply(const uint8_t* Xr, int64_t ldr, int64_t n, int ntree, int M,
+                              const int32_t* feat, const int32_t* thr, const double* value,
+                              double* f, hipStream_t st) {
+  const int RW = gbdt_apply_rows(ldr);
+  hipLaunchKernelGGL(gbdt_apply_kernel, dim3((unsigned)((n + RW - 1) / RW)), dim3(NT),
+                     (size_t)RW * ldr, st, Xr, ldr, n, RW, ntree, M, feat, thr, value, f);
 }
 
 }  // namespace
 
-ATE_API int ate_gbdt_grad(int loss, const void* f, const void* y, const void* train, int64_t n,
-                          void* gh, void* node, void* root, void* stream) {
-  hipLaunchKernelGGL(gbdt_grad_kernel, dim3(ate::grid_for(n, NT, 1024)), dim3(NT), 0,
-                     (hipStream_t)stream, loss, (const double*)f, (const double*)y,
-                     (const uint8_t*)train, n, (int64_t*)gh, (int32_t*)node, (int64_t*)root);
+// Everything one fit needs; layout mirrored by models/gbdt.py::FitArgs.
+struct GbdtFitArgs {
+  const uint8_t* Xr;      // [n][ldr] row-major bins
+  int64_t ldr, n, n_train;
+  int p, depth, n_trees, loss, rule, W;
+  double lam, min_gain, lr;
+  int64_t min_child, R;
+  const double* y;        // [n] (original row order)
+  double* f;              // [n] raw scores (in: base, out: final)
+  int32_t* idx[2];        // [n_train] positions -> row (idx[0] holds the training rows)
+  int64_t* gh[2];         // [n_train] packed fixed-point (g, h) (gbdt_pack)
+  uint8_t* bkt;           // [n_train]
+  int32_t* cnt;           // [MAXB * W]
+  int32_t* base;          // [MAXB * W]
+  int32_t* btot;          // [MAXB]
+  int32_t* seg[2];        // [MAXB + 1]
+  int64_t* tot;           // [2 M]
+  int32_t* feat;          // [T][M]
+  int32_t* thr;
+  double* value;
+  int64_t* H[2];          // [2^(depth-1)][2][256][p]
+  u64* slab;              // [slab_cap] partial histograms
+  int64_t slab_cap;
+  Cand* cand;             // [32 * ceil(p / 32)] split candidates (32 B each)
+};
+
+typedef int (*GbdtReduceFn)(void* ptr, int64_t count);
+
+// chunk length and (upper bound of the) workgroup count of level d's histogram
+static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH, int64_t* nwg) {
+  const int ydim = (p + FB - 1) / FB;
+  // rows histogrammed: all of them at the root, at most half (count rule) or all
+  // (hessian rule) of them below; `target` workgroups of full chunks (two resident per
+  // CU; each pays a fixed 64-KB LDS clear + slab store, so not too many)
+  const int64_t rows = (d == 0 || rule == 1) ? n_train : (n_train + 1) / 2;
+  static const int target = [] {
+    const char* e = getenv("ATE_GBDT_HIST_TARGET");
+    return e ? std::max(64, atoi(e)) : 512;
+  }();
+  int64_t ch = (rows * ydim + target - 1) / target;
+  ch = std::max<int64_t>(1024, (ch + 255) / 256 * 256);
+  const int64_t wg = (((n_train + ch - 1) / ch + (1 << d)) * ydim + 7) / 8 * 8;
+  *CH = ch;
+  *nwg = wg;
+}
+
+ATE_API int64_t ate_gbdt_slab_entries(int64_t n_train, int p, int depth, int rule) {
+  int64_t m = 0;
+  for (int d = 0; d < depth; ++d) {
+    int64_t ch, wg;
+    gbdt_hist_geom(n_train, p, d, rule, &ch, &wg);
+    m = std::max(m, wg);
+  }
+  return m * SLAB;
+}
+
+ATE_API int ate_gbdt_fit(const void* args, void* reduce, void* stream) {
+  const GbdtFitArgs& a = *static_cast<const GbdtFitArgs*>(args);
+  GbdtReduceFn red = reinterpret_cast<GbdtReduceFn>(reduce);
+  hipStream_t st = (hipStream_t)stream;
+  if (a.depth < 1 || a.depth > 6 || (a.ldr & 31) || a.n_train < 1 || a.W < 1 || a.W > 4 * NT)
+    return -1;
+  if ((a.n_train + a.R - 1) / a.R > a.W) return -2;
+  if (a.slab_cap < ate_gbdt_slab_entries(a.n_train, a.p, a.depth, a.rule)) return -5;
+  const int M = (1 << (a.depth + 1)) - 1;
+  const int ydim = (a.p + FB - 1) / FB, ydim_s = (a.p + SFB - 1) / SFB;
+  const int64_t per = 512LL * a.p;
+  const char* hm = getenv("ATE_GBDT_HIST_MODE");          // ablation switch (profiling only)
+  const int hmode = hm ? atoi(hm) : 0;
+  for (int t = 0; t < a.n_trees; ++t) {
+    int32_t* ft = a.feat + (int64_t)t * M;
+    int32_t* th = a.thr + (int64_t)t * M;
+    double* vt = a.value + (int64_t)t * M;
+    int cur = 0;                                          // ping-pong index of idx/gh/seg
+    hipLaunchKernelGGL(gbdt_grad_kernel, dim3((unsigned)((a.n_train + 4 * NT - 1) / (4 * NT))),
+                       dim3(NT), 0, st, a.loss, a.f, a.y, a.idx[0], a.n_train, a.gh[0],
+                       a.seg[0]);
+    for (int d = 0; d <= a.depth; ++d) {
+      const int nn = 1 << d;
+      int64_t* Hc = a.H[d & 1];
+      const int64_t* Hp = a.H[(d + 1) & 1];
+      if (d < a.depth) {
+        int64_t CH, nwg;
+        gbdt_hist_geom(a.n_train, a.p, d, a.rule, &CH, &nwg);
+        hipLaunchKernelGGL(gbdt_hist_kernel, dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr, a.ldr,
+                           a.idx[cur], a.gh[cur], a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
+                           ydim, a.slab, hmode, a.loss);
+        hipLaunchKernelGGL(gbdt_hist_reduce_kernel,
+                           dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 256), nn),
+                           dim3(NT), 0, st, a.slab, a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
+                           ydim, Hc);
+        if (red && red(Hc, nn * per)) return -4;
+        if (d == 0) hipLaunchKernelGGL(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, Hc, a.p, a.tot);
+        if (d > 0)
+          hipLaunchKernelGGL(gbdt_derive_kernel,
+                             dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 64), nn / 2),
+                             dim3(NT), 0, st, Hp, Hc, a.seg[cur], a.tot, ft, a.rule, nn, a.p, d);
+      }
+      if (d < a.depth)
+        hipLaunchKernelGGL(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc, a.p, d,
+                           a.depth, a.lam, a.min_child, a.tot, ft, a.cand);
+      hipLaunchKernelGGL(gbdt_split_final_kernel, dim3(nn), dim3(64), 0, st, a.cand, ydim_s, d,
+                         a.depth, a.min_gain, a.lam, a.lr, a.tot, ft, th, vt);
+      if (d + 1 < a.depth) {
+        const int nb = 2 * nn + 1;
+        const int W = (int)((a.n_train + a.R - 1) / a.R);
+        hipLaunchKernelGGL(gbdt_part_count_kernel, dim3(W), dim3(NT), 0, st, a.Xr, a.ldr,
+                           a.idx[cur], a.n_train, a.seg[cur], nn, d, ft, th, a.R, W, a.bkt,
+                           a.cnt);
+        hipLaunchKernelGGL(gbdt_part_scan_kernel, dim3(nb), dim3(NT), 0, st, a.cnt, W, a.base,
+                           a.btot);
+        hipLaunchKernelGGL(gbdt_part_scatter_kernel, dim3(W), dim3(NT), 0, st, a.idx[cur],
+                           a.gh[cur], a.bkt, a.n_train, nb, a.R, W, a.base, a.btot,
+                           a.idx[cur ^ 1], a.gh[cur ^ 1], a.seg[cur ^ 1]);
+        cur ^= 1;
+      }
+    }
+    // the next tree starts from whichever order this one left: keep idx[0] current
+    if (cur == 1 &&
+        hipMemcpyAsync(a.idx[0], a.idx[1], a.n_train * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                       st) != hipSuccess)
+      return -3;
+    gbdt_launch_apply(a.Xr, a.ldr, a.n, 1, M, ft, th, vt, a.f, st);
+  }
   ATE_CHECK_LAUNCH();
   return 0;
 }
 
-// H must be zeroed by the caller ([nn][p][256][2] int64); nn <= 32
-ATE_API int ate_gbdt_hist(const void* Xb, int64_t ld, const void* node, const void* gh, int64_t n,
-                          int nn, int p, void* H, void* stream) {
-  if (nn < 1 || nn > 32) return -1;
-  const int F = max(1, min(p, 32 / nn));
-  const int64_t chunk = 16384;
-  dim3 grid((unsigned)((n + chunk - 1) / chunk), (unsigned)((p + F - 1) / F));
-  const size_t shb = (size_t)F * nn * 512 * sizeof(u64);
-  hipLaunchKernelGGL(gbdt_hist_kernel, grid, dim3(NT), shb, (hipStream_t)stream,
-                     (const uint8_t*)Xb, ld, (const int32_t*)node, (const int64_t*)gh, n, nn, p, F,
-                     chunk, (int64_t*)H);
-  ATE_CHECK_LAUNCH();
-  return 0;
-}
-
-ATE_API int ate_gbdt_split(const void* H, int nn, int p, int d, int depth, double lam,
-                           int64_t min_child, double min_gain, double lr, void* tot, void* feat,
-                           void* thr, void* value, void* stream) {
-  hipLaunchKernelGGL(gbdt_split_kernel, dim3(nn), dim3(NT), 0, (hipStream_t)stream,
-                     (const int64_t*)H, nn, p, d, depth, lam, min_child, min_gain, lr,
-                     (int64_t*)tot, (int32_t*)feat, (int32_t*)thr, (double*)value);
-  ATE_CHECK_LAUNCH();
-  return 0;
-}
-
-ATE_API int ate_gbdt_partition(const void* Xb, int64_t ld, void* node, int64_t n, int d,
-                               const void* feat, const void* thr, void* stream) {
-  hipLaunchKernelGGL(gbdt_partition_kernel, dim3(ate::grid_for(n, NT, 2048)), dim3(NT), 0,
-                     (hipStream_t)stream, (const uint8_t*)Xb, ld, (int32_t*)node, n, d,
-                     (const int32_t*)feat, (const int32_t*)thr);
-  ATE_CHECK_LAUNCH();
-  return 0;
-}
-
-ATE_API int ate_gbdt_apply(const void* Xb, int64_t ld, int64_t n, int ntree, int M,
+ATE_API int ate_gbdt_apply(const void* Xr, int64_t ldr, int64_t n, int ntree, int M,
                            const void* feat, const void* thr, const void* value, void* f,
                            void* stream) {
-  hipLaunchKernelGGL(gbdt_apply_kernel, dim3(ate::grid_for(n, NT, 2048)), dim3(NT), 0,
-                     (hipStream_t)stream, (const uint8_t*)Xb, ld, n, ntree, M,
-                     (const int32_t*)feat, (const int32_t*)thr, (const double*)value,
-                     (double*)f);
+  if (M > 127 || (ldr & 15)) return -1;
+  gbdt_launch_apply((const uint8_t*)Xr, ldr, n, ntree, M, (const int32_t*)feat,
+                    (const int32_t*)thr, (const double*)value, (double*)f, (hipStream_t)stream);
   ATE_CHECK_LAUNCH();
   return 0;
 }

@@ -43,3 +43,42 @@ def test_dml_gbdt_gpu_vs_host(gpu, tutorial):
     b = dml_plr_gbdt(m.Y, m.W, m.X, n_trees=10, depth=4, device="cpu")
     assert a.ate == pytest.approx(b.ate, abs=2e-3)
     assert a.se == pytest.approx(b.se, rel=0.05)
+
+
+def _wide(n=20000, p=70, seed=3):
+    r = np.random.default_rng(seed)
+    X = r.normal(size=(n, p))
+    X[:, 3] = np.round(X[:, 3])                 # a few-distinct-values feature
+    y = np.sin(X[:, 0]) + 0.5 * (X[:, 40] > 0) + X[:, 69] * X[:, 3] + 0.1 * r.normal(size=n)
+    return X, y
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_gbdt_gpu_wide_identical(gpu, sharded):
+    """p > 32 (several 32-feature histogram blocks, a partial last block), depth 6
+    (five partitions, histogram subtraction at every level); ``sharded`` runs the
+    row-shard path (hessian child rule + reduce callback) on a one-rank context."""
+    from ate_replication_causalml_amd.parallel.comm import LocalComm
+    from ate_replication_causalml_amd.parallel.dist import DistContext
+    X, y = _wide()
+    tr = np.arange(len(y)) % 5 != 2
+    edges = G.global_bin_edges(X, None)
+    kw = dict(n_trees=4, depth=6, lr=0.3, train=tr, edges=edges)
+    dist = DistContext(LocalComm(), 0, len(y)) if sharded else None
+    a = G.fit_gbdt(X, y, backend="gpu", dist=dist, **kw)
+    b = G.fit_gbdt(X, y, backend="cpu", **kw)
+    np.testing.assert_array_equal(a.feat.cpu().numpy(), b.feat)
+    np.testing.assert_array_equal(a.thr.cpu().numpy()[b.feat >= 0], b.thr[b.feat >= 0])
+    np.testing.assert_array_equal(a.value.cpu().numpy(), b.value)
+    # scores of every row (train and held out) equal the host reference's
+    np.testing.assert_allclose(a.scores.cpu().numpy(), b.scores, rtol=0, atol=1e-12)
+
+
+def test_bin_edges_device_matches_host(gpu):
+    import torch
+    from ate_replication_causalml_amd.models import forest as F
+    X, _ = _wide(5000, 70)
+    e1, n1 = F.bin_edges(X)
+    e2, n2 = F.bin_edges_device(torch.as_tensor(X, device=gpu))
+    np.testing.assert_array_equal(n1, n2)
+    np.testing.assert_array_equal(e1, e2)
