@@ -221,7 +221,7 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
     rule = 0 if dist is None else 1
     cap = int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule))
     slab = torch.empty(cap, **i64)
-    cand = torch.empty(32 * (-(-p // 32)) * 4, **i64)
+    cand = torch.empty(32 * (-(-p // 8)) * 4, **i64)
     P = ctypes.c_void_p
     a = FitArgs(Xr=Xr.data_ptr(), ldr=ldr, n=n, n_train=n_train, p=p, depth=depth,
                 n_trees=n_trees, loss=LOSS[loss], rule=rule, W=W, lam=lam,

@@ -19,8 +19,8 @@
 //   sums each node's slabs into H[node][c][bin][feature] — no global atomics. Only the
 //   SMALLER child of each split parent is histogrammed — the sibling is parent - child
 //   (histogram subtraction), so levels >= 1 touch at most half of the rows;
-// * split search: workgroup = (node, 32-feature block) staged in LDS, thread = (feature,
-//   16-bin segment); a one-wave finalize picks each node's best block candidate;
+// * split search: workgroup = (node, 8-feature block) staged in LDS, wave = feature,
+//   lane = 4 bins; a one-wave finalize picks each node's best block candidate;
 // * the whole boosting loop (grad -> per level: hist / [reduce] / derive / split /
 //   partition -> apply) is issued from C++ on one stream; row-sharded fits pass a
 //   host callback that all-reduces each level's histograms (root totals come from the
@@ -35,7 +35,7 @@ namespace {
 constexpr int NT = 256;
 constexpr int NTH = 512;             // histogram workgroup (two per CU: 2 x 64-KB LDS images)
 constexpr int FB = 16;               // features per histogram workgroup
-constexpr int SFB = 32;              // features per split-search workgroup
+constexpr int SFB = 8;               // features per split-search workgroup (one per wave)
 constexpr int HS = 257;              // padded bins per (feature, channel) in LDS
 constexpr int MAXB = 65;             // partition buckets: 2 * 32 children + retired
 constexpr double GFIX = 268435456.0;   // 2^28
@@ -323,7 +323,7 @@ __device__ __forceinline__ bool better(double g, int j, int b, const Best& o) {
   return j < o.j || (j == o.j && b < o.b);
 }
 
-constexpr int NTS = 512;   // split search workgroup: 32 features x 16 bin segments
+constexpr int NTS = 512;   // split search workgroup: one wave per feature of an 8-feature block
 
 struct Cand {               // best split of one (node, feature block)
   double gain;
@@ -331,54 +331,64 @@ struct Cand {               // best split of one (node, feature block)
   int64_t gl, hl;
 };
 
-// grid (node, 32-feature block): the block's [c][bin][32] histogram slice is staged in
-// LDS (256-B rows: conflict-free 8-B reads, lane = feature); thread = (feature, 16-bin
-// segment); segment totals are scanned through LDS; each thread scores its 16 split
-// points (ascending bins, strict > keeps the lowest on ties) and the workgroup's best
-// (gain desc, feature asc, bin asc) goes to cand[node][block].
+// grid (node, 8-feature block): the block's histograms are staged feature-major in LDS
+// ([c][f][bin], so a lane's 4 consecutive bins are two 16-B reads); wave = feature,
+// lane = 4 bins: lane totals, in-wave exclusive scan, running prefix and the gains of
+// the 4 split points (ascending bins, strict > keeps the lowest on ties), wave argmax
+// (gain desc, feature asc, bin asc); the workgroup's best goes to cand[node][block].
 __global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
     const int64_t* __restrict__ H, int p, int d, int depth, double lam, int64_t min_child,
     const int64_t* __restrict__ tot, const int32_t* __restrict__ feat, Cand* __restrict__ cand) {
-  __shared__ int64_t sh[2 * 256 * SFB];
-  __shared__ int64_t segs[2][16][SFB];
+  __shared__ __attribute__((aligned(16))) int64_t sh[2 * SFB * 256];
   __shared__ Cand wb[NTS / 64];
   const int k = blockIdx.x, yb = blockIdx.y, ydim = gridDim.y;
   const int hk = (1 << d) - 1 + k;
   if (d >= depth || (d > 0 && feat[(hk - 1) / 2] < 0)) return;
   const int j0 = yb * SFB, nf = min(SFB, p - j0);
   const int64_t* Hk = H + (int64_t)k * 512 * p + j0;
-  for (int t = threadIdx.x; t < 512 * SFB; t += NTS) {
-    const int cb = t >> 5, fl = t & 31;
-    const int64_t v = Hk[(int64_t)cb * p + min(fl, nf - 1)];
-    sh[t] = fl < nf ? v : 0;
-  }
-  const int f = threadIdx.x & 31, sg = threadIdx.x >> 5;       // 16 segments of 16 bins
-  __syncthreads();
-  int64_t sgs = 0, shs = 0;
+  {
+    constexpr int PER = 2 * SFB * 256 / NTS;                // entries per thread
+    const int fl = threadIdx.x & (SFB - 1), fc = min(fl, nf - 1);
+    int64_t v[PER];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    sgs += sh[(sg * 16 + i) * SFB + f];
-    shs += sh[(256 + sg * 16 + i) * SFB + f];
+    for (int i = 0; i < PER; ++i) {
+      const int cb = (threadIdx.x + i * NTS) / SFB;
+      v[i] = Hk[(int64_t)cb * p + fc];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int cb = (threadIdx.x + i * NTS) / SFB;
+      sh[((cb >> 8) * SFB + fl) * 256 + (cb & 255)] = v[i];
+    }
   }
-  segs[0][sg][f] = sgs;
-  segs[1][sg][f] = shs;
   __syncthreads();
-  int64_t GL = 0, HL = 0;
-  for (int q = 0; q < sg; ++q) { GL += segs[0][q][f]; HL += segs[1][q][f]; }
+  const int lane = threadIdx.x & 63, f = threadIdx.x >> 6;
   const int64_t G = tot[2 * hk], Hh = tot[2 * hk + 1];
   const double gf = (double)G / GFIX, hf = (double)Hh / GFIX;
   const double parent = gf * gf / (hf + lam);
   Cand lb{-INFINITY, j0 + f, 0x7fffffff, 0, 0};
-  if (f < nf) {
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      GL += sh[(sg * 16 + i) * SFB + f];
-      HL += sh[(256 + sg * 16 + i) * SFB + f];
+  if (f < nf) {                                             // uniform per wave
+    const longlong2* pg = reinterpret_cast<const longlong2*>(sh + f * 256 + 4 * lane);
+    const longlong2* ph = reinterpret_cast<const longlong2*>(sh + (SFB + f) * 256 + 4 * lane);
+    const longlong2 g01 = pg[0], g23 = pg[1], h01 = ph[0], h23 = ph[1];
+    const int64_t gv[4] = {g01.x, g01.y, g23.x, g23.y}, hv[4] = {h01.x, h01.y, h23.x, h23.y};
+    const int64_t sg = gv[0] + gv[1] + gv[2] + gv[3], sh2 = hv[0] + hv[1] + hv[2] + hv[3];
+    int64_t eg = sg, eh = sh2;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t tg = __shfl_up(eg, o, 64), th = __shfl_up(eh, o, 64);
+      if (lane >= o) { eg += tg; eh += th; }
+    }
+    int64_t GL = eg - sg, HL = eh - sh2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      GL += gv[i];
+      HL += hv[i];
       if (HL >= min_child && Hh - HL >= min_child) {
         const double glf = (double)GL / GFIX, hlf = (double)HL / GFIX;
         const double grf = gf - glf, hrf = hf - hlf;
         const double gain = glf * glf / (hlf + lam) + grf * grf / (hrf + lam) - parent;
-        if (gain > lb.gain) lb = {gain, j0 + f, sg * 16 + i, GL, HL};
+        if (gain > lb.gain) lb = {gain, j0 + f, 4 * lane + i, GL, HL};
       }
     }
   }
@@ -392,8 +402,7 @@ __global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
     ob.hl = __shfl_xor(lb.hl, o, 64);
     if (better(ob.gain, ob.j, ob.b, Best{lb.gain, lb.j, lb.b})) lb = ob;
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0) wb[wid] = lb;
+  if (lane == 0) wb[f] = lb;
   __syncthreads();
   if (threadIdx.x == 0) {
     Cand b = wb[0];
@@ -634,7 +643,7 @@ struct GbdtFitArgs {
   int64_t* H[2];          // [2^(depth-1)][2][256][p]
   u64* slab;              // [slab_cap] partial histograms
   int64_t slab_cap;
-  Cand* cand;             // [32 * ceil(p / 32)] split candidates (32 B each)
+  Cand* cand;             // [32 * ceil(p / 8)] split candidates (32 B each)
 };
 
 typedef int (*GbdtReduceFn)(void* ptr, int64_t count);
