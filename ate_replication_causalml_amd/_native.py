@@ -65,6 +65,9 @@ _SIGS = {
     "ate_gbdt_slab_entries": "liii",
     "ate_gbdt_apply": "plliipppp" + "p",
     "ate_panel_xv": "iplpipiplpp",
+    "ate_col_moments": "pllipppp",
+    "ate_standardize": "pllippp",
+    "ate_interactions": "pllipl" + "p",
 }
 _RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}

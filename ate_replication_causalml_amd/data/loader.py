@@ -10,6 +10,7 @@ uses a Philox permutation (purpose P_SAMPLE_ROWS) instead of R's Mersenne-Twiste
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from ..parallel import rng
 from .dgp import BIN_NAMES, CTS_NAMES, TutorialData, r_scale
@@ -17,7 +18,9 @@ from .dgp import BIN_NAMES, CTS_NAMES, TutorialData, r_scale
 OUTCOME, TREATMENT = "outcome_voted", "treat_neighbors"
 
 
-def load_social_pressure(path, n_obs: int = 50_000, seed: int = 1991) -> TutorialData:
+def load_social_pressure(path, n_obs: int = 50_000, seed: int = 1991,
+                         device=None) -> TutorialData:
+    """``device="cuda"`` standardises on the GPU (K02, csrc/prep.hip); same formulas."""
     import pandas as pd
     cols = list(CTS_NAMES) + list(BIN_NAMES) + [OUTCOME, TREATMENT]
     raw = pd.read_csv(path, usecols=cols)
@@ -30,9 +33,13 @@ def load_social_pressure(path, n_obs: int = 50_000, seed: int = 1991) -> Tutoria
     sub = raw[cols].astype(np.float64)
     cts = sub[list(CTS_NAMES)].to_numpy()
     # R scale() ignores NA within a column; rows with any NA are dropped afterwards
-    cm = np.nanmean(cts, 0)
-    cs = np.nanstd(cts, 0, ddof=1)
-    cts = (cts - cm) / np.where(cs > 0, cs, 1.0)
+    if device is not None and torch.device(device).type == "cuda":
+        from ..ops.prep import r_scale as dev_scale
+        cts = dev_scale(torch.as_tensor(cts, device=device), constant_to_one=True).cpu().numpy()
+    else:
+        cm = np.nanmean(cts, 0)
+        cs = np.nanstd(cts, 0, ddof=1)
+        cts = (cts - cm) / np.where(cs > 0, cs, 1.0)
     X = np.column_stack([cts, sub[list(BIN_NAMES)].to_numpy()])
     Y = sub[OUTCOME].to_numpy()
     W = sub[TREATMENT].to_numpy()

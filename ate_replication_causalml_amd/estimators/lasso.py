@@ -65,9 +65,10 @@ def lasso_usual(Y, W, X, seed=1991, nfolds=10, fold_stream=6, method="Usual LASS
 
 
 def interaction_expand(x: torch.Tensor) -> torch.Tensor:
-    """K21 (small p): [x, x_c1 * x_c2 for all ordered pairs incl. squares] (Q10)."""
-    n, p = x.shape
-    return torch.cat([x, (x[:, :, None] * x[:, None, :]).reshape(n, p * p)], 1)
+    """K21 (small p): [x, x_c1 * x_c2 for all ordered pairs incl. squares] (Q10);
+    a HIP kernel on device tensors (ops/prep.py)."""
+    from ..ops.prep import interactions
+    return interactions(x)
 
 
 def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni et.al",
