@@ -3,9 +3,10 @@
 // For every row i of held-out segment k:
 //   yr_i = y_i - (cy[k][0] + x_i . cy[k][1:]) ,  wr_i = w_i - (cw[k][0] + x_i . cw[k][1:])
 // and the orthogonal-score moments {S_wy, S_ww, S_yyww, S_yw3, S_w4, n, S_yy} are
-// accumulated in fp64 -- the residual vectors are never written to HBM. The panel
-// is read exactly once (bandwidth-bound: one column-major stream per feature,
-// coalesced across the 256 rows of a block). Coefficients for all folds are staged
+// accumulated in fp64 -- the residual vectors are never written to HBM. Only the
+// columns in the fold's LASSO support (nonzero Y- or W-coefficient) are read, once
+// each (bandwidth-bound: one column-major stream per feature, coalesced across the
+// 256 rows of a block). Coefficients for all folds are staged
 // in LDS. y/w are reconstructed from their hi+lo bf16 columns on bf16 panels.
 #include "common.hpp"
 
@@ -22,6 +23,36 @@ __device__ __forceinline__ double ld_col<bf16_t>(const bf16_t* X, int64_t ld, in
 
 struct Seg { int64_t r0, r1; };
 
+// Ordered compaction (ascending j, so the dot products keep their summation order and
+// the result is bit-identical to the dense loop) of the feature columns whose Y- or
+// W-coefficient is nonzero: LASSO nuisances are sparse, so the pass reads only the
+// selected columns of the panel. cy/cw/xc: dense staged arrays; outputs in place
+// (cy[1+q], cw[1+q], xc[q] for q < *nnz). Whole block must call it.
+template <typename C>
+__device__ int compact_support(C* cy, C* cw, int* xc, int p, int* wcnt /* [>= 4] */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int base = 0;
+  for (int j0 = 0; j0 < p; j0 += blockDim.x) {
+    const int j = j0 + threadIdx.x;
+    const bool keep = j < p && (cy[1 + j] != C(0) || cw[1 + j] != C(0));
+    C vy = j < p ? cy[1 + j] : C(0), vw = j < p ? cw[1 + j] : C(0);
+    const int c = j < p ? xc[j] : 0;
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) wcnt[wid] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wid; ++w) off += wcnt[w];
+    int tot = base;
+    for (int w = 0; w < nw; ++w) tot += wcnt[w];
+    const int pos = off + __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();                                      // all reads of the dense slots done
+    if (keep) { cy[1 + pos] = vy; cw[1 + pos] = vw; xc[pos] = c; }
+    __syncthreads();
+    base = tot;
+  }
+  return base;
+}
+
 template <typename T, int RPT>
 __global__ __launch_bounds__(256) void dml_resid_kernel(
     const T* __restrict__ X, int64_t ld, const int* __restrict__ xcols, int p,
@@ -32,6 +63,7 @@ __global__ __launch_bounds__(256) void dml_resid_kernel(
   double* cw = sh + (p + 1);          // [p+1]
   int* xc = (int*)(sh + 2 * (p + 1)); // [p]
   __shared__ double red[16 * 7];
+  __shared__ int wcnt[16];
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int j = threadIdx.x; j < p; j += blockDim.x) xc[j] = xcols[j];
   // grid: blockIdx.y = segment; blocks stride over that segment's rows
@@ -41,6 +73,7 @@ __global__ __launch_bounds__(256) void dml_resid_kernel(
     cw[j] = coef[((int64_t)k * 2 + 1) * (p + 1) + j];
   }
   __syncthreads();
+  p = compact_support(cy, cw, xc, p, wcnt);
   const Seg sg = segs[k];
   for (int64_t base = sg.r0 + (int64_t)blockIdx.x * 256 * RPT; base < sg.r1;
        base += (int64_t)gridDim.x * 256 * RPT) {
@@ -124,6 +157,7 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
   float* cw = shf + (p + 1);       // [p+1]
   int* xc = (int*)(shf + 2 * (p + 1));
   __shared__ double red[16 * 7];
+  __shared__ int wcnt[16];
   const int k = blockIdx.y;
   for (int j = threadIdx.x; j < p; j += blockDim.x) xc[j] = xcols[j];
   for (int j = threadIdx.x; j <= p; j += blockDim.x) {
@@ -131,6 +165,7 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
     cw[j] = (float)coef[((int64_t)k * 2 + 1) * (p + 1) + j];
   }
   __syncthreads();
+  p = compact_support(cy, cw, xc, p, wcnt);
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   const Seg sg = segs[k];
   auto ld8 = [&](int c, int64_t i, float (&o)[8]) {
