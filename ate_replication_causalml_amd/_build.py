@@ -24,7 +24,7 @@ ARCH = os.environ.get("ATE_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             "-ffp-contract=fast", "-Wno-unused-result"]
+             "-ffp-contract=fast-honor-pragmas", "-Wno-unused-result"]
 NO_CONTRACT = {"forest.hip", "gbdt.hip"}
 CPU_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-march=x86-64-v2"]
 

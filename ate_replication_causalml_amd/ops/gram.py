@@ -21,6 +21,12 @@ BF16_TILE_BIG = 256
 SMALL_TILE, SMALL_K = 64, 16
 TARGET_WG = 2048   # workgroups per launch (>= 8 per CU on 256 CUs)
 
+# 256-tile kernel: 1 = 2-stage BK=64 LDS-DMA (default), 0 = 4-stage BK=32 pipeline.
+# Measured at N=1e7, p=500 (tools/gram_only.py, tools/pmc_gram.sh): 4.0 vs 5.0 ms -- the
+# BK=32 stages fetch half cache lines (TA busy 3x, L2 requests 2x) and lose more than the
+# deeper prefetch gains.
+GRAM_VARIANT = int(os.environ.get("ATE_GRAM_VARIANT", "1"))
+
 _plan_cache = {}
 
 
@@ -95,7 +101,8 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     G = pl.G if out is None else out
     s = _stream()
     if X.dtype == torch.bfloat16:
-        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.T, pl.tiles.data_ptr(),
+        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.T, GRAM_VARIANT,
+                     pl.tiles.data_ptr(),
                      pl.ntiles, pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(),
                      panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
     else:

@@ -381,25 +381,60 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         // deferred (delta + the gradient it was computed from), so the loop body is the
         // bare coordinate recurrence.
         double gbef = 0.0;
-        int last = -1;
-        while (true) {
+        // Candidate test folded into ONE compare: a lane > last moves iff it is eligible
+        // and (nonzero, or |u| > vp*lambda). `at` of a lane > last is constant during the
+        // visit, so the nonzero case becomes threshold -1 (always passes) and ineligible
+        // lanes get +inf; lanes <= last are cut with a scalar mask. The proposed step
+        // an - at of every lane is computed alongside the ballot, so the serial chain is
+        // fma -> add -> compare/ballot -> ff1 -> readlane -> fma. Per update the loop only
+        // records the new coefficient and the gradient it came from for the moving lane;
+        // the delta (an - at, the same operation on the same operands as the broadcast
+        // step) and the new coefficient are applied after the loop. Unrolled twice: one
+        // taken branch per two updates.
+        const double thr0 = elig ? (at != 0.0 ? -1.0 : thr_l) : __builtin_inf();
+        uint64_t live = ~0ull, moved = 0ull;
+        double anv = at;
+#ifdef ENET_PROF
+        unsigned long long nupd_ = 0;
+#endif
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): dg_* landed; no waits in the loop
+        auto step = [&]() -> bool {
+#pragma clang fp contract(off)
           const double u = gt + at;
-          const bool cand = elig & (lane > last) & ((at != 0.0) | (fabs(u) > thr_l));
-          const uint64_t msk = __builtin_amdgcn_ballot_w64(cand);
-          if (!msk) break;
+          const double au = fabs(u);
+          const uint64_t msk = __builtin_amdgcn_ballot_w64(au > thr0) & live;
+          const double an = __dmul_rn(copysign(fmax(au - thr_l, 0.0), u), rden);   // no fma: d == an - at
+          const double dd = an - at;
+          asm volatile("" : : "v"(dd));    // keep the step computation ahead of the branch
+          if (!msk) return false;
           const int i = __ffsll((unsigned long long)msk) - 1;
-          last = i;
           const float clo = dg_lo[i & 31], chi = dg_hi[i & 31];   // masked: stays in VGPRs
           const float ci = i < 32 ? clo : chi;
-          const double vv = fabs(u) - thr_l;
-          const double an = vv > 0.0 ? copysign(vv, u) * rden : 0.0;
-          const double d = readlane_d(an - at, i);
+          const double d = readlane_d(dd, i);
           const bool me = lane == i;
-          at = me ? an : at;               // d == 0 -> an == at
           gbef = me ? gt : gbef;
-          dblk = me ? d : dblk;
           gt -= (double)ci * d;
+          __builtin_amdgcn_sched_barrier(0);   // bookkeeping below stays off the chain
+          live = i == 63 ? 0ull : (~0ull << (i + 1));
+          moved |= 1ull << i;
+          anv = me ? an : anv;
+#ifdef ENET_PROF
+          if (lane == 0) ++nupd_;
+#endif
+          return true;
+        };
+        while (step() && step()) {
         }
+        if ((moved >> lane) & 1ull) {
+          dblk = anv - at;                 // == the broadcast step d of this lane
+          at = anv;
+        }
+#ifdef ENET_PROF
+        if (lane == 0) {
+          atomicAdd(&enet_prof[q][6], (unsigned long long)(wall_clock64() - ta_));
+          atomicAdd(&enet_prof[q][7], nupd_);
+        }
+#endif
         if (dblk != 0.0) {
           rsq_l += dblk * (2.0 * gbef - dblk);
           dlx_l = fmax(dlx_l, dblk * dblk);

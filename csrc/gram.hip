@@ -211,6 +211,122 @@ __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
       }
 }
 
+// ------------------------------------------------------------------ bf16 256x256, 4-stage pipeline
+// Same 8-wave 2x4 decomposition as above, but the K-step is ONE MFMA deep (32 rows) and
+// the LDS holds NST = 4 stages (4 x (A+B) x 256 cols x 64 B = 128 KB), so three stages of
+// LDS-DMA are in flight while a stage is consumed (~3 x 1000 MFMA cycles of prefetch
+// distance instead of one step). The barrier is a raw s_barrier preceded by a COUNTED
+// vmcnt (stages still allowed in flight x glds per stage), never a vmcnt(0) drain.
+// LDS image of a stage: column-major, 64 B (4 chunks of 8 rows) per column; logical
+// chunk cc of column c sits at position cc ^ H[(c >> 2) & 3] with H = {0,3,2,1}, which
+// makes every 16-lane group of a ds_read_b128 fragment load hit 16 distinct 4-bank
+// groups (conflict-free). The swizzle is applied on the DMA source address.
+constexpr int PK = 32;
+constexpr int NST = 4;
+
+__device__ __forceinline__ int pk_swz(int col) { return (0x1230 >> (((col >> 2) & 3) * 4)) & 3; }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 16, "vmcnt immediate");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+}
+
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    default: wait_vm<8>(); break;
+  }
+}
+
+__global__ __launch_bounds__(512) void gram_bf16_256p_kernel(
+    const bf16_t* __restrict__ X, int64_t ld, const int2* __restrict__ tiles, int ntiles,
+    const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NST][2][GT * PK];   // 128 KB
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = L / ntiles, t = L % ntiles;
+  const Chunk ch = chunks[c];
+  const int2 tl = tiles[t];
+  const bool diag = tl.x == tl.y;
+  const int a0 = tl.x * GT, b0 = tl.y * GT;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // a stage = 16 pieces of 1 KB (16 columns x 64 B) per operand; wave w stages pieces
+  // 2w, 2w+1 of A (and of B off the diagonal): 2 or 4 glds per wave per stage
+  const int per_stage = diag ? 2 : 4;
+  const int scol = lane >> 2;
+  auto stage = [&](int st, int64_t i0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int q = wid * 2 + r;
+      const int col = q * 16 + scol;
+      const int cc = (lane & 3) ^ pk_swz(col);
+      glds16(X + (int64_t)(a0 + col) * ld + i0 + cc * 8, &lds[st][0][q * 16 * PK]);
+      if (!diag) glds16(X + (int64_t)(b0 + col) * ld + i0 + cc * 8, &lds[st][1][q * 16 * PK]);
+    }
+  };
+
+  const int nsteps = (int)((ch.row1 - ch.row0) / PK);
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (j < nsteps) stage(j, ch.row0 + (int64_t)j * PK);
+
+  const int fc = lane & 15, kc = lane >> 4;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s % NST;
+    // stage s landed (this wave's part) once at most `ahead` later stages are pending
+    const int ahead = min(NST - 2, nsteps - 1 - s);
+    wait_vm_rt(ahead * per_stage);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // ... and every wave's part; also retires reads of s-1
+    asm volatile("" ::: "memory");
+    if (s + NST - 1 < nsteps) stage((s + NST - 1) % NST, ch.row0 + (int64_t)(s + NST - 1) * PK);
+    const bf16_t* As = lds[cur][0];
+    const bf16_t* Bs = diag ? lds[cur][0] : lds[cur][1];
+    bf16x8 af[8], bfr[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = wc * 64 + n * 16 + fc;
+      bfr[n] = *reinterpret_cast<const bf16x8*>(&Bs[col * PK + ((kc ^ pk_swz(col)) << 3)]);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int col = wr * 128 + m * 16 + fc;
+      af[m] = *reinterpret_cast<const bf16x8*>(&As[col * PK + ((kc ^ pk_swz(col)) << 3)]);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+  }
+  float* out = slab + ((int64_t)c * ntiles + t) * (GT * GT);
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 128 + m * 16 + (lane >> 4) * 4 + r;
+        const int col = wc * 64 + n * 16 + (lane & 15);
+        out[row * GT + col] = acc[m][n][r];
+      }
+}
+
 // ------------------------------------------------------------------ fp32 / fp64 64x64
 constexpr int FT = 64;
 constexpr int FK = 16;
@@ -318,15 +434,20 @@ __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2
 // chunks/tiles/seg_chunk0 are device arrays prepared by the caller (ops/gram.py).
 // tile = 128 (4 waves, register-staged) or 256 (8 waves, LDS-DMA staged); the caller's
 // tile table and chunk plan must use the same tile size.
-ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile, const void* tiles,
-                          int ntiles, const void* chunks, int nchunks, const void* seg_chunk0,
-                          int nseg, void* slab, void* G, void* stream) {
+// variant (tile 256 only): 0 = 4-stage BK=32 pipelined kernel, 1 = 2-stage BK=64 kernel.
+ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile, int variant,
+                          const void* tiles, int ntiles, const void* chunks, int nchunks,
+                          const void* seg_chunk0, int nseg, void* slab, void* G, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int nwg = nchunks * ntiles;
   if (tile == GT) {
     if (P % GT) return -1;
-    hipLaunchKernelGGL(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
-                       (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
+    if (variant == 0)
+      hipLaunchKernelGGL(gram_bf16_256p_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
+                         (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
+    else
+      hipLaunchKernelGGL(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
+                         (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
   } else if (tile == BT) {
     if (P % BT) return -1;
     hipLaunchKernelGGL(gram_bf16_kernel, dim3(nwg), dim3(256), 0, s, (const bf16_t*)X, ld,

@@ -44,6 +44,21 @@ def test_gram_kernel_vs_fp64(gpu, dtype, p):
     assert torch.allclose(G, G.transpose(1, 2))
 
 
+def test_gram_256_variants_agree(gpu, monkeypatch):
+    # 4-stage pipelined (default) and 2-stage 256-tile kernels: same sums per tile
+    rs = np.random.RandomState(3)
+    n = 20000
+    X = rs.randn(n, 400)
+    pan = build_panel(X, rs.rand(n), rs.randint(0, 2, n), folds=rs.randint(0, 5, n),
+                      dtype="bf16", device=gpu)
+    G0 = gram_op.gram(pan).clone()
+    monkeypatch.setattr(gram_op, "GRAM_VARIANT", 1)
+    G1 = gram_op.gram(pan)
+    ref = gram_op.gram_reference(pan).to(gpu)
+    assert ((G0 - ref).abs().max() / ref.abs().max()) < 2e-6
+    assert ((G0 - G1).abs().max() / ref.abs().max()) < 2e-6
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_weighted_gram_kernel(gpu, dtype):
     rs = np.random.RandomState(1)

@@ -24,7 +24,7 @@ def build():
     objs = [o for o in objs if o.name != "enet.hip.o"]
     prof_o = ROOT / "build" / "enet_prof.o"
     subprocess.run([B.HIPCC, "-O3", "-fPIC", "-std=c++17", f"--offload-arch={B.ARCH}",
-                    "-ffp-contract=fast", "-munsafe-fp-atomics", "-DENET_PROF", "-c",
+                    "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-DENET_PROF", "-c",
                     str(ROOT / "csrc" / "enet.hip"), "-o", str(prof_o)], check=True)
     subprocess.run([B.HIPCC, "-shared", f"--offload-arch={B.ARCH}", "-o", str(LIB),
                     *map(str, objs), str(prof_o)], check=True)
@@ -55,8 +55,8 @@ def run(n, p):
     rows = buf[:40]
     live = rows[rows[:, 3] > 0]
     print(json.dumps({"step_ms": t[0].elapsed_time(t[1]),
-                      "per_problem": [[int(v) for v in r[:6]] for r in live],
-                      "note": "wall_clock64 ticks (100 MHz): pull, recurrence, -, visits, -, cols"}))
+                      "per_problem": [[int(v) for v in r[:8]] for r in live],
+                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates"}))
 
 
 if __name__ == "__main__":

@@ -1,4 +1,5 @@
-"""Run the bf16 Gram kernel alone on the N=1e7, p=500 bench panel (for PMC profiling)."""
+"""Run the bf16 Gram kernel alone on the N=1e7, p=500 bench panel (A/B of the 256-tile
+kernel variants, and for PMC profiling). Usage: gram_only.py [N] [variant ...]"""
 import os
 import sys
 
@@ -6,17 +7,25 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from ate_replication_causalml_amd.data.device_dgp import synthetic_panel  # noqa: E402
-from ate_replication_causalml_amd.ops.gram import gram  # noqa: E402
+from ate_replication_causalml_amd.ops import gram as gram_mod  # noqa: E402
 
-pan = synthetic_panel(int(float(sys.argv[1]) if len(sys.argv) > 1 else 1e7), p=500, folds=5,
-                      seed=1991, dtype="bf16", device=torch.device("cuda", 0))
-for _ in range(3):
-    gram(pan)
-torch.cuda.synchronize()
-e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e[0].record()
-for _ in range(5):
-    gram(pan)
-e[1].record()
-torch.cuda.synchronize()
-print("gram ms", e[0].elapsed_time(e[1]) / 5)
+n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e7)
+variants = [int(v) for v in sys.argv[2:]] or [gram_mod.GRAM_VARIANT]
+pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.device("cuda", 0))
+ref = None
+for v in variants:
+    gram_mod.GRAM_VARIANT = v
+    for _ in range(3):
+        G = gram_mod.gram(pan)
+    torch.cuda.synchronize()
+    e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e[0].record()
+    for _ in range(10):
+        gram_mod.gram(pan)
+    e[1].record()
+    torch.cuda.synchronize()
+    G = G.clone()
+    diff = 0.0 if ref is None else float((G - ref).abs().max() / ref.abs().max())
+    ref = G if ref is None else ref
+    print(f"variant {v}: gram ms {e[0].elapsed_time(e[1]) / 10:.3f}  rel-diff vs first {diff:.2e}",
+          flush=True)
