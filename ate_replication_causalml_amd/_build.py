@@ -67,7 +67,7 @@ def build_hip(verbose: bool = False) -> Path:
         list(ex.map(_run, jobs))
     lib = LIBDIR / "libatehip.so"
     if jobs or not lib.exists():
-        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(lib), *map(str, objs)])
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-Wl,-z,defs", "-o", str(lib), *map(str, objs)])
     if verbose:
         print(f"built {lib} ({len(jobs)} recompiled)")
     return lib

@@ -122,7 +122,7 @@ constexpr int PMAX = 512;
 #ifdef ENET_PROF
 // cycle accounting per problem (debug builds): [0] pull, [1] recurrence, [2] other,
 // [3] block visits, [4] coordinate updates, [5] pending columns pulled, [6] passes
-__device__ unsigned long long enet_prof[256][8];
+__device__ unsigned long long enet_prof[256][16];
 #define PROF_T(var) const unsigned long long var = wall_clock64()
 #define PROF_ADD(k, v) do { if (tid == 0) enet_prof[q][k] += (v); } while (0)
 #else
@@ -137,6 +137,12 @@ __device__ __forceinline__ float vdot(float4 a, float4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
 __device__ __forceinline__ double vdot(double2 a, double2 b) { return a.x * b.x + a.y * b.y; }
+
+// LDS-DMA: each lane copies 16 B from its own global address to dst + 16 * lane
+__device__ __forceinline__ void glds16f(const float* src, float* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+__device__ __forceinline__ void glds16f(const double*, float*) {}   // fp64 C: unused
 
 __device__ __forceinline__ double readlane_d(double v, int i) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), i);
@@ -186,7 +192,8 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   __shared__ __attribute__((aligned(16))) CT sdelta2[576];
   __shared__ int scl[64];                 // wave 0: changed coordinates of the block
   __shared__ CT scd[64];
-  __shared__ float sCn[64 * 64];          // next block's diagonal block
+  __shared__ __attribute__((aligned(16))) float sCn[64 * 64];     // next block's diagonal block
+  __shared__ __attribute__((aligned(16))) float sCorr[64 * 64];   // C[t rows][tn cols] (fp32 C)
   __shared__ int svis[8], snv, sblk_any[8];
   __shared__ double sdl;
   __shared__ int sany;
@@ -298,8 +305,23 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   // pending for block tn (sdc is frozen until the first barrier) and stage tn's diagonal
   // block in LDS. After the barrier wave 0 publishes block t, completes block tn's
   // gradient and snapshot, and moves tn's diagonal block into registers.
-  auto pull_rest = [&](int tn) {            // waves 1..3
+  auto pull_rest = [&](int t, int tn) {     // waves 1..3
     const int my = wid - 1;
+    if constexpr (sizeof(CT) == 4) {
+      // fp32 C: tn's diagonal block and the (t rows x tn cols) block that wave 0 needs
+      // for block t's own deltas go global -> LDS by DMA (16 B per lane = 4 row segments
+      // of 64 floats per wave instruction), issued first so their latency overlaps the
+      // pending-column gathers below: one memory round trip per visit. Rows >= p are
+      // clamped (finite) and masked where used.
+      for (int pc = my; pc < 32; pc += 3) {
+        const int blk = pc < 16 ? tn : t;
+        const int i = (pc & 15) * 4 + (lane >> 4);
+        const int r = min(blk * 64 + i, p - 1);
+        const CT* src = Cq + (int64_t)r * ldc + tn * 64 + (lane & 15) * 4;
+        float* dst = (pc < 16 ? sCn : sCorr) + (pc & 15) * 256;
+        glds16f(src, dst);
+      }
+    }
     int cnt = 0;
     const int base0 = my * 192;             // private slist/sdelta region (<= 3 * 192 = 576)
     for (int c = my; c < T; c += 3) {
@@ -323,7 +345,8 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     }
     for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     spart[wid][lane] = (double)acc;
-    // tn's diagonal block -> LDS: rows my + 3*ii in two batches of 11 loads in flight
+    if constexpr (sizeof(CT) == 4) return;
+    // fp64 C: tn's diagonal block -> LDS (fp32) through registers, 2 batches of 11 rows
 #pragma unroll
     for (int b2 = 0; b2 < 2; ++b2) {
       float dr[11];
@@ -362,12 +385,16 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     pull(svis[0]);
     PROF_T(tp1_);
     PROF_ADD(0, tp1_ - tp0_);
+    PROF_ADD(8, tp1_ - tp0_);
     for (int v = 0; v < nv; ++v) {
       const int t = svis[v];
       const int tn = v + 1 < nv ? svis[v + 1] : -1;
       const int k = t * 64 + lane;
       PROF_T(ta_);
       double gt = 0.0, at = 0.0, dblk = 0.0;
+      CT corr = 0;                          // wave 0: block t's own deltas applied to tn
+      int nc = 0;                           // wave 0: coordinates of block t that changed
+      uint64_t chm = 0;                     // wave 0: their lane mask
       int fl = 0;
       if (wid == 0) {
         gt = sg[k];
@@ -441,15 +468,16 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
           fl |= 2;
         }
         // block t's own deltas -> block tn (wave-private list, contiguous segments)
-        CT corr = 0;
         if (tn >= 0) {
           const bool ch = dblk != 0.0;
           const uint64_t bal = __builtin_amdgcn_ballot_w64(ch);
           const int pos = __popcll(bal & ((1ull << lane) - 1ull));
           if (ch) { scl[pos] = k; scd[pos] = (CT)dblk; }
-          const int nc = __popcll(bal);
+          nc = __popcll(bal);
+          chm = bal;
           const CT* colt = Cq + tn * 64 + lane;
           int e = 0;
+          if constexpr (sizeof(CT) == 4) e = nc;   // fp32: from sCorr after the barrier
           for (; e + 16 <= nc; e += 16) {
             CT w[16];
 #pragma unroll
@@ -459,12 +487,12 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
           }
           for (; e < nc; ++e) corr += colt[(int64_t)scl[e] * ldc] * scd[e];
         }
-        spart[0][lane] = (double)corr;
+        if constexpr (sizeof(CT) != 4) spart[0][lane] = (double)corr;
 #ifdef ENET_PROF
         if (lane == 0) atomicAdd(&enet_prof[q][2], (unsigned long long)(wall_clock64() - ta_));
 #endif
       } else if (tn >= 0) {
-        pull_rest(tn);
+        pull_rest(t, tn);
 #ifdef ENET_PROF
         if (wid == 1 && lane == 0)
           atomicAdd(&enet_prof[q][4], (unsigned long long)(wall_clock64() - ta_));
@@ -483,15 +511,33 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         sds[t][k] += dblk;       // own changes are already in g_t
         if (tn >= 0) {
           const int kn = tn * 64 + lane;
+          if constexpr (sizeof(CT) == 4) {
+            // block t's own deltas -> block tn from the DMA'd (t rows x tn cols) block.
+            // All 64 rows in ascending order: an unchanged row has d = 0 and adds
+            // fma(c, 0, corr) = corr exactly, so the sum equals the gather over the changed
+            // rows (same order) while the LDS reads stay independent and pipelined.
+            if (chm) {
+              const float dcf = (float)dblk;
+#pragma unroll
+              for (int r = 0; r < 64; ++r)
+                corr += sCorr[r * 64 + lane] *
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dcf), r));
+            }
+            spart[0][lane] = (double)corr;
+          }
           sg[kn] -= spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane];
           sds[tn][k] = dnew;     // block t's columns; waves 1-3 copy the others
 
+          const int rlim = p - tn * 64;    // rows >= p of the DMA'd block are clamped copies
 #pragma unroll
           for (int i = 0; i < 32; ++i) {
-            dg_lo[i] = sCn[i * 64 + lane];
-            dg_hi[i] = sCn[(i + 32) * 64 + lane];
+            dg_lo[i] = i < rlim ? sCn[i * 64 + lane] : 0.f;
+            dg_hi[i] = i + 32 < rlim ? sCn[(i + 32) * 64 + lane] : 0.f;
           }
         }
+#ifdef ENET_PROF
+        if (lane == 0) atomicAdd(&enet_prof[q][9], (unsigned long long)(wall_clock64() - tb_));
+#endif
       } else if (tn >= 0) {
         // snapshot of block tn for every column block except t (unchanged since B1)
         for (int j = (wid - 1) * 64 + lane; j < ldc; j += 192)

@@ -50,13 +50,13 @@ def run(n, p):
     _, _, cv = dml_crossfit_panel(pan, 5, "min")
     t[1].record()
     torch.cuda.synchronize()
-    buf = np.zeros((256, 8), dtype=np.uint64)
+    buf = np.zeros((256, 16), dtype=np.uint64)
     lib.ate_enet_prof_read(buf.ctypes.data_as(ctypes.c_void_p))
     rows = buf[:40]
     live = rows[rows[:, 3] > 0]
     print(json.dumps({"step_ms": t[0].elapsed_time(t[1]),
-                      "per_problem": [[int(v) for v in r[:8]] for r in live],
-                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates"}))
+                      "per_problem": [[int(v) for v in r[:10]] for r in live],
+                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B"}))
 
 
 if __name__ == "__main__":
