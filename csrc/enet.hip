@@ -124,7 +124,7 @@ constexpr int PMAX = 512;
 // [3] block visits, [4] coordinate updates, [5] pending columns pulled, [6] passes
 __device__ unsigned long long enet_prof[256][16];
 #define PROF_T(var) const unsigned long long var = wall_clock64()
-#define PROF_ADD(k, v) do { if (tid == 0) enet_prof[q][k] += (v); } while (0)
+#define PROF_ADD(k, v) do { if (tid == 0) atomicAdd(&enet_prof[q][k], (unsigned long long)(v)); } while (0)
 #else
 #define PROF_T(var)
 #define PROF_ADD(k, v) do { } while (0)
@@ -514,25 +514,33 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
           if constexpr (sizeof(CT) == 4) {
             // block t's own deltas -> block tn from the DMA'd (t rows x tn cols) block.
             // All 64 rows in ascending order: an unchanged row has d = 0 and adds
-            // fma(c, 0, corr) = corr exactly, so the sum equals the gather over the changed
-            // rows (same order) while the LDS reads stay independent and pipelined.
+            // fma(c, 0, corr) = corr exactly, so the sum equals the fma chain over the
+            // changed rows in gather order. 16 LDS reads in flight per batch.
             if (chm) {
               const float dcf = (float)dblk;
 #pragma unroll
-              for (int r = 0; r < 64; ++r)
-                corr += sCorr[r * 64 + lane] *
-                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dcf), r));
+              for (int r0 = 0; r0 < 64; r0 += 16) {
+                float v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = sCorr[(r0 + u) * 64 + lane];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                  corr = __builtin_fmaf(
+                      v[u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dcf), r0 + u)),
+                      corr);
+              }
             }
             spart[0][lane] = (double)corr;
           }
           sg[kn] -= spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane];
           sds[tn][k] = dnew;     // block t's columns; waves 1-3 copy the others
 
-          const int rlim = p - tn * 64;    // rows >= p of the DMA'd block are clamped copies
+          // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] is only read
+          // for a moving coordinate i, and coordinates >= p never move
 #pragma unroll
           for (int i = 0; i < 32; ++i) {
-            dg_lo[i] = i < rlim ? sCn[i * 64 + lane] : 0.f;
-            dg_hi[i] = i + 32 < rlim ? sCn[(i + 32) * 64 + lane] : 0.f;
+            dg_lo[i] = sCn[i * 64 + lane];
+            dg_hi[i] = sCn[(i + 32) * 64 + lane];
           }
         }
 #ifdef ENET_PROF
