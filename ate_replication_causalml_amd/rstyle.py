@@ -29,7 +29,19 @@ def _df(r):
                           "upper_ci": r.upper_ci}])
 
 
+def _compat(run):
+    return (run or RunConfig()).compat
+
+
 def naive_ate(dataset, treatment_var, outcome_var, method="naive", run=None):
+    """Q1: the reference groups by ``treatment_var`` but then reads the group means
+    through the hard-coded column ``mean_df$W`` (ate_functions.R:11-12); with any other
+    treatment name R builds ``data.frame(ATE = numeric(0), ...)`` and stops with
+    "arguments imply differing number of rows". ``compat="reference"`` raises the same
+    way; ``"textbook"`` uses ``treatment_var``."""
+    if treatment_var != "W" and _compat(run) == "reference":
+        raise ValueError("naive_ate: arguments imply differing number of rows: 1, 0 "
+                         "(the reference reads mean_df$W; treatment_var must be 'W')")
     Y, W, _ = _split(dataset, treatment_var, outcome_var)
     return _df(api.ate_naive(Y, W, method=method, run=run))
 
@@ -74,7 +86,10 @@ def prop_score_lasso(dataset, treatment_var, covariates=None, run=None):
 
 
 def doubly_robust(dataset, treatment_var, outcome_var, num_trees=100, bootstrap_se=False,
-                  method="Doubly Robust with Random Forest PS", covariates=None, run=None):
+                  method="Doubly Robust with Random Forest PS", covariates=None, run=None,
+                  **_swallowed):
+    """``**_swallowed``: like randomForest's ``...`` (Q8), extra arguments such as
+    ``seed=`` / ``type=`` are accepted and have no effect."""
     return _df(api.ate_aipw_rf(*_split(dataset, treatment_var, outcome_var, covariates),
                                num_trees=num_trees, bootstrap_se=bootstrap_se, method=method,
                                run=run))
@@ -95,17 +110,28 @@ def belloni(dataset, treatment_var, outcome_var, method="Belloni et.al", covaria
 
 def double_ml(dataset, treatment_var, outcome_var, num_trees=100,
               method="Double Machine Learning", covariates=None, run=None, **kw):
-    # the driver passes num_tree= (R partial matching, ate_replication.Rmd:232)
+    # the driver passes num_tree= (R partial matching, ate_replication.Rmd:232, Q19);
+    # anything else is swallowed like randomForest's `...` (Q8)
     num_trees = kw.pop("num_tree", num_trees)
     return _df(api.ate_double_ml(*_split(dataset, treatment_var, outcome_var, covariates),
                                  num_trees=num_trees, method=method, run=run))
 
 
 def residual_balance_ATE(dataset, treatment_var, outcome_var, optimizer="quadprog",
-                         method="residual_balancing", covariates=None, run=None):
-    """``optimizer`` is accepted for compatibility; the QP is solved exactly by the IPM."""
-    return _df(api.ate_residual_balance(*_split(dataset, treatment_var, outcome_var, covariates),
-                                        BalanceConfig(), method=method, run=run))
+                         method="residual_balancing", covariates=None, run=None, df_mod=None):
+    """``optimizer`` is accepted for compatibility; the QP is solved exactly by the IPM.
+
+    Q16/Q20 (ate_functions.R:394-400, ate_replication.Rmd:240): the reference reads the
+    GLOBAL ``df_mod`` and ignores ``dataset`` (the driver even passes an undefined
+    symbol, harmless under lazy evaluation) and always labels the row
+    "residual_balancing", ignoring ``method``. Under ``compat="reference"`` a given
+    ``df_mod`` replaces ``dataset`` (which may then be None) and the label is fixed;
+    ``"textbook"`` uses ``dataset`` and ``method``."""
+    ref = _compat(run) == "reference"
+    data = df_mod if (ref and df_mod is not None) else dataset
+    label = "residual_balancing" if ref else method
+    return _df(api.ate_residual_balance(*_split(data, treatment_var, outcome_var, covariates),
+                                        BalanceConfig(), method=label, run=run))
 
 
 def causal_forest_ate(dataset, treatment_var, outcome_var, num_trees=2000, seed=12345,
