@@ -47,7 +47,7 @@ _SIGS = {
     "ate_enet_prepare": "piipipiipipipppppppp",
     "ate_enet_path": "pipiippppidddipppppipp",
     "ate_enet_coef": "ppiiiipppppppp",
-    "ate_enet_cvloss_gauss": "pippiipppiipp",
+    "ate_enet_cvloss_gauss": "pippiipppiiipp",
     "ate_cv_select": "pppiipipppp",
     "ate_enet_pick": "ppiiiipp",
     "ate_dml_resid_moments": "iplpipipiiiiiippp",

@@ -179,7 +179,7 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     ycol_p = const([0] * nf + list(fold_ycol), torch.int32, dev)
     cvraw = torch.empty((nq, L), **f64)
     _native.call("ate_enet_cvloss_gauss", G.data_ptr(), P, hold.data_ptr(), xc.data_ptr(), p, one,
-                 ycol_p.data_ptr(), coef.data_ptr(), nlam.data_ptr(), L, nq,
+                 ycol_p.data_ptr(), coef.data_ptr(), nlam.data_ptr(), L, nf, nq - nf,
                  cvraw.data_ptr(), s)
     fidx = const(fold_index + nf, torch.int32, dev)
     nfold_t = const(nfold, torch.float64, dev)

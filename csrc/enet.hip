@@ -739,69 +739,121 @@ ATE_API int ate_enet_coef(const void* apath, const void* probs, int nprob, int p
 // cvraw[q][m] = SSE / n_hold using the raw held-out Gram G[hold] (panel columns).
 // The nonzero coefficients are compacted first (ordered ballot scan), so the quadratic
 // form costs nnz^2 instead of p^2 — LASSO paths are sparse over most lambdas.
+// One workgroup per (fold problem, chunk of CVL lambdas): every entry of the held-out
+// Gram is read ONCE per chunk and applied to all CVL coefficient vectors, which each lane
+// keeps in registers for its own columns j = lane + 64 k (dense: zeros off the support).
+// quad_m = b_m' Gxx b_m accumulates per lane as sum_a b_m[a] * sum_{j in lane} G[a][j] b_m[j];
+// lin_m = b_m' Gxy, sx_m = b_m' Sx come from the same lane-owned columns.
+constexpr int CVL = 8;
+constexpr int CVK = PMAX / 64;
+
 __global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
     const double* __restrict__ G, int P, const int* __restrict__ hold,
     const int* __restrict__ xcols, int p, int ones_col, const int* __restrict__ ycol_of_prob,
-    const double* __restrict__ coef, const int* __restrict__ nlam_out, int L,
+    const double* __restrict__ coef, const int* __restrict__ nlam_out, int L, int q0,
     double* __restrict__ cvraw) {
-  const int q = blockIdx.y, m = blockIdx.x;
-  if (m >= nlam_out[q]) { if (threadIdx.x == 0) cvraw[(int64_t)q * L + m] = NAN; return; }
-  const double* Gh = G + (int64_t)hold[q] * P * P;
-  const double* cf = coef + ((int64_t)q * L + m) * (p + 1);
-  const int yc = ycol_of_prob[q];
-  const double a0 = cf[0];
-  __shared__ int sc[PMAX];        // panel column of the i-th nonzero
-  __shared__ double sb[PMAX];
-  __shared__ int wcnt[4];
-  __shared__ int snnz;
-  __shared__ double smem[16 * 3];
+  const int q = q0 + blockIdx.y, m0 = blockIdx.x * CVL;
+  const int nl = nlam_out[q];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) snnz = 0;
+  if (m0 >= nl) {
+    if (tid < CVL && m0 + tid < L) cvraw[(int64_t)q * L + m0 + tid] = NAN;
+    return;
+  }
+  const double* Gh = G + (int64_t)hold[q] * P * P;
+  const int yc = ycol_of_prob[q];
+  __shared__ double sbeta[CVL][PMAX];
+  __shared__ int sxc[PMAX];
+  __shared__ double sred[4][3 * CVL];
+  for (int e = tid; e < CVL * PMAX; e += 256) {
+    const int m = e / PMAX, j = e % PMAX;
+    const bool ok = j < p && m0 + m < nl;
+    sbeta[m][j] = ok ? coef[((int64_t)q * L + m0 + m) * (p + 1) + 1 + j] : 0.0;
+  }
+  for (int j = tid; j < PMAX; j += 256) sxc[j] = j < p ? xcols[j] : xcols[0];
   __syncthreads();
-  for (int base = 0; base < p; base += 256) {
-    const int j = base + tid;
-    const double bj = j < p ? cf[1 + j] : 0.0;
-    const bool nz = bj != 0.0;
-    const uint64_t bal = __ballot(nz);
-    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wcnt[wid] = __popcll(bal);
-    __syncthreads();
-    int off = snnz;
-    for (int w = 0; w < wid; ++w) off += wcnt[w];
-    if (nz) { sc[off + pre] = xcols[j]; sb[off + pre] = bj; }
-    __syncthreads();
-    if (tid == 0) snnz += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-    __syncthreads();
+  double bl[CVK][CVL];          // this lane's columns
+#pragma unroll
+  for (int k = 0; k < CVK; ++k)
+#pragma unroll
+    for (int m = 0; m < CVL; ++m) bl[k][m] = sbeta[m][k * 64 + lane];
+  int cl[CVK];
+#pragma unroll
+  for (int k = 0; k < CVK; ++k) cl[k] = sxc[k * 64 + lane];
+  double quad[CVL], lin[CVL], sx[CVL];
+#pragma unroll
+  for (int m = 0; m < CVL; ++m) { quad[m] = 0.0; lin[m] = 0.0; sx[m] = 0.0; }
+  if (wid == 0) {
+    // linear terms: b' Gxy and b' Sx over this lane's columns
+#pragma unroll
+    for (int k = 0; k < CVK; ++k) {
+      if (k * 64 + lane >= p) continue;
+      const double gy = Gh[(int64_t)cl[k] * P + yc], g1 = Gh[(int64_t)cl[k] * P + ones_col];
+#pragma unroll
+      for (int m = 0; m < CVL; ++m) {
+        lin[m] = fma(bl[k][m], gy, lin[m]);
+        sx[m] = fma(bl[k][m], g1, sx[m]);
+      }
+    }
   }
-  const int nnz = snnz;
-  // quad = b' Gxx b, lin = b' (Gxy - a0 Sx)
-  double v[3] = {0.0, 0.0, 0.0};
-  for (int a = wid; a < nnz; a += 4) {
-    const double* Gr = Gh + (int64_t)sc[a] * P;
-    double r = 0.0;
-    for (int b = lane; b < nnz; b += 64) r += sb[b] * Gr[sc[b]];
-    v[0] += sb[a] * r;
+  for (int a = wid; a < p; a += 4) {
+    bool any = false;
+#pragma unroll
+    for (int m = 0; m < CVL; ++m) any |= sbeta[m][a] != 0.0;
+    if (!any) continue;                              // row outside every support (uniform)
+    const double* Gr = Gh + (int64_t)sxc[a] * P;
+    double g[CVK];
+#pragma unroll
+    for (int k = 0; k < CVK; ++k) g[k] = (k * 64 + lane < p) ? Gr[cl[k]] : 0.0;
+#pragma unroll
+    for (int m = 0; m < CVL; ++m) {
+      double t = 0.0;
+#pragma unroll
+      for (int k = 0; k < CVK; ++k) t = fma(g[k], bl[k][m], t);
+      quad[m] = fma(sbeta[m][a], t, quad[m]);
+    }
   }
-  for (int a = tid; a < nnz; a += 256) {
-    v[1] += sb[a] * Gh[(int64_t)sc[a] * P + yc];
-    v[2] += sb[a] * Gh[(int64_t)sc[a] * P + ones_col];
+#pragma unroll
+  for (int m = 0; m < CVL; ++m) {
+    quad[m] = wave_sum(quad[m]);
+    lin[m] = wave_sum(lin[m]);
+    sx[m] = wave_sum(sx[m]);
   }
-  block_sum<3>(v, smem);
-  if (tid == 0) {
-    double n = Gh[(int64_t)ones_col * P + ones_col];
-    double yy = Gh[(int64_t)yc * P + yc], sy = Gh[(int64_t)ones_col * P + yc];
-    double sse = yy - 2.0 * a0 * sy - 2.0 * v[1] + n * a0 * a0 + 2.0 * a0 * v[2] + v[0];
-    cvraw[(int64_t)q * L + m] = sse / n;
+  if (lane == 0)
+#pragma unroll
+    for (int m = 0; m < CVL; ++m) {
+      sred[wid][m] = quad[m];
+      sred[wid][CVL + m] = lin[m];
+      sred[wid][2 * CVL + m] = sx[m];
+    }
+  __syncthreads();
+  if (tid < CVL && m0 + tid < L) {
+    const int m = tid;
+    if (m0 + m >= nl) {
+      cvraw[(int64_t)q * L + m0 + m] = NAN;
+    } else {
+      const double qd = sred[0][m] + sred[1][m] + sred[2][m] + sred[3][m];
+      const double ln = sred[0][CVL + m], s1 = sred[0][2 * CVL + m];
+      const double a0 = coef[((int64_t)q * L + m0 + m) * (p + 1)];
+      const double n = Gh[(int64_t)ones_col * P + ones_col];
+      const double yy = Gh[(int64_t)yc * P + yc], sy = Gh[(int64_t)ones_col * P + yc];
+      const double sse = yy - 2.0 * a0 * sy - 2.0 * ln + n * a0 * a0 + 2.0 * a0 * s1 + qd;
+      cvraw[(int64_t)q * L + m0 + m] = sse / n;
+    }
   }
 }
 
+// q0: first problem to score (problems before it -- the full-data fits -- have no
+// held-out fold); nprob: number of problems from q0.
 ATE_API int ate_enet_cvloss_gauss(const void* G, int P, const void* hold, const void* xcols, int p,
                                   int ones_col, const void* ycol_of_prob, const void* coef,
-                                  const void* nlam_out, int L, int nprob, void* cvraw, void* stream) {
-  hipLaunchKernelGGL(enet_cvloss_gauss_kernel, dim3(L, nprob), dim3(256), 0, (hipStream_t)stream,
-                     (const double*)G, P, (const int*)hold, (const int*)xcols, p, ones_col,
-                     (const int*)ycol_of_prob, (const double*)coef, (const int*)nlam_out, L,
-                     (double*)cvraw);
+                                  const void* nlam_out, int L, int q0, int nprob, void* cvraw,
+                                  void* stream) {
+  if (p > PMAX) return -1;
+  if (nprob <= 0) return 0;
+  hipLaunchKernelGGL(enet_cvloss_gauss_kernel, dim3((L + CVL - 1) / CVL, nprob), dim3(256), 0,
+                     (hipStream_t)stream, (const double*)G, P, (const int*)hold,
+                     (const int*)xcols, p, ones_col, (const int*)ycol_of_prob,
+                     (const double*)coef, (const int*)nlam_out, L, q0, (double*)cvraw);
   ATE_CHECK_LAUNCH();
   return 0;
 }
