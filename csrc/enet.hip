@@ -25,61 +25,81 @@ using namespace ate;
 // xcols[p], ones_col, ycols[ny]. Outputs per training set s:
 //   C[s][p][p], g[s][ny][p], xm[s][p], xs[s][p] (1 where constant), ju[s][p],
 //   ym[s][ny], ys[s][ny], nobs[s]
-template <typename CT>
-__global__ void enet_prepare_kernel(const double* __restrict__ G, int nseg, int P,
-                                    const unsigned char* __restrict__ masks, int ntrain,
-                                    const int* __restrict__ xcols, int p, int ldc, int ones_col,
-                                    const int* __restrict__ ycols, int ny, CT* __restrict__ C,
-                                    double* __restrict__ g, double* __restrict__ xm,
-                                    double* __restrict__ xs, unsigned char* __restrict__ ju,
-                                    double* __restrict__ ym, double* __restrict__ ys,
-                                    double* __restrict__ nobs) {
+// Two launches: per-set column statistics (means, SDs, constant flags, n), then the
+// standardised Gram / gradient entries, each reading only its own masked segment sum.
+__device__ __forceinline__ double seg_sum(const double* __restrict__ G, int nseg, int P,
+                                          const unsigned char* __restrict__ mk, int a, int b) {
+  double acc = 0.0;
+  for (int q = 0; q < nseg; ++q)
+    if (mk[q]) acc += G[((int64_t)q * P + a) * P + b];
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void enet_prep_stats_kernel(
+    const double* __restrict__ G, int nseg, int P, const unsigned char* __restrict__ masks,
+    const int* __restrict__ xcols, int p, int ones_col, const int* __restrict__ ycols, int ny,
+    double* __restrict__ xm, double* __restrict__ xs, unsigned char* __restrict__ ju,
+    double* __restrict__ ym, double* __restrict__ ys, double* __restrict__ nobs) {
   const int s = blockIdx.y;
   const unsigned char* mk = masks + (int64_t)s * nseg;
-  auto gsum = [&](int a, int b) {
-    double acc = 0.0;
-    for (int q = 0; q < nseg; ++q)
-      if (mk[q]) acc += G[((int64_t)q * P + a) * P + b];
-    return acc;
-  };
-  const double n = gsum(ones_col, ones_col);
-  // each block recomputes the (cheap) means/sds it needs
-  const int64_t total = (int64_t)p * p + (int64_t)ny * p + p + ny;
+  const double n = seg_sum(G, nseg, P, mk, ones_col, ones_col);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < p) {
+    const int j = e;
+    const double mj = seg_sum(G, nseg, P, mk, ones_col, xcols[j]) / n;
+    const double vj = seg_sum(G, nseg, P, mk, xcols[j], xcols[j]) / n - mj * mj;
+    xm[(int64_t)s * p + j] = mj;
+    xs[(int64_t)s * p + j] = vj > 0 ? sqrt(vj) : 1.0;
+    ju[(int64_t)s * p + j] = vj > 0 ? 1 : 0;
+    if (j == 0) nobs[s] = n;
+  } else if (e < p + ny) {
+    const int y = e - p;
+    const double my = seg_sum(G, nseg, P, mk, ones_col, ycols[y]) / n;
+    const double vy = seg_sum(G, nseg, P, mk, ycols[y], ycols[y]) / n - my * my;
+    ym[(int64_t)s * ny + y] = my;
+    ys[(int64_t)s * ny + y] = vy > 0 ? sqrt(vy) : 1.0;
+  }
+}
+
+// G: [nseg][P][P] raw Gram stack (panel columns). masks: [ntrain][nseg] (1 = in training set).
+// Outputs per training set s: C[s][p][ldc] = D^-1 (G/n - m m') D^-1 (glmnet `standard`:
+// population SD, centred; identity row/col for constant columns), g[s][ny][p].
+template <typename CT>
+__global__ __launch_bounds__(256) void enet_prepare_kernel(
+    const double* __restrict__ G, int nseg, int P, const unsigned char* __restrict__ masks,
+    const int* __restrict__ xcols, int p, int ldc, const int* __restrict__ ycols, int ny,
+    const double* __restrict__ xm, const double* __restrict__ xs,
+    const unsigned char* __restrict__ ju, const double* __restrict__ ym,
+    const double* __restrict__ ys, const double* __restrict__ nobs, CT* __restrict__ C,
+    double* __restrict__ g) {
+  const int s = blockIdx.y;
+  const unsigned char* mk = masks + (int64_t)s * nseg;
+  const double n = nobs[s];
+  const int64_t total = (int64_t)p * p + (int64_t)ny * p;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < (int64_t)p * p) {
-      int j = (int)(e / p), k = (int)(e % p);
-      double mj = gsum(ones_col, xcols[j]) / n, mk2 = gsum(ones_col, xcols[k]) / n;
-      double vj = gsum(xcols[j], xcols[j]) / n - mj * mj;
-      double vk = gsum(xcols[k], xcols[k]) / n - mk2 * mk2;
-      double sj = vj > 0 ? sqrt(vj) : 1.0, sk = vk > 0 ? sqrt(vk) : 1.0;
-      double cjk = (gsum(xcols[j], xcols[k]) / n - mj * mk2) / (sj * sk);
-      if (!(vj > 0) || !(vk > 0)) cjk = (j == k) ? 1.0 : 0.0;
+      const int j = (int)(e / p), k = (int)(e % p);
+      const bool okj = ju[(int64_t)s * p + j], okk = ju[(int64_t)s * p + k];
+      double cjk;
+      if (!okj || !okk) {
+        cjk = (j == k) ? 1.0 : 0.0;
+      } else {
+        const double mj = xm[(int64_t)s * p + j], mk2 = xm[(int64_t)s * p + k];
+        cjk = (seg_sum(G, nseg, P, mk, xcols[j], xcols[k]) / n - mj * mk2) /
+              (xs[(int64_t)s * p + j] * xs[(int64_t)s * p + k]);
+      }
       C[((int64_t)s * p + j) * ldc + k] = (CT)cjk;
-    } else if (e < (int64_t)p * p + (int64_t)ny * p) {
-      int64_t r = e - (int64_t)p * p;
-      int y = (int)(r / p), j = (int)(r % p);
-      double mj = gsum(ones_col, xcols[j]) / n;
-      double vj = gsum(xcols[j], xcols[j]) / n - mj * mj;
-      double my = gsum(ones_col, ycols[y]) / n;
-      double vy = gsum(ycols[y], ycols[y]) / n - my * my;
-      double sj = vj > 0 ? sqrt(vj) : 1.0, sy = vy > 0 ? sqrt(vy) : 1.0;
-      double gj = vj > 0 ? (gsum(xcols[j], ycols[y]) / n - mj * my) / (sj * sy) : 0.0;
-      g[((int64_t)s * ny + y) * p + j] = gj;
-    } else if (e < (int64_t)p * p + (int64_t)ny * p + p) {
-      int j = (int)(e - (int64_t)p * p - (int64_t)ny * p);
-      double mj = gsum(ones_col, xcols[j]) / n;
-      double vj = gsum(xcols[j], xcols[j]) / n - mj * mj;
-      xm[(int64_t)s * p + j] = mj;
-      xs[(int64_t)s * p + j] = vj > 0 ? sqrt(vj) : 1.0;
-      ju[(int64_t)s * p + j] = vj > 0 ? 1 : 0;
-      if (j == 0) nobs[s] = n;
     } else {
-      int y = (int)(e - (int64_t)p * p - (int64_t)ny * p - p);
-      double my = gsum(ones_col, ycols[y]) / n;
-      double vy = gsum(ycols[y], ycols[y]) / n - my * my;
-      ym[(int64_t)s * ny + y] = my;
-      ys[(int64_t)s * ny + y] = vy > 0 ? sqrt(vy) : 1.0;
+      const int64_t r = e - (int64_t)p * p;
+      const int y = (int)(r / p), j = (int)(r % p);
+      double gj = 0.0;
+      if (ju[(int64_t)s * p + j]) {
+        const double mj = xm[(int64_t)s * p + j], my = ym[(int64_t)s * ny + y];
+        gj = (seg_sum(G, nseg, P, mk, xcols[j], ycols[y]) / n - mj * my) /
+             (xs[(int64_t)s * p + j] * ys[(int64_t)s * ny + y]);
+      }
+      g[((int64_t)s * ny + y) * p + j] = gj;
     }
   }
 }
@@ -88,21 +108,27 @@ ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, 
                              const void* xcols, int p, int ones_col, const void* ycols, int ny,
                              void* C, int c_f32, void* g, void* xm, void* xs, void* ju, void* ym,
                              void* ys, void* nobs, void* stream) {
-  int64_t total = (int64_t)p * p + (int64_t)ny * p + p + ny;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(enet_prep_stats_kernel, dim3((p + ny + 255) / 256, ntrain), dim3(256), 0, st,
+                     (const double*)G, nseg, P, (const unsigned char*)masks, (const int*)xcols,
+                     p, ones_col, (const int*)ycols, ny, (double*)xm, (double*)xs,
+                     (unsigned char*)ju, (double*)ym, (double*)ys, (double*)nobs);
+  ATE_CHECK_LAUNCH();
+  const int64_t total = (int64_t)p * p + (int64_t)ny * p;
   dim3 grid(grid_for(total, 256, 512), ntrain);
   const int ldc = (p + 63) / 64 * 64;   // padded row stride (C buffer must be zeroed)
   if (c_f32)
-    hipLaunchKernelGGL(enet_prepare_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream,
-                       (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
-                       (const int*)xcols, p, ldc, ones_col, (const int*)ycols, ny, (float*)C, (double*)g,
-                       (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
-                       (double*)nobs);
+    hipLaunchKernelGGL(enet_prepare_kernel<float>, grid, dim3(256), 0, st, (const double*)G, nseg,
+                       P, (const unsigned char*)masks, (const int*)xcols, p, ldc,
+                       (const int*)ycols, ny, (const double*)xm, (const double*)xs,
+                       (const unsigned char*)ju, (const double*)ym, (const double*)ys,
+                       (const double*)nobs, (float*)C, (double*)g);
   else
-    hipLaunchKernelGGL(enet_prepare_kernel<double>, grid, dim3(256), 0, (hipStream_t)stream,
-                       (const double*)G, nseg, P, (const unsigned char*)masks, ntrain,
-                       (const int*)xcols, p, ldc, ones_col, (const int*)ycols, ny, (double*)C, (double*)g,
-                       (double*)xm, (double*)xs, (unsigned char*)ju, (double*)ym, (double*)ys,
-                       (double*)nobs);
+    hipLaunchKernelGGL(enet_prepare_kernel<double>, grid, dim3(256), 0, st, (const double*)G, nseg,
+                       P, (const unsigned char*)masks, (const int*)xcols, p, ldc,
+                       (const int*)ycols, ny, (const double*)xm, (const double*)xs,
+                       (const unsigned char*)ju, (const double*)ym, (const double*)ys,
+                       (const double*)nobs, (double*)C, (double*)g);
   ATE_CHECK_LAUNCH();
   return 0;
 }
@@ -862,18 +888,27 @@ ATE_API int ate_enet_cvloss_gauss(const void* G, int P, const void* hold, const 
 // For full problem f with K fold problems fold_probs[f*K + k] and fold sizes nfold[f*K+k]:
 // cvm = weighted mean, cvsd = sqrt(weighted var/(K-1)); idx_min = first (largest lambda)
 // attaining min cvm; idx_1se = first with cvm <= cvm[min] + cvsd[min].
-__global__ void cv_select_kernel(const double* __restrict__ cvraw, const int* __restrict__ fold_probs,
-                                 const double* __restrict__ nfold, int K, int nfull,
-                                 const int* __restrict__ nlam_full, int L, double* __restrict__ cvm,
-                                 double* __restrict__ cvsd, int* __restrict__ sel) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per full problem; lanes own lambdas m = lane + 64 c (c < 4, L <= 256) with the
+// per-lambda arithmetic of a serial scan, then wave reductions pick the first indices.
+__global__ __launch_bounds__(64) void cv_select_kernel(
+    const double* __restrict__ cvraw, const int* __restrict__ fold_probs,
+    const double* __restrict__ nfold, int K, int nfull, const int* __restrict__ nlam_full, int L,
+    double* __restrict__ cvm, double* __restrict__ cvsd, int* __restrict__ sel) {
+  const int f = blockIdx.x;
+  const int lane = threadIdx.x;
   if (f >= nfull) return;
   const int nl = nlam_full[f];
   double wsum = 0.0;
   for (int k = 0; k < K; ++k) wsum += nfold[f * K + k];
-  int imin = 0;
+  double mus[4], sds[4];
   double best = INFINITY;
-  for (int m = 0; m < nl; ++m) {
+  int imin = 0x7fffffff;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int m = c * 64 + lane;
+    mus[c] = INFINITY;
+    sds[c] = 0.0;
+    if (m >= nl) continue;
     double mu = 0.0;
     for (int k = 0; k < K; ++k) mu += nfold[f * K + k] * cvraw[(int64_t)fold_probs[f * K + k] * L + m];
     mu /= wsum;
@@ -882,24 +917,45 @@ __global__ void cv_select_kernel(const double* __restrict__ cvraw, const int* __
       double d = cvraw[(int64_t)fold_probs[f * K + k] * L + m] - mu;
       var += nfold[f * K + k] * d * d;
     }
-    double sd = sqrt(var / wsum / (double)(K - 1));
+    const double sd = sqrt(var / wsum / (double)(K - 1));
     cvm[(int64_t)f * L + m] = mu;
     cvsd[(int64_t)f * L + m] = sd;
-    if (mu < best) { best = mu; imin = m; }
+    mus[c] = mu;
+    sds[c] = sd;
+    if (mu < best) { best = mu; imin = m; }     // per lane: first of its own minima
   }
-  // lambda.min = max(lambda[cvm <= min(cvm)]) -> first index attaining the min
+  // lambda.min = largest lambda attaining min(cvm) -> first index attaining the minimum
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(imin, o, 64);
+    if (ob < best || (ob == best && oi < imin)) { best = ob; imin = oi; }
+  }
+  if (imin == 0x7fffffff) imin = 0;
+  // thr1 = cvm[imin] + cvsd[imin], read from the owning lane's registers
+  const int oc = imin >> 6, ol = imin & 63;
+  double mine = 0.0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c == oc) mine = mus[c] + sds[c];
+  const double thr1 = __shfl(mine, ol, 64);
   int i1 = imin;
-  double thr1 = cvm[(int64_t)f * L + imin] + cvsd[(int64_t)f * L + imin];
-  for (int m = 0; m < nl; ++m)
-    if (cvm[(int64_t)f * L + m] <= thr1) { i1 = m; break; }
-  sel[2 * f] = imin;
-  sel[2 * f + 1] = i1;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint64_t b = __ballot(c * 64 + lane < nl && mus[c] <= thr1);
+    if (b) { i1 = c * 64 + __ffsll((unsigned long long)b) - 1; break; }
+  }
+  if (lane == 0) {
+    sel[2 * f] = imin;
+    sel[2 * f + 1] = i1;
+  }
 }
 
 ATE_API int ate_cv_select(const void* cvraw, const void* fold_probs, const void* nfold, int K,
                           int nfull, const void* nlam_full, int L, void* cvm, void* cvsd, void* sel,
                           void* stream) {
-  hipLaunchKernelGGL(cv_select_kernel, dim3((nfull + 63) / 64), dim3(64), 0, (hipStream_t)stream,
+  if (L > 256) return -1;
+  hipLaunchKernelGGL(cv_select_kernel, dim3(nfull), dim3(64), 0, (hipStream_t)stream,
                      (const double*)cvraw, (const int*)fold_probs, (const double*)nfold, K, nfull,
                      (const int*)nlam_full, L, (double*)cvm, (double*)cvsd, (int*)sel);
   ATE_CHECK_LAUNCH();
