@@ -21,11 +21,12 @@ BF16_TILE_BIG = 256
 SMALL_TILE, SMALL_K = 64, 16
 TARGET_WG = 2048   # workgroups per launch (>= 8 per CU on 256 CUs)
 
-# 256-tile kernel: 1 = 2-stage BK=64 LDS-DMA (default), 0 = 4-stage BK=32 pipeline.
-# Measured at N=1e7, p=500 (tools/gram_only.py, tools/pmc_gram.sh): 4.0 vs 5.0 ms -- the
-# BK=32 stages fetch half cache lines (TA busy 3x, L2 requests 2x) and lose more than the
-# deeper prefetch gains.
-GRAM_VARIANT = int(os.environ.get("ATE_GRAM_VARIANT", "1"))
+# bf16 kernel for P % 512 == 0: "pair" (symmetry-aware paired tiles, default) or "tile256"
+# (three full 256 tiles per 512 columns). For P % 256 == 0 otherwise: tile256; else 128.
+# (A 4-stage BK=32 variant of tile256 measured 5.0 vs 4.0 ms and was dropped: BK=32
+# stages fetch half cache lines; profiles/r01_pmc/gram_variant*.txt.)
+GRAM_KERNEL = os.environ.get("ATE_GRAM_KERNEL", "pair")
+PAIR_SLOTS = 272
 
 _plan_cache = {}
 
@@ -40,6 +41,7 @@ class GramPlan:
         if bf16 and weighted:
             raise ValueError("weighted Gram needs an fp32/fp64 panel")
         P = panel.P
+        self.pair = bf16 and P % (2 * BF16_TILE_BIG) == 0 and GRAM_KERNEL == "pair"
         if bf16:
             T = BF16_TILE_BIG if P % BF16_TILE_BIG == 0 else BF16_TILE
         else:
@@ -48,13 +50,18 @@ class GramPlan:
         if P % T:
             raise ValueError(f"panel P={P} must be a multiple of {T}")
         nt = P // T
-        tiles = [(a, b) for a in range(nt) for b in range(a, nt)]
+        if self.pair:
+            tiles, blocks = _pair_tiles(nt)
+        else:
+            tiles = [(a, b) for a in range(nt) for b in range(a, nt)]
         ntiles = len(tiles)
         rows_total = int((panel.seg_bounds[:, 1] - panel.seg_bounds[:, 0]).sum())
-        # 256-tile: 1 WG (128 KB LDS) per CU; ~12 short-lived WGs per CU keep the three tiles
+        # 256-tile / pair: 1 WG (128 KB LDS) per CU; ~12 short-lived WGs per CU keep the three tiles
         # of a row chunk close in time so their shared panels are L2 hits (measured 4.65 ->
         # 4.09 ms at N=1e7, p=500 going from 768 to 3072 WGs)
         target = 3072 if T == BF16_TILE_BIG else TARGET_WG
+        if self.pair:
+            target = int(os.environ.get("ATE_GRAM_PAIR_WG", 2048))
         target = int(os.environ.get("ATE_GRAM_WG", target))
         nchunk_target = max(1, target // ntiles)
         ch_rows = max(K, (rows_total // nchunk_target) // K * K)
@@ -70,6 +77,8 @@ class GramPlan:
         dev = panel.device
         self.T, self.K, self.ntiles, self.nchunks = T, K, ntiles, len(chunks)
         self.tiles = torch.tensor(tiles, dtype=torch.int32, device=dev)
+        if self.pair:
+            self.blocks = torch.tensor(blocks, dtype=torch.int32, device=dev)
         ch = np.zeros(len(chunks), dtype=[("r0", "<i8"), ("r1", "<i8"), ("seg", "<i4"),
                                           ("pad", "<i4")])
         for i, c in enumerate(chunks):
@@ -77,8 +86,54 @@ class GramPlan:
         self.chunks = torch.from_numpy(ch.view(np.uint8).copy()).to(dev)
         self.seg_chunk0 = torch.tensor(seg_chunk0, dtype=torch.int32, device=dev)
         slab_dtype = torch.float32 if panel.dtype != torch.float64 else torch.float64
-        self.slab = torch.empty(self.nchunks * ntiles * T * T, dtype=slab_dtype, device=dev)
+        per_tile = PAIR_SLOTS * 256 if self.pair else T * T
+        self.slab = torch.empty(self.nchunks * ntiles * per_tile, dtype=slab_dtype, device=dev)
         self.G = torch.empty((panel.nseg, P, P), dtype=torch.float64, device=dev)
+
+
+def _pair_tiles(nt: int):
+    """Tile list (a, b, type, 0) and slab block table for the paired-tile kernel
+    (csrc/gram.hip gram_bf16_pair_kernel): every diagonal pair (a, b) follows the
+    off-diagonal tile (a, b) that streams the same columns; remaining off-diagonal tiles
+    after. Returns (tiles, blocks[ntiles][PAIR_SLOTS] of 16-column block (I, J))."""
+    tiles = []
+    for a in range(0, nt - 1, 2):
+        tiles.append((a, a + 1, 0, 0))
+        tiles.append((a, a + 1, 1, 0))
+    if nt % 2:
+        tiles.append((nt - 1, nt - 1, 2, 0))
+    paired = {(a, a + 1) for a in range(0, nt - 1, 2)}
+    tiles += [(a, b, 0, 0) for a in range(nt) for b in range(a + 1, nt) if (a, b) not in paired]
+    blocks = []
+    for (a, b, typ, _) in tiles:
+        tb = [(-1, -1)] * PAIR_SLOTS
+        if typ == 0:
+            for w in range(8):
+                wr, wc = w >> 2, w & 3
+                for m in range(8):
+                    for n in range(4):
+                        tb[w * 32 + m * 4 + n] = (a * 16 + wr * 8 + m, b * 16 + wc * 4 + n)
+        else:
+            for w in range(4):                         # rectangles rows 0-7 x cols 8-15
+                region, half = w >> 1, w & 1
+                if typ == 2 and region == 1:
+                    continue
+                base = (a if region == 0 else b) * 16
+                for m in range(8):
+                    for n in range(4):
+                        tb[w * 32 + m * 4 + n] = (base + m, base + 8 + half * 4 + n)
+            for w in range(4):                         # triangles I <= J in 0-7 / 8-15
+                region, half = w >> 1, w & 1
+                if typ == 2 and region == 1:
+                    continue
+                base = (a if region == 0 else b) * 16 + half * 8
+                idx = 0
+                for m in range(8):
+                    for n in range(m, 8):
+                        tb[128 + w * 36 + idx] = (base + m, base + n)
+                        idx += 1
+        blocks.append(tb)
+    return tiles, blocks
 
 
 def plan_for(panel: DevicePanel, weighted=False) -> GramPlan:
@@ -100,9 +155,12 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     pl = plan_for(panel, weighted=w is not None)
     G = pl.G if out is None else out
     s = _stream()
-    if X.dtype == torch.bfloat16:
-        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.T, GRAM_VARIANT,
-                     pl.tiles.data_ptr(),
+    if X.dtype == torch.bfloat16 and pl.pair:
+        _native.call("ate_gram_bf16_pair", X.data_ptr(), panel.ld, panel.P, pl.tiles.data_ptr(),
+                     pl.ntiles, pl.blocks.data_ptr(), pl.chunks.data_ptr(), pl.nchunks,
+                     pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
+    elif X.dtype == torch.bfloat16:
+        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.T, pl.tiles.data_ptr(),
                      pl.ntiles, pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(),
                      panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
     else:

@@ -211,120 +211,174 @@ __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
       }
 }
 
-// ------------------------------------------------------------------ bf16 256x256, 4-stage pipeline
-// Same 8-wave 2x4 decomposition as above, but the K-step is ONE MFMA deep (32 rows) and
-// the LDS holds NST = 4 stages (4 x (A+B) x 256 cols x 64 B = 128 KB), so three stages of
-// LDS-DMA are in flight while a stage is consumed (~3 x 1000 MFMA cycles of prefetch
-// distance instead of one step). The barrier is a raw s_barrier preceded by a COUNTED
-// vmcnt (stages still allowed in flight x glds per stage), never a vmcnt(0) drain.
-// LDS image of a stage: column-major, 64 B (4 chunks of 8 rows) per column; logical
-// chunk cc of column c sits at position cc ^ H[(c >> 2) & 3] with H = {0,3,2,1}, which
-// makes every 16-lane group of a ds_read_b128 fragment load hit 16 distinct 4-bank
-// groups (conflict-free). The swizzle is applied on the DMA source address.
-constexpr int PK = 32;
-constexpr int NST = 4;
+// ------------------------------------------------------------------ bf16 paired-tile kernel
+// Symmetry-aware decomposition for P % 512 == 0. For a pair of 256-column tiles (a, b)
+// two workgroups stream the SAME 512 columns of a row chunk:
+//   type 0: the off-diagonal tile (a, b), 8 waves x (128 x 64) = 256 16x16 MFMA blocks;
+//   type 1: the upper TRIANGLES of both diagonal tiles (a, a) and (b, b) = 2 x 136 blocks.
+//           Per diagonal tile: two waves own the 8 x 8-block rectangle (rows 0-127 x cols
+//           128-255, 32 blocks each) and two waves the triangles I <= J inside rows/cols
+//           0-127 and 128-255 (36 blocks each, 8 fragments serve as both A and B);
+//   type 2: type 1 for a single diagonal tile (odd tile count; b's waves idle).
+// So MFMA work is 528 blocks per 512 columns instead of 768 (three full 256 tiles), and
+// the two workgroups of a chunk read identical byte streams in lockstep (one of them
+// hits L2 on what the other fetched). Every wave writes its 16x16 blocks contiguously
+// into a 272-block slab slot; a host-built table maps slab blocks to Gram blocks.
+constexpr int PAIR_SLOTS = 272;
 
-__device__ __forceinline__ int pk_swz(int col) { return (0x1230 >> (((col >> 2) & 3) * 4)) & 3; }
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 16, "vmcnt immediate");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+__device__ __forceinline__ int tri_index(int m, int n) {   // m <= n < 8, row-major triangle
+  return m * 8 - (m * (m - 1)) / 2 + (n - m);
 }
 
-__device__ __forceinline__ void wait_vm_rt(int n) {
-  switch (n) {
-    case 0: wait_vm<0>(); break;
-    case 1: wait_vm<1>(); break;
-    case 2: wait_vm<2>(); break;
-    case 3: wait_vm<3>(); break;
-    case 4: wait_vm<4>(); break;
-    case 5: wait_vm<5>(); break;
-    case 6: wait_vm<6>(); break;
-    case 7: wait_vm<7>(); break;
-    default: wait_vm<8>(); break;
+// One wave role for the whole K-loop: TRI = triangle wave (8 fragments as both A and B,
+// 36 blocks), else rectangle wave (8 A + 4 B fragments, 32 blocks). Each instantiation
+// keeps only its own accumulators live; every wave runs the same number of barriers.
+template <bool TRI>
+__device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t ld, int a0,
+                                          int b0, bool haveB, bool idle, int abuf, int bbuf,
+                                          int arow0, int bcol0, const Chunk& ch,
+                                          bf16_t (*lds)[2][GT * GK], float* __restrict__ out) {
+  constexpr int NB = TRI ? 36 : 32;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  f32x4 acc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int st, int64_t i0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = wid * 4 + r;
+      const int col = q * 8 + (lane >> 3);
+      const int cc = (lane & 7) ^ (col & 7);
+      glds16(X + (int64_t)(a0 + col) * ld + i0 + cc * 8, &lds[st][0][q * 8 * GK]);
+      if (haveB) glds16(X + (int64_t)(b0 + col) * ld + i0 + cc * 8, &lds[st][1][q * 8 * GK]);
+    }
+  };
+  auto frag = [&](const bf16_t* P_, int col, int cc) {
+    return *reinterpret_cast<const bf16x8*>(&P_[col * GK + ((cc ^ (col & 7)) << 3)]);
+  };
+  const int64_t nsteps = (ch.row1 - ch.row0) / GK;
+  if (nsteps > 0) stage(0, ch.row0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  __syncthreads();
+  for (int64_t s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) stage(cur ^ 1, ch.row0 + (s + 1) * GK);
+    const bf16_t* As = lds[cur][abuf];
+    const bf16_t* Bs = lds[cur][bbuf];
+    if (!idle) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int cc = kk * 4 + (lane >> 4);
+        if constexpr (!TRI) {
+          bf16x8 af[8], bfr[4];
+#pragma unroll
+          for (int m = 0; m < 8; ++m) af[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) bfr[n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
+#pragma unroll
+          for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+              acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n],
+                                                                        acc[m * 4 + n], 0, 0, 0);
+        } else {
+          bf16x8 fr[8];
+#pragma unroll
+          for (int m = 0; m < 8; ++m) fr[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+#pragma unroll
+          for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int n = m; n < 8; ++n)
+              acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  fr[m], fr[n], acc[tri_index(m, n)], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): next stage landed
+    __syncthreads();
   }
+  if (idle) return;
+  // acc reg r of lane l = (row (l>>4)*4+r, col l&15) of the 16x16 block
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      out[i * 256 + ((lane >> 4) * 4 + r) * 16 + (lane & 15)] = acc[i][r];
 }
 
-__global__ __launch_bounds__(512) void gram_bf16_256p_kernel(
-    const bf16_t* __restrict__ X, int64_t ld, const int2* __restrict__ tiles, int ntiles,
+__global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
+    const bf16_t* __restrict__ X, int64_t ld, const int4* __restrict__ tiles, int ntiles,
     const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[NST][2][GT * PK];   // 128 KB
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][GT * GK];   // 128 KB
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int c = L / ntiles, t = L % ntiles;
   const Chunk ch = chunks[c];
-  const int2 tl = tiles[t];
-  const bool diag = tl.x == tl.y;
+  const int4 tl = tiles[t];
+  const int type = tl.z;
+  const bool haveB = type != 2;
   const int a0 = tl.x * GT, b0 = tl.y * GT;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
+  const int wid = threadIdx.x >> 6;
+  const bool tri = type != 0 && wid >= 4;
+  const int region = type == 0 ? 0 : (tri ? (wid - 4) >> 1 : wid >> 1);   // 0: tile a, 1: tile b
+  const int half = type == 0 ? 0 : (wid & 1);
+  const bool idle = type == 2 && region == 1;
+  int arow0, bcol0;
+  if (type == 0) { arow0 = (wid >> 2) * 128; bcol0 = (wid & 3) * 64; }
+  else if (!tri) { arow0 = 0; bcol0 = 128 + half * 64; }
+  else { arow0 = half * 128; bcol0 = half * 128; }
+  const int abuf = type == 0 ? 0 : region;
+  const int bbuf = type == 0 ? 1 : region;
+  const int base = tri ? 128 + (wid - 4) * 36 : wid * 32;
+  float* out = slab + ((int64_t)c * ntiles + t) * (PAIR_SLOTS * 256) + (int64_t)base * 256;
+  if (tri)
+    pair_wave<true>(X, ld, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
+  else
+    pair_wave<false>(X, ld, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
+}
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // a stage = 16 pieces of 1 KB (16 columns x 64 B) per operand; wave w stages pieces
-  // 2w, 2w+1 of A (and of B off the diagonal): 2 or 4 glds per wave per stage
-  const int per_stage = diag ? 2 : 4;
-  const int scol = lane >> 2;
-  auto stage = [&](int st, int64_t i0) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int q = wid * 2 + r;
-      const int col = q * 16 + scol;
-      const int cc = (lane & 3) ^ pk_swz(col);
-      glds16(X + (int64_t)(a0 + col) * ld + i0 + cc * 8, &lds[st][0][q * 16 * PK]);
-      if (!diag) glds16(X + (int64_t)(b0 + col) * ld + i0 + cc * 8, &lds[st][1][q * 16 * PK]);
-    }
-  };
-
-  const int nsteps = (int)((ch.row1 - ch.row0) / PK);
-#pragma unroll
-  for (int j = 0; j < NST - 1; ++j)
-    if (j < nsteps) stage(j, ch.row0 + (int64_t)j * PK);
-
-  const int fc = lane & 15, kc = lane >> 4;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s % NST;
-    // stage s landed (this wave's part) once at most `ahead` later stages are pending
-    const int ahead = min(NST - 2, nsteps - 1 - s);
-    wait_vm_rt(ahead * per_stage);
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // ... and every wave's part; also retires reads of s-1
-    asm volatile("" ::: "memory");
-    if (s + NST - 1 < nsteps) stage((s + NST - 1) % NST, ch.row0 + (int64_t)(s + NST - 1) * PK);
-    const bf16_t* As = lds[cur][0];
-    const bf16_t* Bs = diag ? lds[cur][0] : lds[cur][1];
-    bf16x8 af[8], bfr[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int col = wc * 64 + n * 16 + fc;
-      bfr[n] = *reinterpret_cast<const bf16x8*>(&Bs[col * PK + ((kc ^ pk_swz(col)) << 3)]);
-    }
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const int col = wr * 128 + m * 16 + fc;
-      af[m] = *reinterpret_cast<const bf16x8*>(&As[col * PK + ((kc ^ pk_swz(col)) << 3)]);
-    }
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+// blocks: [ntiles][PAIR_SLOTS] int2 (I, J) = 16-column block coordinates of the Gram (I: A
+// side = row), (-1, -1) = unused slot. Blocks with I == J are full 16x16 diagonal blocks: only
+// their r <= c entries are written (plus mirror), so every Gram entry has ONE writer.
+__global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const int2* __restrict__ blocks,
+                                        int ntiles, const int* __restrict__ seg_chunk0, int nseg,
+                                        int P, double* __restrict__ G) {
+  const int64_t per = (int64_t)ntiles * PAIR_SLOTS * 256;
+  const int64_t total = (int64_t)nseg * per;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int s = (int)(e / per);
+    const int64_t rem = e % per;
+    const int tb = (int)(rem >> 8);                 // tile * PAIR_SLOTS + slot
+    const int rc = (int)(rem & 255), r = rc >> 4, cl = rc & 15;
+    const int2 bl = blocks[tb];
+    if (bl.x < 0) continue;
+    if (bl.x == bl.y && r > cl) continue;
+    double acc = 0.0;
+    for (int ci = seg_chunk0[s]; ci < seg_chunk0[s + 1]; ++ci)
+      acc += (double)slab[(int64_t)ci * per + rem];
+    const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
+    double* Gs = G + (int64_t)s * P * P;
+    Gs[(int64_t)a * P + b] = acc;
+    Gs[(int64_t)b * P + a] = acc;
   }
-  float* out = slab + ((int64_t)c * ntiles + t) * (GT * GT);
-#pragma unroll
-  for (int m = 0; m < 8; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr * 128 + m * 16 + (lane >> 4) * 4 + r;
-        const int col = wc * 64 + n * 16 + (lane & 15);
-        out[row * GT + col] = acc[m][n][r];
-      }
+}
+
+ATE_API int ate_gram_bf16_pair(const void* X, int64_t ld, int P, const void* tiles, int ntiles,
+                               const void* blocks, const void* chunks, int nchunks,
+                               const void* seg_chunk0, int nseg, void* slab, void* G,
+                               void* stream) {
+  if (P % (2 * GT)) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gram_bf16_pair_kernel, dim3(nchunks * ntiles), dim3(512), 0, s,
+                     (const bf16_t*)X, ld, (const int4*)tiles, ntiles, (const Chunk*)chunks,
+                     nchunks, (float*)slab);
+  ATE_CHECK_LAUNCH();
+  const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
+  hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+                     (const float*)slab, (const int2*)blocks, ntiles, (const int*)seg_chunk0, nseg,
+                     P, (double*)G);
+  ATE_CHECK_LAUNCH();
+  return 0;
 }
 
 // ------------------------------------------------------------------ fp32 / fp64 64x64
@@ -434,20 +488,15 @@ __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2
 // chunks/tiles/seg_chunk0 are device arrays prepared by the caller (ops/gram.py).
 // tile = 128 (4 waves, register-staged) or 256 (8 waves, LDS-DMA staged); the caller's
 // tile table and chunk plan must use the same tile size.
-// variant (tile 256 only): 0 = 4-stage BK=32 pipelined kernel, 1 = 2-stage BK=64 kernel.
-ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile, int variant,
+ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile,
                           const void* tiles, int ntiles, const void* chunks, int nchunks,
                           const void* seg_chunk0, int nseg, void* slab, void* G, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int nwg = nchunks * ntiles;
   if (tile == GT) {
     if (P % GT) return -1;
-    if (variant == 0)
-      hipLaunchKernelGGL(gram_bf16_256p_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
-                         (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
-    else
-      hipLaunchKernelGGL(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
-                         (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
+    hipLaunchKernelGGL(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
+                       (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
   } else if (tile == BT) {
     if (P % BT) return -1;
     hipLaunchKernelGGL(gram_bf16_kernel, dim3(nwg), dim3(256), 0, s, (const bf16_t*)X, ld,

@@ -44,19 +44,27 @@ def test_gram_kernel_vs_fp64(gpu, dtype, p):
     assert torch.allclose(G, G.transpose(1, 2))
 
 
-def test_gram_256_variants_agree(gpu, monkeypatch):
-    # 4-stage pipelined (default) and 2-stage 256-tile kernels: same sums per tile
+@pytest.mark.parametrize("p", [400, 1000])
+def test_gram_pair_kernel_vs_tile256(gpu, monkeypatch, p):
+    # paired-tile (P % 512 == 0: 512, 1024 -> odd/even tile counts incl. extra off-diagonal
+    # tiles) vs the three-tile 256 kernel vs fp64; symmetric by construction
     rs = np.random.RandomState(3)
-    n = 20000
-    X = rs.randn(n, 400)
+    n = 6000
+    X = rs.randn(n, p)
     pan = build_panel(X, rs.rand(n), rs.randint(0, 2, n), folds=rs.randint(0, 5, n),
                       dtype="bf16", device=gpu)
+    monkeypatch.setattr(gram_op, "GRAM_KERNEL", "pair")
+    gram_op._plan_cache.clear()
+    assert gram_op.plan_for(pan).pair
     G0 = gram_op.gram(pan).clone()
-    monkeypatch.setattr(gram_op, "GRAM_VARIANT", 1)
+    monkeypatch.setattr(gram_op, "GRAM_KERNEL", "tile256")
+    gram_op._plan_cache.clear()
     G1 = gram_op.gram(pan)
+    gram_op._plan_cache.clear()
     ref = gram_op.gram_reference(pan).to(gpu)
     assert ((G0 - ref).abs().max() / ref.abs().max()) < 2e-6
     assert ((G0 - G1).abs().max() / ref.abs().max()) < 2e-6
+    assert torch.equal(G0, G0.transpose(1, 2))
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64"])

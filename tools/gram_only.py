@@ -1,5 +1,5 @@
 """Run the bf16 Gram kernel alone on the N=1e7, p=500 bench panel (A/B of the 256-tile
-kernel variants, and for PMC profiling). Usage: gram_only.py [N] [variant ...]"""
+kernel variants, and for PMC profiling). Usage: gram_only.py [N] [pair|tile256 ...]"""
 import os
 import sys
 
@@ -10,11 +10,12 @@ from ate_replication_causalml_amd.data.device_dgp import synthetic_panel  # noqa
 from ate_replication_causalml_amd.ops import gram as gram_mod  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e7)
-variants = [int(v) for v in sys.argv[2:]] or [gram_mod.GRAM_VARIANT]
+variants = sys.argv[2:] or [gram_mod.GRAM_KERNEL]
 pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.device("cuda", 0))
 ref = None
 for v in variants:
-    gram_mod.GRAM_VARIANT = v
+    gram_mod.GRAM_KERNEL = v
+    gram_mod._plan_cache.clear()
     for _ in range(3):
         G = gram_mod.gram(pan)
     torch.cuda.synchronize()
@@ -27,5 +28,5 @@ for v in variants:
     G = G.clone()
     diff = 0.0 if ref is None else float((G - ref).abs().max() / ref.abs().max())
     ref = G if ref is None else ref
-    print(f"variant {v}: gram ms {e[0].elapsed_time(e[1]) / 10:.3f}  rel-diff vs first {diff:.2e}",
+    print(f"kernel {v}: gram ms {e[0].elapsed_time(e[1]) / 10:.3f}  rel-diff vs first {diff:.2e}",
           flush=True)
