@@ -353,9 +353,19 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
     const int2 bl = blocks[tb];
     if (bl.x < 0) continue;
     if (bl.x == bl.y && r > cl) continue;
+    // fixed chunk order; 8 independent loads in flight per batch
+    const int c0 = seg_chunk0[s], c1 = seg_chunk0[s + 1];
+    const float* src = slab + rem;
     double acc = 0.0;
-    for (int ci = seg_chunk0[s]; ci < seg_chunk0[s + 1]; ++ci)
-      acc += (double)slab[(int64_t)ci * per + rem];
+    int ci = c0;
+    for (; ci + 8 <= c1; ci += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(ci + u) * per];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)v[u];
+    }
+    for (; ci < c1; ++ci) acc += (double)src[(int64_t)ci * per];
     const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
     double* Gs = G + (int64_t)s * P * P;
     Gs[(int64_t)a * P + b] = acc;
