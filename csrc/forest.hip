@@ -177,21 +177,45 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
     const int ncur = sncur;
     if (ncur == 0) break;
     // ---- decisions: one wave per node
+    // Nodes with <= 64 rows (most nodes of a fully grown tree) keep their rows' index,
+    // weight, label / outcome and pseudo-outcome in registers (one row per lane) and
+    // fetch the bins of all drawn features in batches of 16 independent loads, so a node
+    // costs a few memory round trips instead of two per feature. Larger nodes stream
+    // their rows per feature. Both paths add the same values to the same histograms.
     for (int j = wid; j < ncur; j += 4) {
       const Rng3 nd = S.cur[j];
       const int v = nd.id;
+      const bool small = nd.hi - nd.lo <= 64;
+      const int qs = nd.lo + lane;
+      const bool cvalid = small && qs < nd.hi;
+      int ci = 0, cy = 0;
+      int64_t cw = 0, cr1 = 0, cr2 = 0, crho = 0;
+      if (cvalid) {
+        ci = S.idx[qs];
+        cw = S.w[ci];
+        if (fp.kind == 0) cy = ycls[ci];
+        else { cr1 = r1[ci]; if (fp.kind == 2) cr2 = r2[ci]; }
+      }
       int64_t nw = 0, n1 = 0, s1 = 0, sw = 0, sy = 0, sww = 0, swy = 0;
-      for (int q = nd.lo + lane; q < nd.hi; q += 64) {
-        const int i = S.idx[q];
-        const int64_t wi = S.w[i];
+      for (int q = nd.lo + lane; q < nd.hi; q += 64) {   // small: one pass, cached values
+        int64_t wi, a1 = 0, a2 = 0;
+        int yi = 0;
+        if (small) {
+          wi = cw; yi = cy; a1 = cr1; a2 = cr2;
+        } else {
+          const int i = S.idx[q];
+          wi = S.w[i];
+          if (fp.kind == 0) yi = ycls[i];
+          else { a1 = r1[i]; if (fp.kind == 2) a2 = r2[i]; }
+        }
         nw += wi;
-        if (fp.kind == 0) n1 += wi * ycls[i];
-        else if (fp.kind == 1) s1 += wi * r1[i];
+        if (fp.kind == 0) n1 += wi * yi;
+        else if (fp.kind == 1) s1 += wi * a1;
         else {
-          sw += r1[i];
-          sy += r2[i];
-          sww += to_fix(__dmul_rn(from_fix(r1[i]), from_fix(r1[i])));
-          swy += to_fix(__dmul_rn(from_fix(r1[i]), from_fix(r2[i])));
+          sw += a1;
+          sy += a2;
+          sww += to_fix(__dmul_rn(from_fix(a1), from_fix(a1)));
+          swy += to_fix(__dmul_rn(from_fix(a1), from_fix(a2)));
         }
       }
       nw = wsum64(nw); n1 = wsum64(n1); s1 = wsum64(s1);
@@ -208,11 +232,16 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
       if (!terminal) {
         int64_t stot = 0;
         if (fp.kind == 2) {
-          for (int q = nd.lo + lane; q < nd.hi; q += 64) {
-            const int i = S.idx[q];
-            const int64_t rv = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
-            S.rho[i] = rv;
-            stot += rv;
+          if (small) {
+            if (cvalid) crho = to_fix(causal_rho(cn, from_fix(cr1), from_fix(cr2)));
+            stot = crho;
+          } else {
+            for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+              const int i = S.idx[q];
+              const int64_t rv = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
+              S.rho[i] = rv;
+              stot += rv;
+            }
           }
           stot = wsum64(stot);
         } else if (fp.kind == 1) {
@@ -228,10 +257,16 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
         }
         const int minc = min_child(fp, dn);
         const int nf = draw_num_features(fp, tg, v);
+        // partial Fisher-Yates: draws k < 64 in parallel (lane k), swaps in order by lane 0
+        for (int k = lane; k < p; k += 64) perm[wid][k] = (int16_t)k;
+        const uint32_t rk = lane < nf ? rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg,
+                                                   node_index(v, lane), (uint32_t)(p - lane)) : 0u;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
         if (lane == 0) {
-          for (int k = 0; k < p; ++k) perm[wid][k] = (int16_t)k;
           for (int k = 0; k < nf; ++k) {
-            const uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, k), (uint32_t)(p - k));
+            const uint32_t r = k < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rk, k)
+                                      : rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg,
+                                                   node_index(v, k), (uint32_t)(p - k));
             const int16_t tmpv = perm[wid][k];
             perm[wid][k] = perm[wid][k + r];
             perm[wid][k + r] = tmpv;
@@ -240,30 +275,27 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
         __builtin_amdgcn_s_waitcnt(0xC07F);
         double best = -INFINITY;
         int64_t ntreat = 0;
-        for (int k = 0; k < nf; ++k) {
-          const int f = perm[wid][k];
-          const uint8_t* xf = Xb + (int64_t)f * n;
+        auto hist_row = [&](int b, int64_t wi, int yi, int64_t a1, int64_t rho) {
+          if (fp.kind == 0) {
+            if (yi) atomicAdd((unsigned long long*)&hist[wid][1][b], (unsigned long long)wi);
+            else atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
+          } else if (fp.kind == 1) {
+            atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
+            atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)(wi * a1));
+          } else {
+            atomicAdd((unsigned long long*)&hist[wid][0][b], 1ull);
+            atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)rho);
+            if (from_fix(a1) > cn.wbar) atomicAdd((unsigned long long*)&hist[wid][3][b], 1ull);
+          }
+        };
+        // per feature: clear, accumulate (by the caller), scan, evaluate, argmax
+        auto clear_hist = [&]() {
           for (int b = lane; b < NBINS; b += 64) {
             hist[wid][0][b] = 0; hist[wid][1][b] = 0; hist[wid][2][b] = 0; hist[wid][3][b] = 0;
           }
           __builtin_amdgcn_s_waitcnt(0xC07F);
-          for (int q = nd.lo + lane; q < nd.hi; q += 64) {
-            const int i = S.idx[q];
-            const int b = xf[i];
-            if (fp.kind == 0) {
-              const int64_t wi = S.w[i];
-              if (ycls[i]) atomicAdd((unsigned long long*)&hist[wid][1][b], (unsigned long long)wi);
-              else atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
-            } else if (fp.kind == 1) {
-              const int64_t wi = S.w[i];
-              atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
-              atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)(wi * r1[i]));
-            } else {
-              atomicAdd((unsigned long long*)&hist[wid][0][b], 1ull);
-              atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)S.rho[i]);
-              if (from_fix(r1[i]) > cn.wbar) atomicAdd((unsigned long long*)&hist[wid][3][b], 1ull);
-            }
-          }
+        };
+        auto scan_eval = [&](int f) {
           __builtin_amdgcn_s_waitcnt(0xC07F);
           // wave prefix scan: lane owns bins 4*lane .. 4*lane+3
           int64_t c0[4], c1[4], cs[4], ct[4];
@@ -313,6 +345,37 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
             if (oc > lbest || (oc == lbest && ob < lbin)) { lbest = oc; lbin = ob; }
           }
           if (lbin < NBINS && lbest > best) { best = lbest; bf = f; bb = lbin; }
+        };
+        if (small) {
+          for (int k0 = 0; k0 < nf; k0 += 16) {
+            int bins[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int k = k0 + u;
+              bins[u] = (cvalid && k < nf) ? (int)Xb[(int64_t)perm[wid][k] * n + ci] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int k = k0 + u;
+              if (k >= nf) break;
+              const int f = perm[wid][k];
+              clear_hist();
+              if (cvalid) hist_row(bins[u], cw, cy, cr1, crho);
+              scan_eval(f);
+            }
+          }
+        } else {
+          for (int k = 0; k < nf; ++k) {
+            const int f = perm[wid][k];
+            const uint8_t* xf = Xb + (int64_t)f * n;
+            clear_hist();
+            for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+              const int i = S.idx[q];
+              hist_row(xf[i], S.w[i], fp.kind == 0 ? ycls[i] : 0, fp.kind != 0 ? r1[i] : 0,
+                       fp.kind == 2 ? S.rho[i] : 0);
+            }
+            scan_eval(f);
+          }
         }
         if (!(bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent)))) bf = -1;
       }
