@@ -3,9 +3,11 @@ social-pressure GOTV file ``socialpresswgeooneperhh_NEIGH.csv``.
 
 Not shipped (no network here); users who have it get the same ``df`` the driver
 builds: ``sample_n(n_obs)`` -> select covariates + outcome_voted + treat_neighbors ->
-``scale()`` the 15 continuous columns -> rename to Y/W -> ``na.omit``. The row sample
-uses a Philox permutation (purpose P_SAMPLE_ROWS) instead of R's Mersenne-Twister
-``sample_n``, so the 50k rows differ from R's draw but are reproducible by seed.
+``scale()`` the 15 continuous columns -> rename to Y/W -> ``na.omit``. The row sample is
+R's own draw by default (``sampler="r"``: ``set.seed(seed); sample_n(df, n_obs)`` with R's
+Mersenne-Twister and rejection sampler, parallel/rrng.py), in R's sampled row order -- the
+order the selection transform's "first 85%" rule (Q18) sees. ``sampler="philox"`` uses a
+counter-based Philox permutation (purpose P_SAMPLE_ROWS) kept in file order instead.
 """
 from __future__ import annotations
 
@@ -19,13 +21,16 @@ OUTCOME, TREATMENT = "outcome_voted", "treat_neighbors"
 
 
 def load_social_pressure(path, n_obs: int = 50_000, seed: int = 1991,
-                         device=None) -> TutorialData:
+                         device=None, sampler: str = "r") -> TutorialData:
     """``device="cuda"`` standardises on the GPU (K02, csrc/prep.hip); same formulas."""
     import pandas as pd
     cols = list(CTS_NAMES) + list(BIN_NAMES) + [OUTCOME, TREATMENT]
     raw = pd.read_csv(path, usecols=cols)
     n = len(raw)
-    if n_obs < n:
+    if sampler == "r":
+        from ..parallel.rrng import r_sample_rows
+        raw = raw.iloc[r_sample_rows(n, min(n_obs, n), seed)]
+    elif n_obs < n:
         r = rng.random_u32(seed, rng.P_SAMPLE_ROWS, 0, np.arange(n, dtype=np.uint64))
         keys = (r[:, 0].astype(np.uint64) << np.uint64(32)) | r[:, 1].astype(np.uint64)
         take = np.sort(np.argsort(keys, kind="stable")[:n_obs])
