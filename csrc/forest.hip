@@ -16,6 +16,20 @@
 using namespace atef;
 
 constexpr int PMAX_F = 512;   // max features for the per-wave permutation buffer
+constexpr int COOP_ROWS = 1024;   // nodes above this are decided by all 4 waves together
+constexpr int COOP_CAP = 256;     // per level (the rest fall back to one wave per node)
+
+#ifdef FOREST_PROF
+// per tree (debug builds, tools/forest_profile.py): [0] decisions, [1] child ids,
+// [2] partition (wall_clock64 ticks, thread 0 at the level barriers), [3] levels,
+// [4] nodes, [5] nodes <= 16 rows, [6] nodes <= 64 rows, [7] setup (sampling, rows)
+__device__ unsigned long long forest_prof[1024][8];
+#define FPROF_T(var) const unsigned long long var = wall_clock64()
+#define FPROF_ADD(k, v) do { if (threadIdx.x == 0) atomicAdd(&forest_prof[t & 1023][k], (unsigned long long)(v)); } while (0)
+#else
+#define FPROF_T(var)
+#define FPROF_ADD(k, v) do { } while (0)
+#endif
 
 namespace {
 
@@ -92,6 +106,8 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   __shared__ int64_t hist[4][4][NBINS];
   __shared__ int16_t perm[4][PMAX_F];
   __shared__ int shi[8];
+  __shared__ int64_t sred[4][8];          // cooperative nodes: per-wave partial sums
+  __shared__ int sbig[COOP_CAP];          // this chunk's nodes with > COOP_ROWS rows
   __shared__ int sncur, snext_id, sm, sestn;
   const int t = blockIdx.x;
   const int tg = fp.t0 + t;          // global tree id (RNG key)
@@ -99,6 +115,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   Scratch S = scratch_for(scratch_base, n, t);
   uint8_t* inb = inbag + (int64_t)t * n;
+  FPROF_T(tstart_);
   // ------------------------------------------------------------ sampling (K10)
   for (int i = tid; i < n; i += 256) S.w[i] = 0;
   __syncthreads();
@@ -173,19 +190,39 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   }
   __syncthreads();
   // ------------------------------------------------------------ levels
+  FPROF_T(tsetup_);
+  FPROF_ADD(7, tsetup_ - tstart_);
   for (int depth = 0;; ++depth) {
     const int ncur = sncur;
     if (ncur == 0) break;
+    FPROF_T(tl0_);
+    FPROF_ADD(3, 1);
+    FPROF_ADD(4, ncur);
     // ---- decisions: one wave per node
     // Nodes with <= 64 rows (most nodes of a fully grown tree) keep their rows' index,
     // weight, label / outcome and pseudo-outcome in registers (one row per lane) and
     // fetch the bins of all drawn features in batches of 16 independent loads, so a node
     // costs a few memory round trips instead of two per feature. Larger nodes stream
     // their rows per feature. Both paths add the same values to the same histograms.
-    for (int j = wid; j < ncur; j += 4) {
+    // Nodes with more than COOP_ROWS rows (the top levels) are decided by all four waves
+    // together: rows split over the waves, integer sums combined through LDS in wave
+    // order, every wave evaluates the same combined histogram (identical decisions).
+    auto decide = [&](int j, bool coop) {
       const Rng3 nd = S.cur[j];
       const int v = nd.id;
-      const bool small = nd.hi - nd.lo <= 64;
+      const bool small = !coop && nd.hi - nd.lo <= 64;
+      const int q0 = nd.lo + lane + (coop ? wid * 64 : 0);
+      const int qstep = coop ? 256 : 64;
+      // sum over the node's rows: one wave, or all four (fixed wave order)
+      auto red = [&](int64_t x, int slot) -> int64_t {
+        x = wsum64(x);
+        if (!coop) return x;
+        if (lane == 0) sred[wid][slot] = x;
+        __syncthreads();
+        const int64_t r = sred[0][slot] + sred[1][slot] + sred[2][slot] + sred[3][slot];
+        __syncthreads();
+        return r;
+      };
       const int qs = nd.lo + lane;
       const bool cvalid = small && qs < nd.hi;
       int ci = 0, cy = 0;
@@ -197,7 +234,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
         else { cr1 = r1[ci]; if (fp.kind == 2) cr2 = r2[ci]; }
       }
       int64_t nw = 0, n1 = 0, s1 = 0, sw = 0, sy = 0, sww = 0, swy = 0;
-      for (int q = nd.lo + lane; q < nd.hi; q += 64) {   // small: one pass, cached values
+      for (int q = q0; q < nd.hi; q += qstep) {   // small: one pass, cached values
         int64_t wi, a1 = 0, a2 = 0;
         int yi = 0;
         if (small) {
@@ -218,8 +255,8 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
           swy += to_fix(__dmul_rn(from_fix(a1), from_fix(a2)));
         }
       }
-      nw = wsum64(nw); n1 = wsum64(n1); s1 = wsum64(s1);
-      sw = wsum64(sw); sy = wsum64(sy); sww = wsum64(sww); swy = wsum64(swy);
+      nw = red(nw, 0); n1 = red(n1, 1); s1 = red(s1, 2);
+      sw = red(sw, 3); sy = red(sy, 4); sww = red(sww, 5); swy = red(swy, 6);
       const double dn = (double)nw;
       bool terminal = nw <= fp.min_node || depth >= MAX_DEPTH - 1;
       if (fp.kind == 0 && (n1 == 0 || n1 == nw)) terminal = true;
@@ -236,14 +273,14 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
             if (cvalid) crho = to_fix(causal_rho(cn, from_fix(cr1), from_fix(cr2)));
             stot = crho;
           } else {
-            for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+            for (int q = q0; q < nd.hi; q += qstep) {
               const int i = S.idx[q];
               const int64_t rv = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
               S.rho[i] = rv;
               stot += rv;
             }
           }
-          stot = wsum64(stot);
+          stot = small ? wsum64(stot) : red(stot, 7);
         } else if (fp.kind == 1) {
           stot = s1;
         }
@@ -295,6 +332,29 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
           }
           __builtin_amdgcn_s_waitcnt(0xC07F);
         };
+        // split criterion of "bin <= b" from the left-side sums; -inf when not admissible
+        auto crit_at = [&](int64_t L0, int64_t L1, int64_t LS, int64_t LT) -> double {
+          const int64_t nl = fp.kind == 0 ? L0 + L1 : L0;
+          const int64_t nr = nw - nl;
+          if (nl < minc || nr < minc) return -INFINITY;
+          if (fp.kind == 0)
+            return gini_crit((double)L0, (double)L1, (double)(nw - n1 - L0), (double)(n1 - L1));
+          if (fp.kind == 2) {
+            const int64_t tr = ntreat - LT;
+            if (LT < 1 || nl - LT < 1 || tr < 1 || nr - tr < 1) return -INFINITY;
+          }
+          return mse_crit(from_fix(LS), (double)nl, from_fix(stot - LS), (double)nr);
+        };
+        // wave argmax (max crit, then lowest bin), then the strict cross-feature update
+        auto take_best = [&](double lbest, int lbin, int f) {
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            const double oc = __shfl_xor(lbest, o, 64);
+            const int ob = __shfl_xor(lbin, o, 64);
+            if (oc > lbest || (oc == lbest && ob < lbin)) { lbest = oc; lbin = ob; }
+          }
+          if (lbin < NBINS && lbest > best) { best = lbest; bf = f; bb = lbin; }
+        };
         auto scan_eval = [&](int f) {
           __builtin_amdgcn_s_waitcnt(0xC07F);
           // wave prefix scan: lane owns bins 4*lane .. 4*lane+3
@@ -303,7 +363,14 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int b = 4 * lane + e;
-            a0 += hist[wid][0][b]; a1 += hist[wid][1][b]; as += hist[wid][2][b]; at_ += hist[wid][3][b];
+            if (coop) {
+#pragma unroll
+              for (int w = 0; w < 4; ++w) {
+                a0 += hist[w][0][b]; a1 += hist[w][1][b]; as += hist[w][2][b]; at_ += hist[w][3][b];
+              }
+            } else {
+              a0 += hist[wid][0][b]; a1 += hist[wid][1][b]; as += hist[wid][2][b]; at_ += hist[wid][3][b];
+            }
             c0[e] = a0; c1[e] = a1; cs[e] = as; ct[e] = at_;
           }
           int64_t x0 = a0, x1 = a1, xs = as, xt = at_;
@@ -321,32 +388,79 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
           for (int e = 0; e < 4; ++e) {
             const int b = 4 * lane + e;
             if (b >= NBINS - 1) continue;
-            const int64_t L0 = p0 + c0[e], L1 = p1 + c1[e], LS = ps + cs[e], LT = pt + ct[e];
-            const int64_t nl = fp.kind == 0 ? L0 + L1 : L0;
-            const int64_t nr = nw - nl;
-            if (nl < minc || nr < minc) continue;
-            double crit;
-            if (fp.kind == 0) {
-              crit = gini_crit((double)L0, (double)L1, (double)(nw - n1 - L0), (double)(n1 - L1));
-            } else {
-              if (fp.kind == 2) {
-                const int64_t tr = ntreat - LT;
-                if (LT < 1 || nl - LT < 1 || tr < 1 || nr - tr < 1) continue;
-              }
-              crit = mse_crit(from_fix(LS), (double)nl, from_fix(stot - LS), (double)nr);
-            }
+            const double crit = crit_at(p0 + c0[e], p1 + c1[e], ps + cs[e], pt + ct[e]);
             if (crit > lbest) { lbest = crit; lbin = b; }
           }
-          // wave argmax: max crit, then lowest bin
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            const double oc = __shfl_xor(lbest, o, 64);
-            const int ob = __shfl_xor(lbin, o, 64);
-            if (oc > lbest || (oc == lbest && ob < lbin)) { lbest = oc; lbin = ob; }
-          }
-          if (lbin < NBINS && lbest > best) { best = lbest; bf = f; bb = lbin; }
+          take_best(lbest, lbin, f);
         };
-        if (small) {
+        const int mrows = nd.hi - nd.lo;
+#ifdef FOREST_PROF
+        if (lane == 0 && small) atomicAdd(&forest_prof[t & 1023][mrows <= 16 ? 5 : 6], 1ull);
+#endif
+        if (small && mrows <= 16) {
+          // Tiny node: every row is a lane; the candidate thresholds are the bins present
+          // (an absent bin splits like the present bin below it, which wins the lowest-bin
+          // tie-break), and each lane sums its own threshold's left side over the node's
+          // rows. Same integer sums and criteria as the histogram path.
+          if (fp.kind == 2) {
+            int64_t t = 0;
+            for (int j = 0; j < mrows; ++j) {
+              const int64_t r1j = ((int64_t)__builtin_amdgcn_readlane((int)(cr1 >> 32), j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)cr1, j);
+              t += from_fix(r1j) > cn.wbar ? 1 : 0;
+            }
+            ntreat = t;
+          }
+          for (int k0 = 0; k0 < nf; k0 += 16) {
+            int bins[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int k = k0 + u;
+              bins[u] = (cvalid && k < nf) ? (int)Xb[(int64_t)perm[wid][k] * n + ci] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int k = k0 + u;
+              if (k >= nf) break;
+              const int f = perm[wid][k];
+              const int bme = bins[u];
+              int64_t L0 = 0, L1 = 0, LS = 0, LT = 0;
+              for (int j = 0; j < mrows; ++j) {
+                const int bj = __builtin_amdgcn_readlane(bins[u], j);
+                const bool in = bj <= bme;
+                const int64_t wj = ((int64_t)__builtin_amdgcn_readlane((int)(cw >> 32), j) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)cw, j);
+                if (fp.kind == 0) {
+                  const int yj = __builtin_amdgcn_readlane(cy, j);
+                  if (in) { if (yj) L1 += wj; else L0 += wj; }
+                } else {
+                  const int64_t r1j =
+                      ((int64_t)__builtin_amdgcn_readlane((int)(cr1 >> 32), j) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)cr1, j);
+                  if (fp.kind == 1) {
+                    if (in) { L0 += wj; LS += wj * r1j; }
+                  } else {
+                    const int64_t rhoj =
+                        ((int64_t)__builtin_amdgcn_readlane((int)(crho >> 32), j) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)crho, j);
+                    if (in) {
+                      L0 += 1;
+                      LS += rhoj;
+                      LT += from_fix(r1j) > cn.wbar ? 1 : 0;
+                    }
+                  }
+                }
+              }
+              double lbest = -INFINITY;
+              int lbin = NBINS;
+              if (cvalid && bme < NBINS - 1) {
+                const double crit = crit_at(L0, L1, LS, LT);
+                if (crit > lbest) { lbest = crit; lbin = bme; }
+              }
+              take_best(lbest, lbin, f);
+            }
+          }
+        } else if (small) {
           for (int k0 = 0; k0 < nf; k0 += 16) {
             int bins[16];
 #pragma unroll
@@ -369,18 +483,40 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
             const int f = perm[wid][k];
             const uint8_t* xf = Xb + (int64_t)f * n;
             clear_hist();
-            for (int q = nd.lo + lane; q < nd.hi; q += 64) {
+            // 4 rows per lane per iteration: all gathers issued before the (integer,
+            // order-independent) LDS atomics, so 4x more loads are in flight
+            int q = q0;
+            for (; q + 3 * qstep < nd.hi; q += 4 * qstep) {
+              int ii[4], bb[4], yy[4];
+              int64_t ww[4], aa[4], rr[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) ii[u] = S.idx[q + qstep * u];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int i = ii[u];
+                bb[u] = xf[i];
+                ww[u] = S.w[i];
+                yy[u] = fp.kind == 0 ? ycls[i] : 0;
+                aa[u] = fp.kind != 0 ? r1[i] : 0;
+                rr[u] = fp.kind == 2 ? S.rho[i] : 0;
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u) hist_row(bb[u], ww[u], yy[u], aa[u], rr[u]);
+            }
+            for (; q < nd.hi; q += qstep) {
               const int i = S.idx[q];
               hist_row(xf[i], S.w[i], fp.kind == 0 ? ycls[i] : 0, fp.kind != 0 ? r1[i] : 0,
                        fp.kind == 2 ? S.rho[i] : 0);
             }
+            if (coop) __syncthreads();      // every wave's rows are in
             scan_eval(f);
+            if (coop) __syncthreads();      // histograms read before the next clear
           }
         }
         if (!(bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent)))) bf = -1;
       }
-      // ---- record the decision (lane 0)
-      if (lane == 0) {
+      // ---- record the decision (lane 0; wave 0 for a cooperative node)
+      if (lane == 0 && (!coop || wid == 0)) {
         int nl_rows = 0;
         if (bf >= 0) {
           feat[v] = bf;
@@ -404,8 +540,27 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
         }
         S.dec[j] = make_int4(bf >= 0 ? 1 : 0, bf, bb, nl_rows);
       }
+    };
+    // big nodes in level order, in chunks of 256 candidates (block compaction), each
+    // decided by the whole workgroup; then every other node by one wave
+    for (int base = 0; base < ncur; base += 256) {
+      const int j = base + tid;
+      const bool big = j < ncur && S.cur[j].hi - S.cur[j].lo > COOP_ROWS;
+      int tot;
+      const int pos = block_scan_excl(big ? 1 : 0, shi, &tot);
+      if (big) sbig[pos] = j;
+      __syncthreads();
+      for (int e = 0; e < tot; ++e) decide(sbig[e], true);
+      __syncthreads();
+    }
+    for (int j = wid; j < ncur; j += 4) {
+      const Rng3 nd = S.cur[j];
+      if (nd.hi - nd.lo > COOP_ROWS) continue;
+      decide(j, false);
     }
     __syncthreads();
+    FPROF_T(tl1_);
+    FPROF_ADD(0, tl1_ - tl0_);
     // ---- child ids in level order (block scan over split flags)
     int id_base = snext_id;
     int nsplit_total = 0;
@@ -422,6 +577,8 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
       nsplit_total += tot;
     }
     __syncthreads();
+    FPROF_T(tl2_);
+    FPROF_ADD(1, tl2_ - tl1_);
     // ---- stable partition of each split node (one wave per node) + next level list
     for (int j = wid; j < ncur; j += 4) {
       const int4 d = S.dec[j];
@@ -457,6 +614,8 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
       sncur = 2 * nsplit_total;
       snext_id = id_base + 2 * nsplit_total;
     }
+    FPROF_T(tl3_);
+    FPROF_ADD(2, tl3_ - tl2_);
     // swap lists
     Rng3* tswap = S.cur; S.cur = S.nxt; S.nxt = tswap;
     __syncthreads();
@@ -753,3 +912,13 @@ ATE_API int ate_bin_matrix(const void* X, int64_t n, int p, const void* edges, c
   ATE_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef FOREST_PROF
+extern "C" __attribute__((visibility("default"))) int ate_forest_prof_read(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(forest_prof), sizeof(forest_prof));
+}
+extern "C" __attribute__((visibility("default"))) int ate_forest_prof_reset() {
+  static unsigned long long z[1024][8];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(forest_prof), z, sizeof(z));
+}
+#endif
