@@ -161,17 +161,26 @@ def run_simulated(world_size: int, fn):
     return results
 
 
+def local_device() -> int:
+    """GPU of this rank: LOCAL_RANK, wrapped over the visible devices (one rank per GPU on
+    a full node; ranks share GPUs only when launched with more ranks than devices)."""
+    return int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+
+
 def from_env():
     """TorchComm if launched under torch.distributed.run (WORLD_SIZE>1), else LocalComm."""
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch.distributed as dist
         if not dist.is_initialized():
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # ATE_DIST_BACKEND=gloo: host-staged collectives (e.g. several ranks sharing one
+            # GPU in a rehearsal); default RCCL ("nccl") when a GPU is visible
+            backend = os.environ.get("ATE_DIST_BACKEND") or \
+                ("nccl" if torch.cuda.is_available() else "gloo")
             # RCCL errors (a failed peer, a timed-out collective) abort the process
             # instead of leaving the other ranks blocked
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-            if backend == "nccl":
-                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            if torch.cuda.is_available():
+                torch.cuda.set_device(local_device())
             dist.init_process_group(backend=backend)
         return TorchComm()
     return LocalComm()

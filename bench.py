@@ -59,7 +59,7 @@ def main():
     comm = C.from_env()
     world, rank = comm.world_size, comm.rank
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(C.local_device())
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
