@@ -757,3 +757,87 @@ ATE_API int ate_gbdt_apply(const void* Xr, int64_t ldr, int64_t n, int ntree, in
   ATE_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------ K11 on a device panel
+// Bins the feature columns of an HBM-resident column-major panel (bf16 or fp32 storage,
+// fold segments with padding) straight into the row-major uint8 layout of the trainer:
+// out[i][j] (stride ldr) for compact real row i = seg_c0[s] + (row - seg_r0[s]).
+// bin(x) = #{edges < x} (first edge >= x), the rule of csrc/forest.hip::bin_kernel.
+// Workgroup = 256 rows x 16 features: reads are row-contiguous per feature, each thread
+// writes its row's 16 bins as one 16-byte store; the 16 features' edges sit in LDS.
+template <typename T>
+__device__ __forceinline__ double panel_val(const T* X, int64_t off);
+template <> __device__ __forceinline__ double panel_val<uint16_t>(const uint16_t* X, int64_t off) {
+  return (double)__uint_as_float(((uint32_t)X[off]) << 16);
+}
+template <> __device__ __forceinline__ double panel_val<float>(const float* X, int64_t off) {
+  return (double)X[off];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gbdt_bin_panel_kernel(
+    const T* __restrict__ X, int64_t ld, const int* __restrict__ xcols, int p,
+    const int64_t* __restrict__ seg_r0, const int64_t* __restrict__ seg_n,
+    const int64_t* __restrict__ seg_c0, int nseg, int64_t nreal,
+    const double* __restrict__ edges, const int* __restrict__ nedges,
+    uint8_t* __restrict__ out, int64_t ldr) {
+  __shared__ double se[16][255];
+  __shared__ int sne[16];
+  const int f0 = blockIdx.y * 16;
+  for (int e = threadIdx.x; e < 16 * 255; e += 256) {
+    const int k = e / 255, b = e % 255;
+    se[k][b] = f0 + k < p ? edges[(int64_t)(f0 + k) * 255 + b] : 0.0;
+  }
+  if (threadIdx.x < 16) sne[threadIdx.x] = f0 + threadIdx.x < p ? nedges[f0 + threadIdx.x] : 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < nreal;
+       i += (int64_t)gridDim.x * 256) {
+    int s = 0;
+    while (s + 1 < nseg && seg_c0[s + 1] <= i) ++s;
+    const int64_t row = seg_r0[s] + (i - seg_c0[s]);
+    uint8_t b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      b[k] = 0;
+      if (f0 + k < p) {
+        const double x = panel_val<T>(X, (int64_t)xcols[f0 + k] * ld + row);
+        int lo = 0, hi = sne[k];
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (se[k][mid] < x) lo = mid + 1; else hi = mid;
+        }
+        b[k] = (uint8_t)lo;
+      }
+    }
+    uint4 v;
+    v.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+    v.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+    v.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+    v.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+    *reinterpret_cast<uint4*>(out + i * ldr + f0) = v;
+  }
+}
+
+// dtype: 0 = bf16 storage, 1 = fp32. ldr must be a multiple of 16 and >= p rounded to 16.
+ATE_API int ate_gbdt_bin_panel(const void* X, int dtype, int64_t ld, const void* xcols, int p,
+                               const void* seg_r0, const void* seg_n, const void* seg_c0,
+                               int nseg, int64_t nreal, const void* edges, const void* nedges,
+                               void* out, int64_t ldr, void* stream) {
+  if (ldr % 16 || ldr < (p + 15) / 16 * 16) return -1;
+  dim3 grid(ate::grid_for(nreal, 256, 4096), (p + 15) / 16);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 0)
+    hipLaunchKernelGGL(gbdt_bin_panel_kernel<uint16_t>, grid, dim3(256), 0, st,
+                       (const uint16_t*)X, ld, (const int*)xcols, p, (const int64_t*)seg_r0,
+                       (const int64_t*)seg_n, (const int64_t*)seg_c0, nseg, nreal,
+                       (const double*)edges, (const int*)nedges, (uint8_t*)out, ldr);
+  else if (dtype == 1)
+    hipLaunchKernelGGL(gbdt_bin_panel_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ld,
+                       (const int*)xcols, p, (const int64_t*)seg_r0, (const int64_t*)seg_n,
+                       (const int64_t*)seg_c0, nseg, nreal, (const double*)edges,
+                       (const int*)nedges, (uint8_t*)out, ldr);
+  else
+    return -1;
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
