@@ -17,6 +17,7 @@ Learners: ``"rf"`` (histogram forests; ``comm`` shards the trees over ranks, C05
 from __future__ import annotations
 
 import math
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -85,7 +86,34 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
         from ..models import gbdt as G
         edges = G.sample_bin_edges(Xn, device=dev)
         Xb = G.binned(Xn, edges, dev)
+    concurrent = learner == "rf" and dev.type == "cuda" and (comm is None or comm.world_size == 1)
+    if concurrent:
+        # the 3K forests are independent: grow them concurrently, one HIP stream per host
+        # thread, so a 100-tree forest (100 workgroups) does not leave most CUs idle;
+        # every forest is a deterministic function of its inputs (same trees as serially)
+        jobs = []
+        for k in range(folds):
+            ho = fid == k
+            tr = ~ho
+            t1, t0 = tr & (Wn == 1), tr & (Wn == 0)
+            s = seed + 1000 * (k + 1)
+            jobs += [(e, ho, tr, Wn, s), (mu1, ho, t1, Yn, s + 1), (mu0, ho, t0, Yn, s + 2)]
+
+        def run(job):
+            out, ho, rows, target, sd = job
+            st = torch.cuda.Stream(device=dev)
+            with torch.cuda.device(dev), torch.cuda.stream(st):
+                r = _rf_fit_predict(Xn[rows], target[rows], Xn[ho], num_trees, sd, dev, None,
+                                    edges)
+            st.synchronize()
+            return r
+
+        with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
+            for (out, ho, _, _, _), r in zip(jobs, ex.map(run, jobs)):
+                out[ho] = r
     for k in range(folds):
+        if concurrent:
+            break
         ho = fid == k
         tr = ~ho
         t1, t0 = tr & (Wn == 1), tr & (Wn == 0)
