@@ -390,6 +390,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     }
   };
 
+  int ready = -1;   // block whose gradient and diagonal registers a pass end left current
   auto pass = [&](bool full) -> double {
     double dlx_l = 0.0;
     for (int t = wid; t < T; t += 4) {      // blocks holding an active coordinate
@@ -408,13 +409,17 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     const int nv = snv;
     if (nv == 0) return 0.0;
     PROF_T(tp0_);
-    pull(svis[0]);
+    if (ready != svis[0]) pull(svis[0]);   // else: brought up to date by the last visit
+    ready = -1;
     PROF_T(tp1_);
     PROF_ADD(0, tp1_ - tp0_);
     PROF_ADD(8, tp1_ - tp0_);
     for (int v = 0; v < nv; ++v) {
       const int t = svis[v];
-      const int tn = v + 1 < nv ? svis[v + 1] : -1;
+      // the last visit prefetches block 0, the first block of the next pass whenever
+      // that pass is a full pass or block 0 holds an active coordinate (checked there)
+      const int tn = v + 1 < nv ? svis[v + 1] : (t != 0 ? 0 : -1);
+      if (v + 1 == nv) ready = tn;
       const int k = t * 64 + lane;
       PROF_T(ta_);
       double gt = 0.0, at = 0.0, dblk = 0.0;
@@ -639,6 +644,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     } else if (m == 1) {
       // lambda_max needs the exact current gradient of every coordinate
       for (int t = 0; t < T; ++t) pull(t);
+      ready = -1;
       double mx = 0.0;
       for (int k = lane; k < p; k += 64)
         if ((sflag[k] & 1) && svp[k] > 0.0) mx = fmax(mx, fabs(sg[k]) / svp[k]);
