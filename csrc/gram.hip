@@ -225,6 +225,9 @@ __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
 // hits L2 on what the other fetched). Every wave writes its 16x16 blocks contiguously
 // into a 272-block slab slot; a host-built table maps slab blocks to Gram blocks.
 constexpr int PAIR_SLOTS = 272;
+#ifndef GRAM_DIAG
+#define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA
+#endif
 
 __device__ __forceinline__ int tri_index(int m, int n) {   // m <= n < 8, row-major triangle
   return m * 8 - (m * (m - 1)) / 2 + (n - m);
@@ -262,10 +265,12 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
   __syncthreads();
   for (int64_t s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
+#if GRAM_DIAG != 2
     if (s + 1 < nsteps) stage(cur ^ 1, ch.row0 + (s + 1) * GK);
+#endif
     const bf16_t* As = lds[cur][abuf];
     const bf16_t* Bs = lds[cur][bbuf];
-    if (!idle) {
+    if (!idle && GRAM_DIAG != 1) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int cc = kk * 4 + (lane >> 4);
