@@ -348,26 +348,46 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         glds16f(src, dst);
       }
     }
-    int cnt = 0;
+    // every wave scans all pending columns and keeps list entries pos = my (mod 3): an even
+    // three-way split however the changed coordinates cluster in the column blocks
+    int tot = 0;
     const int base0 = my * 192;             // private slist/sdelta region (<= 3 * 192 = 576)
-    for (int c = my; c < T; c += 3) {
+    for (int c = 0; c < T; ++c) {
       const int j = c * 64 + lane;
       const double dj = sdc[j] - sds[tn][j];
       const bool nz = dj != 0.0;
       const uint64_t bal = __ballot(nz);
-      const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
-      if (nz) { slist2[base0 + pos] = j; sdelta2[base0 + pos] = (CT)dj; }
-      cnt += __popcll(bal);
+      const int pos = tot + __popcll(bal & ((1ull << lane) - 1ull));
+      if (nz && pos % 3 == my) { slist2[base0 + pos / 3] = j; sdelta2[base0 + pos / 3] = (CT)dj; }
+      tot += __popcll(bal);
     }
+    const int cnt = (tot - my + 2) / 3;
     const CT* colt = Cq + tn * 64 + lane;
     CT acc = 0;
     int e = 0;
-    for (; e + 16 <= cnt; e += 16) {
-      CT v[16];
+    constexpr int GB = sizeof(CT) == 4 ? 32 : 16;   // row segments in flight per wave
+    for (; e + GB <= cnt; e += GB) {
+      CT v[GB];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
+      for (int u = 0; u < GB; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u] * sdelta2[base0 + e + u];
+      for (int u = 0; u < GB; ++u) acc += v[u] * sdelta2[base0 + e + u];
+    }
+    if constexpr (sizeof(CT) == 4) {
+      for (; e + 16 <= cnt; e += 16) {
+        CT v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u] * sdelta2[base0 + e + u];
+      }
+    }
+    for (; e + 8 <= cnt; e += 8) {
+      CT v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u] * sdelta2[base0 + e + u];
     }
     for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     spart[wid][lane] = (double)acc;
