@@ -199,8 +199,13 @@ __device__ __forceinline__ double readlane_d(double v, int i) {
 // deposit the 64x64 diagonal block in LDS for the sequential in-block recurrence (wave 0).
 // Active passes skip blocks without active coordinates (no pull needed: nothing in them
 // can move); full passes pull every block, so every KKT check uses the current gradient.
+#ifndef ENET_NW
+#define ENET_NW 8   // waves per problem: wave 0 = recurrence, waves 1.. = pulls
+#endif
+constexpr int NW = ENET_NW, NTH = NW * 64, NP = NW - 1;
+
 template <typename CT>
-__global__ __launch_bounds__(256) void enet_path_kernel(
+__global__ __launch_bounds__(NTH) void enet_path_kernel(
     const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
     const unsigned char* __restrict__ ju_s, const double* __restrict__ ys_s,
     const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
@@ -211,11 +216,12 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
   __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
   __shared__ int sflag[PMAX];             // bit0 ju, bit1 active
-  __shared__ double spart[4][64];
+  __shared__ double spart[NW][64];
   __shared__ __attribute__((aligned(16))) CT sdelta[PMAX];
   __shared__ int slist[PMAX];             // compacted pending columns (per-wave quarters)
-  __shared__ int slist2[576];             // pipelined pull: waves 1-3, 192 entries each
-  __shared__ __attribute__((aligned(16))) CT sdelta2[576];
+  constexpr int PER = (PMAX + NP - 1) / NP + 1;   // pending entries per pull wave
+  __shared__ int slist2[NP * PER];        // pipelined pull: waves 1.., PER entries each
+  __shared__ __attribute__((aligned(16))) CT sdelta2[NP * PER];
   __shared__ int scl[64];                 // wave 0: changed coordinates of the block
   __shared__ CT scd[64];
   __shared__ __attribute__((aligned(16))) float sCn[64 * 64];     // next block's diagonal block
@@ -237,10 +243,10 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int T = (p + 63) >> 6;
   const int ldc = T * 64;
-  const int cw = ldc / 4;                  // columns per wave in the pull (multiple of 16)
+  const int cw = ldc / NW;                 // columns per wave in the pull (multiple of 8)
   const CT* Cq = C + (int64_t)pr.train * p * ldc;
   const double ysq = ys_s[(int64_t)pr.train * ny + pr.y];
-  for (int k = tid; k < T * 64; k += 256) {
+  for (int k = tid; k < T * 64; k += NTH) {
     bool in = k < p;
     sg[k] = in ? gin[((int64_t)pr.train * ny + pr.y) * p + k] : 0.0;
     sa[k] = 0.0;
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     sdc[k] = 0.0;
     sflag[k] = (in && ju_s[(int64_t)pr.train * p + k]) ? 1 : 0;
   }
-  for (int e = tid; e < TMAX * PMAX; e += 256) (&sds[0][0])[e] = 0.0;
+  for (int e = tid; e < TMAX * PMAX; e += NTH) (&sds[0][0])[e] = 0.0;
   __syncthreads();
   const int nlam = pr.ulam_src >= 0 ? L : pr.nlam_req;
   const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
@@ -260,7 +266,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
   constexpr int W = sizeof(V) / sizeof(CT);
   float dg_lo[32], dg_hi[32];
 
-  // bring block t's gradient up to date (all 256 threads); stage its diagonal block.
+  // bring block t's gradient up to date (all waves); stage its diagonal block.
   // Sparse pull: only coordinates changed since block t's snapshot contribute, and by
   // symmetry coordinate j's contribution is the contiguous row segment C[j][t*64 .. +63].
   // Each wave compacts the nonzero pending deltas of its quarter of the columns (ordered
@@ -319,19 +325,22 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     __syncthreads();
     if (tid < 64) {
       const int k = t * 64 + tid;
-      sg[k] -= spart[0][tid] + spart[1][tid] + spart[2][tid] + spart[3][tid];
+      double sp = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sp += spart[w][tid];
+      sg[k] -= sp;
     }
-    for (int j = tid; j < ldc; j += 256) sds[t][j] = sdc[j];
+    for (int j = tid; j < ldc; j += NTH) sds[t][j] = sdc[j];
     __syncthreads();
   };
 
   // Pipelined pass. Wave 0 runs the sequential recurrence of block t (diagonal block in
   // registers) and then applies block t's own deltas to block tn = next visited block
-  // (contiguous row segments C[k][tn*64..]); meanwhile waves 1-3 pull every OTHER change
+  // (contiguous row segments C[k][tn*64..]); meanwhile the pull waves (1..NW-1) pull every OTHER change
   // pending for block tn (sdc is frozen until the first barrier) and stage tn's diagonal
   // block in LDS. After the barrier wave 0 publishes block t, completes block tn's
   // gradient and snapshot, and moves tn's diagonal block into registers.
-  auto pull_rest = [&](int t, int tn) {     // waves 1..3
+  auto pull_rest = [&](int t, int tn) {     // waves 1..NW-1
     const int my = wid - 1;
     if constexpr (sizeof(CT) == 4) {
       // fp32 C: tn's diagonal block and the (t rows x tn cols) block that wave 0 needs
@@ -339,7 +348,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
       // of 64 floats per wave instruction), issued first so their latency overlaps the
       // pending-column gathers below: one memory round trip per visit. Rows >= p are
       // clamped (finite) and masked where used.
-      for (int pc = my; pc < 32; pc += 3) {
+      for (int pc = my; pc < 32; pc += NP) {
         const int blk = pc < 16 ? tn : t;
         const int i = (pc & 15) * 4 + (lane >> 4);
         const int r = min(blk * 64 + i, p - 1);
@@ -348,20 +357,20 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
         glds16f(src, dst);
       }
     }
-    // every wave scans all pending columns and keeps list entries pos = my (mod 3): an even
-    // three-way split however the changed coordinates cluster in the column blocks
+    // every pull wave scans all pending columns and keeps list entries pos = my (mod NP): an
+    // even split however the changed coordinates cluster in the column blocks
     int tot = 0;
-    const int base0 = my * 192;             // private slist/sdelta region (<= 3 * 192 = 576)
+    const int base0 = my * PER;             // private slist/sdelta region
     for (int c = 0; c < T; ++c) {
       const int j = c * 64 + lane;
       const double dj = sdc[j] - sds[tn][j];
       const bool nz = dj != 0.0;
       const uint64_t bal = __ballot(nz);
       const int pos = tot + __popcll(bal & ((1ull << lane) - 1ull));
-      if (nz && pos % 3 == my) { slist2[base0 + pos / 3] = j; sdelta2[base0 + pos / 3] = (CT)dj; }
+      if (nz && pos % NP == my) { slist2[base0 + pos / NP] = j; sdelta2[base0 + pos / NP] = (CT)dj; }
       tot += __popcll(bal);
     }
-    const int cnt = (tot - my + 2) / 3;
+    const int cnt = (tot - my + NP - 1) / NP;
     const CT* colt = Cq + tn * 64 + lane;
     CT acc = 0;
     int e = 0;
@@ -392,28 +401,26 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
     for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     spart[wid][lane] = (double)acc;
     if constexpr (sizeof(CT) == 4) return;
-    // fp64 C: tn's diagonal block -> LDS (fp32) through registers, 2 batches of 11 rows
+    // fp64 C: tn's diagonal block -> LDS (fp32) through registers, rows i = my (mod NP)
+    constexpr int NR = (64 + NP - 1) / NP;
+    float dr[NR];
 #pragma unroll
-    for (int b2 = 0; b2 < 2; ++b2) {
-      float dr[11];
+    for (int ii = 0; ii < NR; ++ii) {
+      const int i = my + NP * ii;
+      const int r = tn * 64 + i;
+      dr[ii] = (i < 64 && r < p) ? (float)Cq[(int64_t)r * ldc + tn * 64 + lane] : 0.f;
+    }
 #pragma unroll
-      for (int ii = 0; ii < 11; ++ii) {
-        const int i = my + 3 * (b2 * 11 + ii);
-        const int r = tn * 64 + i;
-        dr[ii] = (i < 64 && r < p) ? (float)Cq[(int64_t)r * ldc + tn * 64 + lane] : 0.f;
-      }
-#pragma unroll
-      for (int ii = 0; ii < 11; ++ii) {
-        const int i = my + 3 * (b2 * 11 + ii);
-        if (i < 64) sCn[i * 64 + lane] = dr[ii];
-      }
+    for (int ii = 0; ii < NR; ++ii) {
+      const int i = my + NP * ii;
+      if (i < 64) sCn[i * 64 + lane] = dr[ii];
     }
   };
 
   int ready = -1;   // block whose gradient and diagonal registers a pass end left current
   auto pass = [&](bool full) -> double {
     double dlx_l = 0.0;
-    for (int t = wid; t < T; t += 4) {      // blocks holding an active coordinate
+    for (int t = wid; t < T; t += NW) {     // blocks holding an active coordinate
       const bool a = full || ((sflag[t * 64 + lane] & 3) == 3);
       const uint64_t b = __builtin_amdgcn_ballot_w64(a);
       if (lane == 0) sblk_any[t] = b != 0;
@@ -583,8 +590,11 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
             }
             spart[0][lane] = (double)corr;
           }
-          sg[kn] -= spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane];
-          sds[tn][k] = dnew;     // block t's columns; waves 1-3 copy the others
+          double sp = 0.0;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) sp += spart[w][lane];
+          sg[kn] -= sp;
+          sds[tn][k] = dnew;     // block t's columns; the pull waves copy the others
 
           // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] is only read
           // for a moving coordinate i, and coordinates >= p never move
@@ -599,7 +609,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
 #endif
       } else if (tn >= 0) {
         // snapshot of block tn for every column block except t (unchanged since B1)
-        for (int j = (wid - 1) * 64 + lane; j < ldc; j += 192)
+        for (int j = (wid - 1) * 64 + lane; j < ldc; j += NP * 64)
           if ((j >> 6) != t) sds[tn][j] = sdc[j];
       }
       __syncthreads();
@@ -686,7 +696,7 @@ __global__ __launch_bounds__(256) void enet_path_kernel(
       }
     }
     double* ap = apath + ((int64_t)q * L + m) * p;
-    for (int k = tid; k < p; k += 256) ap[k] = sa[k];
+    for (int k = tid; k < p; k += NTH) ap[k] = sa[k];
     rsq = wave_sum(rsq_l);
     if (tid == 0) sdl = rsq;
     __syncthreads();
@@ -733,7 +743,7 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
   // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nwg)
   const int nwg = (nprob + 7) / 8 * 8;
 #define LAUNCH_C(CTT)                                                                          \
-  hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(256), 0, s, (const CTT*)C,       \
+  hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(NTH), 0, s, (const CTT*)C,       \
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
