@@ -471,7 +471,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         // visit, so the nonzero case becomes threshold -1 (always passes) and ineligible
         // lanes get +inf; lanes <= last are cut with a scalar mask. The proposed step
         // an - at of every lane is computed alongside the ballot, so the serial chain is
-        // fma -> add -> compare/ballot -> ff1 -> readlane -> fma. Per update the loop only
+        // mul -> sub -> compare/ballot -> ff1 -> readlane -> mul. Per update the loop only
         // records the new coefficient and the gradient it came from for the moving lane;
         // the delta (an - at, the same operation on the same operands as the broadcast
         // step) and the new coefficient are applied after the loop. Unrolled twice: one
@@ -479,13 +479,17 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         const double thr0 = elig ? (at != 0.0 ? -1.0 : thr_l) : __builtin_inf();
         uint64_t live = ~0ull, moved = 0ull;
         double anv = at;
+        // u = g + a is carried instead of recomputed: a lane's a is constant while it can
+        // still move (lanes <= last are cut), and u receives the same "- c*d" as g, so the
+        // add drops off the serial chain. For a == 0 lanes u == g bit for bit (same ops on
+        // the same values): every zero-coefficient entry test sees glmnet's gradient.
+        double u = gt + at;
 #ifdef ENET_PROF
         unsigned long long nupd_ = 0;
 #endif
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): dg_* landed; no waits in the loop
         auto step = [&]() -> bool {
 #pragma clang fp contract(off)
-          const double u = gt + at;
           const double au = fabs(u);
           const uint64_t msk = __builtin_amdgcn_ballot_w64(au > thr0) & live;
           const double an = __dmul_rn(copysign(fmax(au - thr_l, 0.0), u), rden);   // no fma: d == an - at
@@ -498,7 +502,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           const double d = readlane_d(dd, i);
           const bool me = lane == i;
           gbef = me ? gt : gbef;
-          gt -= (double)ci * d;
+          const double cd = (double)ci * d;
+          u -= cd;
+          gt -= cd;
           __builtin_amdgcn_sched_barrier(0);   // bookkeeping below stays off the chain
           live = i == 63 ? 0ull : (~0ull << (i + 1));
           moved |= 1ull << i;
