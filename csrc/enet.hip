@@ -226,6 +226,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ CT scd[64];
   __shared__ __attribute__((aligned(16))) float sCn[64 * 64];     // next block's diagonal block
   __shared__ __attribute__((aligned(16))) float sCorr[64 * 64];   // C[t rows][tn cols] (fp32 C)
+  __shared__ __attribute__((aligned(16))) float sdall[64];         // wave 0: block t's deltas
   __shared__ int svis[8], snv, sblk_any[8];
   __shared__ double sdl;
   __shared__ int sany;
@@ -454,7 +455,13 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       int nc = 0;                           // wave 0: coordinates of block t that changed
       uint64_t chm = 0;                     // wave 0: their lane mask
       int fl = 0;
+      // wave 0: phase-B operands that nothing changes during phase A, read now so their
+      // LDS latency hides under the recurrence
+      double dc0 = 0.0, ds0 = 0.0, sgn = 0.0;
       if (wid == 0) {
+        dc0 = sdc[k];
+        ds0 = sds[t][k];
+        if (tn >= 0) sgn = sg[tn * 64 + lane];
         gt = sg[k];
         at = sa[k];
         const double vpt = svp[k];
@@ -570,37 +577,41 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         sg[k] = gt;
         sa[k] = at;
         sflag[k] = fl;
-        const double dnew = sdc[k] + dblk;
+        const double dnew = dc0 + dblk;
         sdc[k] = dnew;
-        sds[t][k] += dblk;       // own changes are already in g_t
+        sds[t][k] = ds0 + dblk;  // own changes are already in g_t
         if (tn >= 0) {
           const int kn = tn * 64 + lane;
           if constexpr (sizeof(CT) == 4) {
-            // block t's own deltas -> block tn from the DMA'd (t rows x tn cols) block.
-            // All 64 rows in ascending order: an unchanged row has d = 0 and adds
-            // fma(c, 0, corr) = corr exactly, so the sum equals the fma chain over the
-            // changed rows in gather order. 16 LDS reads in flight per batch.
+            // block t's own deltas -> block tn from the DMA'd (t rows x tn cols) block:
+            // all 64 rows (an unchanged row has d = 0), the deltas read back from LDS as
+            // broadcast float4s, 4 independent fma chains combined in a fixed order
             if (chm) {
-              const float dcf = (float)dblk;
+              sdall[lane] = (float)dblk;
+              float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
-              for (int r0 = 0; r0 < 64; r0 += 16) {
-                float v[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = sCorr[(r0 + u) * 64 + lane];
-#pragma unroll
-                for (int u = 0; u < 16; ++u)
-                  corr = __builtin_fmaf(
-                      v[u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dcf), r0 + u)),
-                      corr);
+              for (int r0 = 0; r0 < 64; r0 += 4) {
+                const float4 dv = *reinterpret_cast<const float4*>(sdall + r0);
+                a0 = __builtin_fmaf(sCorr[(r0 + 0) * 64 + lane], dv.x, a0);
+                a1 = __builtin_fmaf(sCorr[(r0 + 1) * 64 + lane], dv.y, a1);
+                a2 = __builtin_fmaf(sCorr[(r0 + 2) * 64 + lane], dv.z, a2);
+                a3 = __builtin_fmaf(sCorr[(r0 + 3) * 64 + lane], dv.w, a3);
               }
+              corr = (a0 + a1) + (a2 + a3);
             }
             spart[0][lane] = (double)corr;
           }
+#ifdef ENET_PROF
+          if (lane == 0) atomicAdd(&enet_prof[q][10], (unsigned long long)(wall_clock64() - tb_));
+#endif
           double sp = 0.0;
 #pragma unroll
           for (int w = 0; w < NW; ++w) sp += spart[w][lane];
-          sg[kn] -= sp;
+          sg[kn] = sgn - sp;
           sds[tn][k] = dnew;     // block t's columns; the pull waves copy the others
+#ifdef ENET_PROF
+          if (lane == 0) atomicAdd(&enet_prof[q][11], (unsigned long long)(wall_clock64() - tb_));
+#endif
 
           // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] is only read
           // for a moving coordinate i, and coordinates >= p never move

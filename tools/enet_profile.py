@@ -55,8 +55,8 @@ def run(n, p):
     rows = buf[:40]
     live = rows[rows[:, 3] > 0]
     print(json.dumps({"step_ms": t[0].elapsed_time(t[1]),
-                      "per_problem": [[int(v) for v in r[:10]] for r in live],
-                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B"}))
+                      "per_problem": [[int(v) for v in r[:12]] for r in live],
+                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B, wave0 phase B up to corr, up to before the diagonal reload"}))
 
 
 if __name__ == "__main__":
