@@ -52,7 +52,7 @@ _SIGS = {
     "ate_cv_select": "pppiipipppp",
     "ate_enet_pick": "ppiiiipp",
     "ate_dml_resid_moments": "iplpipipiiiiiippp",
-    "ate_lognet_path": "iplpiipipipdddippippppppp",
+    "ate_lognet_path": "iplpiipipipdddippippppppppp",
     "ate_lognet_cvloss": "iplpiippipppipp",
     "ate_dgp_fill": "ipllllu" + "iip",
     "ate_forest_fit": "pppppi" + "ppppppppp",

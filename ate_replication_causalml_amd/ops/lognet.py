@@ -37,8 +37,13 @@ def _rescale_vp(vp, p):
 
 
 def cv_lognet(panel, xcols, ycol, penalty_factor=None, alpha=1.0, nlambda=100,
-              lambda_min_ratio=None, thresh=1e-7, maxit=100000) -> LognetCvResult:
-    """cv.glmnet(x, y, family="binomial") with the panel's segments as the CV folds."""
+              lambda_min_ratio=None, thresh=1e-7, maxit=100000,
+              concurrent=True) -> LognetCvResult:
+    """cv.glmnet(x, y, family="binomial") with the panel's segments as the CV folds.
+
+    ``concurrent``: full and fold fits in one launch (fold paths follow the full fit's
+    lambdas through device flags); False = two launches, full fit then folds. Same bits.
+    ``npass`` < 0 flags a fold whose wait for the full fit timed out."""
     K = panel.nseg
     p = len(xcols)
     n = int(np.sum(panel.seg_nreal))
@@ -71,17 +76,28 @@ def cv_lognet(panel, xcols, ycol, penalty_factor=None, alpha=1.0, nlambda=100,
     npass = torch.zeros(nq, dtype=torch.int32, device=dev)
     dt = dtype_code(panel.data)
     X = panel.data
-    # full problem: its own lambda sequence
-    _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
-                 segs_t.data_ptr(), K, masks_t.data_ptr(), 1, vp_t.data_ptr(), alpha, flmin,
-                 thresh, maxit, 0, 0, L, a0.data_ptr(), beta.data_ptr(), lam.data_ptr(),
-                 devr.data_ptr(), nlam.data_ptr(), npass.data_ptr(), s)
-    # fold problems on the full lambda sequence (count read on the device)
     off = lambda t: t.data_ptr() + t.element_size() * t.stride(0)
-    _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
-                 segs_t.data_ptr(), K, off(masks_t), K, vp_t.data_ptr(), alpha, flmin, thresh,
-                 maxit, lam.data_ptr(), nlam.data_ptr(), L, off(a0), off(beta), off(lam),
-                 off(devr), nlam.data_ptr() + 4, npass.data_ptr() + 4, s)
+    if concurrent and L >= 3 and nq <= 256:
+        # one launch: the full fit (problem 0) and the K fold fits run side by side, the
+        # folds following the full fit's lambda sequence and stop through device flags
+        progress = torch.zeros(2, dtype=torch.int32, device=dev)
+        lampub = torch.zeros(L, **f64)
+        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+                     segs_t.data_ptr(), K, masks_t.data_ptr(), nq, vp_t.data_ptr(), alpha,
+                     flmin, thresh, maxit, 0, 0, L, a0.data_ptr(), beta.data_ptr(),
+                     lam.data_ptr(), devr.data_ptr(), nlam.data_ptr(), npass.data_ptr(),
+                     progress.data_ptr(), lampub.data_ptr(), s)
+    else:
+        # full problem: its own lambda sequence
+        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+                     segs_t.data_ptr(), K, masks_t.data_ptr(), 1, vp_t.data_ptr(), alpha, flmin,
+                     thresh, maxit, 0, 0, L, a0.data_ptr(), beta.data_ptr(), lam.data_ptr(),
+                     devr.data_ptr(), nlam.data_ptr(), npass.data_ptr(), 0, 0, s)
+        # fold problems on the full lambda sequence (count read on the device)
+        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+                     segs_t.data_ptr(), K, off(masks_t), K, vp_t.data_ptr(), alpha, flmin,
+                     thresh, maxit, lam.data_ptr(), nlam.data_ptr(), L, off(a0), off(beta),
+                     off(lam), off(devr), nlam.data_ptr() + 4, npass.data_ptr() + 4, 0, 0, s)
     hold = torch.arange(K, dtype=torch.int32, device=dev)
     cvraw = torch.empty((K, L), **f64)
     _native.call("ate_lognet_cvloss", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,

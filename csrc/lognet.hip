@@ -20,6 +20,17 @@
 //     gradient from the Gram column in LDS. Exactly the sequential order of cd_solve.
 // p <= 96 (template PM = 32 or 96). Fold problems take the full problem's lambda
 // sequence (ulam, count read from device memory: no host round trip).
+//
+// Concurrent mode (progress != nullptr): ONE launch of 1+K workgroups, problem 0 the full
+// fit, problems 1..K the folds, all co-resident (workgroup 0 is dispatched first, so it is
+// never waiting behind a spinning fold). The full fit knows its whole lambda sequence
+// once lambda_max is known (m = 1): it stores it to lampub (lambda_0 extrapolated as at
+// the end of the path) and releases progress[1]; every later lambda it commits to
+// (past glmnet's early-stop check) releases progress[0] = m+1, and the path end releases
+// progress[0] = FINAL | nlam. A fold waits for the sequence before lambda 0 and, after
+// its own first pass at lambda m, for the full fit's decision on m: the fold path then
+// ends exactly where the two-launch form (nlam read from the finished full fit) ends, with
+// bit-identical outputs, while the two paths run side by side instead of back to back.
 #include "common.hpp"
 
 namespace {
@@ -65,7 +76,8 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     const double* __restrict__ vp_in, double alpha, double flmin, double thresh, int maxit,
     const double* __restrict__ ulam, const int* __restrict__ nlam_in, int L,
     double* __restrict__ a0_out, double* __restrict__ beta_out, double* __restrict__ lam_out,
-    double* __restrict__ dev_out, int* __restrict__ nlam_out, int* __restrict__ npass_out) {
+    double* __restrict__ dev_out, int* __restrict__ nlam_out, int* __restrict__ npass_out,
+    int* __restrict__ progress, double* __restrict__ lampub) {
   using C = Cfg<PM>;
   constexpr int Q = C::Q, QP = C::QP, RB = C::RB, TPT = C::TPT, NCH = C::NCH;
   __shared__ double sC[Q * Q];
@@ -172,13 +184,43 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     ga[c] = xva[c] = cia[c] = 0.0;
   }
 
-  const bool have_ulam = ulam != nullptr;
-  const int nlam = have_ulam ? (nlam_in ? *nlam_in : L) : L;
+  const bool conc = progress != nullptr;
+  const bool have_ulam = conc ? prob > 0 : ulam != nullptr;
+  const int nlam = have_ulam && !conc ? (nlam_in ? *nlam_in : L) : L;
   const double alf = have_ulam ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
   const double shr = thresh * dev0;
   double alm = 0.0, dev_prev = 0.0;
   int npass_tot = 0, nlam_eff = 0;
+  bool timed_out = false;
   double* bo = beta_out + (int64_t)prob * L * p;
+
+  auto publish = [&](int* dst, int v) {   // one thread: agent-scope release of *dst
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // fold side (thread 0): bounded poll of progress[idx] until ready(v); acquire. -1 = timeout
+  auto await = [&](int idx, auto ready) -> int {
+    int v = 0;
+    for (long spin = 0;; ++spin) {
+      v = __hip_atomic_load(progress + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ready(v)) break;
+      if (spin > (1l << 26)) return -1;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return v;
+  };
+  constexpr int FINAL = 1 << 30;
+  if (conc && have_ulam) {                 // the full fit's lambda sequence
+    if (tid == 0) sictl[2] = await(1, [](int v) { return v != 0; });
+    __syncthreads();
+    timed_out = sictl[2] < 0;
+    ulam = lampub;
+    __syncthreads();
+  }
 
   // One pass over the training rows at the current coefficients:
   //   C = Z' diag(v) Z with Z = [1, z, r/v]  ->  Gram, intercept cross terms, gradient;
@@ -287,7 +329,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   };
 
   bool stopped = false;
-  for (int m = 0; m < nlam && !stopped; ++m) {
+  for (int m = 0; m < nlam && !stopped && !timed_out; ++m) {
     const int kind = have_ulam ? 0 : (m == 0 ? 1 : (m == 1 ? 2 : 3));
     if (kind == 0) alm = ulam[m];
     else if (kind == 1) alm = BIG;
@@ -301,6 +343,21 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
         if (!have_ulam && m - 1 >= MNLAM - 1 && (dr - dev_prev < FDEV * dr || dr > DEVMAX)) {
           stopped = true;
           break;
+        }
+        if (conc && !have_ulam && tid == 0) publish(progress, m + 1);
+        if (conc && have_ulam) {
+          // does the full fit go on to lambda m? (this pass's deviance is already the
+          // final one of lambda m-1 if not)
+          if (tid == 0)
+            sictl[2] = await(0, [m](int v) { return (v & (FINAL - 1)) > m || (v & FINAL); });
+          __syncthreads();
+          const int v = sictl[2];
+          __syncthreads();
+          if (v < 0) timed_out = true;
+          if (v < 0 || (v & (FINAL - 1)) <= m) {
+            stopped = true;
+            break;
+          }
         }
         dev_prev = dr;
       }
@@ -322,6 +379,19 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
             if (jua[c] && vpa[c] > 0.0) mx = fmax(mx, fabs(ga[c]) / vpa[c]);
           mx = ate::wave_max(mx);
           alm = alf * mx / fmax(alpha, 1e-3);
+          if (conc && lane == 0) {
+            // the whole sequence, rounded exactly as the path computes it
+            double x = alm;
+            lampub[1] = x;
+            double l2 = x;
+            for (int mm = 2; mm < L; ++mm) {
+              x *= alf;
+              lampub[mm] = x;
+              if (mm == 2) l2 = x;
+            }
+            lampub[0] = L >= 3 ? exp(2.0 * log(alm) - log(l2)) : BIG;
+            publish(progress + 1, 1);
+          }
         }
         const double ab = alm * alpha, dem = alm * (1.0 - alpha);
         double bs[NCH];
@@ -410,7 +480,8 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     nlam_eff = m + 1;
     __syncthreads();
   }
-  if (!stopped) {
+  if (conc && !have_ulam && tid == 0) publish(progress, FINAL | nlam_eff);
+  if (!stopped && !timed_out) {
     const double dev_cur = accumulate();
     if (tid == 0) dev_out[(int64_t)prob * L + nlam_eff - 1] = 1.0 - dev_cur / dev0;
   }
@@ -431,7 +502,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     if (!have_ulam && nlam_eff >= 3) lm[0] = exp(2.0 * log(lm[1]) - log(lm[2]));
     for (int m = nlam_eff; m < L; ++m) lm[m] = __builtin_nan("");
     nlam_out[prob] = nlam_eff;
-    npass_out[prob] = npass_tot;
+    npass_out[prob] = timed_out ? -1 : npass_tot;
   }
 }
 
@@ -469,15 +540,15 @@ int launch_path(const void* X, int64_t ld, const int* xcols, int p, int ycol, co
                 int nseg, const uint8_t* masks, int nprob, const double* vp, double alpha,
                 double flmin, double thresh, int maxit, const double* ulam, const int* nlam_in,
                 int L, double* a0, double* beta, double* lam, double* dev, int* nlam_out,
-                int* npass, hipStream_t st) {
+                int* npass, int* progress, double* lampub, hipStream_t st) {
   if (p <= 32)
     hipLaunchKernelGGL((lognet_path_kernel<T, 32>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
                        xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
-                       nlam_in, L, a0, beta, lam, dev, nlam_out, npass);
+                       nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   else
     hipLaunchKernelGGL((lognet_path_kernel<T, 96>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
                        xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
-                       nlam_in, L, a0, beta, lam, dev, nlam_out, npass);
+                       nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   return 0;
 }
 
@@ -488,13 +559,17 @@ ATE_API int ate_lognet_path(int dt, const void* X, int64_t ld, const void* xcols
                             const void* segs, int nseg, const void* masks, int nprob,
                             const void* vp, double alpha, double flmin, double thresh, int maxit,
                             const void* ulam, const void* nlam_in, int L, void* a0, void* beta,
-                            void* lam, void* dev, void* nlam_out, void* npass, void* stream) {
+                            void* lam, void* dev, void* nlam_out, void* npass, void* progress,
+                            void* lampub, void* stream) {
   if (p < 1 || p > 96 || nseg > MAXSEG || (dt != 1 && dt != 2)) return -1;
+  // concurrent mode: problem 0 = full fit (own lambda sequence), 1.. = folds, co-resident
+  if (progress && (ulam || nprob < 2 || nprob > 256 || L < 3)) return -1;
   hipStream_t st = (hipStream_t)stream;
   auto f = dt == 2 ? launch_path<double> : launch_path<float>;
   f(X, ld, (const int*)xcols, p, ycol, (const int64_t*)segs, nseg, (const uint8_t*)masks, nprob,
     (const double*)vp, alpha, flmin, thresh, maxit, (const double*)ulam, (const int*)nlam_in, L,
-    (double*)a0, (double*)beta, (double*)lam, (double*)dev, (int*)nlam_out, (int*)npass, st);
+    (double*)a0, (double*)beta, (double*)lam, (double*)dev, (int*)nlam_out, (int*)npass,
+    (int*)progress, (double*)lampub, st);
   ATE_CHECK_LAUNCH();
   return 0;
 }

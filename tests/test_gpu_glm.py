@@ -36,6 +36,28 @@ def test_lognet_cv_gpu_vs_reference(gpu, p, alpha, dtype):
     np.testing.assert_allclose(cv.coef_1se.cpu().numpy(), np.r_[a0, b], atol=1e-7)
 
 
+@pytest.mark.parametrize("p,dtype", [(12, "f64"), (40, "f32")])
+def test_lognet_concurrent_equals_two_launch(gpu, p, dtype):
+    """One-launch form (folds follow the full fit's lambdas through device flags) gives
+    the same bits as the full-then-folds two-launch form."""
+    r = np.random.default_rng(7 + p)
+    n = 4000
+    X = r.normal(size=(n, p))
+    eta = 0.2 + X[:, :3] @ np.array([0.6, -0.4, 0.3])
+    y = (r.uniform(size=n) < 1 / (1 + np.exp(-eta))).astype(float)
+    pan = build_panel(X, None, y, folds=rng.fold_ids(n, 10, 5, 9), dtype=dtype, device=gpu)
+    a = cv_lognet(pan, pan.xcols, pan.cols["Y"], concurrent=True)
+    b = cv_lognet(pan, pan.xcols, pan.cols["Y"], concurrent=False)
+    assert (a.npass.cpu().numpy() >= 0).all()
+    assert torch.equal(a.nlam.cpu(), b.nlam.cpu())
+    assert torch.equal(a.npass.cpu(), b.npass.cpu())
+    m = int(a.nlam[0])
+    for f in ("lambdas", "cvm", "cvsd"):
+        assert torch.equal(getattr(a, f)[:m].cpu(), getattr(b, f)[:m].cpu()), f
+    assert torch.equal(a.coef_path[:m].cpu(), b.coef_path[:m].cpu())
+    assert torch.equal(a.sel.cpu(), b.sel.cpu())
+
+
 def test_propensity_lasso_gpu(gpu, tutorial):
     from ate_replication_causalml_amd.estimators import linear as D
     from ate_replication_causalml_amd.reference import estimators as E
