@@ -76,7 +76,7 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
     """E11 ``belloni`` (ate_functions.R:286-328) with quirks Q10-Q13."""
     dev = resolve_device(device)
     Yn, Wn = as_np(Y), as_np(W)
-    xint = interaction_expand(torch.as_tensor(as_np(X), device=dev)).cpu().numpy()
+    xint = interaction_expand(torch.as_tensor(as_np(X), device=dev))   # stays on the device
     n, q = xint.shape
     fits = []
     for target, stream in ((Wn, 8), (Yn, 9)):
@@ -107,7 +107,9 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
     else:
         cols = sorted(set(np.flatnonzero(bw != 0)) | set(np.flatnonzero(by != 0)))
     # post-selection OLS: y ~ 1 + x_int[:, cols] + W
-    pan = build_panel(np.column_stack([xint[:, cols], Wn]), None, Yn, dtype=dtype, device=dev)
+    sel_x = torch.cat([xint[:, torch.as_tensor(cols, dtype=torch.long, device=xint.device)],
+                       torch.as_tensor(Wn, dtype=torch.float64, device=xint.device)[:, None]], 1)
+    pan = build_panel(sel_x, None, Yn, dtype=dtype, device=dev)
     G = gram(pan)[0]
     if dist is not None:
         dist.sum_(G)

@@ -91,7 +91,15 @@ def build_panel(X, W=None, Y=None, folds=None, dtype="f64", device="cpu", extra_
 
     folds: optional (n,) int fold id -> one padded segment per fold (in fold order).
     extra_cols: names of zero-initialised scratch columns to reserve.
+    X may be a torch tensor (e.g. already in HBM): its fold gather and transposition
+    then run on ``device`` (no host round trip of the n x p block); same values.
     """
+    Xt = None
+    if isinstance(X, torch.Tensor):
+        Xt = X.to(device=device, dtype=torch.float64)
+        if Xt.ndim == 1:
+            Xt = Xt[:, None]
+        X = np.empty(tuple(Xt.shape), dtype=np.float64)     # shape only
     X = np.asarray(X, dtype=np.float64)
     if X.ndim == 1:
         X = X[:, None]
@@ -129,22 +137,35 @@ def build_panel(X, W=None, Y=None, folds=None, dtype="f64", device="cpu", extra_
         rows = order[pos:pos + counts[k]]
         row_index[starts[k]:starts[k] + counts[k]] = rows
         pos += counts[k]
-    host = np.zeros((P, ld), dtype=np.float64)
     m = row_index >= 0
     ri = row_index[m]
+    # host rows: everything but the x block when X is on the device
+    host = np.zeros((P if Xt is None else P - p, ld), dtype=np.float64)
+    hrow = (lambda r: r) if Xt is None else (lambda r: r if r == 0 else r - p)
     host[0, m] = 1.0
-    host[1:1 + p, m] = X[ri].T
+    if Xt is None:
+        host[1:1 + p, m] = X[ri].T
     c = 1 + p
     cols = {n_: i for i, n_ in enumerate(names)}
     for k, v in vecs.items():
-        host[cols[k], m] = v[ri]
+        host[hrow(cols[k]), m] = v[ri]
     if split_hi_lo:
         for k, v in vecs.items():
             hi = torch.from_numpy(v[ri]).to(torch.bfloat16).double().numpy()
             lo = v[ri] - hi
-            host[cols[f"{k}_hi"], m] = hi
-            host[cols[f"{k}_lo"], m] = lo
-    data = torch.from_numpy(host).to(tdt).to(device)
+            host[hrow(cols[f"{k}_hi"]), m] = hi
+            host[hrow(cols[f"{k}_lo"]), m] = lo
+    if Xt is None:
+        data = torch.from_numpy(host).to(tdt).to(device)
+    else:
+        data = torch.empty((P, ld), dtype=tdt, device=device)
+        rest = torch.from_numpy(host).to(tdt).to(device)
+        data[:1] = rest[:1]
+        data[1 + p:] = rest[1:]
+        blk = torch.zeros((p, ld), dtype=torch.float64, device=device)
+        blk[:, torch.from_numpy(np.flatnonzero(m)).to(device)] = \
+            Xt[torch.from_numpy(ri).to(device)].T
+        data[1:1 + p] = blk.to(tdt)
     seg_bounds = np.stack([starts, starts + padded], axis=1)
     return DevicePanel(data=data, n=n, cols=cols, seg_bounds=seg_bounds,
                        seg_nreal=counts.astype(np.int64),

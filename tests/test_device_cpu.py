@@ -37,6 +37,20 @@ def test_panel_layout_fold_contiguous():
     assert np.allclose(back.numpy(), X[:, 1])
 
 
+@pytest.mark.parametrize("dtype", ["f64", "f32", "bf16"])
+def test_panel_from_tensor_equals_host_build(dtype):
+    rs = np.random.RandomState(1)
+    X = rs.randn(300, 7)
+    folds = rs.randint(0, 4, 300)
+    w, y = rs.rand(300), rs.rand(300)
+    a = build_panel(X, w, y, folds=folds, dtype=dtype, device=CPU, extra_cols=("s",))
+    b = build_panel(torch.from_numpy(X), w, y, folds=folds, dtype=dtype, device=CPU,
+                    extra_cols=("s",))
+    assert a.cols == b.cols and a.xcols == b.xcols
+    assert torch.equal(a.data, b.data)
+    assert torch.equal(a.row_index, b.row_index)
+
+
 def test_gram_cpu_matches_numpy():
     rs = np.random.RandomState(1)
     X = rs.randn(200, 5)
