@@ -103,7 +103,9 @@ def test_glmnet_path_satisfies_kkt(seed, alpha):
         res = y - a0 - X @ beta
         grad = ((X - xm) / xs).T @ res / n             # standardized coordinates
         b = beta * xs
-        tol = 2e-3 * max(lam, 1e-3)
+        # coordinate descent stops on an objective-change threshold (1e-7 x null
+        # deviance), so the gradient residual carries an absolute floor near the tail
+        tol = 2e-3 * lam + 5e-5
         for j in range(p):
             if b[j] != 0:
                 want = lam * (alpha * np.sign(b[j]) + (1 - alpha) * b[j] / ys)
