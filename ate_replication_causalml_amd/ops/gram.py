@@ -8,6 +8,7 @@ graph capture) allocate nothing.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import numpy as np
@@ -29,6 +30,20 @@ GRAM_KERNEL = os.environ.get("ATE_GRAM_KERNEL", "pair")
 PAIR_SLOTS = 272
 
 _plan_cache = {}
+_slot = 0
+
+
+@contextlib.contextmanager
+def plan_slot(i: int):
+    """Plans (slab + Gram output buffers) made inside this context are private to slot ``i``,
+    so independent estimator calls captured in separate hipGraphs can be in flight on
+    separate streams at once without sharing a workspace (bench.py --inflight)."""
+    global _slot
+    prev, _slot = _slot, int(i)
+    try:
+        yield
+    finally:
+        _slot = prev
 
 
 def _stream():
@@ -138,7 +153,7 @@ def _pair_tiles(nt: int):
 
 def plan_for(panel: DevicePanel, weighted=False) -> GramPlan:
     key = (panel.data.data_ptr(), tuple(panel.data.shape), panel.data.dtype, weighted,
-           tuple(map(tuple, panel.seg_bounds)))
+           tuple(map(tuple, panel.seg_bounds)), _slot)
     pl = _plan_cache.get(key)
     if pl is None:
         pl = GramPlan(panel, weighted)

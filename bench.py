@@ -33,8 +33,8 @@ import time
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=float, default=1e7,
                     help="rows per GPU (weak scaling) or in total (strong scaling)")
     ap.add_argument("--p", type=int, default=500)
@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1991)
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a hipGraph (default: on for 1 GPU, off with RCCL)")
+    ap.add_argument("--inflight", type=int, default=-1,
+                    help="independent cross-fits in flight (one hipGraph + stream + Gram "
+                         "workspace each); every timed step is still one complete DML-ATE")
     args = ap.parse_args()
 
     import torch
@@ -79,21 +82,39 @@ def main():
 
     from ate_replication_causalml_amd.utils.graphs import maybe_graphed
     use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
-    run, graphed = maybe_graphed(step, use_graph and device.type == "cuda")
+    from ate_replication_causalml_amd.ops.gram import plan_slot
+    inflight = (2 if world == 1 else 1) if args.inflight < 0 else max(1, args.inflight)
+    runs, streams = [], []
+    for i in range(inflight):
+        with plan_slot(i):
+            r, graphed = maybe_graphed(step, use_graph and device.type == "cuda")
+        runs.append(r)
+        streams.append(torch.cuda.Stream(device) if graphed and inflight > 1 else None)
+        if not graphed:
+            break
+
+    def run_step(k):
+        i = k % len(runs)
+        if streams[i] is None:
+            return runs[i]()
+        # the CV path solve is a latency-bound serial recurrence that fills few CUs; a second
+        # cross-fit's HBM-bound Gram runs beside it on its own stream
+        with torch.cuda.stream(streams[i]):
+            return runs[i]()
     import contextlib
     from ate_replication_causalml_amd.utils.guards import collective_timeout
     # a dead peer must end the job with a message, not hang the other ranks in RCCL
     guard = collective_timeout(float(os.environ.get("ATE_COLLECTIVE_TIMEOUT", "900")),
                                "bench step") if world > 1 else contextlib.nullcontext()
     guard.__enter__()
-    for _ in range(args.warmup):
-        res = run()
+    for k in range(args.warmup):
+        res = run_step(k)
     sync()
     comm.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = run()
+    for k in range(args.steps):
+        res = run_step(k)
     sync()
     comm.barrier()
     sync()
@@ -133,6 +154,7 @@ def main():
             "ate": ate,
             "se": se,
             "hipgraph": graphed,
+            "inflight": len(runs),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -233,3 +233,29 @@ def test_dml_bf16_vs_f64_panel(gpu):
 def test_smoke_entry(gpu):
     import __graft_entry__
     __graft_entry__.smoke()
+
+
+def test_dml_two_graphs_in_flight_match_eager(gpu):
+    """bench.py --inflight: two captured cross-fits with private Gram workspaces
+    (ops/gram.plan_slot) replayed concurrently on two streams give the eager result."""
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    from ate_replication_causalml_amd.utils.graphs import GraphedStep
+    pan = synthetic_panel(100000, p=500, folds=5, seed=4, dtype="bf16", device=gpu)
+
+    def step():
+        return dml_crossfit_panel(pan, 5, "min")[0]
+
+    want = step().clone()
+    runs = []
+    for i in range(2):
+        with gram_op.plan_slot(i):
+            runs.append(GraphedStep(step))
+    streams = [torch.cuda.Stream(gpu) for _ in runs]
+    assert runs[0].out.data_ptr() != runs[1].out.data_ptr()
+    for k in range(6):
+        with torch.cuda.stream(streams[k % 2]):
+            runs[k % 2]()
+    torch.cuda.synchronize()
+    for r in runs:
+        torch.testing.assert_close(r.out, want, rtol=0, atol=0)
