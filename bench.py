@@ -84,6 +84,10 @@ def main():
     use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
     from ate_replication_causalml_amd.ops.gram import plan_slot
     inflight = (2 if world == 1 else 1) if args.inflight < 0 else max(1, args.inflight)
+    if inflight > 1:
+        # sharing the chip with the other fit's path solve, fewer and longer Gram workgroups
+        # win (profiles/r01_bench/wg_inflight.log: 1024 -> 5.9 ms/step, 2048 -> 6.1)
+        os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024")
     runs, streams = [], []
     for i in range(inflight):
         with plan_slot(i):
