@@ -199,7 +199,7 @@ def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 
     G = gram(pan).clone()
     K = nfolds
     cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
-                          full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha)
+                          full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha).check()
     masks = _arm_masks(pan, K)
     gam, iters = ipm_balance_panel(pan, masks, target, zeta)
     b = cv.coef_1se.to(torch.float64)                      # [2, p+1]: arm 1, arm 0

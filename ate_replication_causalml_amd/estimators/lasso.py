@@ -45,7 +45,7 @@ def _lasso_w_coef(Y, W, X, pf_w, seed, nfolds, fold_stream, device, dtype, dist=
     G, counts = _sharded_gram(pan, dist)
     pf = np.r_[np.ones(pp - 1), pf_w]
     cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf, seg_counts=counts)
-    return cv
+    return cv.check()
 
 
 def lasso_single(Y, W, X, seed=1991, nfolds=10, fold_stream=5, method="Single-equation LASSO",
@@ -84,7 +84,7 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
         pan = build_panel(xint, None, target, folds=fid, dtype=dtype, device=dev)
         G, counts = _sharded_gram(pan, dist)
         fits.append((pan, G, cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
-                                              seg_counts=counts)))
+                                              seg_counts=counts).check()))
     (_, _, cw), (_, _, cy) = fits
     s = float(cw.lambdas[0, int(cw.sel[0, 0])])
     lw = cw.lambdas[0, :int(cw.nlam[0])].cpu().numpy()
@@ -133,29 +133,66 @@ def global_seg_counts(pan, comm):
     return c.numpy()
 
 
+def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G=None):
+    """The cross-fit DML-PLR step as phases for utils.graphs.SegmentedStep:
+
+    A  per-fold Gram stack (K01)                                   device
+    C01 all-reduce of the Gram stack over row shards               collective (world > 1)
+    B  CV-LASSO paths for 5 folds x {Y, W} + inner CV, lambda.min
+       selection (K08/K09), fused held-out residual moments        device
+    C06 all-reduce of the 7 score moments                          collective (world > 1)
+    C  theta / SE (fp64, on device)                                device
+
+    Every phase maps a state dict to a state dict; device phases touch only tensors
+    whose storage is static across calls, so each can be captured in its own hipGraph
+    while RCCL runs eagerly between them on the same stream."""
+    from ..utils.graphs import Collective
+    dist = comm is not None and comm.world_size > 1
+    if dist and seg_counts is None:
+        seg_counts = global_seg_counts(pan, comm)
+    K = folds
+    full_sets = [[s for s in range(K) if s != k] for k in range(K)]
+    ycols = [pan.cols["Y"], pan.cols["W"]]
+
+    def phase_gram(_):
+        return {"G": gram(pan) if G is None else G}
+
+    def phase_fit(st):
+        cv = cv_enet_gaussian(st["G"], pan, pan.xcols, ycols, full_sets=full_sets,
+                              seg_counts=seg_counts)
+        coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1).contiguous()
+        return {**st, "cv": cv, "mom": dml_residual_moments(pan, coef)}
+
+    def phase_final(st):
+        return {**st, "res": S.dml_finalize(st["mom"], "plr")}
+
+    def reduce(name):
+        def f(st):
+            comm.all_reduce_(st[name])
+            return st
+        return Collective(f)
+
+    phases = [phase_gram]
+    if dist:
+        phases.append(reduce("G"))
+    phases.append(phase_fit)
+    if dist:
+        phases.append(reduce("mom"))
+    phases.append(phase_final)
+    return phases
+
+
 def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, seg_counts=None):
     """DML-PLR on a fold-segmented panel (segment k = fold k). Returns (res[2], moments[7], cv).
 
     comm: optional parallel.comm.Communicator — each rank holds a row shard of every
     fold; the fold Gram stack and the score moments are all-reduced (C01, C06).
-    seg_counts: global rows per fold (computed with one all-reduce when omitted)."""
-    if G is None:
-        G = gram(pan)
-    dist = comm is not None and comm.world_size > 1
-    if dist:
-        comm.all_reduce_(G)
-        if seg_counts is None:
-            seg_counts = global_seg_counts(pan, comm)
-    K = folds
-    full_sets = [[s for s in range(K) if s != k] for k in range(K)]
-    ycols = [pan.cols["Y"], pan.cols["W"]]
-    cv = cv_enet_gaussian(G, pan, pan.xcols, ycols, full_sets=full_sets, seg_counts=seg_counts)
-    coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1).contiguous()
-    mom = dml_residual_moments(pan, coef)
-    if comm is not None and comm.world_size > 1:
-        comm.all_reduce_(mom)
-    res = S.dml_finalize(mom, "plr")
-    return res, mom, cv
+    seg_counts: global rows per fold (computed with one all-reduce when omitted).
+    A truncated CV fold path NaN-poisons res (ops/enet.poison_if_truncated)."""
+    st = None
+    for ph in dml_phases(pan, folds, lambda_rule, comm, seg_counts, G):
+        st = ph(st)
+    return st["res"], st["mom"], st["cv"]
 
 
 def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:

@@ -74,7 +74,7 @@ def propensity_lasso(W, X, seed=1991, nfolds=10, fold_stream=7, device=None, dty
     Wn = as_np(W)
     fid = rng.fold_ids(len(Wn), nfolds, seed, fold_stream)
     pan = build_panel(as_np(X), None, Wn, folds=fid, dtype=dtype, device=dev)
-    cv = cv_lognet(pan, pan.xcols, pan.cols["Y"])
+    cv = cv_lognet(pan, pan.xcols, pan.cols["Y"]).check()
     cols = [pan.cols["one"], *pan.xcols]
     mu = predict(pan, cols, cv.coef_1se.to(dev, torch.float64).contiguous(), link="logit")
     return pan.scatter_rows(mu)

@@ -13,6 +13,8 @@ import hashlib
 import numpy as np
 import torch
 
+from ..utils.graphs import pin
+
 _CACHE: dict = {}
 _MAX = 4096
 
@@ -29,7 +31,8 @@ def const(values, dtype, device) -> torch.Tensor:
             _CACHE.clear()
         t = torch.as_tensor(a).to(device=dev, dtype=dtype)
         _CACHE[key] = t
-    return t
+    # a graph capturing this constant keeps it alive even if the cache is cleared later
+    return pin(t)
 
 
 def const_bytes(raw: np.ndarray, device) -> torch.Tensor:

@@ -38,7 +38,28 @@ class EnetCvResult:
     coef_min: torch.Tensor    # [nfull, p+1]
     coef_1se: torch.Tensor    # [nfull, p+1]
     full_keys: list           # (full set index, y index) per full problem
-    npass: torch.Tensor
+    npass: torch.Tensor       # [nfull] passes of the full-data problems
+    fold_npass: torch.Tensor | None = None   # [nfold] (< 0: the fold's wait timed out)
+
+    def check(self):
+        """Raise NumericalError if any fold path was truncated (host sync). The device
+        results are already NaN-poisoned in that case, so graph replays that never call
+        this still cannot return a silently different lambda selection."""
+        bad = [] if self.fold_npass is None else \
+            np.flatnonzero(self.fold_npass.cpu().numpy() < 0).tolist()
+        if bad:
+            from ..utils.guards import NumericalError
+            raise NumericalError(f"CV fold path(s) {bad} timed out waiting for their "
+                                 "full-data lambda sequence; selection is invalid")
+        return self
+
+
+def poison_if_truncated(fold_npass: torch.Tensor, *ts):
+    """NaN every tensor in ``ts`` when any fold path of the launch was truncated
+    (device-side, capturable: no host sync)."""
+    bad = (fold_npass < 0).any()
+    nan = torch.full((), float("nan"), dtype=torch.float64, device=fold_npass.device)
+    return [torch.where(bad, nan, t) for t in ts]
 
 
 def _rescale_vp(vp, p):
@@ -195,8 +216,12 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
                  cmin.data_ptr(), s)
     _native.call("ate_enet_pick", coef.data_ptr(), sel.data_ptr(), 1, p, L, nf,
                  c1se.data_ptr(), s)
+    # a fold whose spin on its source's progress flag timed out (npass = -1; csrc/enet.hip)
+    # has a truncated path: cvm, and so lambda.min / lambda.1se, would silently change
+    fold_npass = npass[nf:]
+    cvm, cvsd, cmin, c1se = poison_if_truncated(fold_npass, cvm, cvsd, cmin, c1se)
     return EnetCvResult(lams[:nf], nlam[:nf], cvm, cvsd, sel, coef[:nf], cmin, c1se, full_keys,
-                        npass[:nf])
+                        npass[:nf], fold_npass)
 
 
 def _cv_cpu(G, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_probs, fold_ycol, fold_holds,

@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from ..utils.graphs import pin
 from .panel import DevicePanel
 
 BF16_TILE, BF16_K = 128, 64
@@ -28,8 +29,9 @@ TARGET_WG = 2048   # workgroups per launch (>= 8 per CU on 256 CUs)
 # stages fetch half cache lines; profiles/r01_pmc/gram_variant*.txt.)
 GRAM_KERNEL = os.environ.get("ATE_GRAM_KERNEL", "pair")
 PAIR_SLOTS = 272
+PLAN_CACHE_MAX = int(os.environ.get("ATE_GRAM_PLAN_CACHE", 8))
 
-_plan_cache = {}
+_plan_cache: dict = {}
 _slot = 0
 
 
@@ -152,13 +154,25 @@ def _pair_tiles(nt: int):
 
 
 def plan_for(panel: DevicePanel, weighted=False) -> GramPlan:
+    """Cached launch plan + workspace. The cache is an LRU of ``PLAN_CACHE_MAX`` entries
+    (a bf16 plan at N=1e7 holds ~0.5 GB of slab): evicting drops only the cache's
+    reference, and a hipGraph that captured the plan keeps it alive (utils/graphs.pin).
+    Keyed by the panel's address too: the plan owns the returned Gram buffer, and two
+    live panels of one shape must not share it."""
     key = (panel.data.data_ptr(), tuple(panel.data.shape), panel.data.dtype, weighted,
            tuple(map(tuple, panel.seg_bounds)), _slot)
-    pl = _plan_cache.get(key)
+    pl = _plan_cache.pop(key, None)
     if pl is None:
+        while len(_plan_cache) >= PLAN_CACHE_MAX:
+            _plan_cache.pop(next(iter(_plan_cache)))
         pl = GramPlan(panel, weighted)
-        _plan_cache[key] = pl
-    return pl
+    _plan_cache[key] = pl          # most recently used last
+    return pin(pl)
+
+
+def clear_plans():
+    """Drop every cached Gram plan (graphs that captured one keep theirs alive)."""
+    _plan_cache.clear()
 
 
 def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor | None = None,

@@ -28,7 +28,17 @@ class LognetCvResult:
     coef_path: torch.Tensor  # [L, p+1] original scale, intercept first
     coef_min: torch.Tensor   # [p+1]
     coef_1se: torch.Tensor
-    npass: torch.Tensor
+    npass: torch.Tensor      # [1 + K]: full fit, then the K fold fits (< 0: wait timed out)
+
+    def check(self):
+        """Raise NumericalError if a fold fit was truncated (its wait for the full fit's
+        lambda timed out). Device outputs are NaN-poisoned in that case already."""
+        bad = np.flatnonzero(self.npass.cpu().numpy()[1:] < 0).tolist()
+        if bad:
+            from ..utils.guards import NumericalError
+            raise NumericalError(f"binomial CV fold fit(s) {bad} timed out waiting for the "
+                                 "full fit's lambda sequence; selection is invalid")
+        return self
 
 
 def _rescale_vp(vp, p):
@@ -112,8 +122,10 @@ def cv_lognet(panel, xcols, ycol, penalty_factor=None, alpha=1.0, nlambda=100,
                  nlam.data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), s)
     coef = torch.cat([a0[0][:, None], beta[0]], 1)
     sl = sel[0].long()
-    return LognetCvResult(lam[0], nlam[:1], cvm[0], cvsd[0], sel[0], coef, coef[sl[0]],
-                          coef[sl[1]], npass)
+    from .enet import poison_if_truncated
+    cvm0, cvsd0, cmin, c1se = poison_if_truncated(npass[1:], cvm[0], cvsd[0], coef[sl[0]],
+                                                  coef[sl[1]])
+    return LognetCvResult(lam[0], nlam[:1], cvm0, cvsd0, sel[0], coef, cmin, c1se, npass)
 
 
 def _cv_cpu(panel, xcols, ycol, vp, alpha, nlambda, flmin, thresh, maxit):

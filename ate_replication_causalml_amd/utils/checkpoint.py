@@ -18,18 +18,15 @@ import numpy as np
 
 
 def fingerprint(*arrays) -> str:
-    h = hashlib.sha256()
+    """Content hash of every byte of every array (blake2b, ~1 GB/s: negligible next to a
+    fit). Any edit to the data changes the key, so stale predictions are never reloaded."""
+    h = hashlib.blake2b(digest_size=16)
     for a in arrays:
         a = np.ascontiguousarray(np.asarray(a))
         h.update(str(a.shape).encode())
         h.update(str(a.dtype).encode())
-        # strided sample + full sums: cheap for 1e7-row panels, sensitive to edits
-        flat = a.reshape(-1)
-        step = max(1, flat.size // 65536)
-        h.update(flat[::step].tobytes())
-        if flat.dtype.kind in "fiu":
-            h.update(np.float64(flat.astype(np.float64).sum()).tobytes())
-    return h.hexdigest()[:16]
+        h.update(memoryview(a.reshape(-1).view(np.uint8)))
+    return h.hexdigest()
 
 
 class Checkpoint:

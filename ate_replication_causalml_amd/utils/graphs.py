@@ -10,21 +10,46 @@ graph launch. Iterative solvers in the step use fixed launch budgets with device
 convergence flags (ops/linalg.logistic_irls), so nothing in them needs the host.
 ``fn`` must return tensors; they are the graph's static outputs (overwritten on
 every replay).
+
+A graph holds raw device addresses of every workspace it touched. Caches that can
+evict (Gram plans, device constants) call :func:`pin` for each object they hand out;
+during a capture the object is appended to the capturing step's pin list, so an
+eviction only drops the cache's reference and the memory lives as long as the graph.
+
+``SegmentedStep`` is the multi-GPU form: a list of phases, each either a device-only
+callable (captured in its own graph) or a collective (run eagerly between replays on
+the same stream). RCCL collectives then stay outside the captured graphs, so capture
+is a purely local operation that succeeds or fails identically on every rank.
 """
 from __future__ import annotations
 
 import torch
 
+_pins: list | None = None
+
+
+def pin(obj):
+    """Keep ``obj`` alive for the lifetime of the graph being captured (no-op otherwise)."""
+    if _pins is not None:
+        _pins.append(obj)
+    return obj
+
 
 class GraphedStep:
     def __init__(self, fn, warmup: int = 1):
+        global _pins
         self.fn = fn
         for _ in range(warmup):
             fn()
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = fn()
+        prev, _pins = _pins, []
+        try:
+            with torch.cuda.graph(self.graph):
+                self.out = fn()
+            self.pins = _pins
+        finally:
+            _pins = prev
         torch.cuda.synchronize()
 
     def __call__(self):
@@ -42,3 +67,99 @@ def maybe_graphed(fn, enable: bool, warmup: int = 1):
         print(f"[graphs] capture failed, running eagerly: {e}", flush=True)
         torch.cuda.synchronize()
         return fn, False
+
+
+class Collective:
+    """Marks a phase of a :class:`SegmentedStep` that must run eagerly (an RCCL call)."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def __call__(self, state):
+        return self.fn(state)
+
+
+def _fuse(phases):
+    """Merge runs of consecutive device phases into one phase (one graph per run: with
+    no collectives in between, e.g. world size 1, the whole step is a single graph)."""
+    out, run = [], []
+
+    def flush():
+        if run:
+            fns = tuple(run)
+
+            def composed(st, fns=fns):
+                for f in fns:
+                    st = f(st)
+                return st
+            out.append(composed)
+            run.clear()
+
+    for ph in phases:
+        if isinstance(ph, Collective):
+            flush()
+            out.append(ph)
+        else:
+            run.append(ph)
+    flush()
+    return out
+
+
+class SegmentedStep:
+    """A step split into phases ``fn(state) -> state``. Device phases are captured in one
+    graph each (when ``graph``), :class:`Collective` phases run eagerly on the current
+    stream between replays. ``state`` is whatever the phases pass along (tensors whose
+    storage is static across calls: graph outputs are overwritten in place on replay).
+
+    Capture runs the phases ``warmup`` times eagerly first (populating plans and
+    constants), then captures each device phase given the state produced by the phases
+    before it. The step's result is the last phase's state."""
+
+    def __init__(self, phases, graph: bool, warmup: int = 1):
+        global _pins
+        self.phases = _fuse(phases)
+        self.graphs = [None] * len(self.phases)
+        self.pins = []
+        for _ in range(warmup):
+            self._eager()
+        if not graph:
+            return
+        torch.cuda.synchronize()
+        state = None
+        for i, ph in enumerate(self.phases):
+            if isinstance(ph, Collective):
+                state = ph(state)
+                continue
+            g = torch.cuda.CUDAGraph()
+            prev, _pins = _pins, []
+            try:
+                with torch.cuda.graph(g):
+                    out = ph(state)
+                self.pins += _pins
+            finally:
+                _pins = prev
+            self.graphs[i] = (g, out)
+            torch.cuda.synchronize()
+            g.replay()          # capture does not execute: produce the state for later phases
+            state = out
+        torch.cuda.synchronize()
+
+    @property
+    def graphed(self) -> bool:
+        return any(g is not None for g in self.graphs)
+
+    def _eager(self):
+        state = None
+        for ph in self.phases:
+            state = ph(state)
+        return state
+
+    def __call__(self):
+        state = None
+        for ph, g in zip(self.phases, self.graphs):
+            if g is None:
+                state = ph(state)
+            else:
+                g[0].replay()
+                state = g[1]
+        return state

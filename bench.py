@@ -11,6 +11,11 @@ fused held-out residual pass + orthogonal-score moments (csrc/dml.hip) ->
 all-reduce of the moments (C06) -> theta / SE on device.
 Nothing is cached across steps; every nuisance is refit each step.
 
+Two cross-fits are in flight at every world size (``--inflight 2``): ``ms_per_step`` is
+the wall time per completed cross-fit (throughput); ``single_fit_ms`` in the JSON is the
+latency of one cross-fit alone. With RCCL the device phases are still graph replays;
+only the two all-reduces run eagerly between them (utils/graphs.SegmentedStep).
+
 Scaling: weak by default (N=1e7 rows per GPU; at N=1 GPU this is exactly the
 BASELINE config); ``--scaling strong`` keeps N=1e7 in total.
 
@@ -25,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -47,7 +53,8 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--seed", type=int, default=1991)
     ap.add_argument("--graph", type=int, default=-1,
-                    help="capture the step in a hipGraph (default: on for 1 GPU, off with RCCL)")
+                    help="capture the step's device phases in hipGraphs (default: on with a GPU; "
+                         "RCCL collectives always run eagerly between the graph replays)")
     ap.add_argument("--inflight", type=int, default=-1,
                     help="independent cross-fits in flight (one hipGraph + stream + Gram "
                          "workspace each); every timed step is still one complete DML-ATE")
@@ -76,35 +83,65 @@ def main():
 
     seg_counts = global_seg_counts(pan, comm)   # fold sizes: data layout, fixed across steps
 
-    def step():
-        res, _, _ = dml_crossfit_panel(pan, args.folds, "min", comm=comm, seg_counts=seg_counts)
-        return res
-
-    from ate_replication_causalml_amd.utils.graphs import maybe_graphed
-    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    from ate_replication_causalml_amd.estimators.lasso import dml_phases
+    from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
     from ate_replication_causalml_amd.ops.gram import plan_slot
-    inflight = (2 if world == 1 else 1) if args.inflight < 0 else max(1, args.inflight)
+    use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
+    # Two independent cross-fits in flight at EVERY world size (same setting for the whole
+    # 1/2/4/8 curve): the CV path solve is a latency-bound serial recurrence that fills few
+    # CUs, so a second fit's HBM-bound Gram runs beside it on its own stream.
+    inflight = 2 if args.inflight < 0 else max(1, args.inflight)
     if inflight > 1:
         # sharing the chip with the other fit's path solve, fewer and longer Gram workgroups
         # win (profiles/r01_bench/wg_inflight.log: 1024 -> 5.9 ms/step, 2048 -> 6.1)
         os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024")
-    runs, streams = [], []
+
+    def in_slot(ph, i):
+        if isinstance(ph, Collective):
+            return ph
+
+        def f(st):
+            with plan_slot(i):  # eager calls too: never share another fit's workspace
+                return ph(st)
+        return f
+
+    def make_run(i):
+        # device phases captured one hipGraph each; RCCL collectives (world > 1) run
+        # eagerly between the replays, so capture is local and identical on every rank
+        with plan_slot(i):      # private Gram workspace per in-flight fit
+            phases = [in_slot(ph, i) for ph in
+                      dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts)]
+            try:
+                return SegmentedStep(phases, graph=use_graph), None
+            except Exception as e:  # noqa: BLE001 - reported, then every rank goes eager
+                torch.cuda.synchronize()
+                return SegmentedStep(phases, graph=False, warmup=0), repr(e)
+
+    runs, errors = [], []
     for i in range(inflight):
-        with plan_slot(i):
-            r, graphed = maybe_graphed(step, use_graph and device.type == "cuda")
+        r, err = make_run(i)
         runs.append(r)
-        streams.append(torch.cuda.Stream(device) if graphed and inflight > 1 else None)
-        if not graphed:
-            break
+        errors.append(err)
+    ok = torch.tensor([float(all(r.graphed for r in runs) if use_graph else 0)], device=device)
+    comm.all_reduce_min_(ok)
+    graphed = bool(ok.item())
+    if use_graph and not graphed:
+        # every rank falls back the same way: one eager fit at a time under slot 0's plan
+        print(f"[bench] rank {rank}: graph capture unavailable ({errors}); eager, inflight 1",
+              flush=True)
+        with plan_slot(0):
+            runs = [SegmentedStep(dml_phases(pan, args.folds, "min", comm=comm,
+                                             seg_counts=seg_counts), graph=False, warmup=0)]
+    streams = [torch.cuda.Stream(device) if device.type == "cuda" and len(runs) > 1 else None
+               for _ in runs]
 
     def run_step(k):
         i = k % len(runs)
         if streams[i] is None:
-            return runs[i]()
-        # the CV path solve is a latency-bound serial recurrence that fills few CUs; a second
-        # cross-fit's HBM-bound Gram runs beside it on its own stream
+            return runs[i]()["res"]
         with torch.cuda.stream(streams[i]):
-            return runs[i]()
+            return runs[i]()["res"]
+
     import contextlib
     from ate_replication_causalml_amd.utils.guards import collective_timeout
     # a dead peer must end the job with a message, not hang the other ranks in RCCL
@@ -128,9 +165,21 @@ def main():
         import torch.distributed as dist
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    # latency of ONE cross-fit alone (no overlap): reported beside the throughput number
+    nlat = max(1, min(args.steps, 10))
+    sync()
+    t1 = time.perf_counter()
+    for k in range(nlat):
+        runs[0]()
+        sync()
+    lat = torch.tensor([(time.perf_counter() - t1) / nlat], dtype=torch.float64, device=device)
+    comm.all_reduce_max_(lat)
     guard.__exit__(None, None, None)
     ms = elapsed / args.steps * 1e3
     ate, se = [float(v) for v in res.detach().cpu()]
+    if not (math.isfinite(ate) and math.isfinite(se)):
+        from ate_replication_causalml_amd.utils.guards import NumericalError
+        raise NumericalError(f"bench step returned ate={ate} se={se} (truncated CV fold path?)")
     rows_per_s = n_total / (ms / 1e3)
     if rank == 0:
         out = {
@@ -154,11 +203,13 @@ def main():
                 "p": args.p,
                 "folds": args.folds,
                 "parallelism": f"dp{world}",
+                "inflight": len(runs),
             },
             "ate": ate,
             "se": se,
             "hipgraph": graphed,
             "inflight": len(runs),
+            "single_fit_ms": float(lat.item()) * 1e3,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

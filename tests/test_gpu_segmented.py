@@ -1,0 +1,70 @@
+"""The multi-GPU bench step on one MI355X: device phases captured in hipGraphs, RCCL
+all-reduces run eagerly between the replays (utils/graphs.SegmentedStep), two fits in
+flight on two streams with private Gram workspaces. RCCL is real (a world-1 ``nccl``
+process group); the communicator reports world 2 so both collectives are in the step."""
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class _WideComm:
+    """Real RCCL collectives on a 1-rank group, reported as world 2 so dml_phases inserts
+    the C01 / C06 all-reduce phases (a sum over one rank is the identity)."""
+    rank = 0
+    world_size = 2
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    def all_reduce_(self, t):
+        return self.inner.all_reduce_(t)
+
+    def all_reduce_min_(self, t):
+        return self.inner.all_reduce_min_(t)
+
+    def barrier(self):
+        self.inner.barrier()
+
+
+@pytest.fixture(scope="module")
+def rccl(gpu):
+    import torch.distributed as dist
+    from ate_replication_causalml_amd.parallel.comm import TorchComm
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=gpu)
+    yield _WideComm(TorchComm())
+    dist.destroy_process_group()
+
+
+def test_segmented_graphs_with_rccl_match_eager(gpu, rccl):
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel, dml_phases
+    from ate_replication_causalml_amd.ops import gram as gram_op
+    from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
+    import numpy as np
+    pan = synthetic_panel(100000, p=500, folds=5, seed=4, dtype="bf16", device=gpu)
+    seg = np.asarray(pan.seg_nreal, dtype=np.float64)
+    want = dml_crossfit_panel(pan, 5, "min")[0].clone()
+    runs = []
+    for i in range(2):
+        with gram_op.plan_slot(i):
+            ph = dml_phases(pan, 5, "min", comm=rccl, seg_counts=seg)
+            assert sum(isinstance(p, Collective) for p in ph) == 2
+            runs.append(SegmentedStep(ph, graph=True))
+    assert all(r.graphed for r in runs)
+    streams = [torch.cuda.Stream(gpu) for _ in runs]
+    outs = [None, None]
+    for k in range(6):
+        with torch.cuda.stream(streams[k % 2]):
+            outs[k % 2] = runs[k % 2]()["res"]
+    torch.cuda.synchronize()
+    assert outs[0].data_ptr() != outs[1].data_ptr()
+    for o in outs:
+        torch.testing.assert_close(o, want, rtol=0, atol=0)
