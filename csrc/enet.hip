@@ -18,6 +18,8 @@
 //  select:   cvm, cvsd, lambda.min, lambda.1se with glmnet's rules.
 #include "common.hpp"
 
+#include <type_traits>
+
 using namespace ate;
 
 // ------------------------------------------------------------------ prepare
@@ -148,9 +150,9 @@ constexpr int PMAX = 512;
 #ifdef ENET_PROF
 // cycle accounting per problem (debug builds): [0] pull, [1] recurrence, [2] other,
 // [3] block visits, [4] coordinate updates, [5] pending columns pulled, [6] passes
-__device__ unsigned long long enet_prof[256][16];
+__device__ unsigned long long enet_prof[256][24];
 #define PROF_T(var) const unsigned long long var = wall_clock64()
-#define PROF_ADD(k, v) do { if (tid == 0) atomicAdd(&enet_prof[q][k], (unsigned long long)(v)); } while (0)
+#define PROF_ADD(k, v) do { if (tid == 0) sprof[0][k] += (unsigned long long)(v); } while (0)
 #else
 #define PROF_T(var)
 #define PROF_ADD(k, v) do { } while (0)
@@ -174,6 +176,23 @@ __device__ __forceinline__ double readlane_d(double v, int i) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), i);
   int hi = __builtin_amdgcn_readlane(__double2hiint(v), i);
   return __hiloint2double(hi, lo);
+}
+
+// a = (lane == i) ? b : a and c = (lane == i) ? d : c for a compile-time lane i
+__device__ __forceinline__ void select_lane(int i, int lane, double& a, double b, double& c, double d) {
+  int a0 = __double2loint(a), a1 = __double2hiint(a), c0 = __double2loint(c), c1 = __double2hiint(c);
+  asm volatile(
+      "v_cmp_eq_u32_e32 vcc, %4, %5\n\t"
+      "v_cndmask_b32_e32 %0, %0, %6, vcc\n\t"
+      "v_cndmask_b32_e32 %1, %1, %7, vcc\n\t"
+      "v_cndmask_b32_e32 %2, %2, %8, vcc\n\t"
+      "v_cndmask_b32_e32 %3, %3, %9, vcc"
+      : "+v"(a0), "+v"(a1), "+v"(c0), "+v"(c1)
+      : "i"(i), "v"(lane), "v"(__double2loint(b)), "v"(__double2hiint(b)), "v"(__double2loint(d)),
+        "v"(__double2hiint(d))
+      : "vcc");
+  a = __hiloint2double(a1, a0);
+  c = __hiloint2double(c1, c0);
 }
 
 // Blocked covariance-mode coordinate descent, ONE WAVE per problem.
@@ -203,6 +222,16 @@ __device__ __forceinline__ double readlane_d(double v, int i) {
 #define ENET_NW 8   // waves per problem: wave 0 = recurrence, waves 1.. = pulls
 #endif
 constexpr int NW = ENET_NW, NTH = NW * 64, NP = NW - 1;
+static_assert(NW >= 3, "phase B uses wave 1 for block tn and waves 2.. for snapshots");
+#ifndef ENET_BALLOT_ONLY
+#define ENET_BALLOT_ONLY 0   // 1: every pass uses the ballot recurrence (A/B timing)
+#endif
+#ifndef ENET_PULL_DENSE      // pull a whole 64-row column block when at least this many of
+#define ENET_PULL_DENSE 32   //   its coordinates are pending, else a compacted row list
+#endif
+#ifndef ENET_DENSE_MIN       // dense (all 64 lanes, static) walk of a block when at least
+#define ENET_DENSE_MIN 28    //   this many lanes move: nonzero lanes (full pass) /
+#endif                       //   eligible lanes (active pass)
 
 template <typename CT>
 __global__ __launch_bounds__(NTH) void enet_path_kernel(
@@ -217,6 +246,17 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
   __shared__ int sflag[PMAX];             // bit0 ju, bit1 active
   __shared__ double spart[NW][64];
+  __shared__ __attribute__((aligned(16))) float sred[NW][256];   // group reduction per wave
+  __shared__ __attribute__((aligned(16))) float sdw[NW][64];     // pull_block deltas per wave
+  __shared__ int srow[NW][64];                                   // pull_block row lists
+  __shared__ float scorr[NP][64];         // phase B1: own-delta correction partials
+#ifdef ENET_PROF
+  // per-wave cycle accumulators in LDS (lane 0 of a wave adds to its own row), flushed to
+  // enet_prof once at kernel end: no global atomics (and their vmcnt waits at barriers)
+  // inside the visit loop
+  __shared__ unsigned long long sprof[NW][24];
+  for (int e = threadIdx.x; e < NW * 24; e += blockDim.x) (&sprof[0][0])[e] = 0ull;
+#endif
   __shared__ __attribute__((aligned(16))) CT sdelta[PMAX];
   __shared__ int slist[PMAX];             // compacted pending columns (per-wave quarters)
   constexpr int PER = (PMAX + NP - 1) / NP + 1;   // pending entries per pull wave
@@ -230,6 +270,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ int svis[8], snv, sblk_any[8];
   __shared__ double sdl;
   __shared__ int sany;
+  __shared__ int schg;                    // wave 0: some coordinate of block t moved
   __shared__ double slam;
   __shared__ int savail;
   int q;
@@ -268,36 +309,123 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   float dg_lo[32], dg_hi[32];
 
   // bring block t's gradient up to date (all waves); stage its diagonal block.
-  // Sparse pull: only coordinates changed since block t's snapshot contribute, and by
-  // symmetry coordinate j's contribution is the contiguous row segment C[j][t*64 .. +63].
-  // Each wave compacts the nonzero pending deltas of its quarter of the columns (ordered
-  // ballot) and streams those segments; then it loads 16 rows of the 64x64 diagonal block.
-  auto pull = [&](int t) {
+  // By symmetry coordinate j's contribution is the contiguous row segment C[j][t*64 .. +63].
+  // fp32 C: dense pull, one column block per wave (pull_block). fp64 C: sparse pull, each
+  // wave compacts the nonzero pending deltas of its share of the columns (ordered ballot)
+  // and streams those segments. Wave 0 then loads its row of the 64x64 diagonal block.
+  // Pull of column block jb into block tb (fp32 C):  sum_j C[j][tb*64 + r] * D_j over the
+  // 64 coordinates j of block jb, D_j = Dcum_j - Dsnap_tb,j (zero for unchanged j). The
+  // pull is bound by the CU's vector-memory bandwidth, so only rows with D_j != 0 are
+  // fetched: none (block skipped), a compacted list (< ENET_PULL_DENSE of them), or the
+  // whole 64-row block. 16-byte loads: one wave instruction fetches 4 row segments (lane
+  // group g = lane/16, 4 columns per lane). Returns the sum for row r = lane (the 4 lane
+  // groups combined through the wave's `sred` area).
+  auto pull_block = [&](int jb, int tb) __attribute__((always_inline)) -> float {
+    const int grp = lane >> 4, c4 = (lane & 15) * 4;
+    const int j = jb * 64 + lane;
+    const double ddj = sdc[j] - sds[tb][j];
+    const uint64_t nzb = __builtin_amdgcn_ballot_w64(ddj != 0.0);
+    if (!nzb) return 0.f;
+    const int n = __popcll(nzb);
+    const float* Cf = reinterpret_cast<const float*>(Cq) + tb * 64 + c4;
+    float* dw = sdw[wid];
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto fma4 = [&](float4 w, float d) __attribute__((always_inline)) {
+      a.x += w.x * d;
+      a.y += w.y * d;
+      a.z += w.z * d;
+      a.w += w.w * d;
+    };
+    if (n >= ENET_PULL_DENSE) {
+      const int r0 = jb * 64 + grp * 16;
+      float4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int r = min(r0 + u, p - 1);  // rows >= p: finite data, zero delta
+        v[u] = *reinterpret_cast<const float4*>(Cf + (int64_t)r * ldc);
+      }
+      dw[lane] = (float)ddj;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 d4 = *reinterpret_cast<const float4*>(dw + grp * 16 + 4 * k);
+        fma4(v[4 * k + 0], d4.x);
+        fma4(v[4 * k + 1], d4.y);
+        fma4(v[4 * k + 2], d4.z);
+        fma4(v[4 * k + 3], d4.w);
+      }
+    } else {
+      int* rw = srow[wid];
+      const int pos = __popcll(nzb & ((1ull << lane) - 1ull));
+      if (ddj != 0.0) {
+        rw[pos] = j;
+        dw[pos] = (float)ddj;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int NS = (ENET_PULL_DENSE + 3) / 4;
+      float4 v[NS];
+      float dv[NS];
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        if (4 * u < n) {                     // uniform
+          const int idx = 4 * u + grp;
+          const bool ok = idx < n;
+          const int ix = ok ? idx : 0;
+          v[u] = *reinterpret_cast<const float4*>(Cf + (int64_t)rw[ix] * ldc);
+          dv[u] = ok ? dw[ix] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NS; ++u)
+        if (4 * u < n) fma4(v[u], dv[u]);
+    }
+    float* red = sred[wid];
+    *reinterpret_cast<float4*>(red + grp * 64 + c4) = a;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]);
+  };
+
+  auto pull = [&](int t) __attribute__((always_inline)) {
     const int c0 = wid * cw;
     int cnt = 0;
-    for (int base = c0; base < c0 + cw; base += 64) {
-      const int j = base + lane;
-      const bool inq = j < c0 + cw;       // cw < 64 when p is small
-      const double dj = inq ? sdc[j] - sds[t][j] : 0.0;
-      const bool nz = dj != 0.0;
-      const uint64_t bal = __ballot(nz);
-      const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
-      if (nz) { slist[c0 + pos] = j; sdelta[c0 + pos] = (CT)dj; }
-      cnt += __popcll(bal);
+    if constexpr (sizeof(CT) != 4) {
+      for (int base = c0; base < c0 + cw; base += 64) {
+        const int j = base + lane;
+        const bool inq = j < c0 + cw;     // cw < 64 when p is small
+        const double dj = inq ? sdc[j] - sds[t][j] : 0.0;
+        const bool nz = dj != 0.0;
+        const uint64_t bal = __ballot(nz);
+        const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+        if (nz) { slist[c0 + pos] = j; sdelta[c0 + pos] = (CT)dj; }
+        cnt += __popcll(bal);
+      }
     }
-    const CT* colt = Cq + t * 64 + lane;
     CT acc = 0;
-    int e = 0;
-    for (; e + 16 <= cnt; e += 16) {
-      CT v[16];
+    if constexpr (sizeof(CT) == 4) {
+      // every column block but t itself (its own changes are already in g_t): wave w
+      // takes the w-th of them
+      const int jb = wid + (wid >= t ? 1 : 0);
+      if (jb < T) acc = pull_block(jb, t);
+    } else {
+      const CT* colt = Cq + t * 64 + lane;
+      int e = 0;
+      for (; e + 16 <= cnt; e += 16) {
+        CT v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = colt[(int64_t)slist[c0 + e + u] * ldc];
+        for (int u = 0; u < 16; ++u) v[u] = colt[(int64_t)slist[c0 + e + u] * ldc];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u] * sdelta[c0 + e + u];
+        for (int u = 0; u < 16; ++u) acc += v[u] * sdelta[c0 + e + u];
+      }
+      for (; e < cnt; ++e) acc += colt[(int64_t)slist[c0 + e] * ldc] * sdelta[c0 + e];
     }
-    for (; e < cnt; ++e) acc += colt[(int64_t)slist[c0 + e] * ldc] * sdelta[c0 + e];
 #ifdef ENET_PROF
-    if (lane == 0) atomicAdd(&enet_prof[q][5], (unsigned long long)cnt);
+    if (lane == 0) sprof[wid][5] += (unsigned long long)cnt;
 #endif
     // wave 0 (the recurrence) keeps its lane's row of the 64x64 diagonal block in
     // registers: dg_lo[i] / dg_hi[i-32] = C[t*64+lane][t*64+i] (uniform-index reads
@@ -341,14 +469,14 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // pending for block tn (sdc is frozen until the first barrier) and stage tn's diagonal
   // block in LDS. After the barrier wave 0 publishes block t, completes block tn's
   // gradient and snapshot, and moves tn's diagonal block into registers.
-  auto pull_rest = [&](int t, int tn) {     // waves 1..NW-1
+  auto pull_rest = [&](int t, int tn) __attribute__((always_inline)) {     // waves 1..NW-1
     const int my = wid - 1;
+    CT acc = 0;
     if constexpr (sizeof(CT) == 4) {
       // fp32 C: tn's diagonal block and the (t rows x tn cols) block that wave 0 needs
       // for block t's own deltas go global -> LDS by DMA (16 B per lane = 4 row segments
-      // of 64 floats per wave instruction), issued first so their latency overlaps the
-      // pending-column gathers below: one memory round trip per visit. Rows >= p are
-      // clamped (finite) and masked where used.
+      // of 64 floats per wave instruction). Rows >= p are clamped (finite) and masked
+      // where used.
       for (int pc = my; pc < 32; pc += NP) {
         const int blk = pc < 16 ? tn : t;
         const int i = (pc & 15) * 4 + (lane >> 4);
@@ -357,33 +485,44 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         float* dst = (pc < 16 ? sCn : sCorr) + (pc & 15) * 256;
         glds16f(src, dst);
       }
-    }
-    // every pull wave scans all pending columns and keeps list entries pos = my (mod NP): an
-    // even split however the changed coordinates cluster in the column blocks
-    int tot = 0;
-    const int base0 = my * PER;             // private slist/sdelta region
-    for (int c = 0; c < T; ++c) {
-      const int j = c * 64 + lane;
-      const double dj = sdc[j] - sds[tn][j];
-      const bool nz = dj != 0.0;
-      const uint64_t bal = __ballot(nz);
-      const int pos = tot + __popcll(bal & ((1ull << lane) - 1ull));
-      if (nz && pos % NP == my) { slist2[base0 + pos / NP] = j; sdelta2[base0 + pos / NP] = (CT)dj; }
-      tot += __popcll(bal);
-    }
-    const int cnt = (tot - my + NP - 1) / NP;
-    const CT* colt = Cq + tn * 64 + lane;
-    CT acc = 0;
-    int e = 0;
-    constexpr int GB = sizeof(CT) == 4 ? 32 : 16;   // row segments in flight per wave
-    for (; e + GB <= cnt; e += GB) {
-      CT v[GB];
+      // every column block but tn (its own changes are in g_tn already); block t's changes
+      // up to this visit are pulled here (sdc is frozen until the barrier), this visit's
+      // arrive through wave 0's correction. Pull wave my takes the my-th such block.
+      const int jb = my + (my >= tn ? 1 : 0);
+      if (jb < T) acc = pull_block(jb, tn);
+    } else {
+      // fp64 C: sparse pull. The pending columns of block tn (ordered ballots over all
+      // column blocks) are split into NP contiguous ranges, one per pull wave.
+      const int base0 = my * PER;           // private slist/sdelta region
+      double dvv[TMAX];
 #pragma unroll
-      for (int u = 0; u < GB; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
+      for (int c = 0; c < TMAX; ++c) {
+        const int j = c * 64 + lane;
+        dvv[c] = c < T ? sdc[j] - sds[tn][j] : 0.0;
+      }
+      uint64_t bals[TMAX];
+      int pref[TMAX];
+      int tot = 0;
 #pragma unroll
-      for (int u = 0; u < GB; ++u) acc += v[u] * sdelta2[base0 + e + u];
-    }
-    if constexpr (sizeof(CT) == 4) {
+      for (int c = 0; c < TMAX; ++c) {
+        bals[c] = __builtin_amdgcn_ballot_w64(dvv[c] != 0.0);
+        pref[c] = tot;
+        tot += __popcll(bals[c]);
+      }
+      const int share = (tot + NP - 1) / NP;
+      const int lo = my * share, hi = min(tot, lo + share);
+      const uint64_t ltmask = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int c = 0; c < TMAX; ++c) {
+        const int pos = pref[c] + __popcll(bals[c] & ltmask);
+        if (((bals[c] >> lane) & 1ull) && pos >= lo && pos < hi) {
+          slist2[base0 + pos - lo] = c * 64 + lane;
+          sdelta2[base0 + pos - lo] = (CT)dvv[c];
+        }
+      }
+      const int cnt = max(0, hi - lo);
+      const CT* colt = Cq + tn * 64 + lane;
+      int e = 0;
       for (; e + 16 <= cnt; e += 16) {
         CT v[16];
 #pragma unroll
@@ -391,15 +530,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #pragma unroll
         for (int u = 0; u < 16; ++u) acc += v[u] * sdelta2[base0 + e + u];
       }
+      for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     }
-    for (; e + 8 <= cnt; e += 8) {
-      CT v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = colt[(int64_t)slist2[base0 + e + u] * ldc];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u] * sdelta2[base0 + e + u];
-    }
-    for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     spart[wid][lane] = (double)acc;
     if constexpr (sizeof(CT) == 4) return;
     // fp64 C: tn's diagonal block -> LDS (fp32) through registers, rows i = my (mod NP)
@@ -419,7 +551,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   };
 
   int ready = -1;   // block whose gradient and diagonal registers a pass end left current
-  auto pass = [&](bool full) -> double {
+  auto pass = [&](bool full) __attribute__((always_inline)) -> double {
     double dlx_l = 0.0;
     for (int t = wid; t < T; t += NW) {     // blocks holding an active coordinate
       const bool a = full || ((sflag[t * 64 + lane] & 3) == 3);
@@ -457,11 +589,10 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       int fl = 0;
       // wave 0: phase-B operands that nothing changes during phase A, read now so their
       // LDS latency hides under the recurrence
-      double dc0 = 0.0, ds0 = 0.0, sgn = 0.0;
+      double dc0 = 0.0, ds0 = 0.0;
       if (wid == 0) {
         dc0 = sdc[k];
         ds0 = sds[t][k];
-        if (tn >= 0) sgn = sg[tn * 64 + lane];
         gt = sg[k];
         at = sa[k];
         const double vpt = svp[k];
@@ -495,7 +626,10 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         unsigned long long nupd_ = 0;
 #endif
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): dg_* landed; no waits in the loop
-        auto step = [&]() -> bool {
+#ifdef ENET_PROF
+        const long long tloop0_ = clock64();
+#endif
+        auto step = [&]() __attribute__((always_inline)) -> bool {
 #pragma clang fp contract(off)
           const double au = fabs(u);
           const uint64_t msk = __builtin_amdgcn_ballot_w64(au > thr0) & live;
@@ -521,16 +655,103 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #endif
           return true;
         };
-        while (step() && step()) {
+        // Active-set passes: every eligible lane of the block is visited in lane order,
+        // unconditionally. An eligible lane the ballot form would skip (a == 0 and
+        // |u| <= vp*lambda) gets an = +-0, d = +-0, and u - c*(+-0) == u: the same sequence
+        // of updates, bit for bit, but the visiting order is known before the loop, so
+        // the compare -> ballot -> branch -> ff1 hop leaves the serial chain (the scalar
+        // unit walks the mask ahead of the vector recurrence).
+        auto step_known = [&](int i) __attribute__((always_inline)) {
+#pragma clang fp contract(off)
+          const double au = fabs(u);
+          const double an = __dmul_rn(copysign(fmax(au - thr_l, 0.0), u), rden);
+          const double dd = an - at;
+          const float clo = dg_lo[i & 31], chi = dg_hi[i & 31];
+          const float ci = i < 32 ? clo : chi;
+          const double d = readlane_d(dd, i);
+          const bool me = lane == i;
+          gbef = me ? gt : gbef;
+          const double cd = (double)ci * d;
+          u -= cd;
+          gt -= cd;
+          __builtin_amdgcn_sched_barrier(0);
+          anv = me ? an : anv;
+#ifdef ENET_PROF
+          if (lane == 0) ++nupd_;
+#endif
+        };
+        // Dense walk: when enough lanes of the block will (or may) move, visit all 64 lanes
+        // in order with STATIC lane indices (fully unrolled): no mask walk, no register-
+        // indexed diagonal row, readlane with an immediate lane. Ineligible lanes get
+        // threshold +inf, so an = +-0 and d = +-0 - 0 (a == 0 there): a no-op, bit for bit.
+        // A wave issues one instruction per ~4 cycles, so the step cost is its instruction
+        // count: ~15 here against ~33 for a dynamic step (profiles/r02_enet).
+        const uint64_t em = __builtin_amdgcn_ballot_w64(elig);
+        const uint64_t nzm = __builtin_amdgcn_ballot_w64(elig && at != 0.0);
+        const int ncand = full ? __popcll(nzm) : __popcll(em);
+        auto dense_walk = [&](auto lasso_tag) __attribute__((always_inline)) {
+          constexpr bool LASSO = decltype(lasso_tag)::value;
+          const double thr_e = elig ? thr_l : __builtin_inf();
+#pragma unroll
+          for (int i = 0; i < 64; ++i) {
+#pragma clang fp contract(off)
+            const double au = fabs(u);
+            const double sv = copysign(fmax(au - thr_e, 0.0), u);
+            const double an = LASSO ? sv : __dmul_rn(sv, rden);
+            const double dd = an - at;
+            const float ci = i < 32 ? dg_lo[i] : dg_hi[i - 32];
+            const double d = readlane_d(dd, i);
+            // lane i's bookkeeping: one compare + four selects (in asm: left to itself the
+            // compiler materialises 64 constant lane masks in SGPRs and spills them)
+            select_lane(i, lane, gbef, gt, anv, an);
+            const double cd = (double)ci * d;
+            u -= cd;
+            gt -= cd;
+          }
+#ifdef ENET_PROF
+          if (lane == 0) nupd_ += 64;
+#endif
+        };
+        if (!ENET_BALLOT_ONLY && ncand >= ENET_DENSE_MIN) {
+          moved = ~0ull;
+          if (dem == 0.0) dense_walk(std::true_type{});
+          else dense_walk(std::false_type{});
+        } else if (full || ENET_BALLOT_ONLY) {
+          while (step() && step()) {
+          }
+        } else {
+          uint64_t rem = em;
+          moved = rem;
+          while (rem) {
+            const int i = __ffsll((unsigned long long)rem) - 1;
+            rem &= rem - 1ull;
+            step_known(i);
+            if (!rem) break;
+            const int i2 = __ffsll((unsigned long long)rem) - 1;
+            rem &= rem - 1ull;
+            step_known(i2);
+          }
         }
+#ifdef ENET_PROF
+        if (lane == 0) sprof[wid][15] += (unsigned long long)(clock64() - tloop0_);
+#endif
         if ((moved >> lane) & 1ull) {
-          dblk = anv - at;                 // == the broadcast step d of this lane
-          at = anv;
+          const double dn = anv - at;      // == the broadcast step d of this lane
+          if (dn != 0.0) {                 // visited but not moved (active pass): keep a
+            dblk = dn;
+            at = anv;
+          }
         }
 #ifdef ENET_PROF
         if (lane == 0) {
-          atomicAdd(&enet_prof[q][6], (unsigned long long)(wall_clock64() - ta_));
-          atomicAdd(&enet_prof[q][7], nupd_);
+          const unsigned long long tl_ = wall_clock64() - ta_;
+          sprof[wid][6] += tl_;
+          sprof[wid][7] += nupd_;
+          if (!full) {
+            sprof[wid][12] += tl_;
+            sprof[wid][13] += nupd_;
+          }
+          sprof[wid][14] += 1ull;    // wave-0 visits (full + active)
         }
 #endif
         if (dblk != 0.0) {
@@ -538,8 +759,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           dlx_l = fmax(dlx_l, dblk * dblk);
           fl |= 2;
         }
-        // block t's own deltas -> block tn (wave-private list, contiguous segments)
-        if (tn >= 0) {
+        // fp64 C: block t's own deltas -> block tn (wave-private list, contiguous segments);
+        // fp32 C: wave 1 applies them from the DMA'd block in phase B
+        if (sizeof(CT) != 4 && tn >= 0) {
           const bool ch = dblk != 0.0;
           const uint64_t bal = __builtin_amdgcn_ballot_w64(ch);
           const int pos = __popcll(bal & ((1ull << lane) - 1ull));
@@ -548,7 +770,6 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           chm = bal;
           const CT* colt = Cq + tn * 64 + lane;
           int e = 0;
-          if constexpr (sizeof(CT) == 4) e = nc;   // fp32: from sCorr after the barrier
           for (; e + 16 <= nc; e += 16) {
             CT w[16];
 #pragma unroll
@@ -558,63 +779,52 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           }
           for (; e < nc; ++e) corr += colt[(int64_t)scl[e] * ldc] * scd[e];
         }
-        if constexpr (sizeof(CT) != 4) spart[0][lane] = (double)corr;
+        if constexpr (sizeof(CT) != 4) {
+          spart[0][lane] = (double)corr;
+        } else if (tn >= 0) {                  // wave 1 applies them in phase B
+          sdall[lane] = (float)dblk;
+          const uint64_t chg = __builtin_amdgcn_ballot_w64(dblk != 0.0);
+          if (lane == 0) schg = chg != 0ull;
+        }
 #ifdef ENET_PROF
-        if (lane == 0) atomicAdd(&enet_prof[q][2], (unsigned long long)(wall_clock64() - ta_));
+        if (lane == 0) sprof[wid][2] += (unsigned long long)(wall_clock64() - ta_);
 #endif
       } else if (tn >= 0) {
         pull_rest(t, tn);
 #ifdef ENET_PROF
         if (wid == 1 && lane == 0)
-          atomicAdd(&enet_prof[q][4], (unsigned long long)(wall_clock64() - ta_));
+          sprof[wid][4] += (unsigned long long)(wall_clock64() - ta_);
+        if (wid == NW - 1 && lane == 0)
+          sprof[wid][18] += (unsigned long long)(wall_clock64() - ta_);
 #endif
       }
       __syncthreads();
       PROF_T(tb_);
       PROF_ADD(1, tb_ - ta_);
       PROF_ADD(3, 1);
+      // phase B1: wave 0 publishes block t; with fp32 C the pull waves split block t's own
+      // deltas of this visit over the rows of the DMA'd (t rows x tn cols) block
+      const bool corr_split = sizeof(CT) == 4 && tn >= 0 && schg;   // uniform
+      const double dnew = dc0 + dblk;
       if (wid == 0) {
         sg[k] = gt;
         sa[k] = at;
         sflag[k] = fl;
-        const double dnew = dc0 + dblk;
         sdc[k] = dnew;
         sds[t][k] = ds0 + dblk;  // own changes are already in g_t
+        if (tn >= 0) sds[tn][k] = dnew;     // block t's columns; waves 2.. copy the others
+      } else if (corr_split) {
+        float a = 0.f;
+        for (int r = wid - 1; r < 64; r += NP) a = __builtin_fmaf(sCorr[r * 64 + lane], sdall[r], a);
+        scorr[wid - 1][lane] = a;
+      }
+      if (corr_split) __syncthreads();
+      // phase B2: wave 0 moves tn's diagonal block into registers, wave 1 completes block
+      // tn's gradient (pull partials + own deltas), waves 2.. copy tn's snapshot
+      if (wid == 0) {
         if (tn >= 0) {
-          const int kn = tn * 64 + lane;
-          if constexpr (sizeof(CT) == 4) {
-            // block t's own deltas -> block tn from the DMA'd (t rows x tn cols) block:
-            // all 64 rows (an unchanged row has d = 0), the deltas read back from LDS as
-            // broadcast float4s, 4 independent fma chains combined in a fixed order
-            if (chm) {
-              sdall[lane] = (float)dblk;
-              float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-              for (int r0 = 0; r0 < 64; r0 += 4) {
-                const float4 dv = *reinterpret_cast<const float4*>(sdall + r0);
-                a0 = __builtin_fmaf(sCorr[(r0 + 0) * 64 + lane], dv.x, a0);
-                a1 = __builtin_fmaf(sCorr[(r0 + 1) * 64 + lane], dv.y, a1);
-                a2 = __builtin_fmaf(sCorr[(r0 + 2) * 64 + lane], dv.z, a2);
-                a3 = __builtin_fmaf(sCorr[(r0 + 3) * 64 + lane], dv.w, a3);
-              }
-              corr = (a0 + a1) + (a2 + a3);
-            }
-            spart[0][lane] = (double)corr;
-          }
-#ifdef ENET_PROF
-          if (lane == 0) atomicAdd(&enet_prof[q][10], (unsigned long long)(wall_clock64() - tb_));
-#endif
-          double sp = 0.0;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) sp += spart[w][lane];
-          sg[kn] = sgn - sp;
-          sds[tn][k] = dnew;     // block t's columns; the pull waves copy the others
-#ifdef ENET_PROF
-          if (lane == 0) atomicAdd(&enet_prof[q][11], (unsigned long long)(wall_clock64() - tb_));
-#endif
-
-          // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] is only read
-          // for a moving coordinate i, and coordinates >= p never move
+          // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] only ever
+          // multiplies the step of coordinate i, which is 0 for coordinates >= p
 #pragma unroll
           for (int i = 0; i < 32; ++i) {
             dg_lo[i] = sCn[i * 64 + lane];
@@ -622,12 +832,33 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           }
         }
 #ifdef ENET_PROF
-        if (lane == 0) atomicAdd(&enet_prof[q][9], (unsigned long long)(wall_clock64() - tb_));
+        if (lane == 0) sprof[wid][9] += (unsigned long long)(wall_clock64() - tb_);
+#endif
+      } else if (tn >= 0 && wid == 1) {
+        double c0 = spart[0][lane];           // fp64 C: wave 0's own-delta correction
+        if constexpr (sizeof(CT) == 4) {
+          float cs = 0.f;
+          if (corr_split) {
+#pragma unroll
+            for (int w = 0; w < NP; ++w) cs += scorr[w][lane];
+          }
+          c0 = (double)cs;
+        }
+        double sp = c0;
+#pragma unroll
+        for (int w = 1; w < NW; ++w) sp += spart[w][lane];
+        const int kn = tn * 64 + lane;
+        sg[kn] = sg[kn] - sp;
+#ifdef ENET_PROF
+        if (lane == 0) sprof[wid][16] += (unsigned long long)(wall_clock64() - tb_);
 #endif
       } else if (tn >= 0) {
         // snapshot of block tn for every column block except t (unchanged since B1)
-        for (int j = (wid - 1) * 64 + lane; j < ldc; j += NP * 64)
+        for (int j = (wid - 2) * 64 + lane; j < ldc; j += (NW - 2) * 64)
           if ((j >> 6) != t) sds[tn][j] = sdc[j];
+#ifdef ENET_PROF
+        if (wid == 2 && lane == 0) sprof[wid][17] += (unsigned long long)(wall_clock64() - tb_);
+#endif
       }
       __syncthreads();
       PROF_T(tc_);
@@ -732,6 +963,14 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     }
     rsq_prev = rsq_all;
   }
+#ifdef ENET_PROF
+  __syncthreads();
+  if (tid < 24) {
+    unsigned long long acc = 0;
+    for (int w = 0; w < NW; ++w) acc += sprof[w][tid];
+    atomicAdd(&enet_prof[q][tid], acc);
+  }
+#endif
   if (tid == 0) {
     nlam_out[q] = m_out;
     npass_out[q] = timed_out ? -1 : npass;
@@ -744,7 +983,7 @@ extern "C" __attribute__((visibility("default"))) int ate_enet_prof_read(void* h
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(enet_prof), sizeof(enet_prof));
 }
 extern "C" __attribute__((visibility("default"))) int ate_enet_prof_reset() {
-  static unsigned long long z[256][8];
+  static unsigned long long z[256][24];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(enet_prof), z, sizeof(z));
 }
 #endif

@@ -50,13 +50,13 @@ def run(n, p):
     _, _, cv = dml_crossfit_panel(pan, 5, "min")
     t[1].record()
     torch.cuda.synchronize()
-    buf = np.zeros((256, 16), dtype=np.uint64)
+    buf = np.zeros((256, 24), dtype=np.uint64)
     lib.ate_enet_prof_read(buf.ctypes.data_as(ctypes.c_void_p))
     rows = buf[:40]
     live = rows[rows[:, 3] > 0]
     print(json.dumps({"step_ms": t[0].elapsed_time(t[1]),
-                      "per_problem": [[int(v) for v in r[:12]] for r in live],
-                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B, wave0 phase B up to corr, up to before the diagonal reload"}))
+                      "per_problem": [[int(v) for v in r[:19]] for r in live],
+                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B, wave0 phase B up to corr, up to before the diagonal reload, active-pass recurrence, active-pass updates, wave-0 visits, loop-only shader cycles, wave-1 pull scan cycles, wave-1 phase B, wave-2 phase B, last pull wave phase A"}))
 
 
 if __name__ == "__main__":
