@@ -245,11 +245,13 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
   __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
   __shared__ int sflag[PMAX];             // bit0 ju, bit1 active
-  __shared__ double spart[NW][64];
+  __shared__ double spart2[2][NW][64];    // pull partials (and fp64 own-delta corr, slot 0),
+                                          // double-buffered by visit parity
   __shared__ __attribute__((aligned(16))) float sred[NW][256];   // group reduction per wave
   __shared__ __attribute__((aligned(16))) float sdw[NW][64];     // pull_block deltas per wave
   __shared__ int srow[NW][64];                                   // pull_block row lists
-  __shared__ float scorr[NP][64];         // phase B1: own-delta correction partials
+  __shared__ float scorr2[2][NP][64];     // phase B: own-delta correction partials (fp32 C)
+  __shared__ int scorr_ok[2];             // ... and whether they were computed
 #ifdef ENET_PROF
   // per-wave cycle accumulators in LDS (lane 0 of a wave adds to its own row), flushed to
   // enet_prof once at kernel end: no global atomics (and their vmcnt waits at barriers)
@@ -450,13 +452,13 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         for (int c = 0; c < 32; ++c) { dg_lo[c] = 0.f; dg_hi[c] = 0.f; }
       }
     }
-    spart[wid][lane] = (double)acc;
+    spart2[0][wid][lane] = (double)acc;
     __syncthreads();
     if (tid < 64) {
       const int k = t * 64 + tid;
       double sp = 0.0;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) sp += spart[w][tid];
+      for (int w = 0; w < NW; ++w) sp += spart2[0][w][tid];
       sg[k] -= sp;
     }
     for (int j = tid; j < ldc; j += NTH) sds[t][j] = sdc[j];
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // pending for block tn (sdc is frozen until the first barrier) and stage tn's diagonal
   // block in LDS. After the barrier wave 0 publishes block t, completes block tn's
   // gradient and snapshot, and moves tn's diagonal block into registers.
-  auto pull_rest = [&](int t, int tn) __attribute__((always_inline)) {     // waves 1..NW-1
+  auto pull_rest = [&](int t, int tn, int vpar) __attribute__((always_inline)) {     // waves 1..NW-1
     const int my = wid - 1;
     CT acc = 0;
     if constexpr (sizeof(CT) == 4) {
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       }
       for (; e < cnt; ++e) acc += colt[(int64_t)slist2[base0 + e] * ldc] * sdelta2[base0 + e];
     }
-    spart[wid][lane] = (double)acc;
+    spart2[vpar][wid][lane] = (double)acc;
     if constexpr (sizeof(CT) == 4) return;
     // fp64 C: tn's diagonal block -> LDS (fp32) through registers, rows i = my (mod NP)
     constexpr int NR = (64 + NP - 1) / NP;
@@ -551,6 +553,26 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   };
 
   int ready = -1;   // block whose gradient and diagonal registers a pass end left current
+  // Block tn's gradient is completed lazily: the visit that pulls for tn leaves the pull
+  // partials (spart2[par]) and the own-delta correction partials (scorr2[par], or slot 0
+  // of spart2 with fp64 C) in LDS, and the next visit's recurrence wave folds them into
+  // g_tn as it loads it (one LDS round trip on wave 0 instead of a second phase-B
+  // barrier). Same additions in the same order as an eager update.
+  auto pending_sum = [&](int par) __attribute__((always_inline)) -> double {
+    double c0 = spart2[par][0][lane];
+    if constexpr (sizeof(CT) == 4) {
+      float cs = 0.f;
+      if (scorr_ok[par]) {
+#pragma unroll
+        for (int w = 0; w < NP; ++w) cs += scorr2[par][w][lane];
+      }
+      c0 = (double)cs;
+    }
+    double sp = c0;
+#pragma unroll
+    for (int w = 1; w < NW; ++w) sp += spart2[par][w][lane];
+    return sp;
+  };
   auto pass = [&](bool full) __attribute__((always_inline)) -> double {
     double dlx_l = 0.0;
     for (int t = wid; t < T; t += NW) {     // blocks holding an active coordinate
@@ -576,6 +598,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     PROF_ADD(8, tp1_ - tp0_);
     for (int v = 0; v < nv; ++v) {
       const int t = svis[v];
+      const int vpar = v & 1;
       // the last visit prefetches block 0, the first block of the next pass whenever
       // that pass is a full pass or block 0 holds an active coordinate (checked there)
       const int tn = v + 1 < nv ? svis[v + 1] : (t != 0 ? 0 : -1);
@@ -594,6 +617,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         dc0 = sdc[k];
         ds0 = sds[t][k];
         gt = sg[k];
+        if (v > 0) gt = gt - pending_sum(vpar ^ 1);   // block t was the last visit's tn
         at = sa[k];
         const double vpt = svp[k];
         fl = sflag[k];
@@ -692,21 +716,40 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         auto dense_walk = [&](auto lasso_tag) __attribute__((always_inline)) {
           constexpr bool LASSO = decltype(lasso_tag)::value;
           const double thr_e = elig ? thr_l : __builtin_inf();
+          if constexpr (LASSO) {
+            // lasso: an = u - clamp(u, -thr, thr) and d = (u - a) - clamp(u), so the serial
+            // chain is max -> min -> sub -> readlane -> fma (u), and the gradient is not
+            // carried per step (g = u - a_visit_start after the walk)
+            const double a0v = at;
 #pragma unroll
-          for (int i = 0; i < 64; ++i) {
+            for (int i = 0; i < 64; ++i) {
+              const double cl = fmin(fmax(u, -thr_e), thr_e);
+              const double w = u - a0v;              // gradient before this step
+              const double dd = w - cl;
+              const double an = u - cl;
+              const float ci = i < 32 ? dg_lo[i] : dg_hi[i - 32];
+              const double d = readlane_d(dd, i);
+              // lane i's bookkeeping: one compare + four selects (in asm: left to itself
+              // the compiler materialises 64 constant lane masks in SGPRs and spills them)
+              select_lane(i, lane, gbef, w, anv, an);
+              u = __builtin_fma(-(double)ci, d, u);
+            }
+            gt = u - a0v;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
 #pragma clang fp contract(off)
-            const double au = fabs(u);
-            const double sv = copysign(fmax(au - thr_e, 0.0), u);
-            const double an = LASSO ? sv : __dmul_rn(sv, rden);
-            const double dd = an - at;
-            const float ci = i < 32 ? dg_lo[i] : dg_hi[i - 32];
-            const double d = readlane_d(dd, i);
-            // lane i's bookkeeping: one compare + four selects (in asm: left to itself the
-            // compiler materialises 64 constant lane masks in SGPRs and spills them)
-            select_lane(i, lane, gbef, gt, anv, an);
-            const double cd = (double)ci * d;
-            u -= cd;
-            gt -= cd;
+              const double au = fabs(u);
+              const double sv = copysign(fmax(au - thr_e, 0.0), u);
+              const double an = __dmul_rn(sv, rden);
+              const double dd = an - at;
+              const float ci = i < 32 ? dg_lo[i] : dg_hi[i - 32];
+              const double d = readlane_d(dd, i);
+              select_lane(i, lane, gbef, gt, anv, an);
+              const double cd = (double)ci * d;
+              u -= cd;
+              gt -= cd;
+            }
           }
 #ifdef ENET_PROF
           if (lane == 0) nupd_ += 64;
@@ -780,7 +823,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           for (; e < nc; ++e) corr += colt[(int64_t)scl[e] * ldc] * scd[e];
         }
         if constexpr (sizeof(CT) != 4) {
-          spart[0][lane] = (double)corr;
+          spart2[vpar][0][lane] = (double)corr;
         } else if (tn >= 0) {                  // wave 1 applies them in phase B
           sdall[lane] = (float)dblk;
           const uint64_t chg = __builtin_amdgcn_ballot_w64(dblk != 0.0);
@@ -790,7 +833,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         if (lane == 0) sprof[wid][2] += (unsigned long long)(wall_clock64() - ta_);
 #endif
       } else if (tn >= 0) {
-        pull_rest(t, tn);
+        pull_rest(t, tn, vpar);
 #ifdef ENET_PROF
         if (wid == 1 && lane == 0)
           sprof[wid][4] += (unsigned long long)(wall_clock64() - ta_);
@@ -802,9 +845,10 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       PROF_T(tb_);
       PROF_ADD(1, tb_ - ta_);
       PROF_ADD(3, 1);
-      // phase B1: wave 0 publishes block t; with fp32 C the pull waves split block t's own
-      // deltas of this visit over the rows of the DMA'd (t rows x tn cols) block
-      const bool corr_split = sizeof(CT) == 4 && tn >= 0 && schg;   // uniform
+      // phase B: wave 0 publishes block t and moves tn's diagonal block into registers;
+      // the pull waves split block t's own deltas of this visit over the rows of the DMA'd
+      // (t rows x tn cols) block (fp32 C) and copy tn's snapshot. Block tn's gradient is
+      // folded in by the next visit (pending_sum).
       const double dnew = dc0 + dblk;
       if (wid == 0) {
         sg[k] = gt;
@@ -812,17 +856,11 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         sflag[k] = fl;
         sdc[k] = dnew;
         sds[t][k] = ds0 + dblk;  // own changes are already in g_t
-        if (tn >= 0) sds[tn][k] = dnew;     // block t's columns; waves 2.. copy the others
-      } else if (corr_split) {
-        float a = 0.f;
-        for (int r = wid - 1; r < 64; r += NP) a = __builtin_fmaf(sCorr[r * 64 + lane], sdall[r], a);
-        scorr[wid - 1][lane] = a;
-      }
-      if (corr_split) __syncthreads();
-      // phase B2: wave 0 moves tn's diagonal block into registers, wave 1 completes block
-      // tn's gradient (pull partials + own deltas), waves 2.. copy tn's snapshot
-      if (wid == 0) {
         if (tn >= 0) {
+          sds[tn][k] = dnew;     // block t's columns; the pull waves copy the others
+          if constexpr (sizeof(CT) == 4) {
+            if (lane == 0) scorr_ok[vpar] = schg;
+          }
           // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] only ever
           // multiplies the step of coordinate i, which is 0 for coordinates >= p
 #pragma unroll
@@ -834,35 +872,39 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #ifdef ENET_PROF
         if (lane == 0) sprof[wid][9] += (unsigned long long)(wall_clock64() - tb_);
 #endif
-      } else if (tn >= 0 && wid == 1) {
-        double c0 = spart[0][lane];           // fp64 C: wave 0's own-delta correction
-        if constexpr (sizeof(CT) == 4) {
-          float cs = 0.f;
-          if (corr_split) {
-#pragma unroll
-            for (int w = 0; w < NP; ++w) cs += scorr[w][lane];
-          }
-          c0 = (double)cs;
-        }
-        double sp = c0;
-#pragma unroll
-        for (int w = 1; w < NW; ++w) sp += spart[w][lane];
-        const int kn = tn * 64 + lane;
-        sg[kn] = sg[kn] - sp;
-#ifdef ENET_PROF
-        if (lane == 0) sprof[wid][16] += (unsigned long long)(wall_clock64() - tb_);
-#endif
       } else if (tn >= 0) {
-        // snapshot of block tn for every column block except t (unchanged since B1)
-        for (int j = (wid - 2) * 64 + lane; j < ldc; j += (NW - 2) * 64)
+        const int my = wid - 1;
+        if (sizeof(CT) == 4 && schg) {
+          constexpr int RPW = (64 + NP - 1) / NP;   // rows per pull wave
+          float cv[RPW], dv[RPW];
+#pragma unroll
+          for (int j = 0; j < RPW; ++j) {
+            const int r = my + NP * j;
+            cv[j] = r < 64 ? sCorr[r * 64 + lane] : 0.f;
+            dv[j] = r < 64 ? sdall[r] : 0.f;
+          }
+          float a = 0.f;
+#pragma unroll
+          for (int j = 0; j < RPW; ++j) a = __builtin_fmaf(cv[j], dv[j], a);
+          scorr2[vpar][my][lane] = a;
+        }
+        // snapshot of block tn for every column block except t (unchanged this phase)
+        for (int j = my * 64 + lane; j < ldc; j += NP * 64)
           if ((j >> 6) != t) sds[tn][j] = sdc[j];
 #ifdef ENET_PROF
-        if (wid == 2 && lane == 0) sprof[wid][17] += (unsigned long long)(wall_clock64() - tb_);
+        if (wid == 1 && lane == 0) sprof[wid][16] += (unsigned long long)(wall_clock64() - tb_);
 #endif
       }
       __syncthreads();
       PROF_T(tc_);
       PROF_ADD(0, tc_ - tb_);
+    }
+    if (ready >= 0) {   // the prefetched block's gradient: fold its pending partials now
+      if (wid == 0) {
+        const int kr = ready * 64 + lane;
+        sg[kr] = sg[kr] - pending_sum((nv - 1) & 1);
+      }
+      __syncthreads();
     }
     const double dlx = wave_max(dlx_l);
     if (tid == 0) sdl = dlx;

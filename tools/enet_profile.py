@@ -55,8 +55,8 @@ def run(n, p):
     rows = buf[:40]
     live = rows[rows[:, 3] > 0]
     print(json.dumps({"step_ms": t[0].elapsed_time(t[1]),
-                      "per_problem": [[int(v) for v in r[:19]] for r in live],
-                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B, wave0 phase B up to corr, up to before the diagonal reload, active-pass recurrence, active-pass updates, wave-0 visits, loop-only shader cycles, wave-1 pull scan cycles, wave-1 phase B, wave-2 phase B, last pull wave phase A"}))
+                      "per_problem": [[int(v) for v in r[:24]] for r in live],
+                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B, wave0 phase B up to corr, up to before the diagonal reload, active-pass recurrence, active-pass updates, wave-0 visits, loop-only shader cycles, wave-1 pull scan cycles, wave-1 phase B, wave-2 phase B, last pull wave phase A, unused, w0 B1 work, w1 B1 work, w0 after B1 barrier, w1 after B1 barrier"}))
 
 
 if __name__ == "__main__":
