@@ -36,6 +36,12 @@ import sys
 import time
 
 
+# BASELINE.md "Measured CPU comparison point": the reference publishes no throughput; the
+# conservative CPU bound is the fp32 fold-Gram stack alone on the 8-core host
+# (tools/cpu_baseline.py -> profiles/r02_cpu_baseline.json), rows/s at N=1e7, p=500.
+CPU_BASELINE_ROWS_PER_S = 1.154e6
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,7 +198,8 @@ def main():
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": args.scaling,
-            "vs_baseline": None,
+            "vs_baseline": rows_per_s / CPU_BASELINE_ROWS_PER_S,
+            "baseline": "CPU bound: fp32 fold Grams alone, 8-core host (BASELINE.md)",
             "dtype": args.dtype,
             "data": "synthetic (tutorial DGP shape, generated on device)",
             "config": {
