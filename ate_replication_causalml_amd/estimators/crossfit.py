@@ -22,6 +22,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 import torch
 
+from .. import _native
 from ..models import forest as F
 from ..ops.linalg import logistic_irls
 from ..ops.panel import build_panel
@@ -138,6 +139,118 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
     tau = float(gamma.mean())
     se = float(gamma.std(ddof=1) / math.sqrt(n))
     return AteResult.make(method or f"AIPW cross-fit ({learner}, K={folds})", tau, se,
+                          e_min=float(e.min()), e_max=float(e.max()))
+
+
+def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
+                           tree_shard=None, concurrent=True, engine="gpu",
+                           method="AIPW cross-fit (rf, HBM panel)") -> AteResult:
+    """Config 3 on an HBM-resident panel (data/device_dgp.synthetic_panel, segment k =
+    fold k): the panel's feature columns are binned on the device (``bin_panel``, no host
+    copy of X) into the forest engine's column-major uint8 layout; per fold, the
+    propensity forest (W on the other folds) and the two outcome forests (Y on the other
+    folds' treated / control rows) are grown from device-gathered training columns and
+    predict the held-out fold's bins; the AIPW scores and their mean / sd are computed in
+    fp64 on the device.
+
+    Trees are sharded over ``comm`` (every rank holds all binned rows and grows its share
+    of every forest; the held-out vote sums are all-reduced, C05), or over a simulated
+    ``tree_shard=(rank, world)`` on one device (the per-GPU work of a multi-GPU run;
+    the ATE is then that of the shard's trees). ``concurrent``: the 3K forests grow side
+    by side on separate streams, in batches that fit free HBM (a forest of T trees fills
+    only T CUs).
+    ``engine="cpu"`` grows the same forests on the host engine from the same device bins
+    (bit-identical trees; the parity test)."""
+    from .boosting import bin_panel
+    dev = pan.device
+    K = pan.nseg
+    Xr, ldr, edges, rows = bin_panel(pan)
+    p = len(pan.xcols)
+    Xb = Xr[:, :p].t().contiguous()                  # [p][n] engine layout
+    del Xr
+    nr = np.asarray(pan.seg_nreal, dtype=np.int64)
+    c0 = np.concatenate([[0], np.cumsum(nr)]).astype(np.int64)
+    n = int(c0[-1])
+    Y = pan.data[pan.cols["Y"]].index_select(0, rows).double()
+    W = pan.data[pan.cols["W"]].index_select(0, rows).double()
+    if comm is not None and comm.world_size > 1:
+        rank, world = comm.rank, comm.world_size
+    elif tree_shard is not None:
+        rank, world = tree_shard
+    else:
+        rank, world = 0, 1
+    t0, cnt = F.tree_shard(num_trees, 1, rank, world)
+    pcomm = comm if comm is not None and comm.world_size > 1 else None
+    e = torch.empty(n, dtype=torch.float64, device=dev)
+    mu1 = torch.empty_like(e)
+    mu0 = torch.empty_like(e)
+    ar = torch.arange(n, device=dev)
+    jobs = []
+    for k in range(K):
+        a, b = int(c0[k]), int(c0[k + 1])
+        tr = (ar < a) | (ar >= b)
+        sd = seed + 1000 * (k + 1)
+        jobs += [(e, tr, W, sd, a, b), (mu1, tr & (W == 1), Y, sd + 1, a, b),
+                 (mu0, tr & (W == 0), Y, sd + 2, a, b)]
+
+    def run(job):
+        out, mask, target, sd, a, b = job
+        idx = mask.nonzero().squeeze(1)
+        yt = target.index_select(0, idx)
+        binary = bool(((yt == 0) | (yt == 1)).all())
+        kw = dict(y=yt) if binary else dict(r1=yt, min_node=5, mtry=max(1, p // 3))
+        Xt = Xb.index_select(1, idx)
+        if engine == "cpu":
+            Xt = Xt.cpu().numpy()
+        fr = F.fit_forest_binned(Xt, edges, F.KIND_CLASS if binary else F.KIND_REG,
+                                 ntree=cnt, seed=sd, tree_offset=t0, **kw)
+        del Xt
+        Xho = Xb[:, a:b].contiguous()
+        pred = F.predict_tree_parallel(fr, pcomm, Xb=Xho) if pcomm is not None else \
+            fr.predict_binned(Xho)
+        out[a:b] = torch.as_tensor(pred, device=dev)
+
+    if concurrent and dev.type == "cuda" and pcomm is None and engine == "gpu":
+        # the 3K forests are independent: grow them side by side (one stream per host
+        # thread; a forest of T trees fills only T CUs), in batches whose working set
+        # (training bins + node arrays + growth scratch) fits a share of free HBM
+        free = torch.cuda.mem_get_info(dev)[0]
+        lib = _native.hip()
+
+        def need(job):
+            nt = int(job[1].sum())
+            return (p * nt + cnt * (2 * nt + 1) * 20 + cnt * nt
+                    + int(lib.ate_forest_scratch_bytes(nt, cnt)))
+
+        batches, cur_b, used = [], [], 0
+        for job in jobs:
+            m = need(job)
+            if cur_b and used + m > 0.6 * free:
+                batches.append(cur_b)
+                cur_b, used = [], 0
+            cur_b.append(job)
+            used += m
+        batches.append(cur_b)
+        main = torch.cuda.current_stream(dev)
+
+        def run_on(job):
+            st = torch.cuda.Stream(device=dev)
+            st.wait_stream(main)
+            with torch.cuda.device(dev), torch.cuda.stream(st):
+                run(job)
+            st.synchronize()
+
+        for bt in batches:
+            with ThreadPoolExecutor(max_workers=len(bt)) as ex:
+                list(ex.map(run_on, bt))
+    else:
+        for job in jobs:
+            run(job)
+    e = e.clamp(clip, 1 - clip)
+    gamma = mu1 - mu0 + W * (Y - mu1) / e - (1 - W) * (Y - mu0) / (1 - e)
+    tau = float(gamma.mean())
+    se = float(gamma.std() / math.sqrt(n))
+    return AteResult.make(method, tau, se, n=n, trees=num_trees, trees_this_device=cnt,
                           e_min=float(e.min()), e_max=float(e.max()))
 
 

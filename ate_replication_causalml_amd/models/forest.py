@@ -208,6 +208,13 @@ class Forest:
                 return None
         return res.reshape(n2, width) if width > 1 else res
 
+    def predict_binned(self, Xb):
+        """Predictions for already binned rows (column-major uint8 [p][n2], a device tensor
+        for GPU forests, host array/tensor for CPU forests)."""
+        if self.backend == "cpu" and isinstance(Xb, torch.Tensor):
+            Xb = Xb.cpu().numpy()
+        return self.predict_state(Xb, False, self.new_state(Xb.shape[1]), phases=7)
+
     # randomForest-style accessors
     def oob_proba(self):
         return self.predict_raw(None, oob=True)
@@ -233,9 +240,30 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
     """Grow a forest. X: (n, p) float; kind 0 needs y in {0,1}; kind 1 needs r1 (response);
     kind 2 needs r1 = W~ and r2 = Y~ (centred treatment / outcome)."""
     X = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
-    n, p = X.shape
     if backend is None:
         backend = "gpu" if torch.cuda.is_available() else "cpu"
+    if edges is None:
+        edges, ne = bin_edges(X)
+    else:
+        edges, ne = edges
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "gpu" else None
+    Xb = bin_matrix(X, edges, ne, dev)
+    return fit_forest_binned(Xb, (edges, ne), kind, y=y, r1=r1, r2=r2, ntree=ntree, mtry=mtry,
+                             min_node=min_node, sampling=sampling, honesty=honesty, group=group,
+                             mtry_poisson=mtry_poisson, alpha=alpha,
+                             sample_fraction=sample_fraction, seed=seed, tree_offset=tree_offset)
+
+
+def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None,
+                      min_node=1, sampling=0, honesty=False, group=1, mtry_poisson=False,
+                      alpha=0.0, sample_fraction=0.5, seed=1, tree_offset=0) -> Forest:
+    """``fit_forest`` on an already binned column-major uint8 matrix ``Xb`` [p][n]: a device
+    tensor grows on the GPU (csrc/forest.hip), a host array on the CPU engine; both grow the
+    same trees. ``edges`` = (edges, nedges) the bins came from. y / r1 / r2 may be device
+    tensors (no host round trip of the responses for HBM-resident panels)."""
+    edges, ne = edges
+    gpu = isinstance(Xb, torch.Tensor) and Xb.is_cuda
+    p, n = Xb.shape
     if mtry is None:
         mtry = max(1, int(math.floor(math.sqrt(p))))
     fp = ForestParams(kind=kind, sampling=sampling, ntree=ntree, mtry=min(mtry, p),
@@ -243,20 +271,25 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
                       mtry_poisson=int(mtry_poisson), alpha=alpha,
                       sample_fraction=sample_fraction, pois0=math.exp(-min(mtry, p)),
                       seed=seed, p=p, n=n, t0=tree_offset)
-    if edges is None:
-        edges, ne = bin_edges(X)
-    else:
-        edges, ne = edges
     cap = 2 * n + 1
-    ycls = None if y is None else np.asarray(y).astype(np.uint8)
-    r1f = None if r1 is None else to_fix(r1)
-    r2f = None if r2 is None else to_fix(r2)
     need_est = sampling == 1
-    if backend == "gpu":
-        dev = torch.device("cuda", torch.cuda.current_device())
-        Xb = bin_matrix(X, edges, ne, dev)
-        t = lambda a, dt: None if a is None else torch.as_tensor(a, device=dev, dtype=dt)
-        yt, r1t, r2t = t(ycls, torch.uint8), t(r1f, torch.int64), t(r2f, torch.int64)
+    if gpu:
+        dev = Xb.device
+
+        def t(a, dt, fix=False):
+            if a is None:
+                return None
+            if isinstance(a, torch.Tensor):
+                a = a.to(dev)
+                if fix:   # 2^-32 fixed point, round half away from zero (to_fix)
+                    v = a.double() * FIX
+                    return torch.where(v >= 0, torch.floor(v + 0.5), torch.ceil(v - 0.5)).to(dt)
+                return a.to(dt)
+            return torch.as_tensor(to_fix(a) if fix else np.asarray(a), device=dev, dtype=dt)
+
+        yt = t(y, torch.uint8)
+        r1t, r2t = t(r1, torch.int64, True), t(r2, torch.int64, True)
+        Xb = Xb.contiguous()
         feat = torch.empty(ntree * cap, dtype=torch.int32, device=dev)
         thr = torch.empty_like(feat)
         left = torch.empty_like(feat)
@@ -273,8 +306,12 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
                      scratch.data_ptr(), torch.cuda.current_stream().cuda_stream)
         del scratch
         return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xb)
-    Xb = bin_matrix(X, edges, ne, None)
-    Xbn = np.ascontiguousarray(Xb.numpy())
+    h = lambda a: None if a is None else (a.cpu().numpy() if isinstance(a, torch.Tensor) else
+                                           np.asarray(a))
+    Xbn = np.ascontiguousarray(h(Xb), dtype=np.uint8)
+    ycls = None if y is None else h(y).astype(np.uint8)
+    r1f = None if r1 is None else to_fix(h(r1))
+    r2f = None if r2 is None else to_fix(h(r2))
     feat = np.empty(ntree * cap, dtype=np.int32)
     thr = np.empty_like(feat)
     left = np.empty_like(feat)
@@ -405,10 +442,12 @@ def fit_forest_sharded(X, kind, ntree, comm, group=1, **kw) -> Forest:
     return fit_forest(X, kind, ntree=max(cnt, 0), group=group, tree_offset=t0, **kw)
 
 
-def predict_tree_parallel(forest: Forest, comm, X=None, oob=False):
+def predict_tree_parallel(forest: Forest, comm, X=None, oob=False, Xb=None):
     """Forest prediction with trees sharded over ranks: all-reduce the per-tree sums
-    (C05), then (causal forests) the little-bag group sums, then finalise locally."""
-    Xb = forest._bins(X)
+    (C05), then (causal forests) the little-bag group sums, then finalise locally.
+    ``Xb``: already binned rows (column-major uint8 [p][n2]) instead of ``X``."""
+    if Xb is None:
+        Xb = forest._bins(X)
     n2 = Xb.shape[1]
     st = forest.new_state(n2)
     t = st if isinstance(st, torch.Tensor) else torch.from_numpy(st)

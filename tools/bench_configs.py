@@ -23,8 +23,9 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def timed(fn, reps=1):
-    fn()
+def timed(fn, reps=1, warm=True):
+    if warm:          # large configs: one cold run (first-call overheads included)
+        fn()
     _sync()
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -42,6 +43,12 @@ def main():
     ap.add_argument("--n5", type=int, default=1_000_000)
     ap.add_argument("--p5", type=int, default=100)
     ap.add_argument("--trees5", type=int, default=50)
+    ap.add_argument("--p3", type=int, default=100)
+    ap.add_argument("--panel3", action="store_true",
+                    help="config 3 from a device-generated bf16 panel (estimators/crossfit."
+                         "aipw_rf_crossfit_panel; use --n3 10000000 --p3 500 --shard3 0/8 for "
+                         "the per-GPU work of the 8-GPU config)")
+    ap.add_argument("--shard3", default=None, help="rank/world tree shard on this device")
     ap.add_argument("--panel5", action="store_true",
                     help="config 5 from a device-generated bf16 panel (use --n5 12500000 "
                          "--p5 2000 for the per-GPU shard of N=1e8)")
@@ -62,7 +69,21 @@ def main():
         del pan
     if 3 in want or 4 in want or 5 in want:
         from ate_replication_causalml_amd.data.dgp import make_tutorial_data
-    if 3 in want:
+    if 3 in want and a.panel3:
+        from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+        from ate_replication_causalml_amd.estimators.crossfit import aipw_rf_crossfit_panel
+        pan = synthetic_panel(a.n3, p=a.p3, folds=5, seed=11, dtype="bf16", device=dev)
+        shard = tuple(int(v) for v in a.shard3.split("/")) if a.shard3 else None
+        r, s = timed(lambda: aipw_rf_crossfit_panel(pan, num_trees=a.trees3, tree_shard=shard),
+                     warm=a.n3 <= 2_000_000)
+        out.append({"config": 3, "estimator": "AIPW 5-fold cross-fit, RF nuisances (3 forests/"
+                    "fold), HBM panel, device binning", "rows": a.n3, "p": a.p3,
+                    "trees_per_forest": a.trees3, "tree_shard": a.shard3,
+                    "trees_this_device": r.diagnostics.get("trees_this_device"),
+                    "seconds": s, "rows_per_s": a.n3 / s, "ate": r.ate, "se": r.se})
+        print(json.dumps(out[-1]), flush=True)
+        del pan
+    elif 3 in want:
         from ate_replication_causalml_amd.estimators.crossfit import aipw_crossfit
         d = make_tutorial_data(a.n3, seed=11, p_extra=79)
         r, s = timed(lambda: aipw_crossfit(d.Y, d.W, d.X, folds=5, learner="rf",
