@@ -49,6 +49,7 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
     for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
         rid[r0:r0 + cnt] = torch.arange(g0, g0 + cnt, device=device)
     pan.row_index = rid
+    pan.identity = len(slices) == 1 and slices[0][0] == 0
     if pan.data.is_cuda:
         s = torch.cuda.current_stream().cuda_stream
         for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):

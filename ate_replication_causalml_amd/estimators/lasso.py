@@ -20,6 +20,7 @@ from ..ops.panel import build_panel, dtype_code
 from ..parallel import rng
 from ..reference.estimators import lambda_interp
 from ..result import AteResult
+from ..utils.graphs import estimator_graphs
 from .common import as_np, read_result, resolve_device
 
 
@@ -36,32 +37,56 @@ def _sharded_gram(pan, dist):
     return G, global_seg_counts(pan, dist.comm)
 
 
-def _lasso_w_coef(Y, W, X, pf_w, seed, nfolds, fold_stream, device, dtype, dist=None):
+def _lasso_w_panel(Y, W, X, seed, nfolds, fold_stream, device, dtype, dist=None):
     dev = resolve_device(device)
     Xn = np.column_stack([as_np(X), as_np(W)])
-    n, pp = Xn.shape
-    fid = _fold_ids(n, nfolds, seed, fold_stream, dist)
-    pan = build_panel(Xn, None, as_np(Y), folds=fid, dtype=dtype, device=dev)
+    fid = _fold_ids(Xn.shape[0], nfolds, seed, fold_stream, dist)
+    return build_panel(Xn, None, as_np(Y), folds=fid, dtype=dtype, device=dev)
+
+
+def _lasso_w_cv(pan, pf_w, G, counts=None):
+    pf = np.r_[np.ones(len(pan.xcols) - 1), pf_w]
+    return cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf,
+                            seg_counts=counts)
+
+
+def _lasso_w_body(pan, pf_w):
+    """Gram stack -> CV-LASSO path -> [coef of W at lambda.1se, lambda.1se, min fold
+    passes] (device-only: the fold truncation flag travels with the result)."""
+    cv = _lasso_w_cv(pan, pf_w, gram(pan))
+    lam = cv.lambdas[0].gather(0, cv.sel[0, 1:2].long())
+    fnp = cv.fold_npass.min().double().reshape(1) if cv.fold_npass is not None else \
+        torch.zeros(1, dtype=torch.float64, device=lam.device)
+    return torch.cat([cv.coef_1se[0, -1:].double(), lam.double(), fnp])
+
+
+def _lasso_w(Y, W, X, pf_w, seed, nfolds, fold_stream, method, device, dtype, dist, graph):
+    pan = _lasso_w_panel(Y, W, X, seed, nfolds, fold_stream, device, dtype, dist)
+    if graph and dist is None and pan.data.is_cuda:
+        out, g = estimator_graphs.run("lasso_w", _lasso_w_body, (pan,), float(pf_w))
+        v = out.cpu().numpy()
+        if v[2] < 0:
+            from ..utils.guards import NumericalError
+            raise NumericalError("CV fold path timed out waiting for its full-data lambda "
+                                 "sequence; selection is invalid")
+        return AteResult.make(method, float(v[0]), None, lambda_1se=float(v[1]), hipgraph=g)
     G, counts = _sharded_gram(pan, dist)
-    pf = np.r_[np.ones(pp - 1), pf_w]
-    cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]], penalty_factor=pf, seg_counts=counts)
-    return cv.check()
+    cv = _lasso_w_cv(pan, pf_w, G, counts).check()
+    return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
+                          lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
 
 
 def lasso_single(Y, W, X, seed=1991, nfolds=10, fold_stream=5, method="Single-equation LASSO",
-                 device=None, dtype="f64", dist=None):
-    """E5 ``ate_condmean_lasso`` (ate_functions.R:89-108): W unpenalised, coef at lambda.1se."""
-    cv = _lasso_w_coef(Y, W, X, 0.0, seed, nfolds, fold_stream, device, dtype, dist)
-    return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
-                          lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
+                 device=None, dtype="f64", dist=None, graph=True):
+    """E5 ``ate_condmean_lasso`` (ate_functions.R:89-108): W unpenalised, coef at lambda.1se.
+    On a GPU: one hipGraph launch per call after the first (utils/graphs.GraphCache)."""
+    return _lasso_w(Y, W, X, 0.0, seed, nfolds, fold_stream, method, device, dtype, dist, graph)
 
 
 def lasso_usual(Y, W, X, seed=1991, nfolds=10, fold_stream=6, method="Usual LASSO", device=None,
-                dtype="f64", dist=None):
+                dtype="f64", dist=None, graph=True):
     """E6 ``ate_lasso`` (ate_functions.R:111-130): W penalised."""
-    cv = _lasso_w_coef(Y, W, X, 1.0, seed, nfolds, fold_stream, device, dtype, dist)
-    return AteResult.make(method, float(cv.coef_1se[0, -1]), None,
-                          lambda_1se=float(cv.lambdas[0, int(cv.sel[0, 1])]))
+    return _lasso_w(Y, W, X, 1.0, seed, nfolds, fold_stream, method, device, dtype, dist, graph)
 
 
 def interaction_expand(x: torch.Tensor) -> torch.Tensor:

@@ -11,6 +11,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from .devconst import const
 from .gram import gram
 from .panel import DevicePanel, dtype_code
 
@@ -40,8 +41,7 @@ def chol_solve(G: torch.Tensor, cols, rcol: int = -1, rhs: torch.Tensor | None =
                tol: float = LM_TOL, done: torch.Tensor | None = None,
                ws: SolveWorkspace | None = None) -> SolveResult:
     """Solve G[cols,cols] b = G[cols,rcol] (or rhs) with column-order aliasing (lm rule)."""
-    cols_t = cols if isinstance(cols, torch.Tensor) else torch.tensor(cols, dtype=torch.int32,
-                                                                       device=G.device)
+    cols_t = cols if isinstance(cols, torch.Tensor) else const(cols, torch.int32, G.device)
     k = cols_t.numel()
     if not G.is_cuda:
         return _chol_solve_cpu(G, cols_t.cpu().numpy(), rcol, rhs, tol)
@@ -93,8 +93,7 @@ def predict(panel: DevicePanel, cols, beta: torch.Tensor, override_idx: int = -1
             out: torch.Tensor | None = None) -> torch.Tensor:
     """eta = X[:, cols] beta (NaN beta = aliased -> 0); optional constant override of one
     design column (counterfactual W); link 'logit' applies the logistic function."""
-    cols_t = cols if isinstance(cols, torch.Tensor) else torch.tensor(cols, dtype=torch.int32,
-                                                                       device=panel.device)
+    cols_t = cols if isinstance(cols, torch.Tensor) else const(cols, torch.int32, panel.device)
     lk = 1 if link == "logit" else 0
     if not panel.data.is_cuda:
         X = panel.data.double()[cols_t.long()].clone()
@@ -129,7 +128,7 @@ def logistic_irls(panel: DevicePanel, cols, ycol: int, zcol: int, maxit: int = 2
     iteration all-reduces the weighted Gram and the deviance partials (C01/C02), so
     every rank takes the same Newton step and the same convergence decision."""
     dev = panel.device
-    cols_t = torch.tensor(cols, dtype=torch.int32, device=dev)
+    cols_t = const(cols, torch.int32, dev)
     k = len(cols)
     if not panel.data.is_cuda:
         return _irls_cpu(panel, cols, ycol, zcol, maxit, eps, dist)

@@ -39,6 +39,7 @@ class DevicePanel:
     seg_nreal: np.ndarray              # (nseg,) real rows per segment
     row_index: torch.Tensor            # (ld,) original row id (-1 on padding)
     xcols: list = field(default_factory=list)
+    identity: bool = False             # real rows are rows 0..n-1 in order (one segment)
 
     @property
     def P(self):
@@ -69,12 +70,17 @@ class DevicePanel:
     def gather_rows(self, v: torch.Tensor) -> torch.Tensor:
         """Map a per-original-row vector into panel row order (0 on padding)."""
         out = torch.zeros(self.ld, dtype=v.dtype, device=self.device)
+        if self.identity:                 # no mask indexing: no host sync, capturable
+            out[:self.n] = v.to(self.device)
+            return out
         m = self.row_index >= 0
         out[m] = v.to(self.device)[self.row_index[m]]
         return out
 
     def scatter_rows(self, v: torch.Tensor) -> torch.Tensor:
         """Map a panel-ordered vector (rows on dim 0) back to original row order."""
+        if self.identity:
+            return v[:self.n].clone()
         m = self.row_index >= 0
         out = torch.empty((self.n,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
         out[self.row_index[m]] = v[m]
@@ -170,7 +176,7 @@ def build_panel(X, W=None, Y=None, folds=None, dtype="f64", device="cpu", extra_
     return DevicePanel(data=data, n=n, cols=cols, seg_bounds=seg_bounds,
                        seg_nreal=counts.astype(np.int64),
                        row_index=torch.from_numpy(row_index).to(device),
-                       xcols=[cols[f"x{j}"] for j in range(p)])
+                       xcols=[cols[f"x{j}"] for j in range(p)], identity=K == 1)
 
 
 def empty_panel(n_per_seg, P, dtype="bf16", device="cpu"):
@@ -187,4 +193,4 @@ def empty_panel(n_per_seg, P, dtype="bf16", device="cpu"):
         base += int(c)
     return DevicePanel(data=data, n=int(counts.sum()), cols={"one": 0},
                        seg_bounds=np.stack([starts, starts + padded], axis=1),
-                       seg_nreal=counts, row_index=row_index)
+                       seg_nreal=counts, row_index=row_index, identity=len(counts) == 1)

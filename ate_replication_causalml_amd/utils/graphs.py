@@ -163,3 +163,79 @@ class SegmentedStep:
                 g[0].replay()
                 state = g[1]
         return state
+
+
+def _data(x):
+    """The device buffer behind an estimator input (a tensor, or a DevicePanel's data)."""
+    return x if isinstance(x, torch.Tensor) else x.data
+
+
+def layout_key(*inputs):
+    """Everything a captured body's launch sequence depends on: tensor shapes / dtypes /
+    devices and, for panels, the column map, fold segments and real-row counts."""
+    key = []
+    for x in inputs:
+        t = _data(x)
+        k = (tuple(t.shape), t.dtype, str(t.device))
+        if not isinstance(x, torch.Tensor):
+            k += (x.n, tuple(sorted(x.cols.items())), tuple(map(tuple, x.seg_bounds)),
+                  tuple(int(c) for c in x.seg_nreal), bool(getattr(x, "identity", False)))
+        key.append(k)
+    return tuple(key)
+
+
+class _Captured:
+    """``body(*inputs)`` captured once over STATIC inputs (the first call's own tensors /
+    panels, kept alive here); a later call copies its data into them and replays."""
+
+    def __init__(self, body, inputs, static_args, warmup):
+        self.inputs = list(inputs)
+        self.step = GraphedStep(lambda: body(*self.inputs, *static_args), warmup)
+
+    def __call__(self, inputs):
+        for s, x in zip(self.inputs, inputs):
+            if x is not s:
+                _data(s).copy_(_data(x))
+        return self.step()
+
+
+class GraphCache:
+    """Per-estimator hipGraph cache (SURVEY.md §7.1 "every ate_*() is one hipGraph
+    launch"). ``run(name, body, inputs, *static_args)``: the first call for a (name,
+    static args, input layout) captures ``body(*inputs, *static_args)`` — a device-only
+    function of the inputs
+    (fixed launch budgets, device flags, cached constants; no host sync) — and later
+    calls with the same key replay it: one graph launch per estimator call. LRU of
+    ``maxsize`` entries (each holds its input buffers and the graph's memory pool).
+    A body that cannot be captured is remembered and runs eagerly from then on.
+    Outputs are the graph's static tensors: read them before the next call."""
+
+    def __init__(self, maxsize: int = 8):
+        self.maxsize = maxsize
+        self.entries: dict = {}
+        self.eager: set = set()
+
+    def run(self, name, body, inputs, *static_args, warmup: int = 1):
+        key = (name, static_args, layout_key(*inputs))
+        if key in self.eager:
+            return body(*inputs, *static_args), False
+        g = self.entries.pop(key, None)
+        if g is None:
+            while len(self.entries) >= self.maxsize:
+                self.entries.pop(next(iter(self.entries)))
+            try:
+                g = _Captured(body, inputs, static_args, warmup)
+            except Exception as e:  # noqa: BLE001 - fall back to eager, but say why
+                print(f"[graphs] {name}: capture failed, running eagerly: {e}", flush=True)
+                torch.cuda.synchronize()
+                self.eager.add(key)
+                return body(*inputs, *static_args), False
+        self.entries[key] = g
+        return g(inputs), True
+
+    def clear(self):
+        self.entries.clear()
+        self.eager.clear()
+
+
+estimator_graphs = GraphCache()
