@@ -30,7 +30,7 @@ c_double = ctypes.c_double
 # name -> argtypes (restype int). 'p' pointer, 'i' int32, 'l' int64, 'u' uint64, 'd' double
 _SIGS = {
     "ate_gram_bf16": "pliipipipippp",
-    "ate_gram_bf16_pair": "plipippipippp",
+    "ate_gram_bf16_pair": "pllipippipippp",
     "ate_gram_f32": "plippipipipppp",
     "ate_gram_f64": "plippipipipppp",
     "ate_gram_tile_sizes": "pppp",
@@ -51,10 +51,10 @@ _SIGS = {
     "ate_enet_cvloss_gauss": "pippiipppiiipp",
     "ate_cv_select": "pppiipipppp",
     "ate_enet_pick": "ppiiiipp",
-    "ate_dml_resid_moments": "iplpipipiiiiiippp",
+    "ate_dml_resid_moments": "ipllpipipiiiiiippp",
     "ate_lognet_path": "iplpiipipipdddippippppppppp",
     "ate_lognet_cvloss": "iplpiippipppipp",
-    "ate_dgp_fill": "ipllllu" + "iip",
+    "ate_dgp_fill": "iplllllu" + "iip",
     "ate_forest_fit": "pppppi" + "ppppppppp",
     "ate_forest_predict": "ppiiipppppippip",
     "ate_forest_pack": "pippppppp",

@@ -30,7 +30,8 @@ def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1):
 
 
 def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991,
-                    dtype: str = "bf16", device="cpu", rank: int = 0, world: int = 1) -> DevicePanel:
+                    dtype: str = "bf16", device="cpu", rank: int = 0, world: int = 1,
+                    blocked: bool = False) -> DevicePanel:
     if p < N_TUTORIAL_COLS:
         raise ValueError("p must be >= 21 (tutorial columns)")
     p_extra = p - N_TUTORIAL_COLS
@@ -41,7 +42,7 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
         names += ["W_hi", "W_lo", "Y_hi", "Y_lo"]
     align = 128 if dtype == "bf16" else 64
     P = (len(names) + align - 1) // align * align
-    pan = empty_panel([c for _, c in slices], P, dtype=dtype, device=device)
+    pan = empty_panel([c for _, c in slices], P, dtype=dtype, device=device, blocked=blocked)
     pan.cols = {nm: i for i, nm in enumerate(names)}
     pan.xcols = [pan.cols[f"x{j}"] for j in range(p)]
     # global row ids of this shard (panel order)
@@ -53,15 +54,18 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
     if pan.data.is_cuda:
         s = torch.cuda.current_stream().cuda_stream
         for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
-            _native.call("ate_dgp_fill", dtype_code(pan.data), pan.data.data_ptr(), pan.ld,
-                         int(r0), cnt, g0, seed, p_extra, int(hi_lo), s)
+            _native.call("ate_dgp_fill", dtype_code(pan.data), pan.data.data_ptr(),
+                         *pan.strides(), int(r0), cnt, g0, seed, p_extra, int(hi_lo), s)
     else:
+        cm = torch.zeros((pan.P, pan.ld), dtype=pan.data.dtype) if blocked else pan.data
         for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
             cts, binc, extra, W, Y, _ = host_dgp.raw_columns(cnt, seed, p_extra, row_offset=g0)
             cols = [np.ones(cnt), *cts.T, *binc.T, *extra.T, W, Y]
             if hi_lo:
                 cols += [W, np.zeros(cnt), Y, np.zeros(cnt)]
             block = torch.from_numpy(np.stack(cols)).to(pan.data.dtype)
-            pan.data[:block.shape[0], r0:r0 + cnt] = block
+            cm[:block.shape[0], r0:r0 + cnt] = block
+        if blocked:
+            pan.data.copy_(cm.reshape(pan.P, -1, 64).permute(1, 0, 2))
     pan.n = sum(c for _, c in slices)
     return pan

@@ -83,7 +83,7 @@ def bin_panel(pan, edges=None, edge_rows=200_000):
     e, ne = t(edges[0], torch.float64), t(edges[1], torch.int32)
     xci = t(np.asarray(pan.xcols), torch.int32)
     r0t, nrt, c0t = t(r0, torch.int64), t(nr, torch.int64), t(c0, torch.int64)
-    _native.call("ate_gbdt_bin_panel", X.data_ptr(), code, pan.ld, xci.data_ptr(), p,
+    _native.call("ate_gbdt_bin_panel", X.data_ptr(), code, pan.cm_ld, xci.data_ptr(), p,
                  r0t.data_ptr(), nrt.data_ptr(), c0t.data_ptr(), pan.nseg, n, e.data_ptr(),
                  ne.data_ptr(), Xr.data_ptr(), ldr, torch.cuda.current_stream().cuda_stream)
     return Xr, ldr, edges, rows
@@ -99,8 +99,8 @@ def dml_plr_gbdt_panel(pan, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0
     K = pan.nseg
     nr = np.asarray(pan.seg_nreal, dtype=np.int64)
     n = int(nr.sum())
-    Yn = pan.data[pan.cols["Y"]].index_select(0, rows).double().cpu().numpy()
-    Wn = pan.data[pan.cols["W"]].index_select(0, rows).double().cpu().numpy()
+    Yn = pan.col("Y").index_select(0, rows).double().cpu().numpy()
+    Wn = pan.col("W").index_select(0, rows).double().cpu().numpy()
     fid = np.repeat(np.arange(K), nr)
     kw = dict(n_trees=n_trees, depth=depth, lr=lr, lam=lam, min_child=min_child,
               backend="gpu", edges=edges, Xb=(Xr, ldr))

@@ -171,8 +171,8 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     nr = np.asarray(pan.seg_nreal, dtype=np.int64)
     c0 = np.concatenate([[0], np.cumsum(nr)]).astype(np.int64)
     n = int(c0[-1])
-    Y = pan.data[pan.cols["Y"]].index_select(0, rows).double()
-    W = pan.data[pan.cols["W"]].index_select(0, rows).double()
+    Y = pan.col("Y").index_select(0, rows).double()
+    W = pan.col("W").index_select(0, rows).double()
     if comm is not None and comm.world_size > 1:
         rank, world = comm.rank, comm.world_size
     elif tree_shard is not None:

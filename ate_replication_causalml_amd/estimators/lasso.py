@@ -225,7 +225,7 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
     K = coef.shape[0]
     p = len(pan.xcols)
     if not pan.data.is_cuda:
-        X = pan.data.double()
+        X = pan.colmajor().double()
         moms = torch.zeros(7, dtype=torch.float64)
         for k in range(K):
             r0, r1 = pan.seg_bounds[k]
@@ -249,7 +249,8 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
     # binary Y/W are exact in bf16; continuous targets use the hi+lo split columns
     y0, y1 = (pan.cols["Y_hi"], pan.cols["Y_lo"]) if bf else (pan.cols["Y"], -1)
     w0, w1 = (pan.cols["W_hi"], pan.cols["W_lo"]) if bf else (pan.cols["W"], -1)
-    _native.call("ate_dml_resid_moments", dtype_code(pan.data), pan.data.data_ptr(), pan.ld,
+    cs, bs = pan.strides()
+    _native.call("ate_dml_resid_moments", dtype_code(pan.data), pan.data.data_ptr(), cs, bs,
                  xc.data_ptr(), p, segs.data_ptr(), K, coef.data_ptr(), y0, y1, w0, w1,
                  pan.cols["one"], nbx, part.data_ptr(), mom.data_ptr(),
                  torch.cuda.current_stream().cuda_stream)

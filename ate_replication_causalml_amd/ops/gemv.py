@@ -22,7 +22,7 @@ def xtv(panel, cols, v: torch.Tensor, grp: torch.Tensor, A: int) -> torch.Tensor
         return torch.stack([M @ torch.where(grp == a, v, torch.zeros_like(v)) for a in range(A)])
     out = torch.empty((A, len(cols)), dtype=torch.float64, device=X.device)
     c = _cols(panel, cols)
-    _native.call("ate_panel_xtv", dtype_code(X), X.data_ptr(), panel.ld, c.data_ptr(), len(cols),
+    _native.call("ate_panel_xtv", dtype_code(X), X.data_ptr(), panel.cm_ld, c.data_ptr(), len(cols),
                  v.contiguous().data_ptr(), grp.data_ptr(), panel.ld, A, out.data_ptr(),
                  torch.cuda.current_stream().cuda_stream)
     return out
@@ -38,7 +38,7 @@ def xv(panel, cols, V: torch.Tensor, grp: torch.Tensor) -> torch.Tensor:
         return torch.where(g >= 0, out, torch.zeros_like(out))
     out = torch.empty(panel.ld, dtype=torch.float64, device=X.device)
     c = _cols(panel, cols)
-    _native.call("ate_panel_xv", dtype_code(X), X.data_ptr(), panel.ld, c.data_ptr(), len(cols),
+    _native.call("ate_panel_xv", dtype_code(X), X.data_ptr(), panel.cm_ld, c.data_ptr(), len(cols),
                  V.contiguous().double().data_ptr(), V.shape[0], grp.data_ptr(), panel.ld,
                  out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     return out

@@ -185,18 +185,19 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     G = pl.G if out is None else out
     s = _stream()
     if X.dtype == torch.bfloat16 and pl.pair:
-        _native.call("ate_gram_bf16_pair", X.data_ptr(), panel.ld, panel.P, pl.tiles.data_ptr(),
+        cs, bs = panel.strides()
+        _native.call("ate_gram_bf16_pair", X.data_ptr(), cs, bs, panel.P, pl.tiles.data_ptr(),
                      pl.ntiles, pl.blocks.data_ptr(), pl.chunks.data_ptr(), pl.nchunks,
                      pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
     elif X.dtype == torch.bfloat16:
-        _native.call("ate_gram_bf16", X.data_ptr(), panel.ld, panel.P, pl.T, pl.tiles.data_ptr(),
+        _native.call("ate_gram_bf16", X.data_ptr(), panel.cm_ld, panel.P, pl.T, pl.tiles.data_ptr(),
                      pl.ntiles, pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(),
                      panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
     else:
         name = "ate_gram_f64" if X.dtype == torch.float64 else "ate_gram_f32"
         if w is not None:
             assert w.dtype == X.dtype and w.numel() == panel.ld
-        _native.call(name, X.data_ptr(), panel.ld, panel.P, 0 if w is None else w.data_ptr(),
+        _native.call(name, X.data_ptr(), panel.cm_ld, panel.P, 0 if w is None else w.data_ptr(),
                      pl.tiles.data_ptr(), pl.ntiles, pl.chunks.data_ptr(), pl.nchunks,
                      pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(),
                      0 if done is None else done.data_ptr(), s)
@@ -204,7 +205,7 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
 
 
 def _gram_cpu(panel, w, out):
-    X = panel.data.double()
+    X = panel.colmajor().double()
     Gs = []
     for (r0, r1) in panel.seg_bounds:
         Xs = X[:, r0:r1]

@@ -103,7 +103,7 @@ def predict(panel: DevicePanel, cols, beta: torch.Tensor, override_idx: int = -1
         eta = b @ X
         return torch.sigmoid(eta) if lk else eta
     out = out if out is not None else torch.empty(panel.ld, dtype=torch.float64, device=panel.device)
-    _native.call("ate_predict", dtype_code(panel.data), panel.data.data_ptr(), panel.ld, panel.ld,
+    _native.call("ate_predict", dtype_code(panel.data), panel.data.data_ptr(), panel.cm_ld, panel.ld,
                  cols_t.data_ptr(), beta.data_ptr(), cols_t.numel(), override_idx, override_val, lk,
                  out.data_ptr(), _stream())
     return out
@@ -143,7 +143,7 @@ def logistic_irls(panel: DevicePanel, cols, ycol: int, zcol: int, maxit: int = 2
     dc = dtype_code(panel.data)
     s = _stream()
     X = panel.data
-    _native.call("ate_irls_update", dc, X.data_ptr(), panel.ld, panel.ld, cols_t.data_ptr(),
+    _native.call("ate_irls_update", dc, X.data_ptr(), panel.cm_ld, panel.ld, cols_t.data_ptr(),
                  ws.beta.data_ptr(), k, ycol, panel.cols["one"], zcol, 1, eta.data_ptr(),
                  mu.data_ptr(), w.data_ptr(), devp.data_ptr(), nb, done.data_ptr(), s)
     if dist is not None:
@@ -161,7 +161,7 @@ def logistic_irls(panel: DevicePanel, cols, ycol: int, zcol: int, maxit: int = 2
         if dist is not None:
             dist.sum_(G)
         chol_solve(G, cols_t, zcol, done=done, ws=ws)
-        _native.call("ate_irls_update", dc, X.data_ptr(), panel.ld, panel.ld, cols_t.data_ptr(),
+        _native.call("ate_irls_update", dc, X.data_ptr(), panel.cm_ld, panel.ld, cols_t.data_ptr(),
                      ws.beta.data_ptr(), k, ycol, panel.cols["one"], zcol, 0, eta.data_ptr(),
                      mu.data_ptr(), w.data_ptr(), devp.data_ptr(), nb, done.data_ptr(), s)
         if dist is not None:

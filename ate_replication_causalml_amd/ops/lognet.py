@@ -92,25 +92,25 @@ def cv_lognet(panel, xcols, ycol, penalty_factor=None, alpha=1.0, nlambda=100,
         # folds following the full fit's lambda sequence and stop through device flags
         progress = torch.zeros(2, dtype=torch.int32, device=dev)
         lampub = torch.zeros(L, **f64)
-        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.cm_ld, xc.data_ptr(), p, ycol,
                      segs_t.data_ptr(), K, masks_t.data_ptr(), nq, vp_t.data_ptr(), alpha,
                      flmin, thresh, maxit, 0, 0, L, a0.data_ptr(), beta.data_ptr(),
                      lam.data_ptr(), devr.data_ptr(), nlam.data_ptr(), npass.data_ptr(),
                      progress.data_ptr(), lampub.data_ptr(), s)
     else:
         # full problem: its own lambda sequence
-        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.cm_ld, xc.data_ptr(), p, ycol,
                      segs_t.data_ptr(), K, masks_t.data_ptr(), 1, vp_t.data_ptr(), alpha, flmin,
                      thresh, maxit, 0, 0, L, a0.data_ptr(), beta.data_ptr(), lam.data_ptr(),
                      devr.data_ptr(), nlam.data_ptr(), npass.data_ptr(), 0, 0, s)
         # fold problems on the full lambda sequence (count read on the device)
-        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+        _native.call("ate_lognet_path", dt, X.data_ptr(), panel.cm_ld, xc.data_ptr(), p, ycol,
                      segs_t.data_ptr(), K, off(masks_t), K, vp_t.data_ptr(), alpha, flmin,
                      thresh, maxit, lam.data_ptr(), nlam.data_ptr(), L, off(a0), off(beta),
                      off(lam), off(devr), nlam.data_ptr() + 4, npass.data_ptr() + 4, 0, 0, s)
     hold = torch.arange(K, dtype=torch.int32, device=dev)
     cvraw = torch.empty((K, L), **f64)
-    _native.call("ate_lognet_cvloss", dt, X.data_ptr(), panel.ld, xc.data_ptr(), p, ycol,
+    _native.call("ate_lognet_cvloss", dt, X.data_ptr(), panel.cm_ld, xc.data_ptr(), p, ycol,
                  segs_t.data_ptr(), hold.data_ptr(), K, off(a0), off(beta),
                  nlam.data_ptr() + 4, L, cvraw.data_ptr(), s)
     fidx = torch.arange(K, dtype=torch.int32, device=dev)[None]

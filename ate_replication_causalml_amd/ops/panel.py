@@ -40,14 +40,33 @@ class DevicePanel:
     row_index: torch.Tensor            # (ld,) original row id (-1 on padding)
     xcols: list = field(default_factory=list)
     identity: bool = False             # real rows are rows 0..n-1 in order (one segment)
+    # 64-row blocked layout: data is [ld/64, P, 64], element (c, i) at
+    # (i/64)*64*P + c*64 + i%64. One Gram K-step (64 rows x all P columns) is then one
+    # contiguous 64*P*2-byte run of HBM instead of P runs of 128 bytes ld apart
+    # (profiles/r01_pmc/gram_diag.txt). Kernels that take (cs, bs) strides read both
+    # layouts; the others require column-major (``cm_ld`` raises).
+    blocked: bool = False
 
     @property
     def P(self):
-        return self.data.shape[0]
+        return self.data.shape[1] if self.blocked else self.data.shape[0]
 
     @property
     def ld(self):
+        """Padded row count (and the column stride of a column-major panel)."""
+        return self.data.shape[0] * ROW_ALIGN if self.blocked else self.data.shape[1]
+
+    @property
+    def cm_ld(self):
+        """Leading dimension for kernels that only read column-major panels."""
+        if self.blocked:
+            raise NotImplementedError("this kernel reads column-major panels only; build the "
+                                      "panel with blocked=False")
         return self.data.shape[1]
+
+    def strides(self):
+        """(cs, bs): element (c, i) at c*cs + (i/64)*bs + i%64."""
+        return (ROW_ALIGN, ROW_ALIGN * self.P) if self.blocked else (self.ld, ROW_ALIGN)
 
     @property
     def device(self):
@@ -62,10 +81,17 @@ class DevicePanel:
         return len(self.seg_bounds)
 
     def col(self, name) -> torch.Tensor:
-        return self.data[self.cols[name]]
+        c = self.cols[name]
+        return self.data[:, c, :].reshape(-1) if self.blocked else self.data[c]
 
     def valid(self) -> torch.Tensor:
-        return self.data[self.cols["one"]]
+        return self.col("one")
+
+    def colmajor(self) -> torch.Tensor:
+        """[P, ld] column-major view (a copy for a blocked panel)."""
+        if not self.blocked:
+            return self.data
+        return self.data.permute(1, 0, 2).reshape(self.P, self.ld)
 
     def gather_rows(self, v: torch.Tensor) -> torch.Tensor:
         """Map a per-original-row vector into panel row order (0 on padding)."""
@@ -179,13 +205,14 @@ def build_panel(X, W=None, Y=None, folds=None, dtype="f64", device="cpu", extra_
                        xcols=[cols[f"x{j}"] for j in range(p)], identity=K == 1)
 
 
-def empty_panel(n_per_seg, P, dtype="bf16", device="cpu"):
+def empty_panel(n_per_seg, P, dtype="bf16", device="cpu", blocked=False):
     """Allocate a panel with the given real rows per segment (filled later on device)."""
     counts = np.asarray(n_per_seg, dtype=np.int64)
     padded = np.array([_round_up(max(int(c), 1), ROW_ALIGN) for c in counts])
     starts = np.concatenate([[0], np.cumsum(padded)[:-1]])
     ld = int(padded.sum())
-    data = torch.zeros((P, ld), dtype=_dtype(dtype), device=device)
+    shape = (ld // ROW_ALIGN, P, ROW_ALIGN) if blocked else (P, ld)
+    data = torch.zeros(shape, dtype=_dtype(dtype), device=device)
     row_index = torch.full((ld,), -1, dtype=torch.int64, device=device)
     base = 0
     for s, c in zip(starts, counts):
@@ -193,4 +220,5 @@ def empty_panel(n_per_seg, P, dtype="bf16", device="cpu"):
         base += int(c)
     return DevicePanel(data=data, n=int(counts.sum()), cols={"one": 0},
                        seg_bounds=np.stack([starts, starts + padded], axis=1),
-                       seg_nreal=counts, row_index=row_index, identity=len(counts) == 1)
+                       seg_nreal=counts, row_index=row_index, identity=len(counts) == 1,
+                       blocked=blocked)

@@ -11,10 +11,14 @@ fused held-out residual pass + orthogonal-score moments (csrc/dml.hip) ->
 all-reduce of the moments (C06) -> theta / SE on device.
 Nothing is cached across steps; every nuisance is refit each step.
 
-Two cross-fits are in flight at every world size (``--inflight 2``): ``ms_per_step`` is
+Three cross-fits are in flight at every world size (``--inflight 3``): ``ms_per_step`` is
 the wall time per completed cross-fit (throughput); ``single_fit_ms`` in the JSON is the
-latency of one cross-fit alone. With RCCL the device phases are still graph replays;
-only the two all-reduces run eagerly between them (utils/graphs.SegmentedStep).
+latency of one cross-fit alone. The Grams of all fits run back to back on one
+low-priority stream; each fit's path solve / residual pass / score runs on its own
+high-priority stream beside the next fit's Gram (``--stagger 2``). The panel uses the
+64-row blocked layout (``--blocked 1``: one contiguous HBM run per Gram K-step). With
+RCCL the device phases are still graph replays; only the two all-reduces run eagerly
+between them (utils/graphs.SegmentedStep).
 
 Scaling: weak by default (N=1e7 rows per GPU; at N=1 GPU this is exactly the
 BASELINE config); ``--scaling strong`` keeps N=1e7 in total.
@@ -61,6 +65,15 @@ def main():
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step's device phases in hipGraphs (default: on with a GPU; "
                          "RCCL collectives always run eagerly between the graph replays)")
+    ap.add_argument("--blocked", type=int, default=1,
+                    help="1: 64-row blocked panel layout (one contiguous HBM run per Gram "
+                         "K-step, ops/panel.py); 0: column-major")
+    ap.add_argument("--stagger", type=int, default=2,
+                    help="1: a fit's Gram waits for the previous fit's Gram (event between "
+                         "the streams), so one fit's Gram overlaps the other's path solve "
+                         "instead of both Grams, then both paths, running together; 2: the "
+                         "Grams of all fits run on one low-priority stream and the rest of "
+                         "each fit on its own high-priority stream")
     ap.add_argument("--inflight", type=int, default=-1,
                     help="independent cross-fits in flight (one hipGraph + stream + Gram "
                          "workspace each); every timed step is still one complete DML-ATE")
@@ -81,6 +94,7 @@ def main():
         device = torch.device("cpu")
     n_total = int(args.rows) * (world if args.scaling == "weak" else 1)
     pan = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed, dtype=args.dtype,
+                          blocked=bool(args.blocked) and args.dtype == "bf16",
                           device=device, rank=rank, world=world)
 
     def sync():
@@ -93,14 +107,14 @@ def main():
     from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
     from ate_replication_causalml_amd.ops.gram import plan_slot
     use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
-    # Two independent cross-fits in flight at EVERY world size (same setting for the whole
+    # Independent cross-fits in flight at EVERY world size (same setting for the whole
     # 1/2/4/8 curve): the CV path solve is a latency-bound serial recurrence that fills few
     # CUs, so a second fit's HBM-bound Gram runs beside it on its own stream.
-    inflight = 2 if args.inflight < 0 else max(1, args.inflight)
+    inflight = 3 if args.inflight < 0 else max(1, args.inflight)
     if inflight > 1:
         # sharing the chip with the other fit's path solve, fewer and longer Gram workgroups
         # win (profiles/r01_bench/wg_inflight.log: 1024 -> 5.9 ms/step, 2048 -> 6.1)
-        os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024")
+        os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024" if not args.stagger else "2048")
 
     def in_slot(ph, i):
         if isinstance(ph, Collective):
@@ -111,12 +125,72 @@ def main():
                 return ph(st)
         return f
 
+    # Stagger: with two fits started together on two streams, the two Grams share the chip
+    # and then the two path solves leave it mostly idle, a lockstep that persists (both
+    # fits are identical). One event orders the Grams across the streams: fit k's Gram
+    # starts when fit k-1's Gram has finished, so each Gram runs beside the other fit's
+    # path solve. The hooks are eager phases between the captured graphs (the fit is
+    # split into a Gram graph and a path/residual/score graph).
+    gram_done = {"ev": None}
+
+    def wait_prev_gram(st):
+        if gram_done["ev"] is not None:
+            torch.cuda.current_stream().wait_event(gram_done["ev"])
+        return st
+
+    def record_gram(st):
+        ev = torch.cuda.Event()
+        ev.record()
+        gram_done["ev"] = ev
+        return st
+
+    gram_stream = None
+    fit_streams = []
+    if args.stagger == 2 and inflight > 1 and device.type == "cuda":
+        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
+            else (0, -1)
+        gram_stream = torch.cuda.Stream(device, priority=lo)
+        fit_streams = [torch.cuda.Stream(device, priority=hi) for _ in range(inflight)]
+        fit_done = [None] * inflight
+
+    def split_streams(i):
+        # Gram of fit i on the shared low-priority stream (after fit i's previous solve
+        # has consumed the previous Gram), the rest on fit i's high-priority stream
+        def to_gram(st):
+            if fit_done[i] is not None:
+                gram_stream.wait_event(fit_done[i])
+            torch.cuda.set_stream(gram_stream)
+            return st
+
+        def to_fit(st):
+            ev = torch.cuda.Event()
+            ev.record(gram_stream)
+            fit_streams[i].wait_event(ev)
+            torch.cuda.set_stream(fit_streams[i])
+            return st
+
+        def done(st):
+            ev = torch.cuda.Event()
+            ev.record(fit_streams[i])
+            fit_done[i] = ev
+            return st
+        return to_gram, to_fit, done
+
+    def staggered(phases, i):
+        if not (args.stagger and inflight > 1 and device.type == "cuda"):
+            return phases
+        if gram_stream is not None:
+            to_gram, to_fit, done = split_streams(i)
+            return [Collective(to_gram), phases[0], Collective(to_fit), *phases[1:],
+                    Collective(done)]
+        return [Collective(wait_prev_gram), phases[0], Collective(record_gram), *phases[1:]]
+
     def make_run(i):
         # device phases captured one hipGraph each; RCCL collectives (world > 1) run
         # eagerly between the replays, so capture is local and identical on every rank
         with plan_slot(i):      # private Gram workspace per in-flight fit
-            phases = [in_slot(ph, i) for ph in
-                      dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts)]
+            phases = [in_slot(ph, i) for ph in staggered(
+                dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts), i)]
             try:
                 return SegmentedStep(phases, graph=use_graph), None
             except Exception as e:  # noqa: BLE001 - reported, then every rank goes eager
@@ -124,8 +198,11 @@ def main():
                 return SegmentedStep(phases, graph=False, warmup=0), repr(e)
 
     runs, errors = [], []
+    home = torch.cuda.current_stream() if device.type == "cuda" else None
     for i in range(inflight):
         r, err = make_run(i)
+        if home is not None:
+            torch.cuda.set_stream(home)     # stream-switching phases leave another current
         runs.append(r)
         errors.append(err)
     ok = torch.tensor([float(all(r.graphed for r in runs) if use_graph else 0)], device=device)
@@ -176,7 +253,7 @@ def main():
     sync()
     t1 = time.perf_counter()
     for k in range(nlat):
-        runs[0]()
+        run_step(0)
         sync()
     lat = torch.tensor([(time.perf_counter() - t1) / nlat], dtype=torch.float64, device=device)
     comm.all_reduce_max_(lat)
@@ -211,6 +288,8 @@ def main():
                 "folds": args.folds,
                 "parallelism": f"dp{world}",
                 "inflight": len(runs),
+                "layout": "blocked64" if pan.blocked else "colmajor",
+                "stagger": bool(args.stagger and len(runs) > 1 and device.type == "cuda"),
             },
             "ate": ate,
             "se": se,

@@ -19,17 +19,23 @@ __device__ __forceinline__ float dgp_uniform(uint64_t seed, uint32_t stream, uin
   return (float)(w.x >> 8) * (1.0f / 16777216.0f);
 }
 
+// element (c, i) at c*cs + (i/64)*bs + i%64: column-major panels (cs = ld, bs = 64) or
+// 64-row blocked panels (cs = 64, bs = 64*P; ops/panel.py DevicePanel.blocked)
+__device__ __forceinline__ int64_t pidx(int c, int64_t i, int64_t cs, int64_t bs) {
+  return (int64_t)c * cs + (i >> 6) * bs + (i & 63);
+}
 template <typename T>
-__device__ __forceinline__ void put(T* X, int64_t ld, int c, int64_t i, float v) {
-  X[(int64_t)c * ld + i] = (T)v;
+__device__ __forceinline__ void put(T* X, int64_t cs, int64_t bs, int c, int64_t i, float v) {
+  X[pidx(c, i, cs, bs)] = (T)v;
 }
 template <>
-__device__ __forceinline__ void put<bf16_t>(bf16_t* X, int64_t ld, int c, int64_t i, float v) {
-  X[(int64_t)c * ld + i] = f32_to_bf16_rne(v);
+__device__ __forceinline__ void put<bf16_t>(bf16_t* X, int64_t cs, int64_t bs, int c, int64_t i,
+                                            float v) {
+  X[pidx(c, i, cs, bs)] = f32_to_bf16_rne(v);
 }
 
 template <typename T>
-__global__ void dgp_fill_kernel(T* __restrict__ X, int64_t ld, int64_t row0, int64_t count,
+__global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64_t row0, int64_t count,
                                 int64_t gid0, uint64_t seed, int p_extra, int hi_lo) {
   const float FL = 0.6f, FS = 0.8f;  // factor loading, sqrt(1 - 0.36)
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < count;
@@ -38,55 +44,55 @@ __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t ld, int64_t row0, int
     const int64_t i = row0 + r;
     const float f = dgp_normal(seed, 40, g);
     int c = 0;
-    put(X, ld, c++, i, 1.0f);
+    put(X, cs, bs, c++, i, 1.0f);
     float yob = 0.f;
     for (int j = 0; j < 15; ++j) {
       float z = dgp_normal(seed, j, g);
       float v = j < 3 ? z : FL * f + FS * z;
       if (j == 0) yob = v;
-      put(X, ld, c++, i, v);
+      put(X, cs, bs, c++, i, v);
     }
     const float latent = dgp_normal(seed, 41, g) + 0.3f * yob;
     const float sex = dgp_uniform(seed, 60, g) < 0.5f ? 1.f : 0.f;
-    put(X, ld, c++, i, sex);
+    put(X, cs, bs, c++, i, sex);
     float hsum = 0.f;
     for (int k = 0; k < 5; ++k) {
       float h = (dgp_normal(seed, 50 + k, g) + 0.5f * latent > 0.6f) ? 1.f : 0.f;
       hsum += h;
-      put(X, ld, c++, i, h);
+      put(X, cs, bs, c++, i, h);
     }
     for (int j = 0; j < p_extra; ++j) {
       float z = dgp_normal(seed, 100 + j, g);
       float v = (j % 4 == 3) ? (z > 0.f ? 1.f : 0.f) : FL * f + FS * z;
-      put(X, ld, c++, i, v);
+      put(X, cs, bs, c++, i, v);
     }
     const float w = dgp_uniform(seed, 61, g) < (1.0f / 6.0f) ? 1.f : 0.f;
     const float eta = -1.4f + 0.3f * hsum + 0.2f * latent + 0.45f * w;
     const float y = dgp_uniform(seed, 62, g) < 1.0f / (1.0f + expf(-eta)) ? 1.f : 0.f;
-    put(X, ld, c++, i, w);
-    put(X, ld, c++, i, y);
+    put(X, cs, bs, c++, i, w);
+    put(X, cs, bs, c++, i, y);
     if (hi_lo) {  // binary -> hi exact, lo 0
-      put(X, ld, c++, i, w);
-      put(X, ld, c++, i, 0.f);
-      put(X, ld, c++, i, y);
-      put(X, ld, c++, i, 0.f);
+      put(X, cs, bs, c++, i, w);
+      put(X, cs, bs, c++, i, 0.f);
+      put(X, cs, bs, c++, i, y);
+      put(X, cs, bs, c++, i, 0.f);
     }
   }
 }
 
 // dtype 1 f32, 2 f64, 3 bf16
-ATE_API int ate_dgp_fill(int dtype, void* X, int64_t ld, int64_t row0, int64_t count, int64_t gid0,
+ATE_API int ate_dgp_fill(int dtype, void* X, int64_t cs, int64_t bs, int64_t row0, int64_t count, int64_t gid0,
                          uint64_t seed, int p_extra, int hi_lo, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_for(count, 256, 8192)), block(256);
   if (dtype == 1)
-    hipLaunchKernelGGL(dgp_fill_kernel<float>, grid, block, 0, s, (float*)X, ld, row0, count, gid0,
+    hipLaunchKernelGGL(dgp_fill_kernel<float>, grid, block, 0, s, (float*)X, cs, bs, row0, count, gid0,
                        seed, p_extra, hi_lo);
   else if (dtype == 2)
-    hipLaunchKernelGGL(dgp_fill_kernel<double>, grid, block, 0, s, (double*)X, ld, row0, count,
+    hipLaunchKernelGGL(dgp_fill_kernel<double>, grid, block, 0, s, (double*)X, cs, bs, row0, count,
                        gid0, seed, p_extra, hi_lo);
   else if (dtype == 3)
-    hipLaunchKernelGGL(dgp_fill_kernel<bf16_t>, grid, block, 0, s, (bf16_t*)X, ld, row0, count,
+    hipLaunchKernelGGL(dgp_fill_kernel<bf16_t>, grid, block, 0, s, (bf16_t*)X, cs, bs, row0, count,
                        gid0, seed, p_extra, hi_lo);
   else
     return -1;

@@ -149,7 +149,7 @@ static int dml_resid_t(const void* X, int64_t ld, const void* xcols, int p, cons
 // load (a wave reads 1 KB contiguous per column -- Guideline 13); dot products in fp32
 // (bf16 values are exact in fp32; coefficients rounded to fp32), moments in fp64.
 __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
-    const bf16_t* __restrict__ X, int64_t ld, const int* __restrict__ xcols, int p,
+    const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const int* __restrict__ xcols, int p,
     const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
     int y0, int y1, int w0, int w1, int vcol, double* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float shf[];
@@ -169,7 +169,9 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   const Seg sg = segs[k];
   auto ld8 = [&](int c, int64_t i, float (&o)[8]) {
-    const uint4 u = *reinterpret_cast<const uint4*>(X + (int64_t)c * ld + i);
+    // (c, i) at c*cs + (i/64)*bs + i%64: column-major (cs = ld, bs = 64) or 64-row blocked
+    // (cs = 64, bs = 64*P); the 8 rows never straddle a block (i % 8 == 0)
+    const uint4 u = *reinterpret_cast<const uint4*>(X + (int64_t)c * cs + (i >> 6) * bs + (i & 63));
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -215,11 +217,15 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
 }
 
 // dtype 1 f32, 2 f64, 3 bf16. partial: [nseg*nbx*7]
-ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t ld, const void* xcols, int p,
+// (cs, bs): element (c, i) at c*cs + (i/64)*bs + i%64 (fp32/fp64 panels: column-major only)
+ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t cs, int64_t bs,
+                                  const void* xcols, int p,
                                   const void* segs, int nseg, const void* coef, int y0, int y1,
                                   int w0, int w1, int vcol, int nbx, void* partial, void* moments,
                                   void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (dtype != 3 && bs != 64) return -1;
+  const int64_t ld = cs;
   if (dtype == 1)
     return dml_resid_t<float>(X, ld, xcols, p, segs, nseg, coef, y0, y1, w0, w1, vcol, nbx,
                               partial, moments, s);
@@ -229,7 +235,7 @@ ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t ld, const vo
   if (dtype == 3) {
     size_t sh = (size_t)2 * (p + 1) * sizeof(float) + (size_t)p * sizeof(int);
     dim3 grid(nbx, nseg);
-    hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), sh, s, (const bf16_t*)X, ld,
+    hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), sh, s, (const bf16_t*)X, cs, bs,
                        (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
                        w0, w1, vcol, (double*)partial);
     ATE_CHECK_LAUNCH();

@@ -130,9 +130,13 @@ __global__ __launch_bounds__(256) void gram_bf16_kernel(
 // SOURCE address (chunk (l&7)^(col&7) lands at position l&7) and undone on the read.
 constexpr int GT = 256;
 constexpr int GK = 64;
+#ifndef GRAM_CPOL
+#define GRAM_CPOL 0   // cache policy of the panel stream (2 = nt), A/B builds only
+#endif
 
 __device__ __forceinline__ void glds16(const void* src, bf16_t* lds_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_base), 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_base), 16, 0,
+                                   GRAM_CPOL);
 }
 
 __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
@@ -237,7 +241,7 @@ __device__ __forceinline__ int tri_index(int m, int n) {   // m <= n < 8, row-ma
 // 36 blocks), else rectangle wave (8 A + 4 B fragments, 32 blocks). Each instantiation
 // keeps only its own accumulators live; every wave runs the same number of barriers.
 template <bool TRI>
-__device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t ld, int a0,
+__device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t cs, int64_t bs, int a0,
                                           int b0, bool haveB, bool idle, int abuf, int bbuf,
                                           int arow0, int bcol0, const Chunk& ch,
                                           bf16_t (*lds)[2][GT * GK], float* __restrict__ out) {
@@ -252,8 +256,9 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
       const int q = wid * 4 + r;
       const int col = q * 8 + (lane >> 3);
       const int cc = (lane & 7) ^ (col & 7);
-      glds16(X + (int64_t)(a0 + col) * ld + i0 + cc * 8, &lds[st][0][q * 8 * GK]);
-      if (haveB) glds16(X + (int64_t)(b0 + col) * ld + i0 + cc * 8, &lds[st][1][q * 8 * GK]);
+      const bf16_t* Xk = X + (i0 >> 6) * bs + cc * 8;      // i0: multiple of GK = 64
+      glds16(Xk + (int64_t)(a0 + col) * cs, &lds[st][0][q * 8 * GK]);
+      if (haveB) glds16(Xk + (int64_t)(b0 + col) * cs, &lds[st][1][q * 8 * GK]);
     }
   };
   auto frag = [&](const bf16_t* P_, int col, int cc) {
@@ -312,7 +317,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
 }
 
 __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
-    const bf16_t* __restrict__ X, int64_t ld, const int4* __restrict__ tiles, int ntiles,
+    const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const int4* __restrict__ tiles, int ntiles,
     const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][GT * GK];   // 128 KB
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -336,9 +341,9 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   const int base = tri ? 128 + (wid - 4) * 36 : wid * 32;
   float* out = slab + ((int64_t)c * ntiles + t) * (PAIR_SLOTS * 256) + (int64_t)base * 256;
   if (tri)
-    pair_wave<true>(X, ld, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
+    pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
   else
-    pair_wave<false>(X, ld, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
+    pair_wave<false>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
 }
 
 // blocks: [ntiles][PAIR_SLOTS] int2 (I, J) = 16-column block coordinates of the Gram (I: A
@@ -378,14 +383,14 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
   }
 }
 
-ATE_API int ate_gram_bf16_pair(const void* X, int64_t ld, int P, const void* tiles, int ntiles,
+ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, const void* tiles, int ntiles,
                                const void* blocks, const void* chunks, int nchunks,
                                const void* seg_chunk0, int nseg, void* slab, void* G,
                                void* stream) {
   if (P % (2 * GT)) return -1;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gram_bf16_pair_kernel, dim3(nchunks * ntiles), dim3(512), 0, s,
-                     (const bf16_t*)X, ld, (const int4*)tiles, ntiles, (const Chunk*)chunks,
+                     (const bf16_t*)X, cs, bs, (const int4*)tiles, ntiles, (const Chunk*)chunks,
                      nchunks, (float*)slab);
   ATE_CHECK_LAUNCH();
   const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;

@@ -13,4 +13,6 @@ tail -1 gpurun_out/bench.log
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_bench" -o bench \
   -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 > "$ROOT/gpurun_out/prof_bench.log" 2>&1 || { echo prof failed; exit 1; }
+
+python3 -c "import sys; sys.path.insert(0, '$ROOT/tools'); import timeline; timeline.overlapped(sys.argv[1], 24)" $(find $ROOT/gpurun_out/prof_bench -name "*kernel_trace.csv") > $ROOT/gpurun_out/prof_bench_timeline.txt 2>&1 || true
 echo done

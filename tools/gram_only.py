@@ -1,5 +1,5 @@
 """Run the bf16 Gram kernel alone on the N=1e7, p=500 bench panel (A/B of the 256-tile
-kernel variants, and for PMC profiling). Usage: gram_only.py [N] [pair|tile256 ...]"""
+kernel variants, and for PMC profiling). Usage: gram_only.py [N] [pair|tile256 ...]; ATE_BLOCKED=0 for a column-major panel"""
 import os
 import sys
 
@@ -11,7 +11,8 @@ from ate_replication_causalml_amd.ops import gram as gram_mod  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e7)
 variants = sys.argv[2:] or [gram_mod.GRAM_KERNEL]
-pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.device("cuda", 0))
+pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.device("cuda", 0),
+                      blocked=os.environ.get("ATE_BLOCKED", "1") == "1")
 ref = None
 for v in variants:
     gram_mod.GRAM_KERNEL = v
