@@ -158,15 +158,25 @@ def global_seg_counts(pan, comm):
     return c.numpy()
 
 
-def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G=None):
+def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G=None,
+               shard_paths=True):
     """The cross-fit DML-PLR step as phases for utils.graphs.SegmentedStep:
 
-    A  per-fold Gram stack (K01)                                   device
+    A  per-fold Gram stack (K01): tile kernel, then slab reduce     device (two phases)
     C01 all-reduce of the Gram stack over row shards               collective (world > 1)
     B  CV-LASSO paths for 5 folds x {Y, W} + inner CV, lambda.min
-       selection (K08/K09), fused held-out residual moments        device
+       selection (K08/K09)                                         device
+    C08 all-reduce of the per-fold coefficients (world > 1, sharded paths)  collective
+    B' fused held-out residual moments                             device
     C06 all-reduce of the 7 score moments                          collective (world > 1)
     C  theta / SE (fp64, on device)                                device
+
+    shard_paths (world > 1): the path solves are the N-independent part of the step, so
+    instead of every rank repeating all of them, rank r solves the outer folds
+    k = r, r + world, ... (each outer fold's full-data and inner-CV problems together)
+    and the coefficients are summed over ranks (zeros elsewhere, so the sum is exact and
+    the result equals the unsharded step bit for bit). Each rank's path launch then
+    holds a fifth (or less) of the CUs it would, and the Gram beside it runs faster.
 
     Every phase maps a state dict to a state dict; device phases touch only tensors
     whose storage is static across calls, so each can be captured in its own hipGraph
@@ -178,15 +188,41 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     K = folds
     full_sets = [[s for s in range(K) if s != k] for k in range(K)]
     ycols = [pan.cols["Y"], pan.cols["W"]]
+    sharded = dist and shard_paths
+    mine = [k for k in range(K) if k % comm.world_size == comm.rank] if sharded else list(range(K))
+    p1 = len(pan.xcols) + 1
 
     def phase_gram(_):
-        return {"G": gram(pan) if G is None else G}
+        return {"G": gram(pan, stage="tiles") if G is None else G}
+
+    def phase_gram_reduce(st):
+        return st if G is not None else {"G": gram(pan, stage="reduce", out=st["G"])}
+
+    def fit(st):
+        if not mine:
+            return None
+        cv = cv_enet_gaussian(st["G"], pan, pan.xcols, ycols,
+                              full_sets=[full_sets[k] for k in mine], seg_counts=seg_counts)
+        return cv
+
+    def pick(cv):
+        return (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(
+            len(mine), 2, -1).contiguous()
 
     def phase_fit(st):
-        cv = cv_enet_gaussian(st["G"], pan, pan.xcols, ycols, full_sets=full_sets,
-                              seg_counts=seg_counts)
-        coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1).contiguous()
+        cv = fit(st)
+        coef = pick(cv)
         return {**st, "cv": cv, "mom": dml_residual_moments(pan, coef)}
+
+    def phase_fit_sharded(st):
+        cv = fit(st)
+        coef = torch.zeros((K, 2, p1), dtype=torch.float64, device=pan.device)
+        if cv is not None:
+            coef.index_copy_(0, const(mine, torch.int64, pan.device), pick(cv).double())
+        return {**st, "cv": cv, "coef": coef}
+
+    def phase_resid(st):
+        return {**st, "mom": dml_residual_moments(pan, st["coef"])}
 
     def phase_final(st):
         return {**st, "res": S.dml_finalize(st["mom"], "plr")}
@@ -197,10 +233,13 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
             return st
         return Collective(f)
 
-    phases = [phase_gram]
+    phases = [phase_gram, phase_gram_reduce]
     if dist:
         phases.append(reduce("G"))
-    phases.append(phase_fit)
+    if sharded:
+        phases += [phase_fit_sharded, reduce("coef"), phase_resid]
+    else:
+        phases.append(phase_fit)
     if dist:
         phases.append(reduce("mom"))
     phases.append(phase_final)

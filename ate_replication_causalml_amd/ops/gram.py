@@ -175,12 +175,20 @@ def clear_plans():
     _plan_cache.clear()
 
 
+_STAGES = {"all": 3, "tiles": 1, "reduce": 2}
+
+
 def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor | None = None,
-         out: torch.Tensor | None = None) -> torch.Tensor:
-    """Per-segment Gram stack [nseg, P, P] (fp64). ``w``: optional row weights (panel order)."""
+         out: torch.Tensor | None = None, stage: str = "all") -> torch.Tensor:
+    """Per-segment Gram stack [nseg, P, P] (fp64). ``w``: optional row weights (panel order).
+
+    stage (paired-tile bf16 Gram): "tiles" launches only the tile kernel (slab partials),
+    "reduce" only the fixed-order slab reduce into the returned buffer, "all" both. Split,
+    the reduce can run on another stream than the next Gram (bench.py --stagger 2). Other
+    kernels do everything at "tiles" and nothing at "reduce"."""
     X = panel.data
     if not X.is_cuda:
-        return _gram_cpu(panel, w, out)
+        return _gram_cpu(panel, w, out) if stage != "reduce" else out
     pl = plan_for(panel, weighted=w is not None)
     G = pl.G if out is None else out
     s = _stream()
@@ -188,8 +196,12 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
         cs, bs = panel.strides()
         _native.call("ate_gram_bf16_pair", X.data_ptr(), cs, bs, panel.P, pl.tiles.data_ptr(),
                      pl.ntiles, pl.blocks.data_ptr(), pl.chunks.data_ptr(), pl.nchunks,
-                     pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
-    elif X.dtype == torch.bfloat16:
+                     pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(),
+                     _STAGES[stage], s)
+        return G
+    if stage == "reduce":
+        return G
+    if X.dtype == torch.bfloat16:
         _native.call("ate_gram_bf16", X.data_ptr(), panel.cm_ld, panel.P, pl.T, pl.tiles.data_ptr(),
                      pl.ntiles, pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(),
                      panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)

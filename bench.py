@@ -86,6 +86,15 @@ def main():
     from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel, global_seg_counts
 
     comm = C.from_env()
+    emulate = int(os.environ.get("ATE_BENCH_EMULATE_WORLD", "0"))
+    if emulate > 1 and comm.world_size == 1:
+        # diagnostic only (tools/emulate_ranks.sh): rank 0's share of a world-W step on one
+        # GPU -- its row shard, its path solves -- with no-op collectives (values are not
+        # the world-W result; the JSON says "emulated_world")
+        comm = C.LocalComm()
+        comm.world_size = emulate
+    else:
+        emulate = 0
     world, rank = comm.world_size, comm.rank
     if torch.cuda.is_available():
         torch.cuda.set_device(C.local_device())
@@ -244,9 +253,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        import torch.distributed as dist
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    comm.all_reduce_max_(el)
     elapsed = float(el.item())
     # latency of ONE cross-fit alone (no overlap): reported beside the throughput number
     nlat = max(1, min(args.steps, 10))
@@ -297,8 +304,10 @@ def main():
             "inflight": len(runs),
             "single_fit_ms": float(lat.item()) * 1e3,
         }
+        if emulate > 1:
+            out["emulated_world"] = emulate
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 and not emulate:
         import torch.distributed as dist
         dist.destroy_process_group()
 

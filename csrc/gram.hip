@@ -383,21 +383,27 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
   }
 }
 
+// what: 1 = tile kernel (slab partials), 2 = fixed-order slab reduce into G, 3 = both.
+// Split so a caller can run the reduce on another stream than the next tile kernel.
 ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, const void* tiles, int ntiles,
                                const void* blocks, const void* chunks, int nchunks,
-                               const void* seg_chunk0, int nseg, void* slab, void* G,
+                               const void* seg_chunk0, int nseg, void* slab, void* G, int what,
                                void* stream) {
-  if (P % (2 * GT)) return -1;
+  if (P % (2 * GT) || what < 1 || what > 3) return -1;
   hipStream_t s = (hipStream_t)stream;
+  if (what & 1) {
   hipLaunchKernelGGL(gram_bf16_pair_kernel, dim3(nchunks * ntiles), dim3(512), 0, s,
                      (const bf16_t*)X, cs, bs, (const int4*)tiles, ntiles, (const Chunk*)chunks,
                      nchunks, (float*)slab);
   ATE_CHECK_LAUNCH();
-  const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
-  hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
-                     (const float*)slab, (const int2*)blocks, ntiles, (const int*)seg_chunk0, nseg,
-                     P, (double*)G);
-  ATE_CHECK_LAUNCH();
+  }
+  if (what & 2) {
+    const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
+    hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+                       (const float*)slab, (const int2*)blocks, ntiles, (const int*)seg_chunk0,
+                       nseg, P, (double*)G);
+    ATE_CHECK_LAUNCH();
+  }
   return 0;
 }
 

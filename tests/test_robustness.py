@@ -90,11 +90,16 @@ def test_segmented_step_matches_eager_on_simulated_ranks():
     def rank_fn(comm):
         pan = synthetic_panel(n, p=24, folds=5, seed=3, dtype="f64", device="cpu",
                               rank=comm.rank, world=comm.world_size)
-        step = graphs.SegmentedStep(dml_phases(pan, 5, "min", comm=comm), graph=False,
-                                    warmup=0)
-        assert sum(isinstance(ph, graphs.Collective) for ph in step.phases) == 2
-        return step()["res"]
+        out = []
+        for shard in (True, False):
+            step = graphs.SegmentedStep(dml_phases(pan, 5, "min", comm=comm, shard_paths=shard),
+                                        graph=False, warmup=0)
+            # C01 Gram, C08 coefficients (sharded path solves only), C06 moments
+            assert sum(isinstance(ph, graphs.Collective) for ph in step.phases) == 2 + shard
+            out.append(step()["res"])
+        return out
 
     got = run_simulated(2, rank_fn)
-    for g in got:
-        torch.testing.assert_close(g, want, rtol=1e-9, atol=1e-12)
+    for sharded, unsharded in got:
+        torch.testing.assert_close(sharded, unsharded, rtol=0, atol=0)
+        torch.testing.assert_close(sharded, want, rtol=1e-9, atol=1e-12)
