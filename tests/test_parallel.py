@@ -127,16 +127,20 @@ dist.destroy_process_group()
     assert got[2] == pytest.approx(float(np.nansum(p)), rel=1e-12)
 
 
-def test_bench_two_rank_gloo_contract():
-    """bench.py under torch.distributed.run (2 gloo ranks on the CPU): one JSON line from
+@pytest.mark.parametrize("world", [2, 6])
+def test_bench_multi_rank_gloo_contract(world):
+    """bench.py under torch.distributed.run (gloo ranks on the CPU): one JSON line from
     rank 0 with the driver's fields, weak scaling (rows per rank fixed), and the same
-    ATE / SE as one process holding all the rows."""
+    ATE / SE as one process holding all the rows. World 6 > 5 folds: ranks 5.. solve no
+    CV paths (the path solves are sharded by outer fold) and contribute zeros."""
     import json
     bench = os.path.join(ROOT, "bench.py")
-    args = ["--rows", "3000", "--p", "24", "--dtype", "f64", "--steps", "1", "--warmup", "1"]
+    rows = 3000 if world == 2 else 1000
+    args = ["--rows", str(rows), "--p", "24", "--dtype", "f64", "--steps", "1", "--warmup", "1"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29541", bench, "--gpus", "2", *args]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+           f"--master-port={29541 + world}", bench, "--gpus", str(world), *args]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -145,10 +149,11 @@ def test_bench_two_rank_gloo_contract():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
-    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 6000
-    assert out["value"] == pytest.approx(6000 / (out["ms_per_step"] / 1e3), rel=1e-6)
-    one = subprocess.run([sys.executable, bench, "--rows", "6000", *args[2:]],
+    total = rows * world
+    assert out["n_gpus"] == world and out["scaling"] == "weak"
+    assert out["config"]["parallelism"] == f"dp{world}" and out["config"]["global_batch"] == total
+    assert out["value"] == pytest.approx(total / (out["ms_per_step"] / 1e3), rel=1e-6)
+    one = subprocess.run([sys.executable, bench, "--rows", str(total), *args[2:]],
                          capture_output=True, text=True, env=env, timeout=600)
     assert one.returncode == 0, one.stderr[-3000:]
     ref = json.loads([l for l in one.stdout.splitlines() if l.startswith("{")][0])
