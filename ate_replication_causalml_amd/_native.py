@@ -55,7 +55,7 @@ _SIGS = {
     "ate_lognet_path": "iplpiipipipdddippippppppppp",
     "ate_lognet_cvloss": "iplpiippipppipp",
     "ate_dgp_fill": "iplllllu" + "iip",
-    "ate_forest_fit": "pppppi" + "ppppppppp",
+    "ate_forest_fit": "pppppi" + "pppppppp" + "ip",
     "ate_forest_predict": "ppiiipppppippip",
     "ate_forest_pack": "pippppppp",
     "ate_forest_scratch_bytes": "ii",

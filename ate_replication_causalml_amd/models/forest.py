@@ -55,6 +55,7 @@ def from_fix(v) -> np.ndarray:
 
 
 # ------------------------------------------------------------------ K11 binning
+DEVICE_EDGES_MIN = 1 << 21   # n * p from which a GPU fit sorts for its edges on the device
 def bin_edges(X: np.ndarray, max_bins: int = MAX_BINS):
     """Per-feature sorted edges (<= max_bins-1): midpoints between distinct values when
     there are at most max_bins of them, else distinct quantiles."""
@@ -242,12 +243,19 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
     X = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
     if backend is None:
         backend = "gpu" if torch.cuda.is_available() else "cpu"
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "gpu" else None
+    Xsrc = X
     if edges is None:
-        edges, ne = bin_edges(X)
+        if dev is not None and X.size >= DEVICE_EDGES_MIN:
+            # large inputs: sort on the device (same edges bit for bit), bin from there
+            Xsrc = torch.as_tensor(X, device=dev)
+            edges, ne = bin_edges_device(Xsrc)
+        else:
+            edges, ne = bin_edges(X)
     else:
         edges, ne = edges
-    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "gpu" else None
-    Xb = bin_matrix(X, edges, ne, dev)
+    Xb = bin_matrix(Xsrc, edges, ne, dev)
+    del Xsrc
     return fit_forest_binned(Xb, (edges, ne), kind, y=y, r1=r1, r2=r2, ntree=ntree, mtry=mtry,
                              min_node=min_node, sampling=sampling, honesty=honesty, group=group,
                              mtry_poisson=mtry_poisson, alpha=alpha,
@@ -303,7 +311,8 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
         _native.call("ate_forest_fit", ctypes.addressof(fp), Xb.data_ptr(), p_(yt), p_(r1t),
                      p_(r2t), cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(),
                      val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
-                     scratch.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                     scratch.data_ptr(), int(os.environ.get("ATE_FOREST_NW", "0")),
+                     torch.cuda.current_stream().cuda_stream)
         del scratch
         return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xb)
     h = lambda a: None if a is None else (a.cpu().numpy() if isinstance(a, torch.Tensor) else

@@ -6,8 +6,9 @@
 // K15 forest_predict (row x tree traversal, OOB masks), K16/K17 causal pseudo-outcomes
 // and leaf sufficient statistics.
 //
-// Decomposition: ONE 256-thread workgroup grows ONE tree level by level (trees are
-// independent: tree parallelism across CUs). Within a level the 4 waves take nodes
+// Decomposition: ONE workgroup of NW waves grows ONE tree level by level (trees are
+// independent: tree parallelism across CUs; NW = 4..16 so that a launch of few trees still
+// keeps ~16 waves per CU busy, see ate_forest_fit). Within a level the NW waves take nodes
 // round-robin; a node's decision is made by one wave. Child ids are assigned after the
 // level by a scan in list order, so node numbering equals the CPU reference.
 #include "common.hpp"
@@ -16,8 +17,9 @@
 using namespace atef;
 
 constexpr int PMAX_F = 512;   // max features for the per-wave permutation buffer
-constexpr int COOP_ROWS = 1024;   // nodes above this are decided by all 4 waves together
-constexpr int COOP_CAP = 256;     // per level (the rest fall back to one wave per node)
+// nodes above 256 * NW rows are decided by all NW waves together (COOP_CAP per chunk of
+// candidates; the rest by one wave per node)
+constexpr int COOP_CAP = 256;
 
 #ifdef FOREST_PROF
 // per tree (debug builds, tools/forest_profile.py): [0] decisions, [1] child ids,
@@ -77,8 +79,9 @@ ATE_API int64_t ate_forest_scratch_bytes(int n, int ntree) {
   return (bytes + 255) / 256 * 256 * (int64_t)ntree;
 }
 
-// block-wide exclusive scan of one int per thread (256 threads); returns total via *tot
-__device__ int block_scan_excl(int v, int* sh /*>= 8*/, int* tot) {
+// block-wide exclusive scan of one int per thread (NW waves); returns total via *tot
+template <int NW>
+__device__ int block_scan_excl(int v, int* sh /*>= NW*/, int* tot) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int x = v;
 #pragma unroll
@@ -90,23 +93,28 @@ __device__ int block_scan_excl(int v, int* sh /*>= 8*/, int* tot) {
   __syncthreads();
   int off = 0;
   for (int k = 0; k < wid; ++k) off += sh[k];
-  int total = sh[0] + sh[1] + sh[2] + sh[3];
+  int total = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) total += sh[k];
   __syncthreads();
   *tot = total;
   return off + x - v;
 }
 
-__global__ __launch_bounds__(256) void forest_grow_kernel(
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void forest_grow_kernel(
     ForestParams fp, const uint8_t* __restrict__ Xb, const uint8_t* __restrict__ ycls,
     const int64_t* __restrict__ r1, const int64_t* __restrict__ r2, int cap,
     int32_t* __restrict__ feat_o, int32_t* __restrict__ thr_o, int32_t* __restrict__ left_o,
     double* __restrict__ val_o, int32_t* __restrict__ nnodes, uint8_t* __restrict__ inbag,
     int64_t* __restrict__ est_o, char* __restrict__ scratch_base) {
   // LDS: per wave histogram (256 bins x 4 int64 = 8 KB) + feature permutation
-  __shared__ int64_t hist[4][4][NBINS];
-  __shared__ int16_t perm[4][PMAX_F];
-  __shared__ int shi[8];
-  __shared__ int64_t sred[4][8];          // cooperative nodes: per-wave partial sums
+  constexpr int NT = 64 * NW;
+  constexpr int COOP_ROWS = 256 * NW;
+  __shared__ int64_t hist[NW][4][NBINS];
+  __shared__ int16_t perm[NW][PMAX_F];
+  __shared__ int shi[NW];
+  __shared__ int64_t sred[NW][8];         // cooperative nodes: per-wave partial sums
   __shared__ int sbig[COOP_CAP];          // this chunk's nodes with > COOP_ROWS rows
   __shared__ int sncur, snext_id, sm, sestn;
   const int t = blockIdx.x;
@@ -117,13 +125,13 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   uint8_t* inb = inbag + (int64_t)t * n;
   FPROF_T(tstart_);
   // ------------------------------------------------------------ sampling (K10)
-  for (int i = tid; i < n; i += 256) S.w[i] = 0;
+  for (int i = tid; i < n; i += NT) S.w[i] = 0;
   __syncthreads();
   if (fp.sampling == 0) {
-    for (int j = tid; j < n; j += 256)
+    for (int j = tid; j < n; j += NT)
       atomicAdd(&S.w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)], 1);
     __syncthreads();
-    for (int i = tid; i < n; i += 256) inb[i] = S.w[i] > 0;
+    for (int i = tid; i < n; i += NT) inb[i] = S.w[i] > 0;
     if (tid == 0) sestn = 0;
   } else if (tid == 0) {
     // Algorithm S (sequential by definition): group half-sample H, tree subsample S,
@@ -170,11 +178,11 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   __syncthreads();
   // ------------------------------------------------------------ in-bag rows, ascending
   int m = 0;
-  for (int base = 0; base < n; base += 256) {
+  for (int base = 0; base < n; base += NT) {
     const int i = base + tid;
     const int f = (i < n && S.w[i] > 0) ? 1 : 0;
     int tot;
-    const int pos = block_scan_excl(f, shi, &tot);
+    const int pos = block_scan_excl<NW>(f, shi, &tot);
     if (f) S.idx[m + pos] = i;
     m += tot;
   }
@@ -212,14 +220,16 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
       const int v = nd.id;
       const bool small = !coop && nd.hi - nd.lo <= 64;
       const int q0 = nd.lo + lane + (coop ? wid * 64 : 0);
-      const int qstep = coop ? 256 : 64;
+      const int qstep = coop ? NT : 64;
       // sum over the node's rows: one wave, or all four (fixed wave order)
       auto red = [&](int64_t x, int slot) -> int64_t {
         x = wsum64(x);
         if (!coop) return x;
         if (lane == 0) sred[wid][slot] = x;
         __syncthreads();
-        const int64_t r = sred[0][slot] + sred[1][slot] + sred[2][slot] + sred[3][slot];
+        int64_t r = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) r += sred[w][slot];
         __syncthreads();
         return r;
       };
@@ -365,7 +375,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
             const int b = 4 * lane + e;
             if (coop) {
 #pragma unroll
-              for (int w = 0; w < 4; ++w) {
+              for (int w = 0; w < NW; ++w) {
                 a0 += hist[w][0][b]; a1 += hist[w][1][b]; as += hist[w][2][b]; at_ += hist[w][3][b];
               }
             } else {
@@ -541,19 +551,19 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
         S.dec[j] = make_int4(bf >= 0 ? 1 : 0, bf, bb, nl_rows);
       }
     };
-    // big nodes in level order, in chunks of 256 candidates (block compaction), each
+    // big nodes in level order, in chunks of COOP_CAP candidates (block compaction), each
     // decided by the whole workgroup; then every other node by one wave
-    for (int base = 0; base < ncur; base += 256) {
+    for (int base = 0; base < ncur; base += COOP_CAP) {
       const int j = base + tid;
-      const bool big = j < ncur && S.cur[j].hi - S.cur[j].lo > COOP_ROWS;
+      const bool big = tid < COOP_CAP && j < ncur && S.cur[j].hi - S.cur[j].lo > COOP_ROWS;
       int tot;
-      const int pos = block_scan_excl(big ? 1 : 0, shi, &tot);
+      const int pos = block_scan_excl<NW>(big ? 1 : 0, shi, &tot);
       if (big) sbig[pos] = j;
       __syncthreads();
       for (int e = 0; e < tot; ++e) decide(sbig[e], true);
       __syncthreads();
     }
-    for (int j = wid; j < ncur; j += 4) {
+    for (int j = wid; j < ncur; j += NW) {
       const Rng3 nd = S.cur[j];
       if (nd.hi - nd.lo > COOP_ROWS) continue;
       decide(j, false);
@@ -564,11 +574,11 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
     // ---- child ids in level order (block scan over split flags)
     int id_base = snext_id;
     int nsplit_total = 0;
-    for (int base = 0; base < ncur; base += 256) {
+    for (int base = 0; base < ncur; base += NT) {
       const int j = base + tid;
       const int f = j < ncur ? S.dec[j].x : 0;
       int tot;
-      const int pos = block_scan_excl(f, shi, &tot);
+      const int pos = block_scan_excl<NW>(f, shi, &tot);
       if (f) {
         const int v = S.cur[j].id;
         left[v] = id_base + 2 * (nsplit_total + pos);
@@ -580,7 +590,7 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
     FPROF_T(tl2_);
     FPROF_ADD(1, tl2_ - tl1_);
     // ---- stable partition of each split node (one wave per node) + next level list
-    for (int j = wid; j < ncur; j += 4) {
+    for (int j = wid; j < ncur; j += NW) {
       const int4 d = S.dec[j];
       if (!d.x) continue;
       const Rng3 nd = S.cur[j];
@@ -625,10 +635,10 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
   // ------------------------------------------------------------ grf leaf statistics (J2)
   if (fp.sampling == 1 && est_o) {
     int64_t* est = est_o + obase * 5;
-    for (int e = tid; e < nn * 5; e += 256) est[e] = 0;
+    for (int e = tid; e < nn * 5; e += NT) est[e] = 0;
     __syncthreads();
     const int ne = sestn;
-    for (int q = tid; q < ne; q += 256) {
+    for (int q = tid; q < ne; q += NT) {
       const int i = S.est_rows[q];
       int v = 0;
       while (true) {
@@ -653,14 +663,28 @@ __global__ __launch_bounds__(256) void forest_grow_kernel(
 
 ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, const void* r1,
                            const void* r2, int cap, void* feat, void* thr, void* left, void* val,
-                           void* nnodes, void* inbag, void* est, void* scratch, void* stream) {
+                           void* nnodes, void* inbag, void* est, void* scratch, int nw,
+                           void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
   if (fp.p > PMAX_F || fp.n <= 0) return -1;
-  hipLaunchKernelGGL(forest_grow_kernel, dim3(fp.ntree), dim3(256), 0, (hipStream_t)stream, fp,
-                     (const uint8_t*)Xb, (const uint8_t*)ycls, (const int64_t*)r1,
-                     (const int64_t*)r2, cap, (int32_t*)feat, (int32_t*)thr, (int32_t*)left,
-                     (double*)val, (int32_t*)nnodes, (uint8_t*)inbag, (int64_t*)est,
-                     (char*)scratch);
+  // waves per tree. The kernel needs ~250 VGPRs, so a SIMD holds 2 waves and a CU 8:
+  // with at most two trees per CU an 8-wave workgroup fills it (measured 1.5x faster
+  // than 4 waves for 64 trees at n = 1e6, tools/forest_nw.sh); 16 waves force 128 VGPRs
+  // and spill (slower). nw: 0 = auto, or 4 / 8 / 16.
+  int w = nw;
+  if (w == 0) w = fp.ntree <= 512 ? 8 : 4;
+  hipStream_t s = (hipStream_t)stream;
+#define ATE_FOREST_LAUNCH(NWV)                                                                    \
+  hipLaunchKernelGGL(forest_grow_kernel<NWV>, dim3(fp.ntree), dim3(64 * NWV), 0, s, fp,           \
+                     (const uint8_t*)Xb, (const uint8_t*)ycls, (const int64_t*)r1,                 \
+                     (const int64_t*)r2, cap, (int32_t*)feat, (int32_t*)thr, (int32_t*)left,      \
+                     (double*)val, (int32_t*)nnodes, (uint8_t*)inbag, (int64_t*)est,              \
+                     (char*)scratch)
+  if (w == 4) ATE_FOREST_LAUNCH(4);
+  else if (w == 8) ATE_FOREST_LAUNCH(8);
+  else if (w == 16) ATE_FOREST_LAUNCH(16);
+  else return -1;
+#undef ATE_FOREST_LAUNCH
   ATE_CHECK_LAUNCH();
   return 0;
 }
