@@ -20,6 +20,9 @@ constexpr int PMAX_F = 512;   // max features for the per-wave permutation buffe
 // nodes above 256 * NW rows are decided by all NW waves together (COOP_CAP per chunk of
 // candidates; the rest by one wave per node)
 constexpr int COOP_CAP = 256;
+// bins gathered per batch in the 17-64-row histogram path (register pressure: 16 -> ~60
+// more VGPRs and one wave fewer per SIMD)
+constexpr int SMALL_B = 4;
 
 #ifdef FOREST_PROF
 // per tree (debug builds, tools/forest_profile.py): [0] decisions, [1] child ids,
@@ -101,8 +104,10 @@ __device__ int block_scan_excl(int v, int* sh /*>= NW*/, int* tot) {
   return off + x - v;
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void forest_grow_kernel(
+// NW waves per workgroup (one tree); MINW = waves per SIMD the register allocation must
+// allow (4: <= 128 VGPRs with some scratch spill, 3: <= 168)
+template <int NW, int MINW>
+__global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
     ForestParams fp, const uint8_t* __restrict__ Xb, const uint8_t* __restrict__ ycls,
     const int64_t* __restrict__ r1, const int64_t* __restrict__ r2, int cap,
     int32_t* __restrict__ feat_o, int32_t* __restrict__ thr_o, int32_t* __restrict__ left_o,
@@ -370,17 +375,11 @@ __global__ __launch_bounds__(64 * NW) void forest_grow_kernel(
           // wave prefix scan: lane owns bins 4*lane .. 4*lane+3
           int64_t c0[4], c1[4], cs[4], ct[4];
           int64_t a0 = 0, a1 = 0, as = 0, at_ = 0;
+          const int hw = coop ? 0 : wid;   // cooperative nodes: combined into hist[0]
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int b = 4 * lane + e;
-            if (coop) {
-#pragma unroll
-              for (int w = 0; w < NW; ++w) {
-                a0 += hist[w][0][b]; a1 += hist[w][1][b]; as += hist[w][2][b]; at_ += hist[w][3][b];
-              }
-            } else {
-              a0 += hist[wid][0][b]; a1 += hist[wid][1][b]; as += hist[wid][2][b]; at_ += hist[wid][3][b];
-            }
+            a0 += hist[hw][0][b]; a1 += hist[hw][1][b]; as += hist[hw][2][b]; at_ += hist[hw][3][b];
             c0[e] = a0; c1[e] = a1; cs[e] = as; ct[e] = at_;
           }
           int64_t x0 = a0, x1 = a1, xs = as, xt = at_;
@@ -471,15 +470,15 @@ __global__ __launch_bounds__(64 * NW) void forest_grow_kernel(
             }
           }
         } else if (small) {
-          for (int k0 = 0; k0 < nf; k0 += 16) {
-            int bins[16];
+          for (int k0 = 0; k0 < nf; k0 += SMALL_B) {
+            int bins[SMALL_B];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
+            for (int u = 0; u < SMALL_B; ++u) {
               const int k = k0 + u;
               bins[u] = (cvalid && k < nf) ? (int)Xb[(int64_t)perm[wid][k] * n + ci] : 0;
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
+            for (int u = 0; u < SMALL_B; ++u) {
               const int k = k0 + u;
               if (k >= nf) break;
               const int f = perm[wid][k];
@@ -518,7 +517,17 @@ __global__ __launch_bounds__(64 * NW) void forest_grow_kernel(
               hist_row(xf[i], S.w[i], fp.kind == 0 ? ycls[i] : 0, fp.kind != 0 ? r1[i] : 0,
                        fp.kind == 2 ? S.rho[i] : 0);
             }
-            if (coop) __syncthreads();      // every wave's rows are in
+            if (coop) {
+              __syncthreads();              // every wave's rows are in
+              // combine the per-wave histograms into hist[0] (integer sums: exact)
+              for (int e = tid; e < 4 * NBINS; e += NT) {
+                const int c = e / NBINS, b = e % NBINS;
+                int64_t acc = 0;
+                for (int w = 1; w < NW; ++w) acc += hist[w][c][b];
+                hist[0][c][b] += acc;
+              }
+              __syncthreads();
+            }
             scan_eval(f);
             if (coop) __syncthreads();      // histograms read before the next clear
           }
@@ -667,22 +676,23 @@ ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, co
                            void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
   if (fp.p > PMAX_F || fp.n <= 0) return -1;
-  // waves per tree. The kernel needs ~250 VGPRs, so a SIMD holds 2 waves and a CU 8:
-  // with at most two trees per CU an 8-wave workgroup fills it (measured 1.5x faster
-  // than 4 waves for 64 trees at n = 1e6, tools/forest_nw.sh); 16 waves force 128 VGPRs
-  // and spill (slower). nw: 0 = auto, or 4 / 8 / 16.
+  // waves per tree and register budget (tools/forest_occ.sh, growth alone on MI355X):
+  // <= 256 trees: 16 waves at 4 per SIMD (64 trees, n = 1e6: 1.01 s; 4 waves at 2 per
+  // SIMD 1.83 s); <= 1024 trees: 8 waves at 4 per SIMD (300 trees: 2.11 s vs 2.35 s);
+  // more: 4-wave workgroups at 3 per SIMD (2500 trees, n = 1e4: 33 ms vs 42 ms).
+  // nw: 0 = auto, or 4 / 8 / 16 (A/B).
   int w = nw;
-  if (w == 0) w = fp.ntree <= 512 ? 8 : 4;
+  if (w == 0) w = fp.ntree <= 256 ? 16 : fp.ntree <= 1024 ? 8 : 4;
   hipStream_t s = (hipStream_t)stream;
-#define ATE_FOREST_LAUNCH(NWV)                                                                    \
-  hipLaunchKernelGGL(forest_grow_kernel<NWV>, dim3(fp.ntree), dim3(64 * NWV), 0, s, fp,           \
+#define ATE_FOREST_LAUNCH(NWV, MINW)                                                              \
+  hipLaunchKernelGGL((forest_grow_kernel<NWV, MINW>), dim3(fp.ntree), dim3(64 * NWV), 0, s, fp,   \
                      (const uint8_t*)Xb, (const uint8_t*)ycls, (const int64_t*)r1,                 \
                      (const int64_t*)r2, cap, (int32_t*)feat, (int32_t*)thr, (int32_t*)left,      \
                      (double*)val, (int32_t*)nnodes, (uint8_t*)inbag, (int64_t*)est,              \
                      (char*)scratch)
-  if (w == 4) ATE_FOREST_LAUNCH(4);
-  else if (w == 8) ATE_FOREST_LAUNCH(8);
-  else if (w == 16) ATE_FOREST_LAUNCH(16);
+  if (w == 4) ATE_FOREST_LAUNCH(4, 3);
+  else if (w == 8) ATE_FOREST_LAUNCH(8, 4);
+  else if (w == 16) ATE_FOREST_LAUNCH(16, 4);
   else return -1;
 #undef ATE_FOREST_LAUNCH
   ATE_CHECK_LAUNCH();
