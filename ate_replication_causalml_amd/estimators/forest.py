@@ -32,12 +32,26 @@ def _rf_oob(Xn, y, num_trees, seed, dev, comm):
 
 def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, forest_seed=12325,
             compat="reference", method="Doubly Robust with Random Forest PS", device=None,
-            dtype="f64", comm=None):
+            dtype="f64", comm=None, graph=True):
     """E8 ``doubly_robust`` (ate_functions.R:149-207): logistic outcome model (with the
     mutate_ quirk Q6 under compat="reference"), randomForest OOB propensity clipped (Q9).
     ``comm``: tree-parallel propensity forest over ranks (rows replicated, C05)."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
+    if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
+        # one hipGraph launch: outcome IRLS + counterfactual predictions, the propensity
+        # forest (growth, OOB votes, clipping) and the AIPW score, over the binned matrix
+        # (bin edges come from the data, so binning stays in front of the graph)
+        from ..utils.graphs import estimator_graphs
+        po = D._outcome_panel(Yn, Wn, Xn, dtype, dev)
+        edges = F.bin_edges(Xn)
+        Xb = F.bin_matrix(Xn, *edges, dev)
+        y = torch.as_tensor(Yn, device=dev)
+        w = torch.as_tensor(Wn, device=dev)
+        out, g = estimator_graphs.run("aipw_rf", _aipw_rf_body, (po, Xb, y, w), num_trees,
+                                      forest_seed, compat, bootstrap_se, B, seed)
+        v = out.cpu().numpy()
+        return AteResult.make(method, v[0], v[1], n_oob_nan=int(v[2]), hipgraph=g)
     mu0, mu1 = D.outcome_mu(Yn, Wn, Xn, counterfactual_quirk=(compat == "reference"),
                             device=dev, dtype=dtype)
     p_raw = _rf_oob(Xn, Wn, num_trees, forest_seed, dev, comm)
@@ -46,6 +60,19 @@ def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, fores
     S.clip_propensity_(p)
     return D.aipw_from_nuisances(method, Yn, Wn, p, mu0, mu1, bootstrap_se, B, seed, compat, dev,
                                  n_oob_nan=int(np.isnan(p_raw).sum()))
+
+
+def _aipw_rf_body(po, Xb, y, w, num_trees, forest_seed, compat, bootstrap_se, B, seed):
+    """Device body of aipw_rf (no host sync): [ate, se, #OOB-NaN propensities]."""
+    from ..ops import stats as S
+    mu0, mu1 = D._outcome_fit(po, compat == "reference")
+    fr = F.fit_forest_binned(Xb, (None, None), F.KIND_CLASS, y=w, ntree=num_trees,
+                             seed=forest_seed)
+    p = fr.predict_state(Xb, True, fr.new_state(Xb.shape[1]), 7, host=False).clone()
+    nan = torch.isnan(p).sum().double().reshape(1)
+    S.clip_propensity_(p)
+    res = D._aipw_core(y, w, p, mu0, mu1, bootstrap_se, B, seed, compat)
+    return torch.cat([res, nan])
 
 
 def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, device=None, comm=None):

@@ -164,9 +164,10 @@ class Forest:
             return torch.zeros(10 * n2, dtype=torch.float64, device=self.device)
         return np.zeros(10 * n2)
 
-    def predict_state(self, Xb, oob, state, phases):
+    def predict_state(self, Xb, oob, state, phases, host=True):
         """Run prediction phases (1: per-tree sums, 2: little-bag group sums, 4: finalise)
-        on accumulator ``state`` ([10, n2]); returns the predictions when phase 4 ran."""
+        on accumulator ``state`` ([10, n2]); returns the predictions when phase 4 ran
+        (``host=False``, GPU: the device tensor, no host sync -- capturable)."""
         n2 = Xb.shape[1]
         if oob and n2 != self.params.n:
             raise ValueError("OOB prediction requires the training rows")
@@ -193,6 +194,8 @@ class Forest:
                          leaves.data_ptr(), tchunk, state.data_ptr(), out.data_ptr(), phases, s)
             if not phases & 4:
                 return None
+            if not host:
+                return out.view(n2, width) if width > 1 else out
             res = out.cpu().numpy()
         else:
             res = np.empty(n2 * width)

@@ -26,11 +26,20 @@ CASES = {
     "aipw_glm": lambda L, X, W, Yc, Yb, dev, g: L.aipw_glm(Yb, W, X, device=dev, graph=g),
     "aipw_glm_boot": lambda L, X, W, Yc, Yb, dev, g: L.aipw_glm(
         Yb, W, X, bootstrap_se=True, B=200, device=dev, graph=g),
+    "aipw_rf": lambda L, X, W, Yc, Yb, dev, g: _forest().aipw_rf(
+        Yb, W, X, num_trees=60, device=dev, graph=g),
+    "aipw_rf_boot": lambda L, X, W, Yc, Yb, dev, g: _forest().aipw_rf(
+        Yb, W, X, num_trees=40, bootstrap_se=True, B=100, compat="textbook", device=dev, graph=g),
     "lasso_single": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_single(
         Yc, W, X, device=dev, graph=g),
     "lasso_usual": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_usual(
         Yc, W, X, device=dev, graph=g),
 }
+
+
+def _forest():
+    from ate_replication_causalml_amd.estimators import forest
+    return forest
 
 
 def _lasso():
