@@ -75,6 +75,54 @@ def _aipw_rf_body(po, Xb, y, w, num_trees, forest_seed, compat, bootstrap_se, B,
     return torch.cat([res, nan])
 
 
+def _double_ml_body(Xb, y, w, num_trees, seed):
+    """Device body of double_ml (no host sync): both positional halves (Q14), [tau, se]."""
+    n = Xb.shape[1]
+    h = n // 2
+    halves = []
+    for (a0, a1), (b0, b1), sd in (((0, h), (h, n), seed), ((h, n), (0, h), seed + 2)):
+        rf1 = F.fit_forest_binned(Xb[:, a0:a1].contiguous(), (None, None), F.KIND_CLASS,
+                                  y=w[a0:a1], ntree=num_trees, seed=sd)
+        rf2 = F.fit_forest_binned(Xb[:, b0:b1].contiguous(), (None, None), F.KIND_CLASS,
+                                  y=y[b0:b1], ntree=num_trees, seed=sd + 1)
+        ew = rf1.predict_state(Xb, False, rf1.new_state(n), 7, host=False)
+        ey = rf2.predict_state(Xb, False, rf2.new_state(n), 7, host=False)
+        yr, wr = y - ey, w - ew
+        sww = wr @ wr                                  # lm(Y_resid ~ 0 + W_resid)
+        tau = (wr @ yr) / sww
+        rss = ((yr - tau * wr) ** 2).sum()
+        halves.append(torch.stack([tau, torch.sqrt(rss / (n - 1) / sww)]))
+    return (halves[0] + halves[1]) / 2
+
+
+def _causal_forest_body(Xb, y, w, num_trees, nt, seed):
+    """Device body of causal_forest_ate (models/forest.causal_forest + average_treatment_
+    effect with grf defaults, no host sync): [AIPW ATE, SE, mean CATE, sqrt(mean var)]."""
+    p = Xb.shape[0]
+    grf = dict(mtry=F.grf_mtry(p), min_node=5, sampling=1, honesty=True, group=2,
+               mtry_poisson=True, alpha=0.05, sample_fraction=0.5)
+
+    def oob(fr):
+        return fr.predict_state(Xb, True, fr.new_state(Xb.shape[1]), 7, host=False)
+
+    fy = F.fit_forest_binned(Xb, (None, None), F.KIND_REG, r1=y, ntree=nt, seed=seed + 1, **grf)
+    fw = F.fit_forest_binned(Xb, (None, None), F.KIND_REG, r1=w, ntree=nt, seed=seed + 2, **grf)
+    y_hat, w_hat = oob(fy), oob(fw)
+    y_hat = torch.where(torch.isnan(y_hat), y.mean(), y_hat)
+    w_hat = torch.where(torch.isnan(w_hat), w.mean(), w_hat)
+    fc = F.fit_forest_binned(Xb, (None, None), F.KIND_CAUSAL, r1=w - w_hat, r2=y - y_hat,
+                             ntree=num_trees, seed=seed, **grf)
+    out = oob(fc)
+    tau_oob, var_oob = out[:, 0], out[:, 1]
+    w_res, y_res = w - w_hat, y - y_hat
+    tau = torch.where(torch.isnan(tau_oob), torch.nanmean(tau_oob), tau_oob)
+    what = w_hat.clamp(1e-6, 1 - 1e-6)
+    gamma = tau + w_res / (what * (1 - what)) * (y_res - tau * w_res)
+    n = gamma.numel()
+    return torch.stack([gamma.mean(), gamma.std(unbiased=True) / n ** 0.5,
+                        torch.nanmean(tau_oob), torch.sqrt(torch.nanmean(var_oob))])
+
+
 def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, device=None, comm=None):
     """One half of ``double_ml`` (ate_functions.R:332-369): RF classifier for W on idx1,
     for Y on idx2, both predicted on all rows (in-sample for the training half, Q14)."""
@@ -99,11 +147,24 @@ def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, device=None, comm=Non
 
 
 def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning", device=None,
-              comm=None):
+              comm=None, graph=True):
     """E13 ``double_ml`` (ate_functions.R:372-389): positional halves, swapped, averaged
     tau and averaged SE (Q14)."""
     n = len(as_np(Y))
     h = n // 2
+    dev = resolve_device(device)
+    if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
+        # one hipGraph launch: the four forests, their predictions on all rows and both
+        # residual-on-residual fits, over the binned matrix (edges from the data)
+        from ..utils.graphs import estimator_graphs
+        Xn = as_np(X)
+        edges = F.bin_edges(Xn)
+        Xb = F.bin_matrix(Xn, *edges, dev)
+        y = torch.as_tensor(as_np(Y), device=dev)
+        w = torch.as_tensor(as_np(W), device=dev)
+        out, g = estimator_graphs.run("double_ml", _double_ml_body, (Xb, y, w), num_trees, seed)
+        v = out.cpu().numpy()
+        return AteResult.make(method, v[0], v[1], hipgraph=g)
     idx1, idx2 = np.arange(h), np.arange(h, n)
     t1, s1 = chernozhukov(Y, W, X, idx1, idx2, num_trees, seed, device, comm)
     t2, s2 = chernozhukov(Y, W, X, idx2, idx1, num_trees, seed + 2, device, comm)
@@ -111,10 +172,26 @@ def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning"
 
 
 def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest(GRF)",
-                      device=None, nuisance_trees=None, comm=None):
+                      device=None, nuisance_trees=None, comm=None, graph=True):
     """E15 (ate_replication.Rmd:250-272): grf causal forest; published row = AIPW
     ``estimate_average_effect``; diagnostics carry the "incorrect" mean-CATE ATE and
     sqrt(mean(var)) the reference prints (ate_replication.md:294)."""
+    dev = resolve_device(device)
+    if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
+        # one hipGraph launch: Y.hat / W.hat OOB regression forests, the honest causal
+        # forest on the centred data, its OOB CATEs and the AIPW average effect
+        from ..utils.graphs import estimator_graphs
+        Xn = as_np(X)
+        edges = F.bin_edges(Xn)
+        Xb = F.bin_matrix(Xn, *edges, dev)
+        y = torch.as_tensor(as_np(Y), device=dev)
+        w = torch.as_tensor(as_np(W), device=dev)
+        nt = nuisance_trees or max(50, num_trees // 4)
+        out, g = estimator_graphs.run("causal_forest", _causal_forest_body, (Xb, y, w),
+                                      num_trees, nt, seed)
+        v = out.cpu().numpy()
+        return AteResult.make(method, v[0], v[1], ate_bad=float(v[2]), se_bad=float(v[3]),
+                              hipgraph=g)
     cf = F.causal_forest(as_np(X), as_np(Y), as_np(W), num_trees=num_trees, seed=seed,
                          nuisance_trees=nuisance_trees, backend=_backend(device), comm=comm)
     est, se = F.average_treatment_effect(cf)

@@ -30,6 +30,10 @@ CASES = {
         Yb, W, X, num_trees=60, device=dev, graph=g),
     "aipw_rf_boot": lambda L, X, W, Yc, Yb, dev, g: _forest().aipw_rf(
         Yb, W, X, num_trees=40, bootstrap_se=True, B=100, compat="textbook", device=dev, graph=g),
+    "double_ml": lambda L, X, W, Yc, Yb, dev, g: _forest().double_ml(
+        Yb, W, X, num_trees=40, device=dev, graph=g),
+    "causal_forest": lambda L, X, W, Yc, Yb, dev, g: _forest().causal_forest_ate(
+        Yc, W, X, num_trees=200, device=dev, graph=g),
     "lasso_single": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_single(
         Yc, W, X, device=dev, graph=g),
     "lasso_usual": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_usual(
@@ -57,6 +61,9 @@ def test_graphed_estimator_matches_eager(gpu, name):
         eager = CASES[name](L, X, W, Yc, Yb, gpu, False)
         graphed = CASES[name](L, X, W, Yc, Yb, gpu, True)
         assert graphed.diagnostics.get("hipgraph") is True, name
+        for k, v in eager.diagnostics.items():          # e.g. the mean-CATE "incorrect" ATE
+            if isinstance(v, float) and k != "hipgraph":
+                assert abs(graphed.diagnostics[k] - v) <= 1e-12 * max(1.0, abs(v)), (name, k)
         assert abs(graphed.ate - eager.ate) <= 1e-12 * max(1.0, abs(eager.ate)), name
         if eager.se is not None and np.isfinite(eager.se):
             assert abs(graphed.se - eager.se) <= 1e-12 * max(1.0, abs(eager.se)), name
