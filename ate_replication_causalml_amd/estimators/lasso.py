@@ -300,12 +300,13 @@ class _GraphedDml:
     """One captured DML cross-fit (utils/graphs.SegmentedStep over dml_phases) bound to a
     STATIC panel buffer: a later call on data of the same layout copies its panel into the
     buffer and replays the graph, so the whole estimator (Gram, CV-LASSO paths, selection,
-    residual pass, theta / SE) is ONE graph launch."""
+    residual pass, theta / SE) is ONE graph launch. Built on the second
+    call of a layout, over the panel of the first (eager) call, which was its warm-up."""
 
     def __init__(self, pan, folds, lambda_rule):
         from ..utils.graphs import SegmentedStep
         self.pan = pan
-        self.step = SegmentedStep(dml_phases(pan, folds, lambda_rule), graph=True)
+        self.step = SegmentedStep(dml_phases(pan, folds, lambda_rule), graph=True, warmup=0)
 
     def __call__(self, pan):
         if pan is not self.pan:
@@ -319,18 +320,24 @@ GRAPH_CACHE_MAX = 4
 
 def _dml_graphed(pan, folds, lambda_rule):
     """Graph-cached cross-fit keyed by the panel layout (shape, dtype, fold segments,
-    columns): the first call captures, later calls with the same layout replay. LRU of
-    GRAPH_CACHE_MAX (each entry holds a panel-sized buffer and its Gram workspace)."""
+    columns). First call of a layout: eager, its panel kept; second: copy + capture +
+    replay; later: copy + one graph launch. LRU of GRAPH_CACHE_MAX (each entry holds a
+    panel-sized buffer and its Gram workspace). Returns (res, replayed)."""
     key = (tuple(pan.data.shape), pan.data.dtype, str(pan.device), folds, lambda_rule,
            tuple(map(tuple, pan.seg_bounds)), tuple(pan.seg_nreal.tolist()),
-           tuple(sorted(pan.cols.items())))
+           tuple(sorted(pan.cols.items())), pan.blocked)
     g = _graph_cache.pop(key, None)
     if g is None:
         while len(_graph_cache) >= GRAPH_CACHE_MAX:
             _graph_cache.pop(next(iter(_graph_cache)))
-        g = _GraphedDml(pan, folds, lambda_rule)
+        _graph_cache[key] = pan                     # seen once: keep the warm buffers
+        return dml_crossfit_panel(pan, folds, lambda_rule)[0], False
+    if not isinstance(g, _GraphedDml):
+        torch.cuda.synchronize()
+        g.data.copy_(pan.data)
+        g = _GraphedDml(g, folds, lambda_rule)
     _graph_cache[key] = g
-    return g(pan)
+    return g(pan), True
 
 
 def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cross-fit (LASSO)",
@@ -339,14 +346,14 @@ def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cr
     (inner CV over the other K-1 folds). Matches reference.estimators.dml_plr_lasso.
 
     graph: on a GPU without row sharding, the estimator runs as one captured hipGraph
-    (captured on the first call for a panel layout, replayed afterwards)."""
+    (first call of a panel layout eager, captured on the second, replayed afterwards)."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
     fid = _fold_ids(len(Yn), folds, seed, 0, dist)
     pan = build_panel(Xn, Wn, Yn, folds=fid, dtype=dtype, device=dev)
     if graph and dist is None and pan.data.is_cuda:
-        res = _dml_graphed(pan, folds, lambda_rule)
-        return read_result(res, method, n=len(Yn), hipgraph=True)
+        res, g = _dml_graphed(pan, folds, lambda_rule)
+        return read_result(res, method, n=len(Yn), hipgraph=g)
     res, mom, _ = dml_crossfit_panel(pan, folds, lambda_rule,
                                      comm=dist.comm if dist is not None else None)
     return read_result(res, method, n=dist.n_total if dist is not None else len(Yn))

@@ -64,16 +64,15 @@ def ols(Y, W, X, method="Direct Method", device=None, dtype="f64", dist=None, gr
     """E2 ``ate_condmean_ols`` (ate_functions.R:25-39): lm(Y ~ covariates + W)."""
     dev = resolve_device(device)
     pan = build_panel(as_np(X), as_np(W), as_np(Y), dtype=dtype, device=dev)
-    g = False
+    diag = {}
     if _graph_ok(graph, dist, pan.data):
-        out, g = estimator_graphs.run("ols", _ols_body, (pan,))
+        out, diag["hipgraph"] = estimator_graphs.run("ols", _ols_body, (pan,))
     else:
         G = gram(pan)[0]
         if dist is not None:
             dist.sum_(G)
         out = _ols_finish(pan, G, _n(pan, dist))
     v = out.cpu().numpy()
-    diag = {"hipgraph": True} if g else {}
     return AteResult.make(method, v[0], v[1], rank=int(v[2]), **diag)
 
 

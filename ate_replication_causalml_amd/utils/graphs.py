@@ -185,37 +185,53 @@ def layout_key(*inputs):
 
 
 class _Captured:
-    """``body(*inputs)`` captured once over STATIC inputs (the first call's own tensors /
+    """``body(*inputs)`` captured once over STATIC inputs (an earlier call's own tensors /
     panels, kept alive here); a later call copies its data into them and replays."""
 
     def __init__(self, body, inputs, static_args, warmup):
         self.inputs = list(inputs)
         self.step = GraphedStep(lambda: body(*self.inputs, *static_args), warmup)
 
-    def __call__(self, inputs):
+    def load(self, inputs):
         for s, x in zip(self.inputs, inputs):
             if x is not s:
                 _data(s).copy_(_data(x))
+
+    def __call__(self, inputs):
+        self.load(inputs)
         return self.step()
+
+
+class _Seen:
+    """First call of a key: it ran eagerly on these inputs (which populated the plan and
+    constant caches for exactly these buffers); they become the graph's static inputs."""
+
+    def __init__(self, inputs):
+        self.inputs = list(inputs)
 
 
 class GraphCache:
     """Per-estimator hipGraph cache (SURVEY.md §7.1 "every ate_*() is one hipGraph
-    launch"). ``run(name, body, inputs, *static_args)``: the first call for a (name,
-    static args, input layout) captures ``body(*inputs, *static_args)`` — a device-only
-    function of the inputs
-    (fixed launch budgets, device flags, cached constants; no host sync) — and later
-    calls with the same key replay it: one graph launch per estimator call. LRU of
-    ``maxsize`` entries (each holds its input buffers and the graph's memory pool).
-    A body that cannot be captured is remembered and runs eagerly from then on.
-    Outputs are the graph's static tensors: read them before the next call."""
+    launch"). ``run(name, body, inputs, *static_args)`` calls ``body(*inputs,
+    *static_args)`` -- a device-only function of the inputs (fixed launch budgets, device
+    flags, cached constants; no host sync). Per (name, static args, input layout):
+
+    * 1st call: runs eagerly and keeps its input buffers (a one-off call costs nothing
+      extra, and the eager run is the capture's warm-up on exactly those buffers);
+    * 2nd call: copies its data into the kept buffers, captures the body and replays it;
+    * later calls: copy + ONE graph launch.
+
+    LRU of ``maxsize`` entries (each holds its input buffers and the graph's memory pool).
+    A body that cannot be captured is remembered and runs eagerly from then on. Outputs
+    of a replay are the graph's static tensors: read them before the next call.
+    Returns (output, replayed: bool)."""
 
     def __init__(self, maxsize: int = 8):
         self.maxsize = maxsize
         self.entries: dict = {}
         self.eager: set = set()
 
-    def run(self, name, body, inputs, *static_args, warmup: int = 1):
+    def run(self, name, body, inputs, *static_args):
         key = (name, static_args, layout_key(*inputs))
         if key in self.eager:
             return body(*inputs, *static_args), False
@@ -223,8 +239,15 @@ class GraphCache:
         if g is None:
             while len(self.entries) >= self.maxsize:
                 self.entries.pop(next(iter(self.entries)))
+            self.entries[key] = _Seen(inputs)
+            return body(*inputs, *static_args), False
+        if isinstance(g, _Seen):
             try:
-                g = _Captured(body, inputs, static_args, warmup)
+                torch.cuda.synchronize()
+                for s, x in zip(g.inputs, inputs):
+                    if x is not s:
+                        _data(s).copy_(_data(x))
+                g = _Captured(body, g.inputs, static_args, warmup=0)
             except Exception as e:  # noqa: BLE001 - fall back to eager, but say why
                 print(f"[graphs] {name}: capture failed, running eagerly: {e}", flush=True)
                 torch.cuda.synchronize()
