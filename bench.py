@@ -118,11 +118,12 @@ def main():
     use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
     # Independent cross-fits in flight at EVERY world size (same setting for the whole
     # 1/2/4/8 curve): the CV path solve is a latency-bound serial recurrence that fills few
-    # CUs, so a second fit's HBM-bound Gram runs beside it on its own stream.
+    # CUs, so another fit's HBM-bound Gram runs beside it on its own stream.
     inflight = 3 if args.inflight < 0 else max(1, args.inflight)
     if inflight > 1:
-        # sharing the chip with the other fit's path solve, fewer and longer Gram workgroups
-        # win (profiles/r01_bench/wg_inflight.log: 1024 -> 5.9 ms/step, 2048 -> 6.1)
+        # Gram workgroup count beside another fit's path solve: 1024 for two fits in
+        # lockstep (profiles/r01_bench/wg_inflight.log); staggered, 824-4096 are within 3 %
+        # and 2048 is the default (profiles/r02_overlap/stagger_sweep.log)
         os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024" if not args.stagger else "2048")
 
     def in_slot(ph, i):
@@ -136,10 +137,12 @@ def main():
 
     # Stagger: with two fits started together on two streams, the two Grams share the chip
     # and then the two path solves leave it mostly idle, a lockstep that persists (both
-    # fits are identical). One event orders the Grams across the streams: fit k's Gram
-    # starts when fit k-1's Gram has finished, so each Gram runs beside the other fit's
-    # path solve. The hooks are eager phases between the captured graphs (the fit is
-    # split into a Gram graph and a path/residual/score graph).
+    # fits are identical). --stagger 1: one event orders the Grams across the streams (fit
+    # k's Gram starts when fit k-1's has finished). --stagger 2 (default): the Grams of all
+    # fits run on one low-priority stream, each fit's remaining phases on its own
+    # high-priority stream, so its path solve gets CUs ahead of the next Gram's
+    # workgroups. The hooks are eager phases between the captured graphs (the fit is split
+    # into a Gram-tile graph and a reduce/path/residual/score graph).
     gram_done = {"ev": None}
 
     def wait_prev_gram(st):
