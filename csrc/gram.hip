@@ -230,7 +230,9 @@ __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
 // into a 272-block slab slot; a host-built table maps slab blocks to Gram blocks.
 constexpr int PAIR_SLOTS = 272;
 #ifndef GRAM_DIAG
-#define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA
+#define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA,
+                      // 3 = 1 with only the off-diagonal tile's workgroups (each K-step
+                      // loaded once), 4 = normal work on the off-diagonal tiles only
 #endif
 
 __device__ __forceinline__ int tri_index(int m, int n) {   // m <= n < 8, row-major triangle
@@ -275,7 +277,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
 #endif
     const bf16_t* As = lds[cur][abuf];
     const bf16_t* Bs = lds[cur][bbuf];
-    if (!idle && GRAM_DIAG != 1) {
+    if (!idle && GRAM_DIAG != 1 && GRAM_DIAG != 3) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int cc = kk * 4 + (lane >> 4);
@@ -325,6 +327,9 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   const Chunk ch = chunks[c];
   const int4 tl = tiles[t];
   const int type = tl.z;
+#if GRAM_DIAG >= 3
+  if (type != 0) return;
+#endif
   const bool haveB = type != 2;
   const int a0 = tl.x * GT, b0 = tl.y * GT;
   const int wid = threadIdx.x >> 6;

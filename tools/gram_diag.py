@@ -12,7 +12,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
-LIBS = {m: ROOT / "ate_replication_causalml_amd" / "_lib" / f"libatehip_gdiag{m}.so" for m in (1, 2)}
+LIBS = {m: ROOT / "ate_replication_causalml_amd" / "_lib" / f"libatehip_gdiag{m}.so"
+        for m in (1, 2, 3, 4)}
 
 
 KERNELS = ["pair"]
@@ -36,7 +37,8 @@ def main():
     if "--build" in sys.argv:
         return build()
     n = sys.argv[1] if len(sys.argv) > 1 else "1e7"
-    for tag, lib in [("normal", None), ("no-mfma", LIBS[1]), ("no-dma", LIBS[2])]:
+    for tag, lib in [("normal", None), ("no-mfma", LIBS[1]), ("no-dma", LIBS[2]),
+                     ("no-mfma-offdiag-only", LIBS[3]), ("offdiag-only", LIBS[4])]:
         env = dict(os.environ)
         if lib is not None:
             env["ATE_HIP_LIB"] = str(lib)
