@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step's device phases in hipGraphs (default: on with a GPU; "
                          "RCCL collectives always run eagerly between the graph replays)")
+    ap.add_argument("--parity", type=int, default=1,
+                    help="after the timed steps, fit the same rows from a float64 panel (fp64 "
+                         "Gram, fp64 path solves; untimed) and report the ATE / SE differences")
     ap.add_argument("--blocked", type=int, default=1,
                     help="1: 64-row blocked panel layout (one contiguous HBM run per Gram "
                          "K-step, ops/panel.py); 0: column-major")
@@ -267,9 +270,28 @@ def main():
         sync()
     lat = torch.tensor([(time.perf_counter() - t1) / nlat], dtype=torch.float64, device=device)
     comm.all_reduce_max_(lat)
+    ate, se = [float(v) for v in res.detach().cpu()]
+    n_inflight = len(runs)
+    parity = None
+    if args.parity and args.dtype != "f64":
+        # ATE/SE parity (the metric's second half), untimed: the same rows generated as a
+        # float64 panel, fp64 Gram and fp64 path solves (the path tests/test_gpu.py pins
+        # against the float64 reference estimator at small N)
+        del runs
+        from ate_replication_causalml_amd.ops.gram import clear_plans
+        clear_plans()
+        t2 = time.perf_counter()
+        pan64 = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed,
+                                dtype="f64", device=device, rank=rank, world=world)
+        r64 = dml_crossfit_panel(pan64, args.folds, "min", comm=comm, seg_counts=seg_counts)[0]
+        a64, s64 = [float(v) for v in r64.detach().cpu()]
+        parity = {"reference": "same rows as a float64 panel: fp64 Gram + fp64 CV-LASSO paths",
+                  "ate_f64": a64, "se_f64": s64, "abs_diff_ate": abs(ate - a64),
+                  "rel_diff_se": abs(se - s64) / abs(s64), "seconds": time.perf_counter() - t2}
+        del pan64
+        clear_plans()
     guard.__exit__(None, None, None)
     ms = elapsed / args.steps * 1e3
-    ate, se = [float(v) for v in res.detach().cpu()]
     if not (math.isfinite(ate) and math.isfinite(se)):
         from ate_replication_causalml_amd.utils.guards import NumericalError
         raise NumericalError(f"bench step returned ate={ate} se={se} (truncated CV fold path?)")
@@ -297,15 +319,16 @@ def main():
                 "p": args.p,
                 "folds": args.folds,
                 "parallelism": f"dp{world}",
-                "inflight": len(runs),
+                "inflight": n_inflight,
                 "layout": "blocked64" if pan.blocked else "colmajor",
-                "stagger": bool(args.stagger and len(runs) > 1 and device.type == "cuda"),
+                "stagger": bool(args.stagger and n_inflight > 1 and device.type == "cuda"),
             },
             "ate": ate,
             "se": se,
             "hipgraph": graphed,
-            "inflight": len(runs),
+            "inflight": n_inflight,
             "single_fit_ms": float(lat.item()) * 1e3,
+            "parity": parity,
         }
         if emulate > 1:
             out["emulated_world"] = emulate
