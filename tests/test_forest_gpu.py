@@ -31,8 +31,12 @@ def test_bin_matrix_gpu_matches_host(gpu):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("nw", ["0", "4", "8", "16"])
 @pytest.mark.parametrize("case", ["rf_class", "rf_reg", "grf_reg", "causal"])
-def test_forest_gpu_bit_identical_to_host(gpu, case):
+def test_forest_gpu_bit_identical_to_host(gpu, case, nw, monkeypatch):
+    """Every instantiation of the grow kernel (waves per tree 4 / 8 / 16 with their
+    register budgets, and the automatic choice) grows the host engine's trees."""
+    monkeypatch.setenv("ATE_FOREST_NW", nw)
     X, W, Y = _data()
     kw = dict(ntree=24, seed=17)
     if case == "rf_class":

@@ -12,7 +12,7 @@ one() {  # tag, env..., -- bench args
   python -c "import json,sys; d=json.loads(open(sys.argv[2]).read().strip().splitlines()[-1]); print(sys.argv[1], round(d['ms_per_step'],3), 'single', round(d['single_fit_ms'],3), repr(d['ate']), repr(d['se']))" $tag $R/gpurun_out/b_$tag.log | tee -a $OUT
 }
 for spec in ${SWEEP:-"1 1024 2 0" "1 1024 2 1" "2 2048 3 0" "2 2048 3 1" "2 1024 2 1" "2 4096 3 1"}; do
-  set -- $spec
+  set -- ${spec//,/ }
   BARGS="--stagger $1 --inflight $3 --blocked ${4:-1}" one s$1_wg$2_if$3_b${4:-1} ATE_GRAM_PAIR_WG=$2 || exit 1
 done
 [ -n "$NOPROF" ] && exit 0
