@@ -1,0 +1,36 @@
+"""bench.py with two ranks sharing one MI355X (collectives over gloo, host-staged): the
+multi-GPU step as the driver runs it -- graph-captured device phases, three fits in
+flight on staggered streams, path solves sharded over the ranks -- gives the ATE/SE of
+one process holding all the rows. (RCCL itself: tests/test_gpu_segmented.py.)"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _json(out):
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+
+
+def test_two_ranks_on_one_gpu_match_one_process(gpu):
+    bench = os.path.join(ROOT, "bench.py")
+    args = ["--steps", "3", "--warmup", "1", "--parity", "0"]
+    env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29655",
+                        bench, "--gpus", "2", "--rows", "500000", *args],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = _json(r.stdout)
+    one = subprocess.run([sys.executable, bench, "--rows", "1000000", *args],
+                         capture_output=True, text=True, timeout=240)
+    assert one.returncode == 0, one.stderr[-3000:]
+    ref = _json(one.stdout)
+    assert two["hipgraph"] and two["inflight"] == 3 and two["n_gpus"] == 2
+    assert two["ate"] == pytest.approx(ref["ate"], rel=1e-9, abs=1e-12)
+    assert two["se"] == pytest.approx(ref["se"], rel=1e-9)
