@@ -144,3 +144,31 @@ __all__ = ["naive_ate", "ate_condmean_ols", "prop_score_weight", "prop_score_ols
            "ate_condmean_lasso", "ate_lasso", "prop_score_lasso", "doubly_robust",
            "doubly_robust_glm", "belloni", "double_ml", "residual_balance_ATE",
            "causal_forest_ate", "RunConfig"]
+
+
+def tau_hat_dr_est(w, y, p, tauhat0x, tauhat1x, b=0, seed=1991, compat="reference"):
+    """E10 helper ``tau_hat_dr_est`` (ate_functions.R:267-283): ONE with-replacement
+    resample of the fixed AIPW inputs, ``mean(est1, na.rm=TRUE) + mean(est2)``. R's
+    ``sample()`` is replaced by counter-based Philox draws: replicate ``b`` of ``seed``
+    is the b-th of the replicates ``doubly_robust(..., bootstrap_se=TRUE)`` uses (K20)."""
+    from .ops import stats as S
+    import torch
+    arr = [torch.as_tensor(np.asarray(v, dtype=np.float64)) for v in (w, y, p, tauhat0x,
+                                                                       tauhat1x)]
+    w_, y_, p_, m0, m1 = arr
+    e1, e2 = S.aipw_terms(w_, y_, p_, m0, m1, compat)
+    return float(S.bootstrap_multinomial(e1.contiguous(), e2.contiguous(), 1, seed, b0=b)[0])
+
+
+def chernozhukov(dataset, treatment_var, outcome_var, idx1, idx2, num_trees, seed=123,
+                 covariates=None, run=None):
+    """E12 helper ``chernozhukov`` (ate_functions.R:332-369): RF for W trained on rows
+    ``idx1``, RF for Y on ``idx2`` (0-based row positions), both predicted on all rows,
+    no-intercept regression of the residuals. Returns R's ``list(tau_hat, se_hat)`` as a
+    dict."""
+    from .estimators import forest as DF
+    Y, W, X = _split(dataset, treatment_var, outcome_var, covariates)
+    dev = None if run is None or run.backend != "cpu" else "cpu"
+    tau, se = DF.chernozhukov(Y, W, X, np.asarray(idx1), np.asarray(idx2), num_trees, seed,
+                              device=dev)
+    return {"tau_hat": float(tau), "se_hat": float(se)}

@@ -95,3 +95,29 @@ def test_loader_reads_social_pressure_layout(tmp_path):
     d = load_social_pressure(path, n_obs=400, seed=1)
     assert d.X.shape == (399, 21) or d.X.shape == (400, 21)
     assert np.allclose(d.X[:, :15].mean(0), 0, atol=0.2)
+
+
+def test_rstyle_helpers_tau_hat_dr_est_and_chernozhukov():
+    """The reference's two helpers (E10 tau_hat_dr_est, E12 chernozhukov) by name: one
+    bootstrap replicate equals replicate b of the float64 oracle's bootstrap; one DML half
+    equals the oracle's."""
+    import numpy as np
+    import pandas as pd
+    from ate_replication_causalml_amd import rstyle
+    from ate_replication_causalml_amd.config import RunConfig
+    from ate_replication_causalml_amd.reference import estimators as R
+    rs = np.random.RandomState(0)
+    n = 400
+    w = (rs.rand(n) < .5).astype(float)
+    y = (rs.rand(n) < .4).astype(float)
+    p = np.clip(rs.rand(n), .1, .9)
+    m0, m1 = rs.rand(n), rs.rand(n)
+    taus = [rstyle.tau_hat_dr_est(w, y, p, m0, m1, b=b) for b in range(4)]
+    np.testing.assert_allclose(taus, R.aipw_bootstrap(w, y, p, m0, m1, B=4)[1], rtol=1e-12)
+    X = rs.randn(n, 4)
+    df = pd.DataFrame(X, columns=list("abcd"))
+    df["W"], df["Y"] = w, y
+    got = rstyle.chernozhukov(df, "W", "Y", np.arange(200), np.arange(200, n), 15,
+                              run=RunConfig(backend="cpu"))
+    want = R.chernozhukov(y, w, X, np.arange(200), np.arange(200, n), 15)
+    assert got["tau_hat"] == want[0] and got["se_hat"] == want[1]
