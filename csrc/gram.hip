@@ -310,12 +310,12 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
     __syncthreads();
   }
   if (idle) return;
-  // acc reg r of lane l = (row (l>>4)*4+r, col l&15) of the 16x16 block
+  // Slab block image is lane-major: float4 `lane` holds acc regs r = 0..3 = (row (l>>4)*4+r,
+  // col l&15) of the 16x16 block, so each block is ONE 1-KB dwordx4 store per wave (4x fewer
+  // store instructions than a row-major image; the epilogue is store-issue bound).
 #pragma unroll
   for (int i = 0; i < NB; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      out[i * 256 + ((lane >> 4) * 4 + r) * 16 + (lane & 15)] = acc[i][r];
+    *reinterpret_cast<f32x4*>(out + i * 256 + lane * 4) = acc[i];
 }
 
 __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
@@ -364,7 +364,8 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
     const int s = (int)(e / per);
     const int64_t rem = e % per;
     const int tb = (int)(rem >> 8);                 // tile * PAIR_SLOTS + slot
-    const int rc = (int)(rem & 255), r = rc >> 4, cl = rc & 15;
+    const int ln = (int)(rem & 255) >> 2;           // lane-major image (pair_wave epilogue)
+    const int r = ((ln >> 4) << 2) | (int)(rem & 3), cl = ln & 15;
     const int2 bl = blocks[tb];
     if (bl.x < 0) continue;
     if (bl.x == bl.y && r > cl) continue;

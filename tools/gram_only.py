@@ -14,6 +14,7 @@ variants = sys.argv[2:] or [gram_mod.GRAM_KERNEL]
 pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.device("cuda", 0),
                       blocked=os.environ.get("ATE_BLOCKED", "1") == "1")
 ref = None
+stage = os.environ.get("ATE_GRAM_STAGE", "all")   # "tiles": the tile kernel alone (no slab reduce)
 for v in variants:
     gram_mod.GRAM_KERNEL = v
     gram_mod._plan_cache.clear()
@@ -23,7 +24,7 @@ for v in variants:
     e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e[0].record()
     for _ in range(10):
-        gram_mod.gram(pan)
+        gram_mod.gram(pan, stage=stage)
     e[1].record()
     torch.cuda.synchronize()
     G = G.clone()

@@ -1,0 +1,285 @@
+// HBM read-rate probe on one MI355X (gfx950): is ~4.2 TB/s (the Gram's DMA-only stream and
+// torch reductions over the bench panel) the box's ceiling, or an access-shape limit?
+//   hipcc -O3 --offload-arch=gfx950 tools/hbm_stream.hip -o tools/hbm_stream && tools/hbm_stream
+// A: register loads (global_load_dwordx4), U loads in flight per lane, grid-stride, sweep WGs.
+// B: LDS-DMA stream shaped like the Gram: one 512-thread workgroup per CU (persistent), each
+//    step copies STAGE bytes of a contiguous run into an LDS ring of D stages; vmcnt-counted
+//    waits keep D-1 stages in flight; one barrier per step.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void rd_kernel(const v4u* __restrict__ p, long n16, unsigned* out) {
+  uint32_t acc = 0;
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(p + i + u * stride) : p[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n16; i += stride) { v4u v = p[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+  if (acc == 0x12345678u) out[0] = acc;   // keeps the loads alive
+}
+
+// blocked read: each workgroup owns a contiguous slice, lanes read consecutive 16 B
+__device__ __forceinline__ int xcd_remap(int bid, int nwg);
+template <int U>
+__global__ __launch_bounds__(256) void rd_slice_kernel(const uint4* __restrict__ p, long n16, unsigned* out,
+                                                       int share = 1) {
+  uint32_t acc = 0;
+  const long nsl = gridDim.x / share;
+  const long per = (n16 + nsl - 1) / nsl;
+  const long b0 = (long)(xcd_remap(blockIdx.x, gridDim.x) / share) * per, b1 = b0 + per < n16 ? b0 + per : n16;
+  for (long i = b0 + threadIdx.x; i < b1; i += U * 256) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      long j = i + u * 256;
+      v[u] = j < b1 ? p[j] : uint4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// LDS-DMA ring: STAGE_KB per stage, D stages; 8 waves each issue STAGE_KB/8 1-KB pieces per stage
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg & 7) return bid;
+  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// remap: 1 = consecutive slices on one XCD (the Gram's chunk map); slab: float4 stores per
+// lane at the end (the Gram's per-workgroup slab partial, 256 KB for 512 threads x 32)
+template <int STAGE_KB, int D, int SWZ = 0>
+__global__ __launch_bounds__(512) void dma_kernel(const char* __restrict__ p, long nbytes, unsigned* out,
+                                                  int remap = 0, float4* slab = nullptr, int nslab = 0,
+                                                  int share = 1, int offset = 0) {
+  __shared__ __attribute__((aligned(16))) char lds[D][STAGE_KB * 1024];
+  constexpr int PIECES = STAGE_KB / 8;   // per wave per stage
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long stage_bytes = STAGE_KB * 1024L;
+  const long nst = nbytes / stage_bytes;
+  const long nslices = gridDim.x / share;
+  const long per = (nst + nslices - 1) / nslices;
+  const long Lr = remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const long bid = Lr / share;
+  const long s0 = bid * per, s1 = s0 + per < nst ? s0 + per : nst;
+  const long rot = (Lr % share) * (long)offset;
+  auto issue = [&](long s, int slot) {
+    long sr = s1 > s0 ? s0 + ((s - s0 + rot) % (s1 - s0)) : s;
+    const char* src = p + sr * stage_bytes;
+#pragma unroll
+    for (int r = 0; r < PIECES; ++r) {
+      const int q = wid * PIECES + r;
+      // SWZ 1: the Gram's source order (column col = q*8 + lane/8, 16-B chunk (lane&7)^(col&7))
+      const int col = q * 8 + (lane >> 3);
+      const int off = SWZ == 1 ? col * 128 + (((lane & 7) ^ (col & 7)) << 4)
+                    : SWZ == 2 ? q * 1024 + ((lane & 7) << 7) + ((lane >> 3) << 4)   // column-strided lanes
+                               : q * 1024 + lane * 16;
+      __builtin_amdgcn_global_load_lds(src + off,
+                                       (__attribute__((address_space(3))) void*)(&lds[slot][q * 1024]),
+                                       16, 0, 0);
+    }
+  };
+  // prologue: D-1 stages in flight
+  for (int k = 0; k < D - 1; ++k)
+    if (s0 + k < s1) issue(s0 + k, k);
+  uint32_t acc = 0;
+  for (long s = s0; s < s1; ++s) {
+    const int slot = (int)((s - s0) % D);
+    // stage s landed when at most (D-2) younger stages' pieces are outstanding
+    if (s + D - 1 < s1) {
+      // issue stage s+D-1 after the wait below would serialise; issue first then wait
+      if constexpr (D == 2) __builtin_amdgcn_s_waitcnt(0x0F70);
+      else if constexpr (D == 3) __builtin_amdgcn_s_waitcnt(0x0F70 | ((PIECES) & 0xF) | (((PIECES) >> 4) << 14));
+      else __builtin_amdgcn_s_waitcnt(0x0F70 | ((2 * PIECES) & 0xF) | (((2 * PIECES) >> 4) << 14));
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    __syncthreads();
+    acc ^= *reinterpret_cast<const uint32_t*>(&lds[slot][(threadIdx.x * 16) % (STAGE_KB * 1024)]);
+    __syncthreads();
+    if (s + D - 1 < s1) issue(s + D - 1, (int)((s + D - 1 - s0) % D));
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+  if (slab) {
+    float4* o = slab + (long)blockIdx.x * nslab * 512;
+    for (int i = 0; i < nslab; ++i) o[i * 512 + threadIdx.x] = float4{(float)acc, 0.f, 0.f, 1.f};
+  }
+}
+
+// Paired readers (the Gram's two sibling workgroups per row chunk read the same bytes) with a
+// lag: role 1 issues stage s only after role 0 has landed it (flag), so its reads hit L2.
+// Bounded spin: the flag is a performance hint only (data are read-only).
+__global__ __launch_bounds__(512) void dma_pair_kernel(const char* __restrict__ p, long nbytes, unsigned* out,
+                                                       int* flags, int lag, int spin_max) {
+  __shared__ __attribute__((aligned(16))) char lds[2][64 * 1024];
+  constexpr int PIECES = 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long stage_bytes = 64 * 1024L;
+  const long nst = nbytes / stage_bytes;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int pair = L >> 1, role = L & 1;
+  const long npairs = gridDim.x / 2;
+  const long per = (nst + npairs - 1) / npairs;
+  const long s0 = pair * per, s1 = s0 + per < nst ? s0 + per : nst;
+  int* flag = flags + pair * 16;
+  auto issue = [&](long s, int slot) {
+    const char* src = p + s * stage_bytes;
+#pragma unroll
+    for (int r = 0; r < PIECES; ++r) {
+      const int q = wid * PIECES + r;
+      __builtin_amdgcn_global_load_lds(src + q * 1024 + lane * 16,
+                                       (__attribute__((address_space(3))) void*)(&lds[slot][q * 1024]),
+                                       16, 0, 0);
+    }
+  };
+  auto wait_for = [&](long need) {   // role 1: until role 0 has landed `need` stages
+    if (role == 1 && lag > 0 && threadIdx.x == 0) {
+      for (int it = 0; it < spin_max; ++it) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  };
+  wait_for(lag);
+  __syncthreads();
+  if (s0 < s1) issue(s0, 0);
+  uint32_t acc = 0;
+  for (long s = s0; s < s1; ++s) {
+    const int slot = (int)((s - s0) & 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if (role == 0 && threadIdx.x == 0)
+      __hip_atomic_store(flag, (int)(s - s0 + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s + 1 < s1) wait_for(s - s0 + 1 + lag);
+    __syncthreads();
+    acc ^= *reinterpret_cast<const uint32_t*>(&lds[slot][(threadIdx.x * 16) % (64 * 1024)]);
+    __syncthreads();
+    if (s + 1 < s1) issue(s + 1, slot ^ 1);
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <typename F>
+static float timeit(F f, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+  f();
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(a);
+  for (int i = 0; i < reps; ++i) f();
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms; (void)hipEventElapsedTime(&ms, a, b);
+  return ms / reps;
+}
+
+int main() {
+  const long nbytes = 10240000000L;   // the bench panel: 1e7 x 512 x bf16
+  char* buf; unsigned* out;
+  CHECK(hipMalloc(&buf, nbytes));
+  CHECK(hipMalloc(&out, 64));
+  CHECK(hipMemset(buf, 1, nbytes));
+  CHECK(hipDeviceSynchronize());
+  const long n16 = nbytes / 16;
+  auto rep = [&](const char* tag, float ms) {
+    printf("%-40s %7.3f ms  %5.2f TB/s\n", tag, ms, nbytes / (ms * 1e-3) / 1e12);
+    fflush(stdout);
+  };
+  char tag[128];
+  for (int wg : std::vector<int>{}) {
+    snprintf(tag, sizeof tag, "grid-stride U=4 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((rd_kernel<4, false>), dim3(wg), dim3(256), 0, 0, (const v4u*)buf, n16, out); }, 5));
+    snprintf(tag, sizeof tag, "grid-stride U=8 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((rd_kernel<8, false>), dim3(wg), dim3(256), 0, 0, (const v4u*)buf, n16, out); }, 5));
+    snprintf(tag, sizeof tag, "grid-stride nt U=8 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((rd_kernel<8, true>), dim3(wg), dim3(256), 0, 0, (const v4u*)buf, n16, out); }, 5));
+    snprintf(tag, sizeof tag, "slice U=8 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL(rd_slice_kernel<8>, dim3(wg), dim3(256), 0, 0, (const uint4*)buf, n16, out); }, 5));
+  }
+  float4* slab;
+  CHECK(hipMalloc(&slab, 2048L * 32 * 512 * 16));
+  for (int wg : std::vector<int>{}) {
+    for (int rm = 0; rm < 2; ++rm) {
+      snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d remap=%d", wg, rm);
+      rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, rm, (float4*)nullptr, 0); }, 5));
+      snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d remap=%d +256KB slab", wg, rm);
+      rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, rm, slab, 32); }, 5));
+    }
+  }
+  int* flags;
+  CHECK(hipMalloc(&flags, 4096 * 16 * 4));
+  for (int wg : {256, 1024, 2048}) {
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d linear", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 0>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 1, 0); }, 5));
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d gram-swizzled src", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 1>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 1, 0); }, 5));
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d lane-strided src", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 1, 0); }, 5));
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED gram-swizzled", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 1>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2, 0); }, 5));
+  }
+  for (int wg : std::vector<int>{}) {
+    snprintf(tag, sizeof tag, "slice U=8 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL(rd_slice_kernel<8>, dim3(wg), dim3(256), 0, 0, (const uint4*)buf, n16, out, 1); }, 5));
+    snprintf(tag, sizeof tag, "slice U=8 wg=%d PAIRED", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL(rd_slice_kernel<8>, dim3(wg), dim3(256), 0, 0, (const uint4*)buf, n16, out, 2); }, 5));
+    snprintf(tag, sizeof tag, "slice U=16 wg=%d PAIRED", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL(rd_slice_kernel<16>, dim3(wg), dim3(256), 0, 0, (const uint4*)buf, n16, out, 2); }, 5));
+  }
+  for (int wg : std::vector<int>{}) {
+    for (int off : {1, 2, 4, 8, 16, 32}) {
+      snprintf(tag, sizeof tag, "PAIRED remap offset=%d wg=%d", off, wg);
+      rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2, off); }, 5));
+    }
+  }
+  for (int wg : std::vector<int>{}) {
+    for (int lag : {0, 1, 2, 3}) {
+      snprintf(tag, sizeof tag, "pair-lag wg=%d lag=%d", wg, lag);
+      rep(tag, timeit([&] { (void)hipMemsetAsync(flags, 0, 4096 * 16 * 4, 0);
+                            hipLaunchKernelGGL(dma_pair_kernel, dim3(wg), dim3(512), 0, 0, buf, nbytes, out, flags, lag, 4000); }, 5));
+    }
+  }
+  for (int wg : {256, 2048}) {
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED (unique bytes)", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2); }, 5));
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED no remap", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 0, (float4*)nullptr, 0, 2); }, 5));
+  }
+  for (int wg : {256}) {
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 0, (float4*)nullptr, 0); }, 5));
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d remap", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0); }, 5));
+    snprintf(tag, sizeof tag, "dma 32KB x4 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<32, 4>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out); }, 5));
+    snprintf(tag, sizeof tag, "dma 48KB x3 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<48, 3>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out); }, 5));
+    snprintf(tag, sizeof tag, "dma 32KB x3 wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<32, 3>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out); }, 5));
+  }
+  (void)hipFree(buf);
+  return 0;
+}
+
+// ctypes entry (tools/hbm_buffer_probe.py): the single-reader 64 KB x 2 LDS-DMA stream over a
+// caller-owned buffer (e.g. a torch-allocated bench panel); returns ms per pass.
+extern "C" float hbm_dma_probe(void* ptr, long nbytes, int wg, int reps, int share) {
+  unsigned* out;
+  if (hipMalloc(&out, 64) != hipSuccess) return -1.f;
+  float ms = timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 1>), dim3(wg), dim3(512), 0, 0, (const char*)ptr,
+                                             nbytes, out, 1, (float4*)nullptr, 0, share, 0); }, reps);
+  (void)hipFree(out);
+  return ms;
+}
