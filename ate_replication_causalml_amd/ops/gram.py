@@ -77,20 +77,49 @@ class GramPlan:
         # of a row chunk close in time so their shared panels are L2 hits (measured 4.65 ->
         # 4.09 ms at N=1e7, p=500 going from 768 to 3072 WGs)
         target = 3072 if T == BF16_TILE_BIG else TARGET_WG
+        whole_rounds = False
         if self.pair:
-            target = int(os.environ.get("ATE_GRAM_PAIR_WG", 2048))
+            # one Gram alone on the chip: 5 whole rounds of workgroups (N=1e7, p=500, 5 folds:
+            # 2.48 ms vs 2.61 at 2040 WGs and 2.70 at 2060, profiles/r02c_gram); bench.py's
+            # overlapped fits set ATE_GRAM_PAIR_WG (finer workgroups share CUs with path solves)
+            env = os.environ.get("ATE_GRAM_PAIR_WG")
+            whole_rounds = env is None
+            target = int(env) if env is not None else 5 * _cu_count(panel.device)
         target = int(os.environ.get("ATE_GRAM_WG", target))
         nchunk_target = max(1, target // ntiles)
-        ch_rows = max(K, (rows_total // nchunk_target) // K * K)
         chunks = []
         seg_chunk0 = [0]
-        for s, (r0, r1) in enumerate(panel.seg_bounds):
-            r = int(r0)
-            while r < r1:
-                e = min(int(r1), r + ch_rows)
-                chunks.append((r, e, s, 0))
-                r = e
-            seg_chunk0.append(len(chunks))
+        if self.pair:
+            # equal chunks, the same count in every segment, total workgroups <= target: a
+            # launch of 2 x nseg x k near-equal workgroups fills whole rounds of CUs instead of
+            # leaving a few stragglers of a ~0.3 ms workgroup to run alone at the end (2060 WGs
+            # on 256 CUs = 8 rounds + 12 WGs before this)
+            k = max(1, nchunk_target // max(1, panel.nseg))
+            if whole_rounds:
+                ncu = _cu_count(panel.device)
+                per = ntiles * max(1, panel.nseg)
+                kr = k
+                while kr > 1 and (per * kr) % ncu:
+                    kr -= 1
+                if (per * kr) % ncu == 0 and 2 * kr >= k:
+                    k = kr
+            for s, (r0, r1) in enumerate(panel.seg_bounds):
+                steps = (int(r1) - int(r0)) // K
+                ks = max(1, min(k, steps))
+                for j in range(ks):
+                    a = int(r0) + (steps * j // ks) * K
+                    e = int(r0) + (steps * (j + 1) // ks) * K if j + 1 < ks else int(r1)
+                    chunks.append((a, e, s, 0))
+                seg_chunk0.append(len(chunks))
+        else:
+            ch_rows = max(K, (rows_total // nchunk_target) // K * K)
+            for s, (r0, r1) in enumerate(panel.seg_bounds):
+                r = int(r0)
+                while r < r1:
+                    e = min(int(r1), r + ch_rows)
+                    chunks.append((r, e, s, 0))
+                    r = e
+                seg_chunk0.append(len(chunks))
         dev = panel.device
         self.T, self.K, self.ntiles, self.nchunks = T, K, ntiles, len(chunks)
         self.tiles = torch.tensor(tiles, dtype=torch.int32, device=dev)
@@ -106,6 +135,13 @@ class GramPlan:
         per_tile = PAIR_SLOTS * 256 if self.pair else T * T
         self.slab = torch.empty(self.nchunks * ntiles * per_tile, dtype=slab_dtype, device=dev)
         self.G = torch.empty((panel.nseg, P, P), dtype=torch.float64, device=dev)
+
+
+def _cu_count(dev) -> int:
+    try:
+        return int(torch.cuda.get_device_properties(dev).multi_processor_count)
+    except Exception:  # noqa: BLE001 - CPU / no device: MI355X has 256 CUs
+        return 256
 
 
 def _pair_tiles(nt: int):

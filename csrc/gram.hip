@@ -229,6 +229,15 @@ __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
 // hits L2 on what the other fetched). Every wave writes its 16x16 blocks contiguously
 // into a 272-block slab slot; a host-built table maps slab blocks to Gram blocks.
 constexpr int PAIR_SLOTS = 272;
+#ifndef GRAM_CROSS
+// 1: the two workgroups of a chunk issue a stage's 64 LDS-DMA pieces in crossed orders
+// (type-1 wave w issues what type-0 wave (w+4)%8 issues), so the pair never requests the same
+// line at the same moment; tools/hbm_stream.hip: a paired stream 4.5 -> 5.3 TB/s of unique
+// bytes. 2: type 1 issues its B pieces before its A pieces instead. 0: same order.
+// In the Gram itself neither changed anything (tile kernel 2.63 / 2.62 / 2.69 ms for 1 / 0 /
+// 2, bench step 3.81 / 3.83, profiles/r02c_gram/ab_cross.log): kept as an option, default 0.
+#define GRAM_CROSS 0
+#endif
 #ifndef GRAM_DIAG
 #define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA,
                       // 3 = 1 with only the off-diagonal tile's workgroups (each K-step
@@ -246,21 +255,27 @@ template <bool TRI>
 __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t cs, int64_t bs, int a0,
                                           int b0, bool haveB, bool idle, int abuf, int bbuf,
                                           int arow0, int bcol0, const Chunk& ch,
-                                          bf16_t (*lds)[2][GT * GK], float* __restrict__ out) {
+                                          bf16_t (*lds)[2][GT * GK], float* __restrict__ out,
+                                          bool second) {
   constexpr int NB = TRI ? 36 : 32;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   f32x4 acc[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // which 8-column pieces this wave copies (any wave may copy any piece: the LDS image only
+  // depends on q); `second` = the chunk's type-1 workgroup
+  const int qw = (GRAM_CROSS == 1 && second) ? ((wid + 4) & 7) : wid;
+  const bool bfirst = GRAM_CROSS == 2 && second && haveB;
   auto stage = [&](int st, int64_t i0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = wid * 4 + r;
+      const int q = qw * 4 + r;
       const int col = q * 8 + (lane >> 3);
       const int cc = (lane & 7) ^ (col & 7);
       const bf16_t* Xk = X + (i0 >> 6) * bs + cc * 8;      // i0: multiple of GK = 64
+      if (bfirst) glds16(Xk + (int64_t)(b0 + col) * cs, &lds[st][1][q * 8 * GK]);
       glds16(Xk + (int64_t)(a0 + col) * cs, &lds[st][0][q * 8 * GK]);
-      if (haveB) glds16(Xk + (int64_t)(b0 + col) * cs, &lds[st][1][q * 8 * GK]);
+      if (haveB && !bfirst) glds16(Xk + (int64_t)(b0 + col) * cs, &lds[st][1][q * 8 * GK]);
     }
   };
   auto frag = [&](const bf16_t* P_, int col, int cc) {
@@ -346,9 +361,9 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   const int base = tri ? 128 + (wid - 4) * 36 : wid * 32;
   float* out = slab + ((int64_t)c * ntiles + t) * (PAIR_SLOTS * 256) + (int64_t)base * 256;
   if (tri)
-    pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
+    pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
   else
-    pair_wave<false>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out);
+    pair_wave<false>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
 }
 
 // blocks: [ntiles][PAIR_SLOTS] int2 (I, J) = 16-column block coordinates of the Gram (I: A

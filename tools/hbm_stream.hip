@@ -81,10 +81,13 @@ __global__ __launch_bounds__(512) void dma_kernel(const char* __restrict__ p, lo
     const char* src = p + sr * stage_bytes;
 #pragma unroll
     for (int r = 0; r < PIECES; ++r) {
-      const int q = wid * PIECES + r;
+      // SWZ 3: like 1, but the second reader of a shared stage walks its pieces from the
+      // middle of the stage (crossed order: the two readers first touch different lines)
+      const int q = SWZ == 3 ? (wid * PIECES + r + (int)(Lr % share) * (STAGE_KB / 2)) % STAGE_KB
+                             : wid * PIECES + r;
       // SWZ 1: the Gram's source order (column col = q*8 + lane/8, 16-B chunk (lane&7)^(col&7))
       const int col = q * 8 + (lane >> 3);
-      const int off = SWZ == 1 ? col * 128 + (((lane & 7) ^ (col & 7)) << 4)
+      const int off = (SWZ == 1 || SWZ == 3) ? col * 128 + (((lane & 7) ^ (col & 7)) << 4)
                     : SWZ == 2 ? q * 1024 + ((lane & 7) << 7) + ((lane >> 3) << 4)   // column-strided lanes
                                : q * 1024 + lane * 16;
       __builtin_amdgcn_global_load_lds(src + off,
@@ -220,7 +223,13 @@ int main() {
   }
   int* flags;
   CHECK(hipMalloc(&flags, 4096 * 16 * 4));
-  for (int wg : {256, 1024, 2048}) {
+  for (int wg : {256, 1280}) {
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED crossed order", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 3>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2, 0); }, 5));
+    snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED same order", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 1>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2, 0); }, 5));
+  }
+  for (int wg : std::vector<int>{}) {
     snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d linear", wg);
     rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 0>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 1, 0); }, 5));
     snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d gram-swizzled src", wg);
@@ -251,7 +260,7 @@ int main() {
                             hipLaunchKernelGGL(dma_pair_kernel, dim3(wg), dim3(512), 0, 0, buf, nbytes, out, flags, lag, 4000); }, 5));
     }
   }
-  for (int wg : {256, 2048}) {
+  for (int wg : std::vector<int>{}) {
     snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED (unique bytes)", wg);
     rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2); }, 5));
     snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED no remap", wg);
