@@ -174,6 +174,53 @@ __global__ __launch_bounds__(512) void dma_pair_kernel(const char* __restrict__ 
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Hybrid pair: role 0 stages by LDS-DMA, role 1 (the second reader of every byte) by register
+// loads (8 x dwordx4 per lane per 64 KB stage) + ds_write_b128 into the next LDS slot.
+__global__ __launch_bounds__(512) void hyb_pair_kernel(const char* __restrict__ p, long nbytes, unsigned* out,
+                                                       int role1_regs) {
+  __shared__ __attribute__((aligned(16))) char lds[2][64 * 1024];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long stage_bytes = 64 * 1024L;
+  const long nst = nbytes / stage_bytes;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int pair = L >> 1, role = L & 1;
+  const long npairs = gridDim.x / 2;
+  const long per = (nst + npairs - 1) / npairs;
+  const long s0 = pair * per, s1 = s0 + per < nst ? s0 + per : nst;
+  const bool regs = role == 1 && role1_regs;
+  v4u st[8];
+  auto issue = [&](long s, int slot) {
+    const char* src = p + s * stage_bytes;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int q = wid * 8 + r;
+      if (regs) st[r] = *reinterpret_cast<const v4u*>(src + q * 1024 + lane * 16);
+      else __builtin_amdgcn_global_load_lds(src + q * 1024 + lane * 16,
+                                            (__attribute__((address_space(3))) void*)(&lds[slot][q * 1024]),
+                                            16, 0, 0);
+    }
+  };
+  auto land = [&](int slot) {
+    if (!regs) return;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      *reinterpret_cast<v4u*>(&lds[slot][(wid * 8 + r) * 1024 + lane * 16]) = st[r];
+  };
+  if (s0 < s1) { issue(s0, 0); land(0); }
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  uint32_t acc = 0;
+  for (long s = s0; s < s1; ++s) {
+    const int slot = (int)((s - s0) & 1);
+    if (s + 1 < s1) issue(s + 1, slot ^ 1);
+    acc ^= *reinterpret_cast<const uint32_t*>(&lds[slot][(threadIdx.x * 16) % (64 * 1024)]);
+    if (s + 1 < s1) land(slot ^ 1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 template <typename F>
 static float timeit(F f, int reps) {
   hipEvent_t a, b;
@@ -224,6 +271,10 @@ int main() {
   int* flags;
   CHECK(hipMalloc(&flags, 4096 * 16 * 4));
   for (int wg : {256, 1280}) {
+    snprintf(tag, sizeof tag, "hybrid pair (role 1 regs) wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL(hyb_pair_kernel, dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1); }, 5));
+    snprintf(tag, sizeof tag, "hybrid kernel, both DMA wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL(hyb_pair_kernel, dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 0); }, 5));
     snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED crossed order", wg);
     rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 3>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2, 0); }, 5));
     snprintf(tag, sizeof tag, "dma 64KB x2 wg=%d PAIRED same order", wg);
