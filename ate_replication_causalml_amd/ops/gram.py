@@ -94,23 +94,8 @@ class GramPlan:
             # launch of 2 x nseg x k near-equal workgroups fills whole rounds of CUs instead of
             # leaving a few stragglers of a ~0.3 ms workgroup to run alone at the end (2060 WGs
             # on 256 CUs = 8 rounds + 12 WGs before this)
-            k = max(1, nchunk_target // max(1, panel.nseg))
-            if whole_rounds:
-                ncu = _cu_count(panel.device)
-                per = ntiles * max(1, panel.nseg)
-                kr = k
-                while kr > 1 and (per * kr) % ncu:
-                    kr -= 1
-                if (per * kr) % ncu == 0 and 2 * kr >= k:
-                    k = kr
-            for s, (r0, r1) in enumerate(panel.seg_bounds):
-                steps = (int(r1) - int(r0)) // K
-                ks = max(1, min(k, steps))
-                for j in range(ks):
-                    a = int(r0) + (steps * j // ks) * K
-                    e = int(r0) + (steps * (j + 1) // ks) * K if j + 1 < ks else int(r1)
-                    chunks.append((a, e, s, 0))
-                seg_chunk0.append(len(chunks))
+            chunks, seg_chunk0 = pair_chunks(panel.seg_bounds, K, ntiles, target,
+                                             _cu_count(panel.device) if whole_rounds else 0)
         else:
             ch_rows = max(K, (rows_total // nchunk_target) // K * K)
             for s, (r0, r1) in enumerate(panel.seg_bounds):
@@ -135,6 +120,34 @@ class GramPlan:
         per_tile = PAIR_SLOTS * 256 if self.pair else T * T
         self.slab = torch.empty(self.nchunks * ntiles * per_tile, dtype=slab_dtype, device=dev)
         self.G = torch.empty((panel.nseg, P, P), dtype=torch.float64, device=dev)
+
+
+def pair_chunks(seg_bounds, K: int, ntiles: int, target: int, ncu: int = 0):
+    """Row chunks of the paired-tile Gram: every segment cut into the same number k of
+    near-equal chunks (multiples of the K-step; the last one ends at the segment end), with
+    ntiles x nseg x k <= target workgroups. ncu > 0: lower k (by at most half) until the
+    launch is a whole number of rounds of ncu workgroups. Returns (chunks [(r0, r1, seg, 0)],
+    seg_chunk0 [nseg + 1])."""
+    nseg = max(1, len(seg_bounds))
+    k = max(1, max(1, target // ntiles) // nseg)
+    if ncu > 0:
+        per = ntiles * nseg
+        kr = k
+        while kr > 1 and (per * kr) % ncu:
+            kr -= 1
+        if (per * kr) % ncu == 0 and 2 * kr >= k:
+            k = kr
+    chunks, seg_chunk0 = [], [0]
+    for s, (r0, r1) in enumerate(seg_bounds):
+        r0, r1 = int(r0), int(r1)
+        steps = (r1 - r0) // K
+        ks = max(1, min(k, steps))
+        for j in range(ks):
+            a = r0 + (steps * j // ks) * K
+            e = r0 + (steps * (j + 1) // ks) * K if j + 1 < ks else r1
+            chunks.append((a, e, s, 0))
+        seg_chunk0.append(len(chunks))
+    return chunks, seg_chunk0
 
 
 def _cu_count(dev) -> int:

@@ -1,0 +1,45 @@
+"""Row-chunk planner of the paired-tile bf16 Gram (ops/gram.pair_chunks): pure host
+arithmetic, so it is pinned on the CPU. The kernel's results do not depend on the plan
+beyond fp32 partial-sum order (tests/test_gpu.py checks the Gram values on a GPU)."""
+import pytest
+
+from ate_replication_causalml_amd.ops.gram import pair_chunks
+
+
+def _check(seg_bounds, K, chunks, seg_chunk0):
+    assert seg_chunk0[0] == 0 and seg_chunk0[-1] == len(chunks)
+    for s, (r0, r1) in enumerate(seg_bounds):
+        cs = chunks[seg_chunk0[s]:seg_chunk0[s + 1]]
+        assert cs, "every segment gets at least one chunk"
+        assert cs[0][0] == r0 and cs[-1][1] == r1
+        for (a, e, seg, _), nxt in zip(cs, cs[1:] + [None]):
+            assert seg == s and a <= e
+            if nxt is not None:
+                assert e == nxt[0] and (e - a) % K == 0   # contiguous, whole K-steps
+        lens = [e - a for a, e, _, _ in cs[:-1]]
+        if lens:
+            assert max(lens) - min(lens) <= K              # near-equal
+
+
+@pytest.mark.parametrize("nseg,rows,target,ncu,want", [
+    (5, 2_000_000, 1280, 256, 1280),    # the bench shape: 5 whole rounds on 256 CUs
+    (5, 2_000_000, 2048, 0, 2040),      # explicit target: 2 x 5 x 204
+    (5, 2_000_000, 2048, 256, 1280),    # rounded down to whole rounds (k 204 -> 128)
+    (10, 1_000_000, 1280, 256, 1280),
+    (3, 3_000_000, 1280, 256, 768),
+    (1, 10_000_000, 1280, 256, 1280),
+])
+def test_pair_chunks_counts(nseg, rows, target, ncu, want):
+    segs = [(s * rows, (s + 1) * rows) for s in range(nseg)]
+    chunks, c0 = pair_chunks(segs, 64, 2, target, ncu)
+    assert 2 * len(chunks) == want
+    _check(segs, 64, chunks, c0)
+
+
+def test_pair_chunks_small_segments():
+    # panels pad every segment to a positive multiple of 64 rows (ops/panel.py ROW_ALIGN)
+    segs = [(0, 64), (64, 64 + 64 * 5), (384, 384 + 128)]
+    chunks, c0 = pair_chunks(segs, 64, 2, 2048, 256)
+    _check(segs, 64, chunks, c0)
+    # a segment shorter than its chunk count gets one chunk per K-step
+    assert [c0[s + 1] - c0[s] for s in range(3)] == [1, 5, 2]
