@@ -4,6 +4,19 @@ Capability parity with the R replication of Athey & Imbens' causal-ML ATE tutori
 (ate_functions.R + ate_replication.Rmd): 14 estimators, the synthetic/real data
 pipeline, and the large-N K-fold DML cross-fit. See ``api`` for the entry points.
 """
+import os as _os
+
+# Hardware queues per process (HIP's default is 4). Independent launches on separate HIP
+# streams -- the 3K forests of a cross-fit, the fits in flight of bench.py -- share that
+# many queues, so with 4 at most 4 forest launches ran at once: the per-GPU shard of
+# BASELINE config 3 (15 forests of 13 trees) kept 52 of 256 CUs busy, 77 s -> 35 s with 16
+# (profiles/r02c_gram/cfg3_hwq.log; the headline step is unchanged). HIP reads it when
+# its library loads, so it applies when this package is imported before torch; a lower
+# inherited value (the MI355X boxes export HIP's default, 4) is raised to 16.
+# ATE_HW_QUEUES=<n> picks another value, ATE_HW_QUEUES=0 leaves the environment alone.
+_want = int(_os.environ.get("ATE_HW_QUEUES", "16"))
+if _want > 0 and int(_os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < _want:
+    _os.environ["GPU_MAX_HW_QUEUES"] = str(min(_want, 32))
 from .api import (Replication, ate_aipw_crossfit, ate_aipw_glm, ate_aipw_rf, ate_belloni, ate_causal_forest,
                   ate_causal_forest_bootstrap,
                   ate_dml, ate_double_ml, ate_ipw, ate_ipw_wls, ate_lasso, ate_lasso_single,

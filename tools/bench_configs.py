@@ -15,6 +15,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# imported before the first CUDA call: the package sets its HIP hardware-queue default
+import ate_replication_causalml_amd  # noqa: E402,F401
 
 
 def _sync():
