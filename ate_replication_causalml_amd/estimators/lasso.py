@@ -96,13 +96,97 @@ def interaction_expand(x: torch.Tensor) -> torch.Tensor:
     return interactions(x)
 
 
+def _interp_at(lams: torch.Tensor, nlam: torch.Tensor, path: torch.Tensor, s: torch.Tensor):
+    """Device twin of reference.estimators.lambda_interp + coef_at: the coefficient path
+    [L, p+1] linearly interpolated in lambda at ``s`` over the first ``nlam`` lambdas (no
+    host sync, fixed shapes: capturable)."""
+    L = lams.numel()
+    k = nlam.long().clamp(min=1)
+    ar = torch.arange(L, device=lams.device)
+    valid = ar < k
+    lam0 = lams[0]
+    lamk = lams.gather(0, (k - 1).reshape(1))[0]
+    den = lam0 - lamk
+    single = den == 0
+    dsafe = torch.where(single, torch.ones_like(den), den)
+    sfrac = ((lam0 - s) / dsafe).clamp(0.0, 1.0)
+    ln = torch.where(valid, (lam0 - lams) / dsafe, torch.full_like(lams, 2.0))
+    left = ((ln <= sfrac) & valid).sum().clamp(min=1) - 1
+    ln_l = ln.gather(0, left.reshape(1))[0]
+    exact = (ln_l == sfrac) | single | (left + 1 >= k)
+    right = torch.where(exact, left, left + 1)
+    ln_r = ln.gather(0, right.reshape(1))[0]
+    gap = ln_l - ln_r
+    frac = torch.where(exact | (gap.abs() < np.finfo(float).eps), torch.ones_like(sfrac),
+                       (sfrac - ln_r) / torch.where(gap == 0, torch.ones_like(gap), gap))
+    # index_select, not path[left]: a 0-dim tensor index would be read on the host
+    return (path.index_select(0, left.reshape(1))[0] * frac
+            + path.index_select(0, right.reshape(1))[0] * (1 - frac))
+
+
+def _belloni_body(panw, pany, panpost, compat):
+    """E11 as one device function (GraphCache): the two CV-LASSO fits on the interaction
+    panels, the Q11-Q13 selection as a column mask (W's lambda.min for both paths, positive
+    coefficients, the one-column index shift), and the post-selection OLS over ALL columns
+    with the unselected ones masked to identity rows of the Gram (coefficient 0, removed
+    from the rank). W's coefficient and SE do not depend on the design's column order, so
+    this equals the host path's union-ordered design up to rounding.
+    Returns [ate, se, n_selected, rank, min fold passes]."""
+    cws = cv_enet_gaussian(gram(panw), panw, panw.xcols, [panw.cols["Y"]])
+    cys = cv_enet_gaussian(gram(pany), pany, pany.xcols, [pany.cols["Y"]])
+    q = len(panw.xcols)
+    s = cws.lambdas[0].gather(0, cws.sel[0, 0:1].long())[0]
+    bw = _interp_at(cws.lambdas[0], cws.nlam[0], cws.coef_path[0].double(), s)[1:]
+    if compat == "reference":
+        by = _interp_at(cys.lambdas[0], cys.nlam[0], cys.coef_path[0].double(), s)[1:]
+        pos = (bw > 0) | (by > 0)
+        keep = torch.cat([pos[1:], torch.zeros(1, dtype=torch.bool, device=pos.device)])
+    else:
+        sy = cys.lambdas[0].gather(0, cys.sel[0, 0:1].long())[0]
+        by = _interp_at(cys.lambdas[0], cys.nlam[0], cys.coef_path[0].double(), sy)[1:]
+        keep = (bw != 0) | (by != 0)
+    G = gram(panpost)[0]
+    P = G.shape[0]
+    m = torch.ones(P, dtype=torch.float64, device=G.device)
+    xc = const(panpost.xcols[:q], torch.int64, G.device)
+    m = m.index_copy(0, xc, keep.double())
+    Gm = G * (m[:, None] * m[None, :]) + torch.diag(1.0 - m)
+    dcols = [panpost.cols["one"], *panpost.xcols]
+    r = chol_solve(Gm, dcols, panpost.cols["Y"])
+    nsel = keep.double().sum()
+    rank = r.aux[0] - (q - nsel)
+    se = torch.sqrt(r.aux[1] / (panpost.n - rank) * r.invdiag[-1])
+    fnp = torch.stack([cws.fold_npass.min(), cys.fold_npass.min()]).min().double() \
+        if cws.fold_npass is not None else torch.zeros((), dtype=torch.float64, device=G.device)
+    return torch.stack([r.beta[-1].double(), se.double(), nsel, rank.double(), fnp])
+
+
 def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni et.al",
-            device=None, dtype="f64", dist=None):
-    """E11 ``belloni`` (ate_functions.R:286-328) with quirks Q10-Q13."""
+            device=None, dtype="f64", dist=None, graph=True):
+    """E11 ``belloni`` (ate_functions.R:286-328) with quirks Q10-Q13.
+
+    On a GPU without row sharding: one hipGraph launch per call after the first
+    (utils/graphs.GraphCache over _belloni_body); otherwise the selection is read on
+    the host and the post-selection design is the union-ordered column list."""
     dev = resolve_device(device)
     Yn, Wn = as_np(Y), as_np(W)
     xint = interaction_expand(torch.as_tensor(as_np(X), device=dev))   # stays on the device
     n, q = xint.shape
+    if graph and dist is None and dev.type == "cuda":
+        panw = build_panel(xint, None, Wn, folds=_fold_ids(n, nfolds, seed, 8, None), dtype=dtype,
+                           device=dev)
+        pany = build_panel(xint, None, Yn, folds=_fold_ids(n, nfolds, seed, 9, None), dtype=dtype,
+                           device=dev)
+        post = torch.cat([xint, torch.as_tensor(Wn, dtype=torch.float64, device=dev)[:, None]], 1)
+        panpost = build_panel(post, None, Yn, dtype=dtype, device=dev)
+        out, g = estimator_graphs.run("belloni", _belloni_body, (panw, pany, panpost), compat)
+        v = out.cpu().numpy()
+        if v[4] < 0:
+            from ..utils.guards import NumericalError
+            raise NumericalError("CV fold path timed out waiting for its full-data lambda "
+                                 "sequence; selection is invalid")
+        return AteResult.make(method, float(v[0]), float(v[1]), n_selected=int(round(v[2])),
+                              rank=int(round(v[3])), hipgraph=g)
     fits = []
     for target, stream in ((Wn, 8), (Yn, 9)):
         fid = _fold_ids(n, nfolds, seed, stream, dist)
