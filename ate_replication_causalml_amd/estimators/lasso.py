@@ -15,7 +15,7 @@ from ..ops import stats as S
 from ..ops.devconst import const
 from ..ops.enet import cv_enet_gaussian
 from ..ops.gram import gram
-from ..ops.linalg import chol_solve
+from ..ops.linalg import chol_solve, chol_solve_active
 from ..ops.panel import build_panel, dtype_code
 from ..parallel import rng
 from ..reference.estimators import lambda_interp
@@ -127,10 +127,11 @@ def _interp_at(lams: torch.Tensor, nlam: torch.Tensor, path: torch.Tensor, s: to
 def _belloni_body(panw, pany, panpost, compat):
     """E11 as one device function (GraphCache): the two CV-LASSO fits on the interaction
     panels, the Q11-Q13 selection as a column mask (W's lambda.min for both paths, positive
-    coefficients, the one-column index shift), and the post-selection OLS over ALL columns
-    with the unselected ones masked to identity rows of the Gram (coefficient 0, removed
-    from the rank). W's coefficient and SE do not depend on the design's column order, so
-    this equals the host path's union-ordered design up to rounding.
+    coefficients, the one-column index shift), and the post-selection OLS on [one, the
+    selected columns in natural order, W]: a fixed-length device column list with a device
+    active count (ops/linalg.chol_solve_active). W's coefficient and SE do not depend on
+    the design's column order, so this equals the host path's union-ordered design up to
+    rounding.
     Returns [ate, se, n_selected, rank, min fold passes]."""
     cws = cv_enet_gaussian(gram(panw), panw, panw.xcols, [panw.cols["Y"]])
     cys = cv_enet_gaussian(gram(pany), pany, pany.xcols, [pany.cols["Y"]])
@@ -146,19 +147,25 @@ def _belloni_body(panw, pany, panpost, compat):
         by = _interp_at(cys.lambdas[0], cys.nlam[0], cys.coef_path[0].double(), sy)[1:]
         keep = (bw != 0) | (by != 0)
     G = gram(panpost)[0]
-    P = G.shape[0]
-    m = torch.ones(P, dtype=torch.float64, device=G.device)
-    xc = const(panpost.xcols[:q], torch.int64, G.device)
-    m = m.index_copy(0, xc, keep.double())
-    Gm = G * (m[:, None] * m[None, :]) + torch.diag(1.0 - m)
-    dcols = [panpost.cols["one"], *panpost.xcols]
-    r = chol_solve(Gm, dcols, panpost.cols["Y"])
-    nsel = keep.double().sum()
-    rank = r.aux[0] - (q - nsel)
-    se = torch.sqrt(r.aux[1] / (panpost.n - rank) * r.invdiag[-1])
+    dev = G.device
+    # design = [one, selected x (natural order), W | unselected x]: a fixed-length column
+    # list with the active count on the device (ops/linalg.chol_solve_active)
+    xc = const(panpost.xcols[:q], torch.int32, dev)
+    ki = keep.long()
+    nsel = ki.sum()
+    pos = torch.where(keep, ki.cumsum(0), 1 + nsel + (1 - ki).cumsum(0))
+    wpos = (1 + nsel).reshape(1)
+    dest = torch.cat([const([0], torch.int64, dev), pos, wpos])
+    src = torch.cat([const([panpost.cols["one"]], torch.int32, dev), xc,
+                     const([panpost.xcols[q]], torch.int32, dev)])
+    cols = torch.empty(q + 2, dtype=torch.int32, device=dev).index_copy(0, dest, src)
+    kact = (2 + nsel).to(torch.int32)
+    r = chol_solve_active(G, cols, kact, panpost.cols["Y"])
+    b_w = r.beta.gather(0, wpos)[0]
+    se = torch.sqrt(r.aux[1] / (panpost.n - r.aux[0]) * r.invdiag.gather(0, wpos)[0])
     fnp = torch.stack([cws.fold_npass.min(), cys.fold_npass.min()]).min().double() \
-        if cws.fold_npass is not None else torch.zeros((), dtype=torch.float64, device=G.device)
-    return torch.stack([r.beta[-1].double(), se.double(), nsel, rank.double(), fnp])
+        if cws.fold_npass is not None else torch.zeros((), dtype=torch.float64, device=dev)
+    return torch.stack([b_w.double(), se.double(), nsel.double(), r.aux[0].double(), fnp])
 
 
 def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni et.al",

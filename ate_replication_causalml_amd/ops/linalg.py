@@ -53,6 +53,24 @@ def chol_solve(G: torch.Tensor, cols, rcol: int = -1, rhs: torch.Tensor | None =
     return SolveResult(ws.beta, ws.invdiag, ws.aux)
 
 
+def chol_solve_active(G: torch.Tensor, cols: torch.Tensor, kact: torch.Tensor, rcol: int,
+                      tol: float = LM_TOL, ws: SolveWorkspace | None = None) -> SolveResult:
+    """chol_solve over the first ``kact`` (device int32 scalar) entries of the device column
+    list ``cols`` (fixed length): a data-dependent design size without a host sync. Entries
+    of beta / invdiag past kact are unspecified; aux counts the active columns only."""
+    k = cols.numel()
+    if not G.is_cuda:
+        ka = int(kact)
+        r = _chol_solve_cpu(G, cols[:ka].cpu().numpy(), rcol, None, tol)
+        pad = torch.full((k - ka,), float("nan"), dtype=torch.float64)
+        return SolveResult(torch.cat([r.beta.cpu(), pad]), torch.cat([r.invdiag.cpu(), pad]), r.aux)
+    ws = ws or SolveWorkspace(k, G.device)
+    _native.call("ate_chol_solve_k", G.data_ptr(), G.shape[-1], cols.data_ptr(), k, kact.data_ptr(),
+                 rcol, tol, ws.work.data_ptr(), ws.beta.data_ptr(), ws.invdiag.data_ptr(),
+                 ws.aux.data_ptr(), _stream())
+    return SolveResult(ws.beta, ws.invdiag, ws.aux)
+
+
 def _chol_solve_cpu(G, cols, rcol, rhs, tol):
     Gn = G.detach().cpu().double().numpy()
     A = Gn[np.ix_(cols, cols)].copy()

@@ -17,12 +17,16 @@ using namespace ate;
 // ------------------------------------------------------------------ K05/K06
 // work: >= k*k doubles (L) + k*k (inverse columns). out layout:
 // beta[k], invdiag[k], aux[4] = {rank, yty - beta'Xty, yty, 0}
+// kdev (optional, device): solve over the first min(k, *kdev) entries of cols only -- a
+// graph-captured caller with a data-dependent design size passes a fixed-size column list
+// (active columns first) and the active count (estimators/lasso.py _belloni_body).
 __global__ __launch_bounds__(1024) void chol_solve_kernel(
-    const double* __restrict__ G, int P, const int* __restrict__ cols, int k, int rcol,
+    const double* __restrict__ G, int P, const int* __restrict__ cols, int kmax, int rcol,
     const double* __restrict__ rhs_vec, double tol, double* __restrict__ L, double* __restrict__ Linv,
     double* __restrict__ beta, double* __restrict__ invdiag, double* __restrict__ aux,
-    const int* __restrict__ done) {
+    const int* __restrict__ done, const int* __restrict__ kdev) {
   if (done && *done) return;
+  const int k = kdev ? min(kmax, max(0, *kdev)) : kmax;
   extern __shared__ double sm[];      // b[k], y[k], alias flags as double[k]
   double* b = sm;
   double* y = sm + k;
@@ -127,7 +131,24 @@ ATE_API int ate_chol_solve(const void* G, int P, const void* cols, int k, int rc
   size_t sh = (size_t)3 * k * sizeof(double);
   hipLaunchKernelGGL(chol_solve_kernel, dim3(1), dim3(1024), sh, (hipStream_t)stream,
                      (const double*)G, P, (const int*)cols, k, rcol, (const double*)rhs_vec, tol,
-                     L, Linv, (double*)beta, (double*)invdiag, (double*)aux, (const int*)done);
+                     L, Linv, (double*)beta, (double*)invdiag, (double*)aux, (const int*)done,
+                     (const int*)nullptr);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+// ate_chol_solve over the first *kdev (device int) of the k columns
+ATE_API int ate_chol_solve_k(const void* G, int P, const void* cols, int k, const void* kdev,
+                             int rcol, double tol, void* work, void* beta, void* invdiag, void* aux,
+                             void* stream) {
+  if (k <= 0 || k > 4096) return -1;
+  double* L = (double*)work;
+  double* Linv = L + (int64_t)k * k;
+  size_t sh = (size_t)3 * k * sizeof(double);
+  hipLaunchKernelGGL(chol_solve_kernel, dim3(1), dim3(1024), sh, (hipStream_t)stream,
+                     (const double*)G, P, (const int*)cols, k, rcol, (const double*)nullptr, tol,
+                     L, Linv, (double*)beta, (double*)invdiag, (double*)aux, (const int*)nullptr,
+                     (const int*)kdev);
   ATE_CHECK_LAUNCH();
   return 0;
 }

@@ -38,7 +38,7 @@ CASES = {
         Yc, W, X, device=dev, graph=g),
     "lasso_usual": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_usual(
         Yc, W, X, device=dev, graph=g),
-    # graph=False: host selection + union-ordered design; graph: device mask + masked OLS
+    # graph=False: host selection + union-ordered design; graph: device selection + compacted column list
     "belloni": lambda L, X, W, Yc, Yb, dev, g: _lasso().belloni(Yc, W, X, device=dev, graph=g),
     "belloni_textbook": lambda L, X, W, Yc, Yb, dev, g: _lasso().belloni(
         Yb, W, X, compat="textbook", device=dev, graph=g),
