@@ -36,6 +36,7 @@ _SIGS = {
     "ate_gram_tile_sizes": "pppp",
     "ate_chol_solve": "pipiipdpppppp",
     "ate_chol_solve_k": "pipipidppppp",
+    "ate_spd_solve_batched": "ppiippp",
     "ate_predict": "ipllppiidipp",
     "ate_irls_update": "ipllppiiiiippppipp",
     "ate_irls_check": "piidippp",

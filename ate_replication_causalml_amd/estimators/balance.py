@@ -19,12 +19,15 @@ import numpy as np
 import torch
 
 from ..ops import gemv
+from ..ops.devconst import const
 from ..ops.enet import cv_enet_gaussian
 from ..ops.gram import gram
+from ..ops.linalg import spd_solve
 from ..ops.panel import build_panel
 from ..parallel import rng
 from ..reference.balance import scale_columns
 from ..result import AteResult
+from ..utils.graphs import estimator_graphs
 from .common import as_np, resolve_device
 
 
@@ -55,15 +58,23 @@ def _schur(Garm, xc, one, Dd, W, p):
     K[:, 2 * p, p:2 * p] = -Sm1
     K[:, 2 * p, 2 * p] = S11
     K[:, :2 * p, :2 * p] += (1.0 / Dd)[:, None, None]
-    K[:, range(2 * p), range(2 * p)] += 1.0 / W
+    # diagonal view, not K[:, range, range]: a host index tensor is not capturable
+    torch.diagonal(K, dim1=1, dim2=2)[:, :2 * p] += 1.0 / W
     return K
 
 
-def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
+def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_arm=None,
+                      fixed=False):
     """Balancing weights for every arm a (rows ``masks[a]``) toward ``target`` [p].
-    Returns gamma [ld] (each row carries its own arm's weight) and iteration counts."""
+    Returns gamma [ld] (each row carries its own arm's weight) and iteration counts.
+
+    ``fixed``: no host sync at all (hipGraph capture): run all ``maxit`` iterations; an
+    arm's state is frozen (``torch.where``, so a NaN from a degenerate post-convergence
+    Newton system cannot leak into it) from the iteration at which it converged, and the
+    iteration counts come back as a device tensor. ``seg_arm`` (host, per segment: arm or
+    -1) then has to be given, since deriving it from ``masks`` reads the device."""
     dev, dt = pan.device, torch.float64
-    xc = torch.tensor(pan.xcols, device=dev)
+    xc = const(pan.xcols, torch.int64, dev)
     one = pan.cols["one"]
     p = len(pan.xcols)
     A = masks.shape[0]
@@ -73,16 +84,20 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
     nA = mf.sum(1)
     m = target.to(dev, dt)
     h = torch.cat([m, -m])
-    seg_arm = torch.full((pan.nseg,), -1, dtype=torch.long)
-    for a in range(A):
-        for s in range(pan.nseg):
-            r0, r1 = pan.seg_bounds[s]
-            if r1 > r0 and bool(masks[a, r0:r1].any()):
-                seg_arm[s] = a
+    if seg_arm is None:
+        seg_arm = torch.full((pan.nseg,), -1, dtype=torch.long)
+        for a in range(A):
+            for s in range(pan.nseg):
+                r0, r1 = pan.seg_bounds[s]
+                if r1 > r0 and bool(masks[a, r0:r1].any()):
+                    seg_arm[s] = a
+    seg_arm = torch.as_tensor(seg_arm, dtype=torch.long)
+    seg_idx = const(seg_arm.clamp(min=0).tolist(), torch.int64, dev)
+    seg_on = const((seg_arm >= 0).double().tolist(), torch.float64, dev)
 
     grp = torch.full((pan.ld,), -1, dtype=torch.int8, device=dev)
     for a in range(A):
-        grp[masks[a]] = a
+        grp = torch.where(masks[a], torch.full_like(grp, a), grp)
 
     def per_arm_T(v):            # M_a' v over each arm's rows -> [A, p]
         return gemv.xtv(pan, pan.xcols, v, grp, A)
@@ -107,6 +122,7 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
     ncomp = 2 * p + nA
     done = torch.zeros(A, dtype=torch.bool, device=dev)
     iters = np.zeros(A, dtype=int)
+    iters_dev = torch.zeros(A, dtype=torch.int64, device=dev)
 
     def solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, r_sz, r_gt):
         v = (z * r_g - r_sz) / s                                   # [A, 2p]
@@ -115,14 +131,14 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
         wts = lf / Dg
         Gs = gram(pan, w=wts.to(pan.data.dtype))                  # [nseg, P, P]
         Garm = torch.zeros(A, Gs.shape[1], Gs.shape[2], dtype=dt, device=dev)
-        Garm.index_add_(0, seg_arm.clamp(min=0).to(dev), Gs * (seg_arm >= 0).to(dev, dt)[:, None, None])
+        Gs = torch.where(seg_on[:, None, None] > 0, Gs, torch.zeros_like(Gs))
+        Garm.index_add_(0, seg_idx, Gs)
         K = _schur(Garm, xc, one, Dd, W, p)
         u_g = rhs_g / Dg
         u_d = rhs_d / Dd
         mg = per_arm_T(u_g)
         rk = torch.cat([mg - u_d[:, None], -mg - u_d[:, None], (arm_sum(u_g) + r_p)[:, None]], 1)
-        L, info = torch.linalg.cholesky_ex(K)
-        sol = torch.cholesky_solve(rk[:, :, None], L)[:, :, 0]
+        sol = spd_solve(K, rk)
         uu, dy = sol[:, :2 * p], sol[:, 2 * p]
         dxg = lf * (rhs_g - rows_from(uu[:, :p] - uu[:, p:]) - (mf * dy[:, None]).sum(0)) / Dg
         dxd = (rhs_d + uu.sum(1)) / Dd
@@ -152,11 +168,15 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
                              for a in range(A)])
         conv = (mu < tol / nA) & (r_p.abs() < tol) & (r_g.abs().amax(1) < tol * scale) \
             & (rdmax < tol * scale) & (r_d_d.abs() < tol * scale)
-        done_h = (done | conv).cpu().numpy()
-        iters[~done_h] = it
-        done = done | conv
-        if bool(done_h.all()):
-            break
+        if fixed:
+            done = done | conv
+            iters_dev = iters_dev + (~done).long()
+        else:
+            done_h = (done | conv).cpu().numpy()
+            iters[~done_h] = it
+            done = done | conv
+            if bool(done_h.all()):
+                break
         Dg = c_g + t / gam
         Dd = torch.full((A,), c_d, dtype=dt, device=dev)
         W = z / s
@@ -175,18 +195,60 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100):
                           step(t, dtt, s, ds))
         a = torch.where(done, torch.zeros_like(a), torch.clamp(0.99 * a, max=1.0))
         af = (mf * a[:, None]).sum(0)
+        if fixed:
+            # freeze converged arms with where (0 * NaN would not be 0)
+            frow = (mf * done.to(dt)[:, None]).sum(0) > 0
+            gam = torch.where(frow, gam, gam + af * dxg)
+            t = torch.where(frow, t, t + af * dtt)
+            delta = torch.where(done, delta, delta + a * dxd)
+            y = torch.where(done, y, y + a * dy)
+            z = torch.where(done[:, None], z, z + a[:, None] * dz)
+            s = torch.where(done[:, None], s, s + a[:, None] * ds)
+            continue
         gam = gam + af * dxg
         t = t + af * dtt
         delta = delta + a * dxd
         y = y + a * dy
         z = z + a[:, None] * dz
         s = s + a[:, None] * ds
+    if fixed:
+        return gam * lf, iters_dev
     return gam * lf, iters
 
 
+def _arb_body(pan, target, zeta, alpha, K, seg_arm):
+    """E14 as one device function (utils/graphs.GraphCache): per-arm CV elastic net, the
+    balancing QPs at a fixed interior-point budget (converged arms frozen on the device),
+    and the residual-balancing estimate. Returns [mu1, mu0, var1, var0, iters1, iters0,
+    min fold passes]."""
+    G = gram(pan).clone()
+    cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
+                          full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha)
+    masks = _arm_masks(pan, K)
+    tg = target.to(pan.device, torch.float64)
+    gam, iters = ipm_balance_panel(pan, masks, tg, zeta, seg_arm=seg_arm, fixed=True)
+    b = cv.coef_1se.to(torch.float64)
+    Xd = pan.data.double()
+    fit = b[:, :1] + b[:, 1:] @ Xd.index_select(0, const(pan.xcols, torch.int64, pan.device))
+    resid = Xd[pan.cols["Y"]][None] - fit
+    mf = masks.double()
+    mu = b[:, 0] + b[:, 1:] @ tg + (mf * gam * resid).sum(1)
+    var = (mf * gam ** 2 * resid ** 2).sum(1)
+    fnp = cv.fold_npass.min().double().reshape(1) if cv.fold_npass is not None else \
+        torch.zeros(1, dtype=torch.float64, device=pan.device)
+    return torch.cat([mu, var, iters.double(), fnp])
+
+
 def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 11), nfolds=10,
-                     scale_x=True, method="residual_balancing", device=None, dtype="f64"):
-    """E14 on the device; matches reference.balance.residual_balance_ate."""
+                     scale_x=True, method="residual_balancing", device=None, dtype="f64",
+                     graph=False):
+    """E14 on the device; matches reference.balance.residual_balance_ate.
+
+    graph=True (GPU): one hipGraph launch per call after the first of a panel layout
+    (utils/graphs.GraphCache over _arb_body, the interior point at a fixed budget of 100
+    iterations with converged arms frozen on the device; equal to the eager solver to
+    1e-12). Off by default: the eager solver stops at convergence (~14 iterations on the
+    tutorial data), which is cheaper than replaying the fixed budget."""
     dev = resolve_device(device)
     Yn, Wn = as_np(Y), as_np(W)
     Xs = scale_columns(as_np(X))[0] if scale_x else as_np(X)
@@ -196,6 +258,19 @@ def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 
     seg[arm] = rng.fold_ids(int(arm.sum()), nfolds, seed, fold_streams[0])
     seg[~arm] = nfolds + rng.fold_ids(int((~arm).sum()), nfolds, seed, fold_streams[1])
     pan = build_panel(Xs, None, Yn, folds=seg, dtype=dtype, device=dev)
+    if graph and pan.data.is_cuda:
+        K = nfolds
+        nr = np.asarray(pan.seg_nreal)
+        seg_arm = tuple(int(s // K) if nr[s] > 0 else -1 for s in range(pan.nseg))
+        out, g = estimator_graphs.run("arb", _arb_body, (pan, target.to(dev)), float(zeta),
+                                      float(alpha), K, seg_arm)
+        v = out.cpu().numpy()
+        if v[6] < 0:
+            from ..utils.guards import NumericalError
+            raise NumericalError("CV fold path timed out waiting for its full-data lambda "
+                                 "sequence; selection is invalid")
+        return AteResult.make(method, v[0] - v[1], float(np.sqrt(v[2] + v[3])), mu1=float(v[0]),
+                              mu0=float(v[1]), ipm_iters=(int(v[4]), int(v[5])), hipgraph=g)
     G = gram(pan).clone()
     K = nfolds
     cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],

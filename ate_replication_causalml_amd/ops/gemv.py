@@ -8,11 +8,13 @@ from __future__ import annotations
 import torch
 
 from .. import _native
+from .devconst import const
 from .panel import dtype_code
 
 
 def _cols(panel, cols):
-    return torch.tensor(cols, dtype=torch.int32, device=panel.device)
+    # cached device constant: no host->device copy per call (hipGraph-capturable)
+    return const(list(cols), torch.int32, panel.device)
 
 
 def xtv(panel, cols, v: torch.Tensor, grp: torch.Tensor, A: int) -> torch.Tensor:

@@ -53,6 +53,25 @@ def chol_solve(G: torch.Tensor, cols, rcol: int = -1, rhs: torch.Tensor | None =
     return SolveResult(ws.beta, ws.invdiag, ws.aux)
 
 
+def spd_solve(K: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """x[a] = K[a]^-1 r[a] for a batch [A, k, k] of small SPD systems (unpivoted Cholesky;
+    NaN for a system without a positive pivot). GPU: csrc/linalg.hip spd_solve_kernel, a
+    kernel of ours so the solve can sit inside a hipGraph (torch.linalg.cholesky_ex cannot
+    be captured on ROCm); CPU: torch.linalg."""
+    if not K.is_cuda:
+        L, info = torch.linalg.cholesky_ex(K)
+        x = torch.cholesky_solve(r[:, :, None], L)[:, :, 0]
+        return torch.where((info > 0)[:, None], torch.full_like(x, float("nan")), x)
+    A, k = K.shape[0], K.shape[-1]
+    Kc = K.contiguous().double()
+    rc = r.contiguous().double()
+    work = torch.empty(A * k * k, dtype=torch.float64, device=K.device)
+    x = torch.empty(A, k, dtype=torch.float64, device=K.device)
+    _native.call("ate_spd_solve_batched", Kc.data_ptr(), rc.data_ptr(), A, k, work.data_ptr(),
+                 x.data_ptr(), _stream())
+    return x
+
+
 def chol_solve_active(G: torch.Tensor, cols: torch.Tensor, kact: torch.Tensor, rcol: int,
                       tol: float = LM_TOL, ws: SolveWorkspace | None = None) -> SolveResult:
     """chol_solve over the first ``kact`` (device int32 scalar) entries of the device column

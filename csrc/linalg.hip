@@ -153,6 +153,78 @@ ATE_API int ate_chol_solve_k(const void* G, int P, const void* cols, int k, cons
   return 0;
 }
 
+// ------------------------------------------------------------------ batched SPD solve
+// x[a] = K[a]^-1 r[a] for A small dense SPD systems (the balancing QP's Schur systems,
+// estimators/balance.py): one workgroup per system, unpivoted right-looking Cholesky of the
+// lower triangle in `work` (A * k * k doubles), then forward / back substitution in LDS. A
+// non-positive pivot makes that system's solution NaN (LAPACK's potrf would report info > 0).
+// Own kernel (not rocSOLVER) so the solve can be captured in a hipGraph.
+__global__ __launch_bounds__(1024) void spd_solve_kernel(const double* __restrict__ K,
+                                                         const double* __restrict__ r, int k,
+                                                         double* __restrict__ work,
+                                                         double* __restrict__ x) {
+  extern __shared__ double sy[];          // [k]
+  __shared__ int bad;
+  const int a = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  const double* Ka = K + (int64_t)a * k * k;
+  double* L = work + (int64_t)a * k * k;
+  for (int e = tid; e < k * k; e += nt) L[e] = Ka[e];
+  for (int i = tid; i < k; i += nt) sy[i] = r[(int64_t)a * k + i];
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    const double d = L[j * k + j];
+    if (!(d > 0.0)) {                     // uniform: every thread reads the same value
+      if (tid == 0) bad = 1;
+      break;
+    }
+    const double ljj = sqrt(d);
+    __syncthreads();
+    for (int i = j + 1 + tid; i < k; i += nt) L[i * k + j] /= ljj;
+    if (tid == 0) L[j * k + j] = ljj;
+    __syncthreads();
+    const int rem = k - j - 1;
+    for (int e = tid; e < rem * rem; e += nt) {
+      const int ii = e / rem, mm = e - ii * rem;
+      if (mm <= ii) {
+        const int i = j + 1 + ii, m = j + 1 + mm;
+        L[i * k + m] -= L[i * k + j] * L[m * k + j];
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (bad) {
+    for (int i = tid; i < k; i += nt) x[(int64_t)a * k + i] = NAN;
+    return;
+  }
+  for (int j = 0; j < k; ++j) {           // L y = r
+    const double yj = sy[j] / L[j * k + j];
+    __syncthreads();
+    if (tid == 0) sy[j] = yj;
+    for (int i = j + 1 + tid; i < k; i += nt) sy[i] -= L[i * k + j] * yj;
+    __syncthreads();
+  }
+  for (int j = k - 1; j >= 0; --j) {      // L' x = y
+    const double xj = sy[j] / L[j * k + j];
+    __syncthreads();
+    if (tid == 0) sy[j] = xj;
+    for (int i = tid; i < j; i += nt) sy[i] -= L[j * k + i] * xj;
+    __syncthreads();
+  }
+  for (int i = tid; i < k; i += nt) x[(int64_t)a * k + i] = sy[i];
+}
+
+ATE_API int ate_spd_solve_batched(const void* K, const void* r, int A, int k, void* work, void* x,
+                                  void* stream) {
+  if (A <= 0 || k <= 0 || k > 4096) return -1;
+  hipLaunchKernelGGL(spd_solve_kernel, dim3(A), dim3(256), (size_t)k * sizeof(double),
+                     (hipStream_t)stream, (const double*)K, (const double*)r, k, (double*)work,
+                     (double*)x);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
 // ------------------------------------------------------------------ GEMV predictors
 // eta_i = sum_c beta_c * X[cols_c][i] (NaN beta treated as 0 = aliased), optional
 // override of one design column to a constant (counterfactual W=1 / W=0).

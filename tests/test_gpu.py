@@ -259,3 +259,20 @@ def test_dml_two_graphs_in_flight_match_eager(gpu):
     torch.cuda.synchronize()
     for r in runs:
         torch.testing.assert_close(r.out, want, rtol=0, atol=0)
+
+
+def test_spd_solve_batched_vs_fp64_reference(gpu):
+    """csrc/linalg.hip spd_solve_kernel (the balancing QP's Schur solves, capturable) against
+    torch.linalg.solve in fp64 on the host; a non-SPD system comes back NaN."""
+    import torch
+    from ate_replication_causalml_amd.ops.linalg import spd_solve
+    g = torch.Generator().manual_seed(5)
+    A, k = 3, 43
+    M = torch.randn(A, k, k, generator=g, dtype=torch.float64)
+    K = M @ M.transpose(1, 2) + k * torch.eye(k, dtype=torch.float64)
+    K[2] = -K[2]                                   # not positive definite
+    r = torch.randn(A, k, generator=g, dtype=torch.float64)
+    x = spd_solve(K.to(gpu), r.to(gpu)).cpu()
+    want = torch.linalg.solve(K[:2], r[:2, :, None])[:, :, 0]
+    assert torch.allclose(x[:2], want, rtol=1e-12, atol=1e-14)
+    assert torch.isnan(x[2]).all()

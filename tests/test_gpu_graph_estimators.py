@@ -42,7 +42,22 @@ CASES = {
     "belloni": lambda L, X, W, Yc, Yb, dev, g: _lasso().belloni(Yc, W, X, device=dev, graph=g),
     "belloni_textbook": lambda L, X, W, Yc, Yb, dev, g: _lasso().belloni(
         Yb, W, X, compat="textbook", device=dev, graph=g),
+    # graph=False: interior point stops at convergence; graph: fixed budget, arms frozen.
+    # The per-arm fold segments follow the treated count, so it is held fixed (one layout).
+    "residual_balance": lambda L, X, W, Yc, Yb, dev, g: _balance().residual_balance(
+        Yc, _fixed_count(X), X, device=dev, graph=g),
 }
+
+
+def _fixed_count(X, n1=1000):
+    w = np.zeros(len(X))
+    w[np.argsort(X[:, 0] + X[:, 2])[-n1:]] = 1.0
+    return w
+
+
+def _balance():
+    from ate_replication_causalml_amd.estimators import balance
+    return balance
 
 
 def _forest():
