@@ -92,8 +92,7 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
                 if r1 > r0 and bool(masks[a, r0:r1].any()):
                     seg_arm[s] = a
     seg_arm = torch.as_tensor(seg_arm, dtype=torch.long)
-    seg_idx = const(seg_arm.clamp(min=0).tolist(), torch.int64, dev)
-    seg_on = const((seg_arm >= 0).double().tolist(), torch.float64, dev)
+    arm_of = [const((seg_arm == a).tolist(), torch.bool, dev) for a in range(A)]
 
     grp = torch.full((pan.ld,), -1, dtype=torch.int8, device=dev)
     for a in range(A):
@@ -130,9 +129,10 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
         rhs_d = -r_d_d + v.sum(1)
         wts = lf / Dg
         Gs = gram(pan, w=wts.to(pan.data.dtype))                  # [nseg, P, P]
-        Garm = torch.zeros(A, Gs.shape[1], Gs.shape[2], dtype=dt, device=dev)
-        Gs = torch.where(seg_on[:, None, None] > 0, Gs, torch.zeros_like(Gs))
-        Garm.index_add_(0, seg_idx, Gs)
+        # per-arm sum of the segment Grams as a fixed-order reduction (index_add_ on a GPU
+        # adds with atomics: run-to-run rounding noise the interior point amplifies)
+        Garm = torch.stack([torch.where(arm_of[a][:, None, None], Gs, torch.zeros_like(Gs)).sum(0)
+                            for a in range(A)])
         K = _schur(Garm, xc, one, Dd, W, p)
         u_g = rhs_g / Dg
         u_d = rhs_d / Dd

@@ -23,9 +23,26 @@ is a purely local operation that succeeds or fails identically on every rank.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
+
 import torch
 
 _pins: list | None = None
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """Python's cyclic GC must not run inside a stream capture: an evicted graph reclaimed
+    there destroys its executable / frees its pool while the stream is capturing, which
+    HIP rejects (an error raised in a destructor aborts the process)."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def pin(obj):
@@ -45,7 +62,8 @@ class GraphedStep:
         self.graph = torch.cuda.CUDAGraph()
         prev, _pins = _pins, []
         try:
-            with torch.cuda.graph(self.graph):
+            gc.collect()            # reclaim evicted graphs here, outside the capture
+            with _no_gc(), torch.cuda.graph(self.graph):
                 self.out = fn()
             self.pins = _pins
         finally:
@@ -133,7 +151,8 @@ class SegmentedStep:
             g = torch.cuda.CUDAGraph()
             prev, _pins = _pins, []
             try:
-                with torch.cuda.graph(g):
+                gc.collect()
+                with _no_gc(), torch.cuda.graph(g):
                     out = ph(state)
                 self.pins += _pins
             finally:
@@ -189,8 +208,10 @@ class _Captured:
     panels, kept alive here); a later call copies its data into them and replays."""
 
     def __init__(self, body, inputs, static_args, warmup):
-        self.inputs = list(inputs)
-        self.step = GraphedStep(lambda: body(*self.inputs, *static_args), warmup)
+        self.inputs = inputs = list(inputs)
+        # the closure holds the input list, not self: no reference cycle, so an evicted
+        # entry (and its graph) is freed at once, outside any capture
+        self.step = GraphedStep(lambda: body(*inputs, *static_args), warmup)
 
     def load(self, inputs):
         for s, x in zip(self.inputs, inputs):

@@ -70,10 +70,16 @@ def _lasso():
     return lasso
 
 
+# the graphed interior point replays a fixed budget with converged arms frozen while the
+# eager one stops; the two agree to the solver's tolerance (1e-11), not bit for bit
+TOL = {"residual_balance": 1e-9}
+
+
 @pytest.mark.parametrize("name", list(CASES))
 def test_graphed_estimator_matches_eager(gpu, name):
     from ate_replication_causalml_amd.estimators import linear as L
     rs = np.random.RandomState(11)
+    tol = TOL.get(name, 1e-12)
     seen = []
     for rep in range(4):
         X, W, Yc, Yb = _data(rs)
@@ -82,9 +88,9 @@ def test_graphed_estimator_matches_eager(gpu, name):
         assert graphed.diagnostics.get("hipgraph") is (rep > 0), name
         for k, v in eager.diagnostics.items():          # e.g. the mean-CATE "incorrect" ATE
             if isinstance(v, float) and k != "hipgraph":
-                assert abs(graphed.diagnostics[k] - v) <= 1e-12 * max(1.0, abs(v)), (name, k)
-        assert abs(graphed.ate - eager.ate) <= 1e-12 * max(1.0, abs(eager.ate)), name
+                assert abs(graphed.diagnostics[k] - v) <= tol * max(1.0, abs(v)), (name, k)
+        assert abs(graphed.ate - eager.ate) <= tol * max(1.0, abs(eager.ate)), name
         if eager.se is not None and np.isfinite(eager.se):
-            assert abs(graphed.se - eager.se) <= 1e-12 * max(1.0, abs(eager.se)), name
+            assert abs(graphed.se - eager.se) <= tol * max(1.0, abs(eager.se)), name
         seen.append(graphed.ate)
     assert len(set(seen)) == 4, name      # the replays used the new data
