@@ -51,3 +51,34 @@ def test_device_arb_matches_reference(tutorial):
     b = residual_balance(m.Y, m.W, m.X, device="cpu")
     assert b.ate == pytest.approx(a.ate, abs=1e-9)
     assert b.se == pytest.approx(a.se, rel=1e-7)
+
+
+def test_fixed_budget_ipm_equals_early_stop():
+    """The capturable interior point (fixed iteration budget, converged arms frozen with
+    torch.where, device iteration counts) returns exactly the early-stopping solver's
+    weights and iteration counts (host tensors)."""
+    import numpy as np
+    import torch
+    from ate_replication_causalml_amd.estimators import balance as B
+    from ate_replication_causalml_amd.ops.panel import build_panel
+    from ate_replication_causalml_amd.parallel import rng
+    from ate_replication_causalml_amd.reference.balance import scale_columns
+    rs = np.random.RandomState(3)
+    n, p, K = 1200, 6, 5
+    X = rs.randn(n, p)
+    W = (rs.rand(n) < 0.35).astype(float)
+    Y = X[:, 1] + 0.4 * W + rs.randn(n)
+    Xs = scale_columns(X)[0]
+    arm = W == 1
+    seg = np.empty(n, dtype=np.int64)
+    seg[arm] = rng.fold_ids(int(arm.sum()), K, 1991, 10)
+    seg[~arm] = K + rng.fold_ids(int((~arm).sum()), K, 1991, 11)
+    pan = build_panel(Xs, None, Y, folds=seg, dtype="f64", device="cpu")
+    masks = B._arm_masks(pan, K)
+    tg = torch.as_tensor(Xs.mean(0))
+    g1, i1 = B.ipm_balance_panel(pan, masks, tg, 0.5)
+    nr = np.asarray(pan.seg_nreal)
+    sa = tuple(int(s // K) if nr[s] > 0 else -1 for s in range(pan.nseg))
+    g2, i2 = B.ipm_balance_panel(pan, masks, tg, 0.5, seg_arm=sa, fixed=True)
+    assert torch.equal(g1, g2)
+    assert list(i1) == i2.tolist()

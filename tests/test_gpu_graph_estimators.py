@@ -70,9 +70,12 @@ def _lasso():
     return lasso
 
 
-# the graphed interior point replays a fixed budget with converged arms frozen while the
-# eager one stops; the two agree to the solver's tolerance (1e-11), not bit for bit
-TOL = {"residual_balance": 1e-9}
+# residual balancing: the interior point's weights on a GPU are reproducible run to run
+# only to rounding (tools/arb_determinism.py: Gram and CV coefficients bit-identical, the
+# weights not; ATE within ~1e-11 to 1e-9 between runs), so graphed vs eager is checked at
+# 1e-7; the fixed-budget / frozen-arm logic itself equals the eager solver exactly on the
+# host
+TOL = {"residual_balance": 1e-7}
 
 
 @pytest.mark.parametrize("name", list(CASES))
