@@ -521,6 +521,11 @@ __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2
     int s = (int)(e / ((int64_t)ntiles * tt));
     int rem = (int)(e % ((int64_t)ntiles * tt));
     int t = rem / tt, ij = rem % tt;
+    // diagonal tiles: only the upper entry of each (i, j) / (j, i) pair is reduced and it
+    // writes both G[a][b] and G[b][a] -- ONE writer per Gram entry. (With row weights the
+    // tile's (i, j) and (j, i) partials round differently, (x_i w) x_j vs (x_j w) x_i, and
+    // two writers made the weighted Gram differ run to run at rounding level.)
+    if (tiles[t].x == tiles[t].y && ij / T > ij % T) continue;
     double acc = 0.0;
     for (int c = seg_chunk0[s]; c < seg_chunk0[s + 1]; ++c)
       acc += (double)slab[((int64_t)c * ntiles + t) * tt + ij];

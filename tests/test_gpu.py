@@ -276,3 +276,21 @@ def test_spd_solve_batched_vs_fp64_reference(gpu):
     want = torch.linalg.solve(K[:2], r[:2, :, None])[:, :, 0]
     assert torch.allclose(x[:2], want, rtol=1e-12, atol=1e-14)
     assert torch.isnan(x[2]).all()
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_weighted_gram_bitwise_repeatable(gpu, dtype):
+    """Row-weighted Gram (IRLS / WLS / balancing steps): every entry has one writer in the
+    slab reduce, so repeated calls are bit-identical (two writers per diagonal-tile entry
+    made it differ at rounding level) and the result is exactly symmetric."""
+    import torch
+    from ate_replication_causalml_amd.ops.gram import gram
+    from ate_replication_causalml_amd.ops.panel import build_panel
+    rs = np.random.RandomState(4)
+    X = rs.randn(3000, 9)
+    pan = build_panel(X, None, rs.randn(3000), folds=rs.randint(0, 4, 3000), dtype=dtype,
+                      device=gpu)
+    w = torch.as_tensor(rs.rand(pan.ld), device=gpu).to(pan.data.dtype)
+    Gs = [gram(pan, w=w).clone() for _ in range(3)]
+    assert all(torch.equal(Gs[0], g) for g in Gs[1:])
+    assert torch.equal(Gs[0], Gs[0].transpose(1, 2))

@@ -38,3 +38,23 @@ for rep in range(3):
     gam, it = B.ipm_balance_panel(pan, masks, torch.as_tensor(Xs.mean(0)), 0.5)
     r = B.residual_balance(Y, W, X, device=dev)
     print(rep, "G", h(G), "cv", h(cv.coef_1se), "gam", h(gam), it, f"ate {r.ate:.17g}", flush=True)
+
+# pieces of one IPM step, three times each on identical inputs
+from ate_replication_causalml_amd.ops import gemv  # noqa: E402
+from ate_replication_causalml_amd.ops.linalg import spd_solve  # noqa: E402
+pan = build_panel(Xs, None, Y, folds=seg, dtype="f64", device=dev)
+masks = B._arm_masks(pan, K)
+grp = torch.where(masks[0], 0, torch.where(masks[1], 1, -1)).to(torch.int8)
+g = torch.Generator().manual_seed(1)
+v = torch.rand(pan.ld, generator=g, dtype=torch.float64).to(dev)
+V = torch.rand(2, p, generator=g, dtype=torch.float64).to(dev)
+Kb = torch.rand(2, 17, 17, generator=g, dtype=torch.float64)
+Kb = (Kb @ Kb.transpose(1, 2) + 17 * torch.eye(17, dtype=torch.float64)).to(dev)
+rb = torch.rand(2, 17, generator=g, dtype=torch.float64).to(dev)
+for name, fn in [("gram_w", lambda: gram(pan, w=v).clone()),
+                 ("xtv", lambda: gemv.xtv(pan, pan.xcols, v, grp, 2)),
+                 ("xv", lambda: gemv.xv(pan, pan.xcols, V, grp)),
+                 ("spd", lambda: spd_solve(Kb, rb)),
+                 ("sum", lambda: (masks.double() * v).sum(1)),
+                 ("amin", lambda: torch.where(masks[0], v, torch.full_like(v, 9.0)).amin())]:
+    print(name, [h(fn()) for _ in range(3)], flush=True)
