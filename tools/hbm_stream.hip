@@ -83,11 +83,14 @@ __global__ __launch_bounds__(512) void dma_kernel(const char* __restrict__ p, lo
     for (int r = 0; r < PIECES; ++r) {
       // SWZ 3: like 1, but the second reader of a shared stage walks its pieces from the
       // middle of the stage (crossed order: the two readers first touch different lines)
+      // SWZ 4: the Gram's piece order (per r: A piece wid*4 + r/2, then the B piece 32 KB
+      // further; r even = A, odd = B)
       const int q = SWZ == 3 ? (wid * PIECES + r + (int)(Lr % share) * (STAGE_KB / 2)) % STAGE_KB
+                  : SWZ == 4 ? ((r & 1) ? STAGE_KB / 2 : 0) + wid * (PIECES / 2) + (r >> 1)
                              : wid * PIECES + r;
       // SWZ 1: the Gram's source order (column col = q*8 + lane/8, 16-B chunk (lane&7)^(col&7))
       const int col = q * 8 + (lane >> 3);
-      const int off = (SWZ == 1 || SWZ == 3) ? col * 128 + (((lane & 7) ^ (col & 7)) << 4)
+      const int off = (SWZ == 1 || SWZ == 3 || SWZ == 4) ? col * 128 + (((lane & 7) ^ (col & 7)) << 4)
                     : SWZ == 2 ? q * 1024 + ((lane & 7) << 7) + ((lane >> 3) << 4)   // column-strided lanes
                                : q * 1024 + lane * 16;
       __builtin_amdgcn_global_load_lds(src + off,
@@ -270,7 +273,15 @@ int main() {
   }
   int* flags;
   CHECK(hipMalloc(&flags, 4096 * 16 * 4));
-  for (int wg : {256, 1280}) {
+  for (int wg : {1024, 2048}) {
+    snprintf(tag, sizeof tag, "single reader, gram piece order wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 4>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 1, 0); }, 5));
+    snprintf(tag, sizeof tag, "single reader, linear order wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 1>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 1, 0); }, 5));
+    snprintf(tag, sizeof tag, "PAIRED, gram piece order wg=%d", wg);
+    rep(tag, timeit([&] { hipLaunchKernelGGL((dma_kernel<64, 2, 4>), dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1, (float4*)nullptr, 0, 2, 0); }, 5));
+  }
+  for (int wg : std::vector<int>{}) {
     snprintf(tag, sizeof tag, "hybrid pair (role 1 regs) wg=%d", wg);
     rep(tag, timeit([&] { hipLaunchKernelGGL(hyb_pair_kernel, dim3(wg), dim3(512), 0, 0, buf, nbytes, out, 1); }, 5));
     snprintf(tag, sizeof tag, "hybrid kernel, both DMA wg=%d", wg);
