@@ -218,7 +218,7 @@ def ate_residual_balance(Y, W, X, balance: BalanceConfig | None = None,
     run = _run(run)
     bc = balance or BalanceConfig()
     with trace("ate_residual_balance"):
-        if _ref(run) or bc.allow_negative_weights:
+        if _ref(run):
             from .reference.balance import residual_balance_ate
             return residual_balance_ate(Y, W, X, zeta=bc.zeta, alpha=bc.alpha, seed=run.seed,
                                         scale_x=bc.scale_x,
@@ -226,7 +226,8 @@ def ate_residual_balance(Y, W, X, balance: BalanceConfig | None = None,
         from .estimators.balance import residual_balance
         return residual_balance(Y, W, X, zeta=bc.zeta, alpha=bc.alpha, seed=run.seed,
                                 scale_x=bc.scale_x, method=method, device=run.device(),
-                                dtype="f64" if run.dtype == "bf16" else run.dtype)
+                                dtype="f64" if run.dtype == "bf16" else run.dtype,
+                                allow_negative=bc.allow_negative_weights)
 
 
 def ate_causal_forest(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest(GRF)",

@@ -64,7 +64,7 @@ def _schur(Garm, xc, one, Dd, W, p):
 
 
 def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_arm=None,
-                      fixed=False):
+                      fixed=False, allow_negative=False):
     """Balancing weights for every arm a (rows ``masks[a]``) toward ``target`` [p].
     Returns gamma [ld] (each row carries its own arm's weight) and iteration counts.
 
@@ -72,7 +72,12 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
     arm's state is frozen (``torch.where``, so a NaN from a degenerate post-convergence
     Newton system cannot leak into it) from the iteration at which it converged, and the
     iteration counts come back as a device tensor. ``seg_arm`` (host, per segment: arm or
-    -1) then has to be given, since deriving it from ``masks`` reads the device."""
+    -1) then has to be given, since deriving it from ``masks`` reads the device.
+
+    ``allow_negative``: drop gamma >= 0 (balanceHD ``allow.negative.weights``): no row
+    barrier (t), the step length is limited by the (s, z) pairs only
+    (reference/balance.ipm_balance, same algorithm)."""
+    neg = bool(allow_negative)
     dev, dt = pan.device, torch.float64
     xc = const(pan.xcols, torch.int64, dev)
     one = pan.cols["one"]
@@ -118,14 +123,14 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
     s = h[None] - Gx(gam, delta)
     z = torch.ones(A, 2 * p, dtype=dt, device=dev)
     t = torch.ones(pan.ld, dtype=dt, device=dev)
-    ncomp = 2 * p + nA
+    ncomp = 2 * p + (0 * nA if neg else nA)
     done = torch.zeros(A, dtype=torch.bool, device=dev)
     iters = np.zeros(A, dtype=int)
     iters_dev = torch.zeros(A, dtype=torch.int64, device=dev)
 
     def solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, r_sz, r_gt):
         v = (z * r_g - r_sz) / s                                   # [A, 2p]
-        rhs_g = lf * (-r_d_g - rows_from(v[:, :p] - v[:, p:]) - r_gt / gam)
+        rhs_g = lf * (-r_d_g - rows_from(v[:, :p] - v[:, p:]) - (0.0 if neg else r_gt / gam))
         rhs_d = -r_d_d + v.sum(1)
         wts = lf / Dg
         Gs = gram(pan, w=wts.to(pan.data.dtype))                  # [nseg, P, P]
@@ -139,13 +144,17 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
         mg = per_arm_T(u_g)
         rk = torch.cat([mg - u_d[:, None], -mg - u_d[:, None], (arm_sum(u_g) + r_p)[:, None]], 1)
         sol = spd_solve(K, rk)
+        # a converged arm's Schur system may have lost its positive pivots (spd_solve then
+        # returns NaN); its step is discarded anyway, but dy enters every row through the
+        # mask product below (0 * NaN = NaN), so zero it before use
+        sol = torch.where(done[:, None], torch.zeros_like(sol), sol)
         uu, dy = sol[:, :2 * p], sol[:, 2 * p]
         dxg = lf * (rhs_g - rows_from(uu[:, :p] - uu[:, p:]) - (mf * dy[:, None]).sum(0)) / Dg
         dxd = (rhs_d + uu.sum(1)) / Dd
         dz = uu + v
         mdx = per_arm_T(dxg)
         ds = -r_g - torch.cat([mdx - dxd[:, None], -mdx - dxd[:, None]], 1)
-        dtt = lf * (-r_gt - t * dxg) / gam
+        dtt = torch.zeros_like(gam) if neg else lf * (-r_gt - t * dxg) / gam
         return dxg, dxd, dy, dz, ds, dtt
 
     def step(vr, dv, vs, dvs):
@@ -156,12 +165,23 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
         rs = torch.where(dvs < 0, -vs / dvs, torch.full_like(vs, float("inf"))).amin(1)
         return torch.minimum(torch.minimum(ra, rs), torch.ones_like(ra))
 
+    def step_sz(vs, dvs):
+        rs = torch.where(dvs < 0, -vs / dvs, torch.full_like(vs, float("inf"))).amin(1)
+        return torch.minimum(rs, torch.ones_like(rs))
+
+    def max_step(ds, dz, dxg, dtt):
+        if neg:
+            return step_sz(torch.cat([s, z], 1), torch.cat([ds, dz], 1))
+        return torch.minimum(step(gam, dxg, torch.cat([s, z], 1), torch.cat([ds, dz], 1)),
+                             step(t, dtt, s, ds))
+
     for it in range(1, maxit + 1):
-        r_d_g = lf * (c_g * gam + rows_from(z[:, :p] - z[:, p:]) + (mf * y[:, None]).sum(0) - t)
+        r_d_g = lf * (c_g * gam + rows_from(z[:, :p] - z[:, p:]) + (mf * y[:, None]).sum(0)
+                      - (0.0 if neg else t))
         r_d_d = c_d * delta - z.sum(1)
         r_p = arm_sum(gam) - 1.0
         r_g = Gx(gam, delta) + s - h[None]
-        mu = ((s * z).sum(1) + arm_sum(gam * t)) / ncomp
+        mu = ((s * z).sum(1) + (0.0 if neg else arm_sum(gam * t))) / ncomp
         scale = torch.clamp(torch.maximum(arm_sum(gam.abs()) * 0 + delta.abs(),
                                           torch.ones_like(delta)), min=1.0)
         rdmax = torch.stack([torch.where(masks[a], r_d_g.abs(), torch.zeros_like(r_d_g)).amax()
@@ -177,22 +197,20 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
             done = done | conv
             if bool(done_h.all()):
                 break
-        Dg = c_g + t / gam
+        Dg = c_g + (0.0 * gam if neg else t / gam)
         Dd = torch.full((A,), c_d, dtype=dt, device=dev)
         W = z / s
         dxg, dxd, dy, dz, ds, dtt = solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, s * z, lf * gam * t)
-        a_aff = torch.minimum(step(gam, dxg, torch.cat([s, z], 1), torch.cat([ds, dz], 1)),
-                              step(t, dtt, s, ds))
+        a_aff = max_step(ds, dz, dxg, dtt)
         af = (mf * a_aff[:, None]).sum(0)
         mu_aff = (((s + a_aff[:, None] * ds) * (z + a_aff[:, None] * dz)).sum(1)
-                  + arm_sum((gam + af * dxg) * (t + af * dtt))) / ncomp
+                  + (0.0 if neg else arm_sum((gam + af * dxg) * (t + af * dtt)))) / ncomp
         sigma = (mu_aff / mu) ** 3
         sm = (mf * (sigma * mu)[:, None]).sum(0)
         r_sz = s * z + ds * dz - (sigma * mu)[:, None]
         r_gt = lf * (gam * t + dxg * dtt - sm)
         dxg, dxd, dy, dz, ds, dtt = solve(Dg, Dd, W, r_d_g, r_d_d, r_p, r_g, r_sz, r_gt)
-        a = torch.minimum(step(gam, dxg, torch.cat([s, z], 1), torch.cat([ds, dz], 1)),
-                          step(t, dtt, s, ds))
+        a = max_step(ds, dz, dxg, dtt)
         a = torch.where(done, torch.zeros_like(a), torch.clamp(0.99 * a, max=1.0))
         af = (mf * a[:, None]).sum(0)
         if fixed:
@@ -216,7 +234,7 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
     return gam * lf, iters
 
 
-def _arb_body(pan, target, zeta, alpha, K, seg_arm):
+def _arb_body(pan, target, zeta, alpha, K, seg_arm, allow_negative=False):
     """E14 as one device function (utils/graphs.GraphCache): per-arm CV elastic net, the
     balancing QPs at a fixed interior-point budget (converged arms frozen on the device),
     and the residual-balancing estimate. Returns [mu1, mu0, var1, var0, iters1, iters0,
@@ -226,7 +244,8 @@ def _arb_body(pan, target, zeta, alpha, K, seg_arm):
                           full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha)
     masks = _arm_masks(pan, K)
     tg = target.to(pan.device, torch.float64)
-    gam, iters = ipm_balance_panel(pan, masks, tg, zeta, seg_arm=seg_arm, fixed=True)
+    gam, iters = ipm_balance_panel(pan, masks, tg, zeta, seg_arm=seg_arm, fixed=True,
+                                   allow_negative=allow_negative)
     b = cv.coef_1se.to(torch.float64)
     Xd = pan.data.double()
     fit = b[:, :1] + b[:, 1:] @ Xd.index_select(0, const(pan.xcols, torch.int64, pan.device))
@@ -241,7 +260,7 @@ def _arb_body(pan, target, zeta, alpha, K, seg_arm):
 
 def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 11), nfolds=10,
                      scale_x=True, method="residual_balancing", device=None, dtype="f64",
-                     graph=False):
+                     graph=False, allow_negative=False):
     """E14 on the device; matches reference.balance.residual_balance_ate.
 
     graph=True (GPU): one hipGraph launch per call after the first of a panel layout
@@ -263,7 +282,7 @@ def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 
         nr = np.asarray(pan.seg_nreal)
         seg_arm = tuple(int(s // K) if nr[s] > 0 else -1 for s in range(pan.nseg))
         out, g = estimator_graphs.run("arb", _arb_body, (pan, target.to(dev)), float(zeta),
-                                      float(alpha), K, seg_arm)
+                                      float(alpha), K, seg_arm, bool(allow_negative))
         v = out.cpu().numpy()
         if v[6] < 0:
             from ..utils.guards import NumericalError
@@ -276,7 +295,7 @@ def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 
     cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
                           full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha).check()
     masks = _arm_masks(pan, K)
-    gam, iters = ipm_balance_panel(pan, masks, target, zeta)
+    gam, iters = ipm_balance_panel(pan, masks, target, zeta, allow_negative=allow_negative)
     b = cv.coef_1se.to(torch.float64)                      # [2, p+1]: arm 1, arm 0
     Xd = pan.data.double()
     fit = b[:, :1] + b[:, 1:] @ Xd[pan.xcols]              # [2, ld]

@@ -387,48 +387,18 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
     return mom
 
 
-class _GraphedDml:
-    """One captured DML cross-fit (utils/graphs.SegmentedStep over dml_phases) bound to a
-    STATIC panel buffer: a later call on data of the same layout copies its panel into the
-    buffer and replays the graph, so the whole estimator (Gram, CV-LASSO paths, selection,
-    residual pass, theta / SE) is ONE graph launch. Built on the second
-    call of a layout, over the panel of the first (eager) call, which was its warm-up."""
-
-    def __init__(self, pan, folds, lambda_rule):
-        from ..utils.graphs import SegmentedStep
-        self.pan = pan
-        self.step = SegmentedStep(dml_phases(pan, folds, lambda_rule), graph=True, warmup=0)
-
-    def __call__(self, pan):
-        if pan is not self.pan:
-            self.pan.data.copy_(pan.data)
-        return self.step()["res"]
-
-
-_graph_cache: dict = {}
-GRAPH_CACHE_MAX = 4
+def _dml_body(pan, folds, lambda_rule):
+    """The whole world-1 cross-fit as one device function (GraphCache captures it: Gram,
+    CV-LASSO paths, selection, residual pass, theta / SE = ONE graph launch)."""
+    return dml_crossfit_panel(pan, folds, lambda_rule)[0]
 
 
 def _dml_graphed(pan, folds, lambda_rule):
-    """Graph-cached cross-fit keyed by the panel layout (shape, dtype, fold segments,
-    columns). First call of a layout: eager, its panel kept; second: copy + capture +
-    replay; later: copy + one graph launch. LRU of GRAPH_CACHE_MAX (each entry holds a
-    panel-sized buffer and its Gram workspace). Returns (res, replayed)."""
-    key = (tuple(pan.data.shape), pan.data.dtype, str(pan.device), folds, lambda_rule,
-           tuple(map(tuple, pan.seg_bounds)), tuple(pan.seg_nreal.tolist()),
-           tuple(sorted(pan.cols.items())), pan.blocked)
-    g = _graph_cache.pop(key, None)
-    if g is None:
-        while len(_graph_cache) >= GRAPH_CACHE_MAX:
-            _graph_cache.pop(next(iter(_graph_cache)))
-        _graph_cache[key] = pan                     # seen once: keep the warm buffers
-        return dml_crossfit_panel(pan, folds, lambda_rule)[0], False
-    if not isinstance(g, _GraphedDml):
-        torch.cuda.synchronize()
-        g.data.copy_(pan.data)
-        g = _GraphedDml(g, folds, lambda_rule)
-    _graph_cache[key] = g
-    return g(pan), True
+    """Graph-cached cross-fit keyed by the panel layout (utils/graphs.GraphCache: first
+    call eager, second captures after a warm-up run, later calls copy + replay; a failed
+    capture falls back to eager with the reason printed; retained HBM is bounded and
+    released by utils.graphs.clear_graph_caches). Returns (res, replayed)."""
+    return estimator_graphs.run("dml_plr", _dml_body, (pan,), folds, lambda_rule)
 
 
 def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cross-fit (LASSO)",

@@ -224,11 +224,27 @@ class _Captured:
 
 
 class _Seen:
-    """First call of a key: it ran eagerly on these inputs (which populated the plan and
-    constant caches for exactly these buffers); they become the graph's static inputs."""
+    """First call of a key: it ran eagerly on these inputs. Small inputs are kept and
+    become the graph's static inputs on the second call (``inputs``); inputs above the
+    cache's retention threshold are not kept (``inputs is None``): the second call's own
+    buffers are captured instead, so a one-off call on a large panel holds no HBM."""
 
     def __init__(self, inputs):
-        self.inputs = list(inputs)
+        self.inputs = None if inputs is None else list(inputs)
+
+
+def _nbytes(inputs):
+    tot = 0
+    for x in inputs:
+        t = _data(x)
+        tot += t.numel() * t.element_size()
+    return tot
+
+
+def _env_bytes(name, default):
+    import os
+    v = os.environ.get(name)
+    return int(float(v)) if v else default
 
 
 class GraphCache:
@@ -237,49 +253,95 @@ class GraphCache:
     *static_args)`` -- a device-only function of the inputs (fixed launch budgets, device
     flags, cached constants; no host sync). Per (name, static args, input layout):
 
-    * 1st call: runs eagerly and keeps its input buffers (a one-off call costs nothing
-      extra, and the eager run is the capture's warm-up on exactly those buffers);
-    * 2nd call: copies its data into the kept buffers, captures the body and replays it;
+    * 1st call: runs eagerly; its input buffers are kept when they are small
+      (``retain_bytes``), so a one-off call on a large panel keeps nothing;
+    * 2nd call: copies its data into the kept buffers (or keeps its own), runs the body
+      once eagerly on them (re-populating plan / constant caches that may have been
+      evicted in between), captures it and replays it;
     * later calls: copy + ONE graph launch.
 
-    LRU of ``maxsize`` entries (each holds its input buffers and the graph's memory pool).
-    A body that cannot be captured is remembered and runs eagerly from then on. Outputs
-    of a replay are the graph's static tensors: read them before the next call.
+    LRU bounded by ``maxsize`` entries and ``max_bytes`` of retained input buffers
+    (``ATE_GRAPH_CACHE_BYTES``, default 24 GiB; each entry also holds its graph's memory
+    pool). A body that cannot be captured is remembered and runs eagerly from then on
+    (the reason is printed). Outputs of a replay are the graph's static tensors: read them
+    before the next call. ``clear()`` drops every entry (and its HBM).
     Returns (output, replayed: bool)."""
 
-    def __init__(self, maxsize: int = 8):
+    def __init__(self, maxsize: int = 8, max_bytes: int | None = None,
+                 retain_bytes: int | None = None):
         self.maxsize = maxsize
+        self.max_bytes = max_bytes if max_bytes is not None else \
+            _env_bytes("ATE_GRAPH_CACHE_BYTES", 24 << 30)
+        self.retain_bytes = retain_bytes if retain_bytes is not None else \
+            _env_bytes("ATE_GRAPH_RETAIN_BYTES", 1 << 30)
         self.entries: dict = {}
+        self.sizes: dict = {}
         self.eager: set = set()
+
+    @property
+    def held_bytes(self):
+        return sum(self.sizes.values())
+
+    def _evict(self, need=0):
+        while self.entries and (len(self.entries) >= self.maxsize or
+                                self.held_bytes + need > self.max_bytes):
+            k = next(iter(self.entries))
+            self.entries.pop(k)
+            self.sizes.pop(k, None)
 
     def run(self, name, body, inputs, *static_args):
         key = (name, static_args, layout_key(*inputs))
         if key in self.eager:
             return body(*inputs, *static_args), False
         g = self.entries.pop(key, None)
+        self.sizes.pop(key, None)
+        nb = _nbytes(inputs)
         if g is None:
-            while len(self.entries) >= self.maxsize:
-                self.entries.pop(next(iter(self.entries)))
-            self.entries[key] = _Seen(inputs)
+            keep = nb <= self.retain_bytes and nb <= self.max_bytes
+            self._evict(nb if keep else 0)
+            self.entries[key] = _Seen(inputs if keep else None)
+            self.sizes[key] = nb if keep else 0
             return body(*inputs, *static_args), False
         if isinstance(g, _Seen):
+            if nb > self.max_bytes:
+                # too large to hold for a replay: run eagerly, stay "seen"
+                self.entries[key] = g
+                self.sizes[key] = 0
+                return body(*inputs, *static_args), False
+            self._evict(nb)
+            static = g.inputs if g.inputs is not None else list(inputs)
             try:
                 torch.cuda.synchronize()
-                for s, x in zip(g.inputs, inputs):
+                for s, x in zip(static, inputs):
                     if x is not s:
                         _data(s).copy_(_data(x))
-                g = _Captured(body, g.inputs, static_args, warmup=0)
+                g = _Captured(body, static, static_args, warmup=1)
             except Exception as e:  # noqa: BLE001 - fall back to eager, but say why
                 print(f"[graphs] {name}: capture failed, running eagerly: {e}", flush=True)
                 torch.cuda.synchronize()
                 self.eager.add(key)
                 return body(*inputs, *static_args), False
         self.entries[key] = g
+        self.sizes[key] = nb
         return g(inputs), True
 
     def clear(self):
         self.entries.clear()
+        self.sizes.clear()
         self.eager.clear()
 
 
 estimator_graphs = GraphCache()
+
+
+def clear_graph_caches():
+    """Release every cached graph, its retained input buffers and the Gram plans (HBM held
+    between estimator calls); call between phases of a long job or at teardown."""
+    estimator_graphs.clear()
+    try:
+        from ..ops.gram import clear_plans
+        clear_plans()
+    except Exception:  # noqa: BLE001 - nothing to clear without the ops module
+        pass
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()

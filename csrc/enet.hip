@@ -223,6 +223,9 @@ __device__ __forceinline__ void select_lane(int i, int lane, double& a, double b
 #endif
 constexpr int NW = ENET_NW, NTH = NW * 64, NP = NW - 1;
 static_assert(NW >= 3, "phase B uses wave 1 for block tn and waves 2.. for snapshots");
+// the fp32 pulls give ONE 64-column block to each pull wave (jb = wid + (wid >= t)), so
+// every block of a PMAX-column problem needs its own wave
+static_assert(NW >= PMAX / 64, "one pull wave per 64-column block: NW >= PMAX / 64");
 #ifndef ENET_BALLOT_ONLY
 #define ENET_BALLOT_ONLY 0   // 1: every pass uses the ballot recurrence (A/B timing)
 #endif
