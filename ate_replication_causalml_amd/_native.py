@@ -64,7 +64,7 @@ _SIGS = {
     "ate_bin_matrix": "plipppp",
     "ate_panel_xtv": "iplpipplipp",
     "ate_select_compact": "plppddpppp" + "p",
-    "ate_gbdt_fit": "ppp",
+    "ate_gbdt_run": "ppp",
     "ate_gbdt_bin_panel": "pilpipppilpppl" + "p",
     "ate_gbdt_slab_entries": "liii",
     "ate_gbdt_apply": "plliipppp" + "p",

@@ -3,9 +3,21 @@ histogram-GBDT nuisance, full panel resident in 8x288 GB HBM").
 
 For each of K folds, E[Y|X] and E[W|X] are boosted on the other folds (``train``
 mask over the resident binned panel — no row copies) and predicted on fold k; the
-held-out residuals feed the Neyman-orthogonal PLR score (same moments/finalisation
-as the LASSO cross-fit, ops/stats.py). ``dist`` shards rows across ranks: histograms
-(C04) and score moments (C06) are all-reduced, CV folds use global fold ids.
+held-out residuals feed the Neyman-orthogonal PLR score (same finalisation as the
+LASSO cross-fit, ops/stats.py). The DML ancestor is ``double_ml``
+(ate_functions.R:372-389), scaled to BASELINE config 5.
+
+Row sharding (``dist``, one rank per GPU): every rank holds its rows of every fold in
+HBM; bin edges come from the global strided row sample (all-gathered, so they equal the
+single-device edges), each level's compact node histograms are all-reduced (C04,
+exact int64) on the fit's stream, the base score is an exact fixed-point mean, and the
+score moments are exact sums (ops/exact.py) all-reduced (C06). The trees, the
+held-out predictions and the ATE / SE are therefore the same bits at every world size.
+Y, W, the scores and the residuals stay on the device.
+
+``checkpoint`` (utils/checkpoint.Checkpoint): the held-out predictions of every finished
+fold are saved (per rank); a rerun loads them and fits only the missing folds, with
+bitwise-identical results.
 """
 from __future__ import annotations
 
@@ -18,13 +30,60 @@ from ..parallel import rng
 from .common import as_np, read_result, resolve_device
 
 
-def _loss(v):
-    return "logistic" if bool(np.all((v == 0) | (v == 1))) else "squared"
+def _loss(v, dist=None):
+    """'logistic' for a 0/1 target (on every rank), else 'squared'."""
+    t = torch.as_tensor(v)
+    flag = torch.tensor([float(bool(torch.all((t == 0) | (t == 1))))], dtype=torch.float64,
+                        device=t.device)
+    if dist is not None:
+        dist.min_(flag)
+    return "logistic" if bool(flag.item()) else "squared"
+
+
+def _response(m, dev):
+    """Raw boosting scores of every row -> response on ``dev`` (no host copy for GPU fits)."""
+    f = m.scores if isinstance(m.scores, torch.Tensor) else torch.from_numpy(np.asarray(m.scores))
+    f = f.to(dev, torch.float64)
+    return torch.sigmoid(f) if m.loss == "logistic" else f
+
+
+def _all_ranks_have(ck, stage, dkey, dist, dev):
+    ok = torch.tensor([float(ck.has(stage, dkey))], dtype=torch.float64,
+                      device=dev if dist is not None and getattr(dist.comm, "capturable", False)
+                      else "cpu")
+    if dist is not None:
+        dist.min_(ok)
+    return bool(ok.item())
+
+
+def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey):
+    """Held-out predictions of E[Y|X], E[W|X] for every fold (device tensors)."""
+    ey = torch.zeros_like(y)
+    ew = torch.zeros_like(w)
+    ly, lw = _loss(y, dist), _loss(w, dist)
+    tag = "" if dist is None else f".r{dist.rank}of{dist.world}"
+    for k in range(K):
+        ho = fid == k
+        stage = f"dml_gbdt_fold{k}{tag}"
+        if checkpoint is not None and _all_ranks_have(checkpoint, stage, dkey, dist, dev):
+            z = checkpoint.load(stage, dkey)
+            py = torch.as_tensor(z["ey"], device=dev)
+            pw = torch.as_tensor(z["ew"], device=dev)
+        else:
+            # held-out predictions = the trainer's running scores of the rows it skipped
+            py = torch.where(ho, _response(fit(y, ly, ~ho), dev), torch.zeros_like(y))
+            pw = torch.where(ho, _response(fit(w, lw, ~ho), dev), torch.zeros_like(w))
+            if checkpoint is not None:
+                checkpoint.save(stage, dkey, ey=py.cpu().numpy(), ew=pw.cpu().numpy())
+        ey = torch.where(ho, py, ey)
+        ew = torch.where(ho, pw, ew)
+    return ey, ew
 
 
 def dml_plr_gbdt(Y, W, X, folds=5, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0,
                  seed=1991, fold_stream=0, method="DML cross-fit (GBDT)", device=None,
-                 dist=None):
+                 dist=None, checkpoint=None):
+    """Host-array entry point: (Y, W, X) are this rank's rows (``dist``) or all rows."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
     n = len(Yn)
@@ -33,36 +92,64 @@ def dml_plr_gbdt(Y, W, X, folds=5, n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
     backend = "gpu" if dev.type == "cuda" else "cpu"
     edges = G.global_bin_edges(Xn, dist, device=dev)
     Xb = G.binned(Xn, edges, dev)          # binned once, shared by all 2K fits
-    ey = np.empty(n)
-    ew = np.empty(n)
     kw = dict(n_trees=n_trees, depth=depth, lr=lr, lam=lam, min_child=min_child,
               backend=backend, edges=edges, dist=dist, Xb=Xb)
+    y = torch.as_tensor(Yn, dtype=torch.float64, device=dev)
+    w = torch.as_tensor(Wn, dtype=torch.float64, device=dev)
+    fid_t = torch.as_tensor(fid, device=dev)
 
-    def response(m):
-        f = m.scores.cpu().numpy() if isinstance(m.scores, torch.Tensor) else m.scores
-        return 1.0 / (1.0 + np.exp(-f)) if m.loss == "logistic" else f
+    def fit(target, loss, train):
+        tr = train if backend == "gpu" else train.cpu().numpy()
+        tg = target if backend == "gpu" else target.cpu().numpy()
+        return G.fit_gbdt(None, tg, loss=loss, train=tr, **kw)
 
-    for k in range(folds):
-        ho = fid == k
-        # held-out predictions = the trainer's running scores of the rows it skipped
-        ey[ho] = response(G.fit_gbdt(None, Yn, loss=_loss(Yn), train=~ho, **kw))[ho]
-        ew[ho] = response(G.fit_gbdt(None, Wn, loss=_loss(Wn), train=~ho, **kw))[ho]
-    yr = torch.as_tensor(Yn - ey, device=dev)
-    wr = torch.as_tensor(Wn - ew, device=dev)
-    mom = S.dml_moments(yr, wr).clone()
-    if dist is not None:
-        dist.sum_(mom)
-    res = S.dml_finalize(mom, "plr")
-    return read_result(res, method, n=dist.n_total if dist is not None else n)
+    dkey = _data_key(checkpoint, Yn, Wn, Xn)
+    ey, ew = _crossfit(y, w, fid_t, folds, fit, dev, dist, checkpoint, dkey)
+    mom = S.dml_moments_exact(y - ey, w - ew, dist)
+    return read_result(S.dml_finalize(mom, "plr"), method,
+                       n=dist.n_total if dist is not None else n)
 
 
-def bin_panel(pan, edges=None, edge_rows=200_000):
+def _data_key(checkpoint, *arrays):
+    if checkpoint is None:
+        return ""
+    from ..utils.checkpoint import fingerprint
+    return fingerprint(*arrays)
+
+
+def panel_bin_edges(pan, rows, dist=None, edge_rows=G.EDGE_SAMPLE):
+    """Bin edges of the panel's feature columns from the GLOBAL strided row sample
+    (models/gbdt.global_sample_ids over global row ids ``pan.row_index``): each rank
+    takes its rows of the sample on the device, the pieces are all-gathered and the
+    edges computed on the device (models/forest.bin_edges_device: per-column sort, so the
+    edges depend on the sample's values only, not on which rank held them)."""
+    from ..models import forest as F
+    dev = pan.device
+    n_total = dist.n_total if dist is not None else pan.n
+    ids = torch.as_tensor(G.global_sample_ids(n_total, edge_rows), device=dev)
+    gid = pan.row_index.index_select(0, rows)
+    pick = rows[torch.isin(gid, ids)]
+    xc = torch.as_tensor(pan.xcols, dtype=torch.long, device=dev)
+    Xcol = pan.colmajor()
+    samp = Xcol.index_select(0, xc).index_select(1, pick).t().double()        # [m, p]
+    if dist is not None and dist.world > 1:
+        cnt = torch.tensor([samp.shape[0]], dtype=torch.float64)
+        on_dev = bool(getattr(dist.comm, "capturable", False))
+        cdev = dev if on_dev else "cpu"
+        counts = [int(c.item()) for c in dist.comm.all_gather(cnt.to(cdev))]
+        buf = torch.zeros((max(counts), samp.shape[1]), dtype=torch.float64, device=cdev)
+        buf[:samp.shape[0]] = samp.to(cdev)
+        parts = dist.comm.all_gather(buf)
+        samp = torch.cat([pp[:c] for pp, c in zip(parts, counts)]).to(dev)
+    return F.bin_edges_device(samp) if dev.type == "cuda" else F.bin_edges(samp.numpy())
+
+
+def bin_panel(pan, edges=None, edge_rows=G.EDGE_SAMPLE, dist=None):
     """Row-major uint8 bins [n_real][ldr] of the panel's feature columns, binned on the
     device (csrc/gbdt.hip gbdt_bin_panel_kernel; no host copy of X). Edges default to
-    quantile edges of an evenly strided device sample of the real rows.
-    Returns (Xr, ldr, edges, rows) with ``rows`` the panel row of each compact row."""
+    ``panel_bin_edges`` (global strided row sample). Returns (Xr, ldr, edges, rows) with
+    ``rows`` the panel row of each compact row."""
     from .. import _native
-    from ..models import forest as F
     dev = pan.device
     X = pan.data
     p = len(pan.xcols)
@@ -72,10 +159,7 @@ def bin_panel(pan, edges=None, edge_rows=200_000):
     n = int(nr.sum())
     rows = torch.cat([torch.arange(int(a), int(a + m), device=dev) for a, m in zip(r0, nr)])
     if edges is None:
-        xc = torch.as_tensor(pan.xcols, dtype=torch.long, device=dev)
-        pick = torch.as_tensor(np.linspace(0, n - 1, num=min(n, edge_rows)).astype(np.int64),
-                               device=dev)
-        edges = F.bin_edges_device(X.index_select(0, xc).index_select(1, rows[pick]).t().double())
+        edges = panel_bin_edges(pan, rows, dist, edge_rows)
     ldr = -(-p // 32) * 32
     Xr = torch.zeros((n, ldr), dtype=torch.uint8, device=dev)
     code = {torch.bfloat16: 0, torch.float32: 1}[X.dtype]
@@ -90,31 +174,31 @@ def bin_panel(pan, edges=None, edge_rows=200_000):
 
 
 def dml_plr_gbdt_panel(pan, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0,
-                       method="DML cross-fit (GBDT)"):
+                       method="DML cross-fit (GBDT)", dist=None, checkpoint=None,
+                       data_key="", edge_rows=G.EDGE_SAMPLE):
     """Config 5 on an HBM-resident panel (data/device_dgp.synthetic_panel, segment k =
-    fold k): device binning (``bin_panel``), then the same K-fold cross-fit as
-    ``dml_plr_gbdt`` on the resident row-major bins."""
+    fold k; with ``dist`` this rank's slice of every fold): device binning from the global
+    edge sample, then the K-fold cross-fit on the resident row-major bins with Y, W,
+    scores and residuals on the device; histograms (C04) and moments (C06) all-reduced.
+    ``checkpoint`` + ``data_key`` (a caller-chosen name of the data, e.g. the synthetic
+    panel's (n, p, seed)): per-fold held-out predictions are saved / resumed."""
     dev = pan.device
-    Xr, ldr, edges, rows = bin_panel(pan)
+    if dev.type != "cuda":
+        raise ValueError("dml_plr_gbdt_panel runs on a GPU panel (use dml_plr_gbdt on host arrays)")
+    Xr, ldr, edges, rows = bin_panel(pan, edge_rows=edge_rows, dist=dist)
     K = pan.nseg
-    nr = np.asarray(pan.seg_nreal, dtype=np.int64)
-    n = int(nr.sum())
-    Yn = pan.col("Y").index_select(0, rows).double().cpu().numpy()
-    Wn = pan.col("W").index_select(0, rows).double().cpu().numpy()
-    fid = np.repeat(np.arange(K), nr)
+    nr = torch.as_tensor(np.asarray(pan.seg_nreal, dtype=np.int64), device=dev)
+    y = pan.col("Y").index_select(0, rows).double()
+    w = pan.col("W").index_select(0, rows).double()
+    fid = torch.repeat_interleave(torch.arange(K, device=dev), nr)
     kw = dict(n_trees=n_trees, depth=depth, lr=lr, lam=lam, min_child=min_child,
-              backend="gpu", edges=edges, Xb=(Xr, ldr))
+              backend="gpu", edges=edges, Xb=(Xr, ldr), dist=dist)
 
-    def response(m):
-        f = m.scores.cpu().numpy() if isinstance(m.scores, torch.Tensor) else m.scores
-        return 1.0 / (1.0 + np.exp(-f)) if m.loss == "logistic" else f
+    def fit(target, loss, train):
+        return G.fit_gbdt(None, target, loss=loss, train=train, **kw)
 
-    ey = np.empty(n)
-    ew = np.empty(n)
-    for k in range(K):
-        ho = fid == k
-        ey[ho] = response(G.fit_gbdt(None, Yn, loss=_loss(Yn), train=~ho, **kw))[ho]
-        ew[ho] = response(G.fit_gbdt(None, Wn, loss=_loss(Wn), train=~ho, **kw))[ho]
-    mom = S.dml_moments(torch.as_tensor(Yn - ey, device=dev),
-                        torch.as_tensor(Wn - ew, device=dev)).clone()
-    return read_result(S.dml_finalize(mom, "plr"), method, n=n)
+    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint,
+                       f"{data_key}.{pan.n}.{len(pan.xcols)}" if checkpoint is not None else "")
+    mom = S.dml_moments_exact(y - ey, w - ew, dist)
+    n_all = dist.n_total if dist is not None else pan.n
+    return read_result(S.dml_finalize(mom, "plr"), method, n=n_all, trees=n_trees, depth=depth)

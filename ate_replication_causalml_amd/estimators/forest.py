@@ -38,18 +38,21 @@ def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, fores
     ``comm``: tree-parallel propensity forest over ranks (rows replicated, C05)."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
-    if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
+    from ..parallel.comm import capturable
+    if graph and capturable(comm) and dev.type == "cuda":
         # one hipGraph launch: outcome IRLS + counterfactual predictions, the propensity
         # forest (growth, OOB votes, clipping) and the AIPW score, over the binned matrix
-        # (bin edges come from the data, so binning stays in front of the graph)
+        # (bin edges come from the data, so binning stays in front of the graph); with a
+        # tree-parallel RCCL comm the OOB-vote all-reduce (C05) is captured in the graph
         from ..utils.graphs import estimator_graphs
         po = D._outcome_panel(Yn, Wn, Xn, dtype, dev)
         edges = F.bin_edges(Xn)
         Xb = F.bin_matrix(Xn, *edges, dev)
         y = torch.as_tensor(Yn, device=dev)
         w = torch.as_tensor(Wn, device=dev)
+        cm = comm if comm is not None and comm.world_size > 1 else None
         out, g = estimator_graphs.run("aipw_rf", _aipw_rf_body, (po, Xb, y, w), num_trees,
-                                      forest_seed, compat, bootstrap_se, B, seed)
+                                      forest_seed, compat, bootstrap_se, B, seed, cm)
         v = out.cpu().numpy()
         return AteResult.make(method, v[0], v[1], n_oob_nan=int(v[2]), hipgraph=g)
     mu0, mu1 = D.outcome_mu(Yn, Wn, Xn, counterfactual_quirk=(compat == "reference"),
@@ -62,13 +65,26 @@ def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, fores
                                  n_oob_nan=int(np.isnan(p_raw).sum()))
 
 
-def _aipw_rf_body(po, Xb, y, w, num_trees, forest_seed, compat, bootstrap_se, B, seed):
-    """Device body of aipw_rf (no host sync): [ate, se, #OOB-NaN propensities]."""
+def _aipw_rf_body(po, Xb, y, w, num_trees, forest_seed, compat, bootstrap_se, B, seed,
+                  comm=None):
+    """Device body of aipw_rf (no host sync): [ate, se, #OOB-NaN propensities]. ``comm``
+    (world > 1): this rank grows its tree shard and the per-tree OOB vote sums are
+    all-reduced (C05) before the vote shares are formed."""
     from ..ops import stats as S
     mu0, mu1 = D._outcome_fit(po, compat == "reference")
-    fr = F.fit_forest_binned(Xb, (None, None), F.KIND_CLASS, y=w, ntree=num_trees,
-                             seed=forest_seed)
-    p = fr.predict_state(Xb, True, fr.new_state(Xb.shape[1]), 7, host=False).clone()
+    if comm is None:
+        fr = F.fit_forest_binned(Xb, (None, None), F.KIND_CLASS, y=w, ntree=num_trees,
+                                 seed=forest_seed)
+        p = fr.predict_state(Xb, True, fr.new_state(Xb.shape[1]), 7, host=False).clone()
+    else:
+        t0, cnt = F.tree_shard(num_trees, 1, comm.rank, comm.world_size)
+        fr = F.fit_forest_binned(Xb, (None, None), F.KIND_CLASS, y=w, ntree=cnt,
+                                 seed=forest_seed, tree_offset=t0)
+        n = Xb.shape[1]
+        st = fr.new_state(n)
+        fr.predict_state(Xb, True, st, 1, host=False)
+        comm.all_reduce_(st[:2 * n])
+        p = fr.predict_state(Xb, True, st, 4, host=False).clone()
     nan = torch.isnan(p).sum().double().reshape(1)
     S.clip_propensity_(p)
     res = D._aipw_core(y, w, p, mu0, mu1, bootstrap_se, B, seed, compat)

@@ -50,10 +50,14 @@ def _lasso_w_cv(pan, pf_w, G, counts=None):
                             seg_counts=counts)
 
 
-def _lasso_w_body(pan, pf_w):
-    """Gram stack -> CV-LASSO path -> [coef of W at lambda.1se, lambda.1se, min fold
-    passes] (device-only: the fold truncation flag travels with the result)."""
-    cv = _lasso_w_cv(pan, pf_w, gram(pan))
+def _lasso_w_body(pan, pf_w, dist=None, counts=None):
+    """Gram stack (all-reduced over row shards with ``dist``: C01) -> CV-LASSO path ->
+    [coef of W at lambda.1se, lambda.1se, min fold passes] (device-only: the fold
+    truncation flag travels with the result; ``counts`` = global rows per segment)."""
+    G = gram(pan)
+    if dist is not None:
+        dist.sum_(G)
+    cv = _lasso_w_cv(pan, pf_w, G, None if counts is None else np.asarray(counts))
     lam = cv.lambdas[0].gather(0, cv.sel[0, 1:2].long())
     fnp = cv.fold_npass.min().double().reshape(1) if cv.fold_npass is not None else \
         torch.zeros(1, dtype=torch.float64, device=lam.device)
@@ -62,8 +66,11 @@ def _lasso_w_body(pan, pf_w):
 
 def _lasso_w(Y, W, X, pf_w, seed, nfolds, fold_stream, method, device, dtype, dist, graph):
     pan = _lasso_w_panel(Y, W, X, seed, nfolds, fold_stream, device, dtype, dist)
-    if graph and dist is None and pan.data.is_cuda:
-        out, g = estimator_graphs.run("lasso_w", _lasso_w_body, (pan,), float(pf_w))
+    if graph and (dist is None or dist.capturable) and pan.data.is_cuda:
+        # row shards over RCCL: the Gram all-reduce is captured inside the graph
+        counts = None if dist is None else tuple(global_seg_counts(pan, dist.comm).tolist())
+        out, g = estimator_graphs.run("lasso_w", _lasso_w_body, (pan,), float(pf_w), dist,
+                                      counts)
         v = out.cpu().numpy()
         if v[2] < 0:
             from ..utils.guards import NumericalError
@@ -262,6 +269,9 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     C06 all-reduce of the 7 score moments                          collective (world > 1)
     C  theta / SE (fp64, on device)                                device
 
+    The collectives are RCCL all-reduces on the current stream: utils.graphs.SegmentedStep
+    captures them inside the step's graph (gloo ones run eagerly between graph segments).
+
     shard_paths (world > 1): the path solves are the N-independent part of the step, so
     instead of every rank repeating all of them, rank r solves the outer folds
     k = r, r + world, ... (each outer fold's full-data and inner-CV problems together)
@@ -270,8 +280,7 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     holds a fifth (or less) of the CUs it would, and the Gram beside it runs faster.
 
     Every phase maps a state dict to a state dict; device phases touch only tensors
-    whose storage is static across calls, so each can be captured in its own hipGraph
-    while RCCL runs eagerly between them on the same stream."""
+    whose storage is static across calls, so the whole step can be captured."""
     from ..utils.graphs import Collective
     dist = comm is not None and comm.world_size > 1
     if dist and seg_counts is None:
@@ -318,11 +327,13 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     def phase_final(st):
         return {**st, "res": S.dml_finalize(st["mom"], "plr")}
 
+    cap = bool(getattr(comm, "capturable", False))
+
     def reduce(name):
         def f(st):
             comm.all_reduce_(st[name])
             return st
-        return Collective(f)
+        return Collective(f, capturable=cap)     # RCCL: captured inside the step's graph
 
     phases = [phase_gram, phase_gram_reduce]
     if dist:
@@ -387,18 +398,25 @@ def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:
     return mom
 
 
-def _dml_body(pan, folds, lambda_rule):
-    """The whole world-1 cross-fit as one device function (GraphCache captures it: Gram,
-    CV-LASSO paths, selection, residual pass, theta / SE = ONE graph launch)."""
-    return dml_crossfit_panel(pan, folds, lambda_rule)[0]
+def _dml_body(pan, folds, lambda_rule, dist=None, counts=None):
+    """The whole cross-fit as one device function (GraphCache captures it: Gram, its
+    all-reduce over row shards, CV-LASSO paths, selection, residual pass, the moment
+    all-reduce, theta / SE = ONE graph launch)."""
+    comm = dist.comm if dist is not None else None
+    return dml_crossfit_panel(pan, folds, lambda_rule, comm=comm,
+                              seg_counts=None if counts is None else np.asarray(counts))[0]
 
 
-def _dml_graphed(pan, folds, lambda_rule):
+def _dml_graphed(pan, folds, lambda_rule, dist=None):
     """Graph-cached cross-fit keyed by the panel layout (utils/graphs.GraphCache: first
     call eager, second captures after a warm-up run, later calls copy + replay; a failed
     capture falls back to eager with the reason printed; retained HBM is bounded and
-    released by utils.graphs.clear_graph_caches). Returns (res, replayed)."""
-    return estimator_graphs.run("dml_plr", _dml_body, (pan,), folds, lambda_rule)
+    released by utils.graphs.clear_graph_caches). ``dist`` over RCCL: the collectives
+    are captured too. Returns (res, replayed)."""
+    counts = None
+    if dist is not None and dist.world > 1:
+        counts = tuple(global_seg_counts(pan, dist.comm).tolist())   # host ints, outside
+    return estimator_graphs.run("dml_plr", _dml_body, (pan,), folds, lambda_rule, dist, counts)
 
 
 def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cross-fit (LASSO)",
@@ -406,15 +424,17 @@ def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cr
     """K-fold cross-fit partially-linear DML with CV-LASSO nuisances E[Y|X], E[W|X]
     (inner CV over the other K-1 folds). Matches reference.estimators.dml_plr_lasso.
 
-    graph: on a GPU without row sharding, the estimator runs as one captured hipGraph
-    (first call of a panel layout eager, captured on the second, replayed afterwards)."""
+    graph: on a GPU (alone, or row-sharded over RCCL with the all-reduces captured), the
+    estimator runs as one captured hipGraph (first call of a panel layout eager, captured
+    on the second, replayed afterwards)."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
     fid = _fold_ids(len(Yn), folds, seed, 0, dist)
     pan = build_panel(Xn, Wn, Yn, folds=fid, dtype=dtype, device=dev)
-    if graph and dist is None and pan.data.is_cuda:
-        res, g = _dml_graphed(pan, folds, lambda_rule)
-        return read_result(res, method, n=len(Yn), hipgraph=g)
+    if graph and (dist is None or dist.capturable) and pan.data.is_cuda:
+        res, g = _dml_graphed(pan, folds, lambda_rule, dist)
+        return read_result(res, method, n=dist.n_total if dist is not None else len(Yn),
+                           hipgraph=g)
     res, mom, _ = dml_crossfit_panel(pan, folds, lambda_rule,
                                      comm=dist.comm if dist is not None else None)
     return read_result(res, method, n=dist.n_total if dist is not None else len(Yn))

@@ -220,10 +220,21 @@ def aipw_from_nuisances(method, Y, W, p, mu0, mu1, bootstrap_se=False, B=1000, s
     return read_result(res, method, **diag)
 
 
-def _aipw_glm_body(po, pp, y, w, bootstrap_se, B, seed, compat):
-    mu0, mu1 = _outcome_fit(po, False)
-    p = pp.scatter_rows(_propensity_fit(pp).mu)
-    return _aipw_core(y, w, p, mu0, mu1, bootstrap_se, B, seed, compat)
+def _aipw_glm_body(po, pp, y, w, bootstrap_se, B, seed, compat, dist=None):
+    """Both IRLS fits (their per-iteration Gram / deviance all-reduces over row shards
+    included, C01/C02), counterfactual predictions and the AIPW score (moments all-reduced,
+    C06; bootstrap replicates sharded, C07): device-only, capturable."""
+    mu0, mu1 = _outcome_fit(po, False, dist)
+    p = pp.scatter_rows(_propensity_fit(pp, dist).mu)
+    if dist is None or dist.world == 1:
+        return _aipw_core(y, w, p, mu0, mu1, bootstrap_se, B, seed, compat)
+    res, mom = S.aipw(w, y, p, mu0, mu1, compat=compat)
+    res = S._aipw_finalize(dist.sum_(mom.clone()))
+    if bootstrap_se:
+        e1, e2 = S.aipw_terms(w, y, p, mu0, mu1, compat)
+        taus = bootstrap_sharded(e1, e2, B, seed, dist)
+        res = torch.stack([res[0], taus.std(unbiased=True).to(res.device)])
+    return res
 
 
 def _aipw_core(y, w, p, mu0, mu1, bootstrap_se, B, seed, compat):
@@ -267,18 +278,19 @@ def bootstrap_replicates(e1, e2, B, seed, comm=None):
 def aipw_glm(Y, W, X, bootstrap_se=False, B=1000, seed=1991, compat="reference",
              method="Doubly Robust with logistic regression PS", device=None, dtype="f64",
              dist=None, graph=True):
-    """E9 ``doubly_robust_glm`` (ate_functions.R:211-264). On a GPU (no row sharding) both
-    IRLS fits, the counterfactual predictions, the AIPW score moments and the optional
-    bootstrap run as ONE captured hipGraph (replayed for later calls of the same shape)."""
+    """E9 ``doubly_robust_glm`` (ate_functions.R:211-264). On a GPU both IRLS fits, the
+    counterfactual predictions, the AIPW score moments and the optional bootstrap run as
+    ONE captured hipGraph (replayed for later calls of the same shape); with ``dist``
+    over RCCL the all-reduces are inside that graph."""
     dev = resolve_device(device)
-    if graph and dist is None and dev.type == "cuda":
+    if graph and (dist is None or dist.capturable) and dev.type == "cuda":
         po = _outcome_panel(Y, W, X, dtype, dev)
         pp = _propensity_panel(W, X, dtype, dev)
         y = torch.as_tensor(as_np(Y), device=dev)
         w = torch.as_tensor(as_np(W), device=dev)
 
         res, g = estimator_graphs.run("aipw_glm", _aipw_glm_body, (po, pp, y, w), bootstrap_se,
-                                      B, seed, compat)
+                                      B, seed, compat, dist)
         return read_result(res, method, hipgraph=g)
     mu0, mu1 = outcome_mu(Y, W, X, counterfactual_quirk=False, device=device, dtype=dtype,
                           dist=dist)

@@ -4,8 +4,11 @@ SURVEY.md K11-K14 + C04).
 ``fit_gbdt`` grows depth-limited trees level by level on the binned uint8 panel:
 GPU (csrc/gbdt.hip) or the numpy reference (reference/gbdt.py) — same spec, same
 integer histogram sums, so the same trees. With ``dist`` (row shards), each level's
-node histograms are all-reduced (C04, exact int64) and every rank takes the same
-split decisions; the bin edges must then be global (``global_bin_edges``).
+compact node histograms are all-reduced (C04, exact int64) on the fit's stream between
+steps of the native level loop (``ate_gbdt_run``), and every rank takes the same split
+decisions; the base score is an exact fixed-point mean and the bin edges come from a
+GLOBAL row sample (``global_bin_edges``), so a row-sharded fit grows the same trees bit
+for bit at every world size.
 """
 from __future__ import annotations
 
@@ -102,21 +105,36 @@ def _rowmajor_bins(X, edges, dev):
     return _to_rowmajor(F.bin_matrix(np.asarray(X, dtype=np.float64), edges[0], edges[1], dev))
 
 
-def global_bin_edges(X_local, dist, rows_per_rank=20000, device=None):
-    """Bin edges every rank agrees on: an evenly strided sample of each shard is
-    all-gathered and binned together."""
+def global_sample_ids(n_total, rows=EDGE_SAMPLE):
+    """Global row ids of the bin-edge sample: evenly strided over ALL rows (the single-
+    device ``sample_bin_edges`` rows), so the edges do not depend on the sharding."""
+    if n_total <= rows:
+        return np.arange(n_total, dtype=np.int64)
+    return np.linspace(0, n_total - 1, num=rows).astype(np.int64)
+
+
+def global_bin_edges(X_local, dist, rows=EDGE_SAMPLE, device=None):
+    """Bin edges every rank agrees on, EQUAL to the single-device edges: each rank
+    contributes its rows of the global strided sample (global_sample_ids), the pieces are
+    all-gathered in rank order (= global row order) and binned together."""
     X_local = np.asarray(X_local, dtype=np.float64)
     if dist is None or dist.world == 1:
-        return sample_bin_edges(X_local, device=device)
-    n = X_local.shape[0]
-    take = np.linspace(0, n - 1, num=min(n, rows_per_rank)).astype(np.int64) if n else \
-        np.zeros(0, dtype=np.int64)
-    s = torch.zeros((rows_per_rank, X_local.shape[1]), dtype=torch.float64)
-    s[:len(take)] = torch.from_numpy(X_local[take])
-    cnt = torch.tensor([float(len(take))])
-    counts = [int(c.item()) for c in dist.comm.all_gather(cnt)]
+        return sample_bin_edges(X_local, rows=rows, device=device)
+    from ..parallel.dist import shard_range
+    ids = global_sample_ids(dist.n_total, rows)
+    mine = ids[(ids >= dist.row_offset) & (ids < dist.row_offset + dist.n_local)] - dist.row_offset
+    counts = [int(((ids >= o) & (ids < o + m)).sum())
+              for o, m in (shard_range(dist.n_total, r, dist.world) for r in range(dist.world))]
+    on_dev = device is not None and torch.device(device).type == "cuda" and \
+        bool(getattr(dist.comm, "capturable", False))          # RCCL gathers device tensors
+    s = torch.zeros((max(counts), X_local.shape[1]), dtype=torch.float64,
+                    device=device if on_dev else "cpu")
+    s[:len(mine)] = torch.as_tensor(X_local[mine], device=s.device)
     parts = dist.comm.all_gather(s)
-    return F.bin_edges(torch.cat([pp[:c] for pp, c in zip(parts, counts)]).numpy())
+    S = torch.cat([pp[:c] for pp, c in zip(parts, counts)])
+    if device is not None and torch.device(device).type == "cuda":
+        return F.bin_edges_device(S.to(device))
+    return F.bin_edges(S.cpu().numpy())
 
 
 def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0,
@@ -127,7 +145,9 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
     predictions come for free). ``Xb=(binned, ld)`` from ``binned()`` reuses one binned
     panel across fits (X and edges are then only used for bookkeeping). ``seed`` is
     reserved for row/column subsampling (not used: full-data boosting is deterministic)."""
-    y = np.asarray(y, dtype=np.float64)
+    on_dev = isinstance(y, torch.Tensor) and y.is_cuda
+    if not on_dev:
+        y = np.asarray(y.cpu() if isinstance(y, torch.Tensor) else y, dtype=np.float64)
     if Xb is None:
         X = np.asarray(X, dtype=np.float64)
         n, p = X.shape
@@ -141,7 +161,11 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
         backend = "gpu" if torch.cuda.is_available() else "cpu"
     if edges is None:
         edges = global_bin_edges(X, dist)
-    train = np.ones(n, dtype=bool) if train is None else np.asarray(train, dtype=bool)
+    if train is None:
+        train = torch.ones(n, dtype=torch.bool, device=y.device) if on_dev else \
+            np.ones(n, dtype=bool)
+    elif not on_dev:
+        train = np.asarray(train.cpu() if isinstance(train, torch.Tensor) else train, dtype=bool)
     if backend != "gpu":
         if Xb is None:
             Xbh = F.bin_matrix(X, edges[0], edges[1], None).numpy()
@@ -174,26 +198,43 @@ class FitArgs(ctypes.Structure):
                 ("lr", ctypes.c_double), ("min_child", ctypes.c_int64), ("R", ctypes.c_int64),
                 ("y", P), ("f", P), ("idx", P * 2), ("gh", P * 2), ("bkt", P), ("cnt", P),
                 ("base", P), ("btot", P), ("seg", P * 2), ("tot", P), ("feat", P), ("thr", P),
-                ("value", P), ("H", P * 2), ("slab", P), ("slab_cap", ctypes.c_int64),
+                ("value", P), ("H", P * 2), ("Hs", P), ("slab", P), ("slab_cap", ctypes.c_int64),
                 ("cand", P)]
 
 
-REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64)
+class RunState(ctypes.Structure):
+    """Mirror of csrc/gbdt.hip::GbdtRunState (resumable position of a fit)."""
+    _fields_ = [("t", ctypes.c_int), ("d", ctypes.c_int), ("cur", ctypes.c_int),
+                ("resume", ctypes.c_int), ("red_count", ctypes.c_int64)]
+
+
 MAXB = 65
+
+
+def exact_base(y_train, n_train, loss, dist=None):
+    """Base score from the EXACT sum of the training targets (2^-28 fixed point, as the
+    histograms): identical bits for any row sharding (reference/gbdt.base_score)."""
+    if isinstance(y_train, torch.Tensor):
+        ys = torch.round(y_train.double() * ref.FIX).to(torch.int64).sum().reshape(1)
+    else:
+        ys = torch.tensor([int(ref.fix(y_train).sum())], dtype=torch.int64)
+    cnt = torch.cat([ys, torch.tensor([int(n_train)], dtype=torch.int64, device=ys.device)])
+    if dist is not None:
+        dist.sum_(cnt)
+    c = cnt.cpu()
+    return ref.base_from_sums(int(c[0]), int(c[1]), loss)
 
 
 def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain, edges,
              dist, dev):
-    n = len(y)
-    yt = torch.as_tensor(y, device=dev)
-    trn = torch.as_tensor(train, device=dev)
+    """y: [n] targets, train: [n] bool (numpy or device tensors: the HBM-panel path keeps
+    them on the device)."""
+    yt = torch.as_tensor(y, device=dev, dtype=torch.float64)
+    trn = torch.as_tensor(train, device=dev, dtype=torch.bool)
+    n = yt.numel()
     order = torch.cat([torch.nonzero(trn).flatten(), torch.nonzero(~trn).flatten()])
-    n_train = int(train.sum())
-    cnt = torch.tensor([float(y[train].sum()), float(n_train)], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.sum_(cnt)
-    mean = float(cnt[0] / cnt[1])
-    base = mean if loss == "squared" else float(np.log(mean / (1 - mean)))
+    n_train = int(trn.sum())
+    base = exact_base(yt[order[:n_train]], n_train, loss, dist)
     M = 2 ** (depth + 1) - 1
     f = torch.full((n,), base, dtype=torch.float64, device=dev)
     feat = torch.full((n_trees, M), -2, dtype=torch.int32, device=dev)
@@ -217,7 +258,11 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
     btot = torch.empty(MAXB, **i32)
     seg = [torch.zeros(MAXB + 1, **i32), torch.zeros(MAXB + 1, **i32)]
     tot = torch.zeros(2 * M, **i64)
-    H = [torch.empty(2 ** (depth - 1) * p * 512, **i64) for _ in range(2)]
+    per = 512 * p
+    H = [torch.empty(2 ** (depth - 1) * per, **i64) for _ in range(2)]
+    Hs = torch.empty(max(1, 2 ** (depth - 2)) * per, **i64)
+    # rule 1 (hessian child rule + a pause per level for the histogram all-reduce) for
+    # every row-sharded fit, world 1 included (the same code path as world W)
     rule = 0 if dist is None else 1
     cap = int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule))
     slab = torch.empty(cap, **i64)
@@ -229,22 +274,22 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
                 y=yt.data_ptr(), f=f.data_ptr(), bkt=bkt.data_ptr(), cnt=cntb.data_ptr(),
                 base=baseb.data_ptr(), btot=btot.data_ptr(), tot=tot.data_ptr(),
                 feat=feat.data_ptr(), thr=thr.data_ptr(), value=value.data_ptr(),
-                slab=slab.data_ptr(), slab_cap=cap, cand=cand.data_ptr())
+                Hs=Hs.data_ptr(), slab=slab.data_ptr(), slab_cap=cap, cand=cand.data_ptr())
     a.idx = (P * 2)(idx[0].data_ptr(), idx[1].data_ptr())
     a.gh = (P * 2)(gh[0].data_ptr(), gh[1].data_ptr())
     a.seg = (P * 2)(seg[0].data_ptr(), seg[1].data_ptr())
     a.H = (P * 2)(H[0].data_ptr(), H[1].data_ptr())
-    cb = None
-    if dist is not None:
-        bufs = {tot.data_ptr(): tot, H[0].data_ptr(): H[0], H[1].data_ptr(): H[1]}
-
-        def _reduce(ptr, count):
-            try:
-                dist.sum_(bufs[ptr][:count])
-                return 0
-            except Exception:          # noqa: BLE001 - reported as a non-zero status
-                return 1
-        cb = REDUCE_FN(_reduce)
-    _native.call("ate_gbdt_fit", ctypes.addressof(a), ctypes.cast(cb, ctypes.c_void_p) if cb
-                 else None, torch.cuda.current_stream().cuda_stream)
+    st = RunState()
+    run = _native.hip().ate_gbdt_run
+    while True:
+        # the stepper enqueues a level's kernels on the current stream; a row-sharded fit
+        # pauses after each level's compact histograms, which are all-reduced (C04) on the
+        # same stream -- no host callback, no host sync
+        rc = run(ctypes.addressof(a), ctypes.addressof(st),
+                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc == 0:
+            break
+        if rc != 1 or dist is None:
+            raise RuntimeError(f"ate_gbdt_run failed with status {rc}")
+        dist.sum_(Hs[:st.red_count])
     return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu", f)

@@ -122,6 +122,16 @@ def dml_moments(yr, wr, valid=None):
     return mom
 
 
+def dml_moments_exact(yr, wr, dist=None):
+    """``dml_moments`` with order-independent sums (ops/exact.py), all-reduced over
+    ``dist``: the same bits for any row sharding (bitwise world-size invariance)."""
+    from .exact import exact_sum
+    y, w = yr.double(), wr.double()
+    w2 = w * w
+    terms = torch.stack([w * y, w2, y * y * w2, y * w2 * w, w2 * w2, torch.ones_like(y), y * y], 1)
+    return exact_sum(terms, dist)
+
+
 def dml_finalize(mom, mode="plr"):
     """mode 'plr': Neyman-score SE; 'lm': lm(Y_resid ~ 0 + W_resid) SE (ate_functions.R:363)."""
     md = 0 if mode == "plr" else 1

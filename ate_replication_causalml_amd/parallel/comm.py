@@ -24,6 +24,7 @@ import torch
 class LocalComm:
     rank = 0
     world_size = 1
+    capturable = True          # no-op collectives: nothing to keep out of a graph
 
     def all_reduce_(self, t):
         return t
@@ -51,6 +52,10 @@ class TorchComm:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
+        # RCCL ("nccl") collectives are enqueued on the current HIP stream and can be
+        # captured in a hipGraph (utils/graphs); gloo stages through the host (not
+        # capturable: estimators run such collectives eagerly between graph segments)
+        self.capturable = dist.get_backend(group) == "nccl"
 
     def all_reduce_(self, t):
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
@@ -95,6 +100,8 @@ class _SimWorld:
 class ThreadSimComm:
     """Rank ``rank`` of an in-process simulated world (use :func:`run_simulated`)."""
 
+    capturable = False
+
     def __init__(self, world: _SimWorld, rank: int):
         self.w = world
         self.rank = rank
@@ -136,6 +143,11 @@ class ThreadSimComm:
 
     def barrier(self):
         self.w.barrier.wait()
+
+
+def capturable(comm) -> bool:
+    """Whether ``comm``'s collectives may sit inside a captured hipGraph."""
+    return comm is None or bool(getattr(comm, "capturable", False))
 
 
 def run_simulated(world_size: int, fn):

@@ -26,7 +26,7 @@ def shard_range(n_total: int, rank: int, world: int):
     return off, base + (1 if rank < rem else 0)
 
 
-@dataclass
+@dataclass(eq=False)          # identity hash: usable as a static GraphCache argument
 class DistContext:
     comm: object
     row_offset: int
@@ -36,6 +36,11 @@ class DistContext:
     def for_rank(cls, comm, n_total: int):
         off, _ = shard_range(n_total, comm.rank, comm.world_size)
         return cls(comm, off, n_total)
+
+    @property
+    def capturable(self):
+        """Collectives of this context can be captured in a hipGraph (RCCL, world 1)."""
+        return self.world == 1 or bool(getattr(self.comm, "capturable", False))
 
     @property
     def world(self):

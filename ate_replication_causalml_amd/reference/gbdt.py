@@ -15,7 +15,9 @@ both implementations:
   HL, HR >= min_child (in hessian units), ties -> lowest feature then lowest bin;
   split only if the gain > min_gain, else the node is a leaf;
 * leaf value -lr * G / (H + lam); heap layout (children of k: 2k+1, 2k+2);
-* base score: mean(y) (squared) or logit(mean(y)) (logistic) over the training rows.
+* base score: mean(y) (squared) or logit(mean(y)) (logistic) over the training rows,
+  the mean taken from the EXACT sum of fix(y) (2^-28 fixed point): order-independent, so
+  row-sharded fits start from the same bits at every world size.
 """
 from __future__ import annotations
 
@@ -28,6 +30,12 @@ FIX = float(2 ** 28)
 
 def fix(v):
     return np.rint(np.asarray(v, dtype=np.float64) * FIX).astype(np.int64)
+
+
+def base_from_sums(ysum_fix: int, n: int, loss: str) -> float:
+    """Base score from the exact fixed-point target sum over n training rows."""
+    mean = (ysum_fix / FIX) / n
+    return mean if loss == "squared" else float(np.log(mean / (1 - mean)))
 
 
 def grad_hess(f, y, loss):
@@ -90,11 +98,10 @@ def fit(Xb, y, train, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min
     p, n = Xb.shape
     M = 2 ** (depth + 1) - 1
     ytr = y[train]
-    cnt = np.array([ytr.sum(), float(train.sum())])
+    cnt = np.array([fix(ytr).sum(), int(train.sum())], dtype=np.int64)
     if hist_reduce is not None:
         cnt = hist_reduce(cnt)
-    mean = cnt[0] / cnt[1]
-    base = mean if loss == "squared" else float(np.log(mean / (1 - mean)))
+    base = base_from_sums(int(cnt[0]), int(cnt[1]), loss)
     f = np.full(n, base)
     feat = np.full((n_trees, M), -2, dtype=np.int32)
     thr = np.zeros((n_trees, M), dtype=np.int32)

@@ -17,9 +17,13 @@ during a capture the object is appended to the capturing step's pin list, so an
 eviction only drops the cache's reference and the memory lives as long as the graph.
 
 ``SegmentedStep`` is the multi-GPU form: a list of phases, each either a device-only
-callable (captured in its own graph) or a collective (run eagerly between replays on
-the same stream). RCCL collectives then stay outside the captured graphs, so capture
-is a purely local operation that succeeds or fails identically on every rank.
+callable or a :class:`Collective`. RCCL collectives (``capturable=True``: enqueued on
+the current HIP stream by torch's ``nccl`` backend) are captured INTO the graph with the
+device phases around them, so a world-W cross-fit is one graph launch like a world-1
+one. Host-side phases (gloo collectives, stream-switch hooks) are
+never captured: they run eagerly between the graphs of the device runs around them.
+If capturing the collectives fails, the step falls back to graphs of the device runs
+with every collective eager between them, and prints why.
 """
 from __future__ import annotations
 
@@ -88,18 +92,23 @@ def maybe_graphed(fn, enable: bool, warmup: int = 1):
 
 
 class Collective:
-    """Marks a phase of a :class:`SegmentedStep` that must run eagerly (an RCCL call)."""
+    """A phase of a :class:`SegmentedStep` that talks to other ranks (or switches streams).
+    ``capturable``: it only enqueues work on the current HIP stream (an RCCL all-reduce),
+    so it may be captured inside the graph of the device phases around it; otherwise it
+    runs eagerly between graph replays."""
 
-    def __init__(self, fn):
+    def __init__(self, fn, capturable: bool = False):
         self.fn = fn
+        self.capturable = capturable
 
     def __call__(self, state):
         return self.fn(state)
 
 
-def _fuse(phases):
+def _fuse(phases, fuse_collectives=False):
     """Merge runs of consecutive device phases into one phase (one graph per run: with
-    no collectives in between, e.g. world size 1, the whole step is a single graph)."""
+    no collectives in between, e.g. world size 1, the whole step is a single graph).
+    ``fuse_collectives``: capturable collectives join the runs."""
     out, run = [], []
 
     def flush():
@@ -114,7 +123,7 @@ def _fuse(phases):
             run.clear()
 
     for ph in phases:
-        if isinstance(ph, Collective):
+        if isinstance(ph, Collective) and not (fuse_collectives and ph.capturable):
             flush()
             out.append(ph)
         else:
@@ -124,27 +133,51 @@ def _fuse(phases):
 
 
 class SegmentedStep:
-    """A step split into phases ``fn(state) -> state``. Device phases are captured in one
-    graph each (when ``graph``), :class:`Collective` phases run eagerly on the current
+    """A step split into phases ``fn(state) -> state``. Device phases (and capturable
+    collectives, when ``capture_collectives``) are captured in one graph per run between
+    host-side phases; host-side :class:`Collective` phases run eagerly on the current
     stream between replays. ``state`` is whatever the phases pass along (tensors whose
     storage is static across calls: graph outputs are overwritten in place on replay).
 
-    Capture runs the phases ``warmup`` times eagerly first (populating plans and
-    constants), then captures each device phase given the state produced by the phases
-    before it. The step's result is the last phase's state."""
+    Capture runs the phases ``warmup`` times eagerly first (populating plans, constants
+    and RCCL communicators), then captures each run given the state produced by the
+    phases before it. If a run with collectives in it cannot be captured, the step is
+    rebuilt with every collective eager (reason printed, ``fallback_reason``). The
+    step's result is the last phase's state. ``graph_count``: graphs replayed per call;
+    ``collectives_captured``: whether collectives sit inside the graphs."""
 
-    def __init__(self, phases, graph: bool, warmup: int = 1):
-        global _pins
-        self.phases = _fuse(phases)
+    def __init__(self, phases, graph: bool, warmup: int = 1, capture_collectives: bool = True):
+        self.raw = list(phases)
+        self.fallback_reason = None
+        has_cc = any(isinstance(p, Collective) and p.capturable for p in self.raw)
+        self.phases = _fuse(self.raw)
         self.graphs = [None] * len(self.phases)
         self.pins = []
+        self.collectives_captured = False
         for _ in range(warmup):
             self._eager()
         if not graph:
             return
+        if capture_collectives and has_cc:
+            try:
+                self._capture(_fuse(self.raw, fuse_collectives=True))
+                self.collectives_captured = True
+                return
+            except Exception as e:  # noqa: BLE001 - fall back, but say why
+                self.fallback_reason = repr(e)
+                print(f"[graphs] capturing the collectives failed, they run eagerly between "
+                      f"graph segments: {e}", flush=True)
+                torch.cuda.synchronize()
+                self.pins = []
+        self._capture(_fuse(self.raw))
+
+    def _capture(self, phases):
+        global _pins
         torch.cuda.synchronize()
+        graphs = [None] * len(phases)
+        pins = []
         state = None
-        for i, ph in enumerate(self.phases):
+        for i, ph in enumerate(phases):
             if isinstance(ph, Collective):
                 state = ph(state)
                 continue
@@ -154,18 +187,23 @@ class SegmentedStep:
                 gc.collect()
                 with _no_gc(), torch.cuda.graph(g):
                     out = ph(state)
-                self.pins += _pins
+                pins += _pins
             finally:
                 _pins = prev
-            self.graphs[i] = (g, out)
+            graphs[i] = (g, out)
             torch.cuda.synchronize()
             g.replay()          # capture does not execute: produce the state for later phases
             state = out
         torch.cuda.synchronize()
+        self.phases, self.graphs, self.pins = phases, graphs, pins
 
     @property
     def graphed(self) -> bool:
         return any(g is not None for g in self.graphs)
+
+    @property
+    def graph_count(self) -> int:
+        return sum(g is not None for g in self.graphs)
 
     def _eager(self):
         state = None

@@ -17,8 +17,14 @@ latency of one cross-fit alone. The Grams of all fits run back to back on one
 low-priority stream; each fit's path solve / residual pass / score runs on its own
 high-priority stream beside the next fit's Gram (``--stagger 2``). The panel uses the
 64-row blocked layout (``--blocked 1``: one contiguous HBM run per Gram K-step). With
-RCCL the device phases are still graph replays; only the two all-reduces run eagerly
-between them (utils/graphs.SegmentedStep).
+RCCL the all-reduces (C01 Gram stack, C08 coefficients, C06 moments) are captured inside
+the fit's graph (utils/graphs.SegmentedStep), so a fit is the same two graph launches
+(Gram tiles on the Gram stream; everything else on the fit's stream) at every world
+size; if capture of the collectives fails they run eagerly between graph segments and
+the JSON says so (``collectives_captured``).
+
+Latency (SURVEY.md §7.5 protocol): ``single_fit_ms`` is the MEDIAN of >= 5 single-call
+replays, each bracketed by device syncs (``single_fit_ms_all`` lists them).
 
 Scaling: weak by default (N=1e7 rows per GPU; at N=1 GPU this is exactly the
 BASELINE config); ``--scaling strong`` keeps N=1e7 in total.
@@ -63,8 +69,8 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--seed", type=int, default=1991)
     ap.add_argument("--graph", type=int, default=-1,
-                    help="capture the step's device phases in hipGraphs (default: on with a GPU; "
-                         "RCCL collectives always run eagerly between the graph replays)")
+                    help="capture the step in hipGraphs (default: on with a GPU; RCCL "
+                         "collectives are captured inside them)")
     ap.add_argument("--parity", type=int, default=1,
                     help="after the timed steps, fit the same rows from a float64 panel (fp64 "
                          "Gram, fp64 path solves; untimed) and report the ATE / SE differences")
@@ -201,8 +207,8 @@ def main():
         return [Collective(wait_prev_gram), phases[0], Collective(record_gram), *phases[1:]]
 
     def make_run(i):
-        # device phases captured one hipGraph each; RCCL collectives (world > 1) run
-        # eagerly between the replays, so capture is local and identical on every rank
+        # device phases and RCCL collectives (world > 1) captured together; the stream
+        # hooks of the stagger stay eager between the Gram graph and the rest
         with plan_slot(i):      # private Gram workspace per in-flight fit
             phases = [in_slot(ph, i) for ph in staggered(
                 dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts), i)]
@@ -221,6 +227,8 @@ def main():
         runs.append(r)
         errors.append(err)
     ok = torch.tensor([float(all(r.graphed for r in runs) if use_graph else 0)], device=device)
+    cc = torch.tensor([float(all(r.collectives_captured for r in runs))], device=device)
+    comm.all_reduce_min_(cc)
     comm.all_reduce_min_(ok)
     graphed = bool(ok.item())
     if use_graph and not graphed:
@@ -230,6 +238,9 @@ def main():
         with plan_slot(0):
             runs = [SegmentedStep(dml_phases(pan, args.folds, "min", comm=comm,
                                              seg_counts=seg_counts), graph=False, warmup=0)]
+    graphs_per_fit = runs[0].graph_count
+    # world 1 has no collectives; at world > 1: whether every rank captured them
+    collectives_captured = bool(cc.item()) if world > 1 and graphed else None
     streams = [torch.cuda.Stream(device) if device.type == "cuda" and len(runs) > 1 else None
                for _ in runs]
 
@@ -261,15 +272,20 @@ def main():
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.all_reduce_max_(el)
     elapsed = float(el.item())
-    # latency of ONE cross-fit alone (no overlap): reported beside the throughput number
-    nlat = max(1, min(args.steps, 10))
-    sync()
-    t1 = time.perf_counter()
+    # latency of ONE cross-fit alone (no overlap), SURVEY.md §7.5: median of >= 5 replays
+    nlat = max(5, min(args.steps, 11))
+    lats = []
     for k in range(nlat):
+        sync()
+        comm.barrier()
+        t1 = time.perf_counter()
         run_step(0)
         sync()
-    lat = torch.tensor([(time.perf_counter() - t1) / nlat], dtype=torch.float64, device=device)
-    comm.all_reduce_max_(lat)
+        lats.append(time.perf_counter() - t1)
+    lat_t = torch.tensor(lats, dtype=torch.float64, device=device)
+    comm.all_reduce_max_(lat_t)                     # per replay: the slowest rank
+    lats = sorted(float(v) for v in lat_t.cpu())
+    lat = lats[len(lats) // 2]
     ate, se = [float(v) for v in res.detach().cpu()]
     n_inflight = len(runs)
     parity = None
@@ -327,7 +343,11 @@ def main():
             "se": se,
             "hipgraph": graphed,
             "inflight": n_inflight,
-            "single_fit_ms": float(lat.item()) * 1e3,
+            "single_fit_ms": lat * 1e3,
+            "single_fit_ms_all": [round(v * 1e3, 4) for v in lats],
+            "single_fit_rows_per_s": n_total / lat,
+            "graphs_per_fit": graphs_per_fit,
+            "collectives_captured": collectives_captured,
             "parity": parity,
         }
         if emulate > 1:

@@ -21,10 +21,18 @@
 //   (histogram subtraction), so levels >= 1 touch at most half of the rows;
 // * split search: workgroup = (node, 8-feature block) staged in LDS, wave = feature,
 //   lane = 4 bins; a one-wave finalize picks each node's best block candidate;
-// * the whole boosting loop (grad -> per level: hist / [reduce] / derive / split /
-//   partition -> apply) is issued from C++ on one stream; row-sharded fits pass a
-//   host callback that all-reduces each level's histograms (root totals come from the
-//   reduced level-0 histogram).
+// * the reduce kernel writes only the histogrammed nodes, COMPACTED: level 0 -> slot 0,
+//   level d >= 1 -> slot m = the histogrammed child of parent m (Hs, nn/2 slots), so a
+//   row-sharded fit all-reduces (C04) half a level's histogram bytes; an expand kernel
+//   then writes the level in node order (histogrammed child = Hs[m], sibling = parent -
+//   Hs[m]);
+// * the whole boosting loop (grad -> per level: hist / reduce / [all-reduce] / expand /
+//   split / partition -> apply) is issued from C++ on one stream by a resumable stepper
+//   (ate_gbdt_run): a row-sharded fit (rule 1) returns to the caller after each level's
+//   compact histogram with the element count to all-reduce; the caller enqueues the
+//   collective on the same stream (torch.distributed / RCCL, no host sync) and calls
+//   again. A single-device fit runs to completion in one call. Root totals come from
+//   the (reduced) level-0 histogram.
 #include <algorithm>
 #include <cstdlib>
 
@@ -261,20 +269,22 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   for (int t = threadIdx.x; t < SLAB / 2; t += NTH) dst[t] = src[t];
 }
 
-// H[k][c][b][j] (node-major, feature-minor) = sum of node k's slabs; zero for nodes
-// without a histogram of their own (gbdt_derive_kernel fills the larger children).
+// Hs[slot][c][b][j] (feature-minor) = sum of the slabs of histogrammed node k, slot 0 at
+// the root, slot k >> 1 below (the histogrammed child of parent k >> 1; gbdt_expand_kernel
+// puts the level in node order). Nodes without a histogram of their own write nothing.
 __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
     const u64* __restrict__ slab, const int32_t* __restrict__ seg, const int64_t* tot, int rule,
-    int nn, int p, int d, int64_t CH, int ydim, int64_t* __restrict__ H) {
+    int nn, int p, int d, int64_t CH, int ydim, int64_t* __restrict__ Hs) {
   __shared__ int sseg[33], sacc[33], snch[32];
   const int k = blockIdx.y;
   if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
   __syncthreads();
+  if (d > 0 && !gbdt_computed(k, d, sseg, tot, rule)) return;   // uniform per workgroup
   if (threadIdx.x == 0) gbdt_plan(sseg, tot, rule, nn, d, CH, sacc, snch);
   __syncthreads();
   const int a = sacc[k], c = snch[k];
   const int64_t per = 512LL * p;
-  int64_t* Hk = H + k * per;
+  int64_t* Hk = Hs + (d == 0 ? 0 : (k >> 1)) * per;
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
     const int cb = (int)(t / p), j = (int)(t - (int64_t)cb * p);
     const int yb = j / FB, fl = j - yb * FB;
@@ -293,23 +303,35 @@ __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
   }
 }
 
-// larger child = parent - histogrammed child (levels >= 1)
-__global__ __launch_bounds__(NT) void gbdt_derive_kernel(const int64_t* __restrict__ Hp,
+// level d in node order from the compact (all-reduced) histograms: the root is Hs[0];
+// below, for every split parent m the histogrammed child is Hs[m] and its sibling is
+// parent - Hs[m] (histogram subtraction, exact in integers)
+__global__ __launch_bounds__(NT) void gbdt_expand_kernel(const int64_t* __restrict__ Hs,
+                                                         const int64_t* __restrict__ Hp,
                                                          int64_t* __restrict__ Hc,
                                                          const int32_t* __restrict__ seg,
                                                          const int64_t* __restrict__ tot,
                                                          const int32_t* __restrict__ feat,
-                                                         int rule, int nn, int p, int d) {
+                                                         int rule, int p, int d) {
   const int m = blockIdx.y;                                 // parent index at level d-1
+  const int64_t per = (int64_t)p * 512;
+  const int64_t* S = Hs + m * per;
+  if (d == 0) {
+    for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT)
+      Hc[t] = S[t];
+    return;
+  }
   if (feat[(1 << (d - 1)) - 1 + m] < 0) return;
   const int small = gbdt_computed(2 * m, d, seg, tot, rule) ? 2 * m : 2 * m + 1;
   const int big = small ^ 1;
-  const int64_t per = (int64_t)p * 512;
   const int64_t* P = Hp + m * per;
-  const int64_t* S = Hc + small * per;
+  int64_t* Cs = Hc + small * per;
   int64_t* B = Hc + big * per;
-  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT)
-    B[t] = P[t] - S[t];
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
+    const int64_t v = S[t];
+    Cs[t] = v;
+    B[t] = P[t] - v;
+  }
 }
 
 struct Best {
@@ -640,13 +662,20 @@ struct GbdtFitArgs {
   int32_t* feat;          // [T][M]
   int32_t* thr;
   double* value;
-  int64_t* H[2];          // [2^(depth-1)][2][256][p]
+  int64_t* H[2];          // [2^(depth-1)][2][256][p] levels in node order (ping-pong)
+  int64_t* Hs;            // [max(1, 2^(depth-2))][2][256][p] compact histogrammed nodes
   u64* slab;              // [slab_cap] partial histograms
   int64_t slab_cap;
   Cand* cand;             // [32 * ceil(p / 8)] split candidates (32 B each)
 };
 
-typedef int (*GbdtReduceFn)(void* ptr, int64_t count);
+// Resumable position of a fit (models/gbdt.py::RunState): tree t, level d, ping-pong
+// index cur, resume = 1 when re-entering after the caller all-reduced level d's compact
+// histograms (red_count int64 entries at the start of Hs).
+struct GbdtRunState {
+  int t, d, cur, resume;
+  int64_t red_count;
+};
 
 // chunk length and (upper bound of the) workgroup count of level d's histogram
 static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH, int64_t* nwg) {
@@ -676,9 +705,12 @@ ATE_API int64_t ate_gbdt_slab_entries(int64_t n_train, int p, int depth, int rul
   return m * SLAB;
 }
 
-ATE_API int ate_gbdt_fit(const void* args, void* reduce, void* stream) {
+// Runs the fit from the position in *state to completion (returns 0), or until a
+// row-sharded fit (rule 1) needs level d's compact histograms all-reduced across ranks
+// (returns 1; state->red_count int64 entries at a.Hs; call again to continue).
+ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
   const GbdtFitArgs& a = *static_cast<const GbdtFitArgs*>(args);
-  GbdtReduceFn red = reinterpret_cast<GbdtReduceFn>(reduce);
+  GbdtRunState& s = *static_cast<GbdtRunState*>(state);
   hipStream_t st = (hipStream_t)stream;
   if (a.depth < 1 || a.depth > 6 || (a.ldr & 31) || a.n_train < 1 || a.W < 1 || a.W > 4 * NT)
     return -1;
@@ -689,38 +721,48 @@ ATE_API int ate_gbdt_fit(const void* args, void* reduce, void* stream) {
   const int64_t per = 512LL * a.p;
   const char* hm = getenv("ATE_GBDT_HIST_MODE");          // ablation switch (profiling only)
   const int hmode = hm ? atoi(hm) : 0;
-  for (int t = 0; t < a.n_trees; ++t) {
-    int32_t* ft = a.feat + (int64_t)t * M;
-    int32_t* th = a.thr + (int64_t)t * M;
-    double* vt = a.value + (int64_t)t * M;
-    int cur = 0;                                          // ping-pong index of idx/gh/seg
-    hipLaunchKernelGGL(gbdt_grad_kernel, dim3((unsigned)((a.n_train + 4 * NT - 1) / (4 * NT))),
-                       dim3(NT), 0, st, a.loss, a.f, a.y, a.idx[0], a.n_train, a.gh[0],
-                       a.seg[0]);
-    for (int d = 0; d <= a.depth; ++d) {
+  for (; s.t < a.n_trees; ++s.t, s.d = 0) {
+    int32_t* ft = a.feat + (int64_t)s.t * M;
+    int32_t* th = a.thr + (int64_t)s.t * M;
+    double* vt = a.value + (int64_t)s.t * M;
+    if (s.d == 0 && !s.resume) {
+      s.cur = 0;                                          // ping-pong index of idx/gh/seg
+      hipLaunchKernelGGL(gbdt_grad_kernel, dim3((unsigned)((a.n_train + 4 * NT - 1) / (4 * NT))),
+                         dim3(NT), 0, st, a.loss, a.f, a.y, a.idx[0], a.n_train, a.gh[0],
+                         a.seg[0]);
+    }
+    for (; s.d <= a.depth; ++s.d) {
+      const int d = s.d, cur = s.cur;
       const int nn = 1 << d;
       int64_t* Hc = a.H[d & 1];
       const int64_t* Hp = a.H[(d + 1) & 1];
       if (d < a.depth) {
-        int64_t CH, nwg;
-        gbdt_hist_geom(a.n_train, a.p, d, a.rule, &CH, &nwg);
-        hipLaunchKernelGGL(gbdt_hist_kernel, dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr, a.ldr,
-                           a.idx[cur], a.gh[cur], a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
-                           ydim, a.slab, hmode, a.loss);
-        hipLaunchKernelGGL(gbdt_hist_reduce_kernel,
-                           dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 256), nn),
-                           dim3(NT), 0, st, a.slab, a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
-                           ydim, Hc);
-        if (red && red(Hc, nn * per)) return -4;
-        if (d == 0) hipLaunchKernelGGL(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, Hc, a.p, a.tot);
-        if (d > 0)
-          hipLaunchKernelGGL(gbdt_derive_kernel,
-                             dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 64), nn / 2),
-                             dim3(NT), 0, st, Hp, Hc, a.seg[cur], a.tot, ft, a.rule, nn, a.p, d);
+        if (!s.resume) {
+          int64_t CH, nwg;
+          gbdt_hist_geom(a.n_train, a.p, d, a.rule, &CH, &nwg);
+          hipLaunchKernelGGL(gbdt_hist_kernel, dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr,
+                             a.ldr, a.idx[cur], a.gh[cur], a.seg[cur], a.tot, a.rule, nn, a.p, d,
+                             CH, ydim, a.slab, hmode, a.loss);
+          hipLaunchKernelGGL(gbdt_hist_reduce_kernel,
+                             dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 256), nn),
+                             dim3(NT), 0, st, a.slab, a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
+                             ydim, a.Hs);
+          if (a.rule == 1) {
+            ATE_CHECK_LAUNCH();
+            s.resume = 1;
+            s.red_count = (d == 0 ? 1 : nn / 2) * per;
+            return 1;                                     // caller all-reduces Hs
+          }
+        }
+        s.resume = 0;
+        if (d == 0) hipLaunchKernelGGL(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, a.Hs, a.p, a.tot);
+        hipLaunchKernelGGL(gbdt_expand_kernel,
+                           dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 128),
+                                d == 0 ? 1 : nn / 2),
+                           dim3(NT), 0, st, a.Hs, Hp, Hc, a.seg[cur], a.tot, ft, a.rule, a.p, d);
+        hipLaunchKernelGGL(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc, a.p,
+                           d, a.depth, a.lam, a.min_child, a.tot, ft, a.cand);
       }
-      if (d < a.depth)
-        hipLaunchKernelGGL(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc, a.p, d,
-                           a.depth, a.lam, a.min_child, a.tot, ft, a.cand);
       hipLaunchKernelGGL(gbdt_split_final_kernel, dim3(nn), dim3(64), 0, st, a.cand, ydim_s, d,
                          a.depth, a.min_gain, a.lam, a.lr, a.tot, ft, th, vt);
       if (d + 1 < a.depth) {
@@ -734,11 +776,11 @@ ATE_API int ate_gbdt_fit(const void* args, void* reduce, void* stream) {
         hipLaunchKernelGGL(gbdt_part_scatter_kernel, dim3(W), dim3(NT), 0, st, a.idx[cur],
                            a.gh[cur], a.bkt, a.n_train, nb, a.R, W, a.base, a.btot,
                            a.idx[cur ^ 1], a.gh[cur ^ 1], a.seg[cur ^ 1]);
-        cur ^= 1;
+        s.cur ^= 1;
       }
     }
     // the next tree starts from whichever order this one left: keep idx[0] current
-    if (cur == 1 &&
+    if (s.cur == 1 &&
         hipMemcpyAsync(a.idx[0], a.idx[1], a.n_train * sizeof(int32_t), hipMemcpyDeviceToDevice,
                        st) != hipSuccess)
       return -3;

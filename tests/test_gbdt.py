@@ -38,33 +38,83 @@ def test_gbdt_leaf_values_are_newton_steps():
         assert np.mean(y[sel]) == pytest.approx(v, abs=1e-7)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_gbdt_row_sharded_equals_single(world):
+    """Row shards (C04 int64 histogram all-reduce, exact base, GLOBAL edge sample) grow
+    the single-device trees bit for bit -- the edges here come from global_bin_edges on
+    each rank's shard, not a pinned host array."""
     X, y = _data(1200, 1)
-    edges = G.global_bin_edges(X, None)
-    m1 = G.fit_gbdt(X, y, n_trees=8, depth=3, backend="cpu", edges=edges)
+    m1 = G.fit_gbdt(X, y, n_trees=8, depth=3, backend="cpu")
 
     def fn(comm):
         d = DistContext.for_rank(comm, len(y))
-        m = G.fit_gbdt(d.local(X), d.local(y), n_trees=8, depth=3, backend="cpu", edges=edges,
-                       dist=d)
-        return m
+        return G.fit_gbdt(d.local(X), d.local(y), n_trees=8, depth=3, backend="cpu", dist=d)
 
     for m in run_simulated(world, fn):
+        np.testing.assert_array_equal(m.edges[0], m1.edges[0])
         np.testing.assert_array_equal(m.feat, m1.feat)
         np.testing.assert_array_equal(m.thr, m1.thr)
-        np.testing.assert_allclose(m.value, m1.value, rtol=0, atol=0)
+        np.testing.assert_array_equal(m.value, m1.value)
+        assert m.base == m1.base
 
 
-def test_dml_gbdt_sharded_equals_single(tutorial):
+def test_global_edges_equal_single_device_edges_large_n():
+    """n > the edge sample: each rank's rows of the global strided sample, gathered, give
+    exactly sample_bin_edges of the whole matrix."""
+    X, _ = _data(5000, 2)
+    want = G.sample_bin_edges(X, rows=701)
+
+    def fn(comm):
+        d = DistContext.for_rank(comm, len(X))
+        return G.global_bin_edges(d.local(X), d, rows=701)
+
+    for e, ne in run_simulated(3, fn):
+        np.testing.assert_array_equal(e, want[0])
+        np.testing.assert_array_equal(ne, want[1])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dml_gbdt_sharded_bitwise_equals_single(tutorial, world):
+    """DML-GBDT on row shards: exact histograms + exact score moments -> the ATE and SE
+    are the SAME BITS as one process (rtol=0)."""
     from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt
     _, m, _ = tutorial
     kw = dict(n_trees=5, depth=3, device="cpu")
     a = dml_plr_gbdt(m.Y, m.W, m.X, **kw)
-    # global edges differ from single-device edges only through the sample; pin them equal
+
     def fn(comm):
         d = DistContext.for_rank(comm, len(m.Y))
         return dml_plr_gbdt(d.local(m.Y), d.local(m.W), d.local(m.X), dist=d, **kw)
-    for b in run_simulated(2, fn):
-        assert b.ate == pytest.approx(a.ate, rel=1e-9)
-        assert b.se == pytest.approx(a.se, rel=1e-9)
+    for b in run_simulated(world, fn):
+        assert b.ate == a.ate and b.se == a.se
+
+
+def test_dml_gbdt_checkpoint_resume(tutorial, tmp_path, monkeypatch):
+    """Kill the cross-fit after fold 2, resume from the checkpoint: the finished folds are
+    loaded (not refit) and the ATE / SE are bitwise identical to an uninterrupted run."""
+    from ate_replication_causalml_amd.estimators import boosting as EB
+    from ate_replication_causalml_amd.utils.checkpoint import Checkpoint
+    _, m, _ = tutorial
+    kw = dict(n_trees=4, depth=3, device="cpu")
+    want = EB.dml_plr_gbdt(m.Y, m.W, m.X, **kw)
+    real = G.fit_gbdt
+    calls = {"n": 0}
+
+    class Killed(RuntimeError):
+        pass
+
+    def dying(*a, **k):
+        calls["n"] += 1
+        if calls["n"] > 6:                      # folds 0-2 done (2 fits each), die in fold 3
+            raise Killed()
+        return real(*a, **k)
+    monkeypatch.setattr(G, "fit_gbdt", dying)
+    ck = Checkpoint(tmp_path, {"cfg": "dml_gbdt"})
+    with pytest.raises(Killed):
+        EB.dml_plr_gbdt(m.Y, m.W, m.X, checkpoint=ck, **kw)
+    assert sorted(p.name.split(".")[0] for p in tmp_path.glob("*.npz")) == \
+        ["dml_gbdt_fold0", "dml_gbdt_fold1", "dml_gbdt_fold2"]
+    calls["n"] = -10**9                          # no more deaths; count the refits
+    got = EB.dml_plr_gbdt(m.Y, m.W, m.X, checkpoint=ck, **kw)
+    assert calls["n"] == -10**9 + 4              # only folds 3 and 4 were fitted
+    assert got.ate == want.ate and got.se == want.se

@@ -107,3 +107,40 @@ def test_dml_gbdt_panel_runs(gpu):
     pan = synthetic_panel(50000, p=30, folds=5, seed=9, dtype="bf16", device=gpu)
     r = dml_plr_gbdt_panel(pan, n_trees=20, depth=4)
     assert r.se > 0 and abs(r.ate - 0.09) < 0.06, r
+
+
+def test_dml_gbdt_panel_dist_world1_equals_plain(gpu):
+    """The row-sharded panel path (rule 1: pause per level, compact histogram all-reduce,
+    here over a one-rank RCCL-free context) equals the single-device path bit for bit."""
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt_panel
+    from ate_replication_causalml_amd.parallel.comm import LocalComm
+    from ate_replication_causalml_amd.parallel.dist import DistContext
+    pan = synthetic_panel(60000, p=37, folds=5, seed=9, dtype="bf16", device=gpu)
+    a = dml_plr_gbdt_panel(pan, n_trees=6, depth=5)
+    b = dml_plr_gbdt_panel(pan, n_trees=6, depth=5, dist=DistContext(LocalComm(), 0, pan.n))
+    assert a.ate == b.ate and a.se == b.se
+
+
+def test_dml_gbdt_panel_matches_host_arrays(gpu):
+    """Panel path (device binning from the global sample, device Y/W/scores) == the
+    host-array path on the same stored values (same edges: the full-data strided sample)."""
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt, dml_plr_gbdt_panel
+    pan = synthetic_panel(40000, p=25, folds=5, seed=4, dtype="f32", device=gpu)
+    a = dml_plr_gbdt_panel(pan, n_trees=5, depth=4)
+    rows = torch.cat([torch.arange(int(s0), int(s0) + int(c), device=gpu)
+                      for (s0, _), c in zip(pan.seg_bounds, pan.seg_nreal)])
+    xc = torch.as_tensor(pan.xcols, device=gpu)
+    X = pan.data.index_select(0, xc).index_select(1, rows).t().double().cpu().numpy()
+    Y = pan.col("Y")[rows].double().cpu().numpy()
+    W = pan.col("W")[rows].double().cpu().numpy()
+    fid = np.repeat(np.arange(5), np.asarray(pan.seg_nreal))
+    import ate_replication_causalml_amd.parallel.rng as R
+    orig = R.fold_ids
+    try:
+        R.fold_ids = lambda n, K, seed, stream: fid      # the panel's fold = its segment
+        b = dml_plr_gbdt(Y, W, X, n_trees=5, depth=4, device=gpu)
+    finally:
+        R.fold_ids = orig
+    assert a.ate == pytest.approx(b.ate, abs=1e-12) and a.se == pytest.approx(b.se, rel=1e-10)

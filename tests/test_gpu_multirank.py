@@ -34,3 +34,23 @@ def test_two_ranks_on_one_gpu_match_one_process(gpu):
     assert two["hipgraph"] and two["inflight"] == 3 and two["n_gpus"] == 2
     assert two["ate"] == pytest.approx(ref["ate"], rel=1e-9, abs=1e-12)
     assert two["se"] == pytest.approx(ref["se"], rel=1e-9)
+
+
+def test_cfg5_gbdt_two_ranks_on_one_gpu_bitwise(gpu):
+    """Config 5's row-sharded DML-GBDT (tools/cfg5.py) with two ranks sharing the GPU
+    (gloo collectives): device edge sample, per-level int64 histogram all-reduce, exact
+    moments -> the SAME BITS as one process holding all rows."""
+    cfg5 = os.path.join(ROOT, "tools", "cfg5.py")
+    args = ["--n", "200000", "--p", "40", "--trees", "6", "--depth", "4"]
+    env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29657",
+                        cfg5, *args], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = _json(r.stdout)
+    one = subprocess.run([sys.executable, cfg5, *args], capture_output=True, text=True,
+                         timeout=240)
+    assert one.returncode == 0, one.stderr[-3000:]
+    ref = _json(one.stdout)
+    assert two["world"] == 2 and ref["world"] == 1
+    assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)

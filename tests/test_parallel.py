@@ -159,3 +159,51 @@ def test_bench_multi_rank_gloo_contract(world):
     ref = json.loads([l for l in one.stdout.splitlines() if l.startswith("{")][0])
     assert out["ate"] == pytest.approx(ref["ate"], rel=1e-9)
     assert out["se"] == pytest.approx(ref["se"], rel=1e-9)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_dml_gbdt_bitwise_equals_single(world, tutorial):
+    """Config 5's algorithm on real gloo ranks: row-sharded DML-GBDT (global edge sample,
+    exact int64 histogram all-reduce per level, exact base and moments) returns the SAME
+    BITS as one process at world 2 and 4."""
+    script = r"""
+import os, sys, json
+sys.path.insert(0, %r)
+import numpy as np, torch, torch.distributed as dist
+dist.init_process_group("gloo")
+from ate_replication_causalml_amd.parallel.comm import TorchComm
+from ate_replication_causalml_amd.parallel.dist import DistContext
+from ate_replication_causalml_amd.data.dgp import make_tutorial_data
+from ate_replication_causalml_amd.data.selection import apply_selection_bias
+from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt
+c = TorchComm()
+m, _ = apply_selection_bias(make_tutorial_data(6000, 1991))
+d = DistContext.for_rank(c, len(m.Y))
+r = dml_plr_gbdt(d.local(m.Y), d.local(m.W), d.local(m.X), n_trees=5, depth=3, device="cpu", dist=d)
+allv = [None] * c.world_size
+dist.all_gather_object(allv, [r.ate.hex(), r.se.hex()])
+if c.rank == 0:
+    print("RESULT", json.dumps(allv), flush=True)
+dist.destroy_process_group()
+""" % ROOT
+    import json
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
+        f.write(script)
+        path = f.name
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+           f"--master-port={29561 + world}", path]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+    finally:
+        os.unlink(path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT")][0].split(" ", 1)[1])
+    assert len(got) == world
+    from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt
+    _, m, _ = tutorial
+    ref = dml_plr_gbdt(m.Y, m.W, m.X, n_trees=5, depth=3, device="cpu")
+    for a, s in got:                               # every rank, every bit
+        assert float.fromhex(a) == ref.ate and float.fromhex(s) == ref.se
