@@ -41,7 +41,7 @@ def test_cfg5_gbdt_two_ranks_on_one_gpu_bitwise(gpu):
     (gloo collectives): device edge sample, per-level int64 histogram all-reduce, exact
     moments -> the SAME BITS as one process holding all rows."""
     cfg5 = os.path.join(ROOT, "tools", "cfg5.py")
-    args = ["--n", "200000", "--p", "40", "--trees", "6", "--depth", "4"]
+    args = ["--rows", "200000", "--cols", "40", "--trees", "6", "--depth", "4"]
     env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29657",

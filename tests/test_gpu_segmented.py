@@ -110,7 +110,7 @@ def test_dist_estimators_single_graph_with_rccl(gpu, rccl):
             g = fn(True)
             assert g.diagnostics.get("hipgraph") is (rep > 0), (name, g.diagnostics)
             assert abs(g.ate - e.ate) < 1e-12, name
-            if e.se is not None:
+            if e.se is not None and e.se == e.se:        # LASSO rows have no SE (NaN)
                 assert abs(g.se - e.se) < 1e-12, name
 
 

@@ -1,9 +1,9 @@
 """BASELINE config 5 (DML-PLR with histogram-GBDT nuisances, N=1e8, p=2000, full panel
 resident across 8 x 288 GB HBM) as one rank per GPU.
 
-    python tools/cfg5.py --n 100000000 --p 2000 --trees 100            # 1 process: all rows
-    torchrun --nproc-per-node 8 tools/cfg5.py --n 100000000 ...       # rank r: its rows
-    python tools/cfg5.py --n 100000000 --shard 0/8                    # rank 0's share, alone
+    python tools/cfg5.py --rows 100000000 --cols 2000 --trees 100            # 1 process: all rows
+    torchrun --nproc-per-node 8 tools/cfg5.py --rows 100000000 ...  # rank r: its rows
+    python tools/cfg5.py --rows 100000000 --shard 0/8                    # rank 0's share, alone
 
 Each rank generates its slice of every fold directly in HBM (data/device_dgp, rows are a
 pure function of (seed, global row)), bins it on the device from the global edge sample and
@@ -44,8 +44,8 @@ class _ShardComm:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=float, default=1e6)
-    ap.add_argument("--p", type=int, default=100)
+    ap.add_argument("--rows", type=float, default=1e6)
+    ap.add_argument("--cols", type=int, default=100)
     ap.add_argument("--trees", type=int, default=100)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--folds", type=int, default=5)
@@ -58,7 +58,7 @@ def main():
     from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt_panel
     from ate_replication_causalml_amd.parallel import comm as C
     from ate_replication_causalml_amd.parallel.dist import DistContext
-    n = int(a.n)
+    n = int(a.rows)
     if a.shard:
         r, w = (int(v) for v in a.shard.split("/"))
         comm = _ShardComm(r, w)
@@ -68,7 +68,7 @@ def main():
     torch.cuda.set_device(C.local_device())
     dev = torch.device("cuda", torch.cuda.current_device())
     t0 = time.perf_counter()
-    pan = synthetic_panel(n, p=a.p, folds=a.folds, seed=a.seed, dtype="bf16", device=dev,
+    pan = synthetic_panel(n, p=a.cols, folds=a.folds, seed=a.seed, dtype="bf16", device=dev,
                           rank=rank, world=world)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
@@ -81,7 +81,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     r = dml_plr_gbdt_panel(pan, n_trees=a.trees, depth=a.depth, dist=dist, checkpoint=ck,
-                           data_key=f"synthetic.{n}.{a.p}.{a.seed}")
+                           data_key=f"synthetic.{n}.{a.cols}.{a.seed}")
     torch.cuda.synchronize()
     comm.barrier()
     secs = time.perf_counter() - t1
@@ -90,7 +90,7 @@ def main():
     if rank == 0:
         print(json.dumps({
             "config": 5, "estimator": "DML-PLR 5-fold, GBDT nuisances (E[Y|X], E[W|X]), HBM panel",
-            "rows_total": n, "rows_this_rank": pan.n, "p": a.p, "trees": a.trees,
+            "rows_total": n, "rows_this_rank": pan.n, "p": a.cols, "trees": a.trees,
             "depth": a.depth, "world": world, "shard": a.shard, "seconds": float(el.item()),
             "generate_s": t_gen, "rows_per_s": n / float(el.item()), "ate": r.ate, "se": r.se,
             "ate_hex": float(r.ate).hex(), "se_hex": float(r.se).hex()}), flush=True)
