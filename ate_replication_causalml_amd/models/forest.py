@@ -265,6 +265,19 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
                              sample_fraction=sample_fraction, seed=seed, tree_offset=tree_offset)
 
 
+LEVEL_MIN_ROWS = 1 << 17     # training rows from which the level engine grows a forest
+
+
+def use_level_engine(fp: ForestParams) -> bool:
+    """ATE_FOREST_ENGINE = "tree" (one workgroup per tree), "level" (GPU-wide level
+    steps; randomForest sampling only) or "auto" (level for >= LEVEL_MIN_ROWS rows)."""
+    from . import forest_level as LV
+    mode = os.environ.get("ATE_FOREST_ENGINE", "auto")
+    if mode == "tree" or not LV.supported(fp):
+        return False
+    return mode == "level" or fp.n >= LEVEL_MIN_ROWS
+
+
 def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None,
                       min_node=1, sampling=0, honesty=False, group=1, mtry_poisson=False,
                       alpha=0.0, sample_fraction=0.5, seed=1, tree_offset=0) -> Forest:
@@ -301,6 +314,13 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
         yt = t(y, torch.uint8)
         r1t, r2t = t(r1, torch.int64, True), t(r2, torch.int64, True)
         Xb = Xb.contiguous()
+        if use_level_engine(fp):
+            # large training sets: all trees grown together, level by level, across the
+            # whole GPU (csrc/forest_level.hip); same trees as the per-tree kernel
+            from . import forest_level as LV
+            cap, feat, thr, left, val, nnodes, inbag = LV.grow(Xb, fp, yt, r1t)
+            return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, None, edges, ne,
+                          Xb)
         feat = torch.empty(ntree * cap, dtype=torch.int32, device=dev)
         thr = torch.empty_like(feat)
         left = torch.empty_like(feat)

@@ -1,0 +1,158 @@
+"""Host driver of the level-synchronous forest engine (csrc/forest_level.hip).
+
+The GPU grows every tree of a forest together, one tree level per step; a node is decided
+by many workgroups (big), one workgroup (mid) or one wave (small) according to its size,
+so an 8e6-row bootstrap tree no longer lives on one CU (BASELINE config 3). Trees are the
+same bits as the one-workgroup-per-tree kernel and the host twin (forest_common.hpp spec):
+randomForest semantics, kinds 0 (classification) / 1 (regression), bootstrap sampling.
+
+Per level the host reads three small things to size the next launches: the node-class
+counts, the position ranges of the big nodes (their work items), and the next level's
+length. Everything else stays on the device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch
+
+from .. import _native
+from . import forest as F
+
+LV_FG = 8
+LV_MAXF = 64
+LV_PMAX = 512
+
+
+class LvHost(ctypes.Structure):
+    """Mirror of csrc/forest_level.hip::LvHost."""
+    P = ctypes.c_void_p
+    _fields_ = [("fp", F.ForestParams), ("Xb", P), ("ycls", P), ("r1", P), ("w", P), ("idx", P),
+                ("idx2", P), ("cur", P), ("dec", P), ("nl", P), ("cap", ctypes.c_int),
+                ("feat", P), ("thr", P), ("left", P), ("val", P), ("depth", ctypes.c_int)]
+
+
+def supported(fp: F.ForestParams) -> bool:
+    return (fp.kind in (F.KIND_CLASS, F.KIND_REG) and fp.sampling == 0 and not fp.mtry_poisson
+            and fp.p <= LV_PMAX and fp.mtry <= LV_MAXF and fp.ntree * fp.n < 2 ** 31 - 1)
+
+
+def _env_int(name, default):
+    v = os.environ.get(name)
+    return int(v) if v else default
+
+
+def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chunk=None,
+         stream=None):
+    """Grow fp.ntree trees on the device. Xb: [p][n] uint8 (cuda), yt: [n] uint8 (kind 0),
+    r1t: [n] int64 fixed point (kind 1). Returns (cap, feat, thr, left, val, nnodes, inbag)."""
+    dev = Xb.device
+    T, n, p = fp.ntree, fp.n, fp.p
+    big = big or _env_int("ATE_FOREST_LV_BIG", 8192)
+    chunk = chunk or _env_int("ATE_FOREST_LV_CH", 4096)
+    s = (stream or torch.cuda.current_stream(dev)).cuda_stream
+    i32 = dict(dtype=torch.int32, device=dev)
+    cap = 2 * n + 1
+    # ---- bootstrap counts, in-bag rows ascending per tree
+    w = torch.zeros(T * n, **i32)
+    _native.call("ate_lv_boot", ctypes.addressof(fp), w.data_ptr(), s)
+    wv = w.view(T, n)
+    inb = wv > 0
+    inbag = inb.to(torch.uint8).reshape(-1)
+    m = inb.sum(1)                                           # in-bag rows per tree
+    nz = torch.nonzero(inb)                                  # (t, i), t-major, i ascending
+    m_h = m.cpu().numpy().astype(np.int64)
+    start = torch.as_tensor(np.concatenate([[0], np.cumsum(m_h)[:-1]]), device=dev)
+    dest = nz[:, 0] * n + (torch.arange(nz.shape[0], device=dev) - start[nz[:, 0]])
+    idx = torch.zeros(T * n, **i32)
+    idx[dest] = nz[:, 1].to(torch.int32)
+    idx2 = torch.zeros_like(idx)
+    del nz, dest
+    # ---- outputs
+    feat = torch.zeros(T * cap, **i32)
+    thr = torch.zeros(T * cap, **i32)
+    left = torch.zeros(T * cap, **i32)
+    val = torch.zeros(T * cap, dtype=torch.float64, device=dev)
+    next_id = torch.ones(T, **i32)
+    # ---- level lists (capacity: every node holds >= 1 in-bag position)
+    lcap = int(m_h.sum()) + T
+    cur = torch.zeros((lcap, 4), **i32)
+    nxt = torch.zeros((lcap, 4), **i32)
+    tt = torch.arange(T, **i32)
+    root = torch.stack([tt, tt * n, tt * n + m.to(torch.int32), torch.zeros_like(tt)], 1)
+    keep = m > 0
+    root = root[keep]
+    ncur = int(root.shape[0])
+    cur[:ncur] = root
+    dec = torch.zeros((lcap, 4), **i32)
+    nl = torch.zeros(lcap, **i32)
+    brank = torch.zeros(T, **i32)
+    counts = torch.zeros(3, **i32)
+    nf_max = min(fp.mtry, p)
+    ngroups = -(-nf_max // LV_FG)
+    hist = None
+    h = LvHost(fp=fp, Xb=Xb.data_ptr(), ycls=yt.data_ptr() if yt is not None else None,
+               r1=r1t.data_ptr() if r1t is not None else None, w=w.data_ptr(), cap=cap,
+               feat=feat.data_ptr(), thr=thr.data_ptr(), left=left.data_ptr(),
+               val=val.data_ptr())
+    depth = 0
+    while ncur > 0:
+        h.idx, h.idx2 = idx.data_ptr(), idx2.data_ptr()
+        h.cur, h.dec, h.nl = cur.data_ptr(), dec.data_ptr(), nl.data_ptr()
+        h.depth = depth
+        lists = torch.empty(3 * ncur, **i32)
+        counts.zero_()
+        _native.call("ate_lv_classify", cur.data_ptr(), ncur, big, lists.data_ptr(),
+                     counts.data_ptr(), s)
+        nsmall, nmid, nbig = (int(v) for v in counts.cpu())
+        items = (None, None, None)
+        nitems = 0
+        drawn = nfo = None
+        if nbig:
+            bl = lists[2 * ncur:2 * ncur + nbig].long()
+            lohi = cur.index_select(0, bl)[:, 1:3].cpu().numpy().astype(np.int64)
+            lens = lohi[:, 1] - lohi[:, 0]
+            per = -(-lens // chunk)
+            slot = np.repeat(np.arange(nbig), per)
+            first = np.repeat(np.concatenate([[0], np.cumsum(per)[:-1]]), per)
+            q0 = lohi[slot, 0] + (np.arange(len(slot)) - first) * chunk
+            q1 = np.minimum(q0 + chunk, lohi[slot, 1])
+            nitems = len(slot)
+            items = tuple(torch.as_tensor(a.astype(np.int32), device=dev) for a in (slot, q0, q1))
+            drawn = torch.empty(nbig * LV_MAXF, dtype=torch.int16, device=dev)
+            nfo = torch.empty(nbig, **i32)
+            need = nbig * nf_max * 2 * F.MAX_BINS
+            if hist is None or hist.numel() < need:
+                hist = torch.empty(need, dtype=torch.int64, device=dev)
+            hist[:need].zero_()
+        P = lambda t: t.data_ptr() if t is not None else None
+        _native.call("ate_lv_decide", ctypes.addressof(h), lists.data_ptr(), ncur, nsmall, nmid,
+                     nbig, P(drawn), P(nfo), P(items[0]), P(items[1]), P(items[2]), nitems,
+                     ngroups, P(hist), nf_max, s)
+        icnt = torch.empty(max(nitems, 1), **i32)
+        _native.call("ate_lv_partition", ctypes.addressof(h), lists.data_ptr(), ncur, nsmall, nmid,
+                     nbig, P(items[0]), P(items[1]), P(items[2]), nitems, icnt.data_ptr(), s)
+        if nbig:
+            ic = icnt[:nitems].long()
+            slot_t = items[0].long()
+            csum = torch.cumsum(ic, 0) - ic                                   # exclusive
+            firsts = torch.as_tensor(np.concatenate([[0], np.cumsum(per)[:-1]]), device=dev)
+            ipre = (csum - csum.index_select(0, firsts).index_select(0, slot_t)).to(torch.int32)
+            nlb = torch.zeros(nbig, dtype=torch.int64, device=dev).index_add_(0, slot_t, ic)
+            nlb32 = nlb.to(torch.int32)
+            nl.index_copy_(0, bl, nlb32)
+            _native.call("ate_lv_scatter", ctypes.addressof(h), lists.data_ptr(), ncur,
+                         P(items[0]), P(items[1]), P(items[2]), nitems, ipre.data_ptr(),
+                         nlb32.data_ptr(), s)
+        flags = dec[:ncur, 0]
+        excl = (torch.cumsum(flags, 0, dtype=torch.int32) - flags).contiguous()
+        total = int((excl[ncur - 1] + flags[ncur - 1]).item())
+        _native.call("ate_lv_children", ctypes.addressof(h), ncur, excl.data_ptr(),
+                     brank.data_ptr(), next_id.data_ptr(), nxt.data_ptr(), s)
+        cur, nxt = nxt, cur
+        idx, idx2 = idx2, idx
+        ncur = 2 * total
+        depth += 1
+    return cap, feat, thr, left, val, next_id, inbag

@@ -1,9 +1,11 @@
 """Forest engine (models/forest.py, csrc/cpu/forest_cpu.cpp) on the host.
 
-R's randomForest/grf are not importable here, so parity with them is "unpinned":
+R's randomForest/grf are not importable here, so exact parity with them is "unpinned":
 these tests pin the engine's own contracts (determinism, thread-count invariance,
-tree well-formedness, statistical sanity on signals with a known answer). The GPU
-twin is checked against this host engine bit-for-bit in tests/test_gpu.py.
+tree well-formedness, statistical sanity on signals with a known answer) and compare it
+statistically with an INDEPENDENT implementation of the same Breiman semantics
+(scikit-learn's RandomForestClassifier / Regressor). The GPU twins are checked against
+this host engine bit-for-bit in tests/test_forest_gpu.py.
 """
 import numpy as np
 import pytest
@@ -132,3 +134,50 @@ def test_causal_forest_heterogeneous_effect():
     assert np.corrcoef(t[ok], tau[ok])[0, 1] > 0.6
     assert np.all(cf.var_oob[ok] >= 0)
     assert 0.01 < np.sqrt(np.nanmean(cf.var_oob)) < 2.0
+
+
+def test_rf_oob_propensity_matches_sklearn_statistically():
+    """Independent cross-check of the randomForest semantics (ate_functions.R:169-174:
+    bootstrap, mtry = floor(sqrt(p)), Gini, fully grown, OOB vote shares) against
+    scikit-learn's RandomForestClassifier with the same settings on the tutorial DGP's
+    selection-biased sample. Exact parity is impossible (different RNG, 256-bin vs exact
+    thresholds); the OOB propensities must agree in distribution, discrimination (AUC)
+    and calibration (Brier) within Monte Carlo error, and row by row (correlation)."""
+    from sklearn.ensemble import RandomForestClassifier
+    from sklearn.metrics import roc_auc_score
+    from ate_replication_causalml_amd.data.dgp import make_tutorial_data
+    from ate_replication_causalml_amd.data.selection import apply_selection_bias
+    m, _ = apply_selection_bias(make_tutorial_data(30000, seed=1991))
+    X, W = m.X, m.W
+    ours = F.rf_classifier(X, W, num_trees=500, seed=7, backend="cpu").oob_proba()
+    sk = RandomForestClassifier(n_estimators=500, max_features="sqrt", bootstrap=True,
+                                min_samples_leaf=1, oob_score=True, random_state=0,
+                                n_jobs=4).fit(X, W).oob_decision_function_[:, 1]
+    ok = ~np.isnan(ours) & ~np.isnan(sk)
+    assert ok.mean() > 0.99
+    a, b, w = ours[ok], sk[ok], W[ok]
+    assert abs(a.mean() - b.mean()) < 0.01
+    assert abs(a.std() - b.std()) < 0.015
+    assert abs(roc_auc_score(w, a) - roc_auc_score(w, b)) < 0.015
+    assert abs(np.mean((a - w) ** 2) - np.mean((b - w) ** 2)) < 0.005
+    assert np.corrcoef(a, b)[0, 1] > 0.93
+    np.testing.assert_allclose(np.quantile(a, [0.1, 0.5, 0.9]), np.quantile(b, [0.1, 0.5, 0.9]),
+                               atol=0.02)
+
+
+def test_rf_regressor_matches_sklearn_statistically():
+    """Breiman regression forest (variance-reduction splits, leaf means, mtry = p/3)
+    against scikit-learn's RandomForestRegressor: held-out R^2 and the predictions agree."""
+    from sklearn.ensemble import RandomForestRegressor
+    r = np.random.default_rng(3)
+    n, p = 4000, 9
+    X = r.normal(size=(n, p))
+    y = np.sin(2 * X[:, 0]) + X[:, 1] * (X[:, 2] > 0) + 0.3 * r.normal(size=n)
+    Xt = r.normal(size=(2000, p))
+    yt = np.sin(2 * Xt[:, 0]) + Xt[:, 1] * (Xt[:, 2] > 0)
+    ours = F.rf_regressor(X, y, num_trees=300, seed=4, backend="cpu").predict_proba(Xt)
+    sk = RandomForestRegressor(n_estimators=300, max_features=1 / 3, min_samples_split=6,
+                               random_state=0, n_jobs=4).fit(X, y).predict(Xt)
+    r2 = lambda f: 1 - np.mean((f - yt) ** 2) / np.var(yt)
+    assert abs(r2(ours) - r2(sk)) < 0.03 and r2(ours) > 0.7
+    assert np.corrcoef(ours, sk)[0, 1] > 0.97

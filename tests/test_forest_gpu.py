@@ -102,3 +102,44 @@ def test_aipw_rf_crossfit_panel_matches_host_engine(gpu):
     # a tree shard of the same forests (rank 1 of 3) is a different, smaller ensemble
     c = aipw_rf_crossfit_panel(pan, num_trees=24, seed=3, tree_shard=(1, 3))
     assert c.diagnostics["trees_this_device"] == 8
+
+
+@pytest.mark.parametrize("big,chunk", [(8192, 4096), (300, 128), (65, 64)])
+@pytest.mark.parametrize("case", ["rf_class", "rf_reg"])
+def test_level_engine_bit_identical_to_host(gpu, case, big, chunk, monkeypatch):
+    """The level-synchronous engine (csrc/forest_level.hip: all trees level by level, big
+    nodes over many workgroups, mid nodes a workgroup, small nodes a wave) grows the host
+    engine's trees bit for bit. Small thresholds push most nodes through the big /
+    chunked-partition path."""
+    monkeypatch.setenv("ATE_FOREST_ENGINE", "level")
+    monkeypatch.setenv("ATE_FOREST_LV_BIG", str(big))
+    monkeypatch.setenv("ATE_FOREST_LV_CH", str(chunk))
+    X, W, Y = _data(6000)
+    kw = dict(ntree=12, seed=23)
+    if case == "rf_class":
+        kw.update(kind=F.KIND_CLASS, y=W, mtry=3)
+    else:
+        kw.update(kind=F.KIND_REG, r1=Y, mtry=3, min_node=5)
+    g = F.fit_forest(X, backend="gpu", **kw)
+    c = F.fit_forest(X, backend="cpu", **kw)
+    assert_same_forest(g, c)
+    np.testing.assert_array_equal(_np(g.inbag), _np(c.inbag))
+    np.testing.assert_array_equal(g.oob_proba(), c.oob_proba())
+
+
+def test_level_engine_wide_many_features(gpu, monkeypatch):
+    """p = 120, mtry = 10 (two feature groups per histogram pass), trees with > 60 levels
+    of nodes: same trees as the per-tree kernel."""
+    monkeypatch.setenv("ATE_FOREST_LV_BIG", "512")
+    monkeypatch.setenv("ATE_FOREST_LV_CH", "256")
+    r = np.random.default_rng(8)
+    n, p = 20000, 120
+    X = r.normal(size=(n, p))
+    X[:, 5] = np.round(X[:, 5])
+    W = (r.uniform(size=n) < 1 / (1 + np.exp(-X[:, 0] - X[:, 7] * X[:, 9]))).astype(float)
+    kw = dict(kind=F.KIND_CLASS, y=W, ntree=6, seed=5, mtry=10)
+    monkeypatch.setenv("ATE_FOREST_ENGINE", "level")
+    g = F.fit_forest(X, backend="gpu", **kw)
+    monkeypatch.setenv("ATE_FOREST_ENGINE", "tree")
+    t = F.fit_forest(X, backend="gpu", **kw)
+    assert_same_forest(g, t)
