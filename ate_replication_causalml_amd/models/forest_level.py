@@ -50,7 +50,7 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     r1t: [n] int64 fixed point (kind 1). Returns (cap, feat, thr, left, val, nnodes, inbag)."""
     dev = Xb.device
     T, n, p = fp.ntree, fp.n, fp.p
-    big = big or _env_int("ATE_FOREST_LV_BIG", 8192)
+    big = min(big or _env_int("ATE_FOREST_LV_BIG", 8192), 8192)   # mid partition: <= 8192 rows
     chunk = chunk or _env_int("ATE_FOREST_LV_CH", 4096)
     s = (stream or torch.cuda.current_stream(dev)).cuda_stream
     i32 = dict(dtype=torch.int32, device=dev)

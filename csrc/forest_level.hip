@@ -187,6 +187,52 @@ struct LvArgs {
   int depth;
 };
 
+
+// accumulate rows [q0, q1) (stride 256 per thread, 4 rows per thread in flight: the idx
+// loads, then every row's weight / label / LV_FG bins, then the LDS atomics) into the LDS
+// histograms sh[k][c][bin] of the nk features xf[0..nk)
+__device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __restrict__ wt,
+                                              const uint8_t* const* xf, int nk, int q0, int q1,
+                                              int64_t (*sh)[2][NBINS]) {
+  constexpr int U = 4;
+  const int kind = a.fp.kind;
+  for (int base = q0 + threadIdx.x; base < q1; base += 256 * U) {
+    int ii[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = base + u * 256;
+      ii[u] = q < q1 ? a.idx[q] : -1;
+    }
+    int64_t wv[U], rv[U];
+    int yv[U];
+    int bins[U][LV_FG];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = ii[u] < 0 ? 0 : ii[u];
+      wv[u] = ii[u] < 0 ? 0 : wt[i];
+      yv[u] = kind == 0 ? a.ycls[i] : 0;
+      rv[u] = kind == 0 ? 0 : a.r1[i];
+#pragma unroll
+      for (int k = 0; k < LV_FG; ++k) bins[u][k] = xf[k][i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ii[u] < 0) continue;
+#pragma unroll
+      for (int k = 0; k < LV_FG; ++k) {
+        if (k >= nk) break;
+        if (kind == 0) {
+          atomicAdd((unsigned long long*)&sh[k][yv[u]][bins[u][k]], (unsigned long long)wv[u]);
+        } else {
+          atomicAdd((unsigned long long*)&sh[k][0][bins[u][k]], (unsigned long long)wv[u]);
+          atomicAdd((unsigned long long*)&sh[k][1][bins[u][k]],
+                    (unsigned long long)(wv[u] * rv[u]));
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ sampling (K10)
 __global__ __launch_bounds__(256) void lv_boot_kernel(ForestParams fp, int32_t* __restrict__ w) {
   const int t = blockIdx.y;
@@ -251,27 +297,7 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   for (int k = 0; k < LV_FG; ++k)
     xf[k] = a.Xb + (int64_t)drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)] * n;
   __syncthreads();
-  const int q1 = item_q1[it];
-  for (int q = item_q0[it] + threadIdx.x; q < q1; q += 256) {
-    const int i = a.idx[q];
-    const int64_t wi = wt[i];
-    int yi = 0;
-    int64_t ri = 0;
-    if (a.fp.kind == 0) yi = a.ycls[i]; else ri = a.r1[i];
-    int bins[LV_FG];
-#pragma unroll
-    for (int k = 0; k < LV_FG; ++k) bins[k] = xf[k][i];
-#pragma unroll
-    for (int k = 0; k < LV_FG; ++k) {
-      if (k >= nk) break;
-      if (a.fp.kind == 0) {
-        atomicAdd((unsigned long long*)&sh[k][yi][bins[k]], (unsigned long long)wi);
-      } else {
-        atomicAdd((unsigned long long*)&sh[k][0][bins[k]], (unsigned long long)wi);
-        atomicAdd((unsigned long long*)&sh[k][1][bins[k]], (unsigned long long)(wi * ri));
-      }
-    }
-  }
+  lv_accumulate(a, wt, xf, nk, item_q0[it], item_q1[it], sh);
   __syncthreads();
   int64_t* hs = hist + ((int64_t)slot * fs + k0) * 2 * NBINS;
   for (int e = threadIdx.x; e < nk * 2 * NBINS; e += 256) {
@@ -375,26 +401,7 @@ __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __
 #pragma unroll
     for (int k = 0; k < LV_FG; ++k) xf[k] = a.Xb + (int64_t)perm[k0 + min(k, nk - 1)] * n;
     __syncthreads();
-    for (int q = nd.lo + threadIdx.x; q < nd.hi; q += 256) {
-      const int i = a.idx[q];
-      const int64_t wi = wt[i];
-      int yi = 0;
-      int64_t ri = 0;
-      if (kind == 0) yi = a.ycls[i]; else ri = a.r1[i];
-      int bins[LV_FG];
-#pragma unroll
-      for (int k = 0; k < LV_FG; ++k) bins[k] = xf[k][i];
-#pragma unroll
-      for (int k = 0; k < LV_FG; ++k) {
-        if (k >= nk) break;
-        if (kind == 0) {
-          atomicAdd((unsigned long long*)&sh[k][yi][bins[k]], (unsigned long long)wi);
-        } else {
-          atomicAdd((unsigned long long*)&sh[k][0][bins[k]], (unsigned long long)wi);
-          atomicAdd((unsigned long long*)&sh[k][1][bins[k]], (unsigned long long)(wi * ri));
-        }
-      }
-    }
+    lv_accumulate(a, wt, xf, nk, nd.lo, nd.hi, sh);
     __syncthreads();
     if (k0 == 0) {
       if (wid == 0) {
@@ -542,9 +549,14 @@ __global__ __launch_bounds__(256) void lv_small_kernel(LvArgs a, const int32_t* 
 }
 
 // ------------------------------------------------------------------ partition
-// one wave per split node of a list (small / mid): stable ballot compaction into idx2
+// one wave per split node of a list (small / mid): stable ballot compaction into idx2.
+// Pass 1 gathers the split feature's bins (4 x 64 rows in flight) and keeps each 64-row
+// block's left mask in LDS; pass 2 re-reads only the positions and writes both sides.
+constexpr int LV_PART_BLK = 8192 / 64;      // mask blocks per wave (mid nodes <= 8192 rows)
+
 __global__ __launch_bounds__(256) void lv_part_wave_kernel(LvArgs a, const int32_t* __restrict__ list,
                                                            int cnt) {
+  __shared__ uint64_t masks[4][LV_PART_BLK];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int s = blockIdx.x * 4 + wid;
   if (s >= cnt) return;
@@ -553,21 +565,46 @@ __global__ __launch_bounds__(256) void lv_part_wave_kernel(LvArgs a, const int32
   if (!d.x) return;
   const LNode nd = a.cur[j];
   const uint8_t* xf = a.Xb + (int64_t)d.y * a.fp.n;
-  int cl = 0;
-  for (int q0 = nd.lo; q0 < nd.hi; q0 += 64) {
-    const int q = q0 + lane;
-    const bool gl = q < nd.hi && xf[a.idx[q]] <= d.z;
-    const uint64_t bl = __ballot(gl);
-    if (gl) a.idx2[nd.lo + cl + __popcll(bl & ((1ull << lane) - 1ull))] = a.idx[q];
-    cl += __popcll(bl);
+  const int m = nd.hi - nd.lo;
+  const int nblk = (m + 63) / 64;
+  if (nblk > LV_PART_BLK) {                                 // (not reached: mid <= LV_BIG)
+    if (lane == 0) a.nl[j] = -1;
+    return;
   }
-  int cr = 0;
-  for (int q0 = nd.lo; q0 < nd.hi; q0 += 64) {
-    const int q = q0 + lane;
-    const bool gr = q < nd.hi && xf[a.idx[q]] > d.z;
-    const uint64_t br = __ballot(gr);
-    if (gr) a.idx2[nd.lo + cl + cr + __popcll(br & ((1ull << lane) - 1ull))] = a.idx[q];
-    cr += __popcll(br);
+  const uint64_t below = (1ull << lane) - 1ull;
+  int cl = 0;
+  for (int b0 = 0; b0 < nblk; b0 += 4) {
+    int ii[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = nd.lo + (b0 + u) * 64 + lane;
+      ii[u] = q < nd.hi ? a.idx[q] : -1;
+    }
+    int bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bv[u] = ii[u] < 0 ? 0 : xf[ii[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (b0 + u >= nblk) break;
+      const uint64_t bl = __ballot(ii[u] >= 0 && bv[u] <= d.z);
+      if (lane == 0) masks[wid][b0 + u] = bl;
+      cl += __popcll(bl);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  int lb = 0;                                               // lefts before this block
+  for (int b = 0; b < nblk; ++b) {
+    const int q = nd.lo + b * 64 + lane;
+    const uint64_t bl = masks[wid][b];
+    if (q < nd.hi) {
+      const int i = a.idx[q];
+      const bool gl = (bl >> lane) & 1ull;
+      const int l = lb + __popcll(bl & below);
+      if (gl) a.idx2[nd.lo + l] = i;
+      else a.idx2[nd.lo + cl + (b * 64 + lane - l)] = i;
+    }
+    lb += __popcll(bl);
   }
   if (lane == 0) a.nl[j] = cl;
 }
