@@ -31,7 +31,8 @@ class LvHost(ctypes.Structure):
     P = ctypes.c_void_p
     _fields_ = [("fp", F.ForestParams), ("Xb", P), ("ycls", P), ("r1", P), ("w", P), ("idx", P),
                 ("idx2", P), ("cur", P), ("dec", P), ("nl", P), ("cap", ctypes.c_int),
-                ("feat", P), ("thr", P), ("left", P), ("val", P), ("depth", ctypes.c_int)]
+                ("feat", P), ("thr", P), ("left", P), ("val", P), ("depth", ctypes.c_int),
+                ("fst", ctypes.c_int64), ("rst", ctypes.c_int64)]
 
 
 def supported(fp: F.ForestParams) -> bool:
@@ -52,6 +53,7 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     T, n, p = fp.ntree, fp.n, fp.p
     big = min(big or _env_int("ATE_FOREST_LV_BIG", 8192), 8192)   # mid partition: <= 8192 rows
     chunk = chunk or _env_int("ATE_FOREST_LV_CH", 4096)
+    items_target = _env_int("ATE_FOREST_LV_ITEMS", 2048)
     s = (stream or torch.cuda.current_stream(dev)).cuda_stream
     i32 = dict(dtype=torch.int32, device=dev)
     cap = 2 * n + 1
@@ -93,12 +95,38 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     nf_max = min(fp.mtry, p)
     ngroups = -(-nf_max // LV_FG)
     hist = None
-    h = LvHost(fp=fp, Xb=Xb.data_ptr(), ycls=yt.data_ptr() if yt is not None else None,
+    # Row-major bins for the growth: a node's rows are scattered over the n positions, so
+    # each (row, feature) gather of a column-major [p][n] matrix touches its own cache
+    # line; in a row-major [n][p] copy a row's drawn features share that row's few lines
+    # (22 of 500 bytes: ~4 lines instead of 22). One transpose (n x p bytes) per forest.
+    if os.environ.get("ATE_FOREST_LV_LAYOUT", "row") == "row":
+        Xg = Xb.t().contiguous()
+        fst, rst = 1, p
+    else:
+        Xg, fst, rst = Xb, n, 1
+    h = LvHost(fp=fp, Xb=Xg.data_ptr(), ycls=yt.data_ptr() if yt is not None else None,
                r1=r1t.data_ptr() if r1t is not None else None, w=w.data_ptr(), cap=cap,
                feat=feat.data_ptr(), thr=thr.data_ptr(), left=left.data_ptr(),
-               val=val.data_ptr())
+               val=val.data_ptr(), fst=fst, rst=rst)
+    prof = os.environ.get("ATE_FOREST_LV_PROF") == "1"
+    if prof:
+        import time
+        tp = {"classify": 0.0, "decide": 0.0, "partition": 0.0, "children": 0.0}
+        lv_rows = []
+        torch.cuda.current_stream(dev).synchronize()
+        t_all = time.perf_counter()
+
+    def tick(name, t0):
+        if not prof:
+            return None
+        torch.cuda.current_stream(dev).synchronize()
+        t1 = time.perf_counter()
+        if name:
+            tp[name] += t1 - t0
+        return t1
     depth = 0
     while ncur > 0:
+        t0 = tick(None, None)
         h.idx, h.idx2 = idx.data_ptr(), idx2.data_ptr()
         h.cur, h.dec, h.nl = cur.data_ptr(), dec.data_ptr(), nl.data_ptr()
         h.depth = depth
@@ -107,6 +135,7 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         _native.call("ate_lv_classify", cur.data_ptr(), ncur, big, lists.data_ptr(),
                      counts.data_ptr(), s)
         nsmall, nmid, nbig = (int(v) for v in counts.cpu())
+        t0 = tick("classify", t0) if prof else None
         items = (None, None, None)
         nitems = 0
         drawn = nfo = None
@@ -114,11 +143,14 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
             bl = lists[2 * ncur:2 * ncur + nbig].long()
             lohi = cur.index_select(0, bl)[:, 1:3].cpu().numpy().astype(np.int64)
             lens = lohi[:, 1] - lohi[:, 0]
-            per = -(-lens // chunk)
+            # items: ~ITEMS per level (every item's histogram is added to its node's with
+            # global atomics, so many small items of one node contend on the same lines)
+            ch = max(chunk, -(-int(lens.sum()) // items_target) // 256 * 256 + 256)
+            per = -(-lens // ch)
             slot = np.repeat(np.arange(nbig), per)
             first = np.repeat(np.concatenate([[0], np.cumsum(per)[:-1]]), per)
-            q0 = lohi[slot, 0] + (np.arange(len(slot)) - first) * chunk
-            q1 = np.minimum(q0 + chunk, lohi[slot, 1])
+            q0 = lohi[slot, 0] + (np.arange(len(slot)) - first) * ch
+            q1 = np.minimum(q0 + ch, lohi[slot, 1])
             nitems = len(slot)
             items = tuple(torch.as_tensor(a.astype(np.int32), device=dev) for a in (slot, q0, q1))
             drawn = torch.empty(nbig * LV_MAXF, dtype=torch.int16, device=dev)
@@ -131,6 +163,10 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         _native.call("ate_lv_decide", ctypes.addressof(h), lists.data_ptr(), ncur, nsmall, nmid,
                      nbig, P(drawn), P(nfo), P(items[0]), P(items[1]), P(items[2]), nitems,
                      ngroups, P(hist), nf_max, s)
+        if prof:
+            td = tick("decide", t0)
+            lv_rows.append((depth, ncur, nsmall, nmid, nbig, nitems, td - t0))
+            t0 = td
         icnt = torch.empty(max(nitems, 1), **i32)
         _native.call("ate_lv_partition", ctypes.addressof(h), lists.data_ptr(), ncur, nsmall, nmid,
                      nbig, P(items[0]), P(items[1]), P(items[2]), nitems, icnt.data_ptr(), s)
@@ -146,13 +182,25 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
             _native.call("ate_lv_scatter", ctypes.addressof(h), lists.data_ptr(), ncur,
                          P(items[0]), P(items[1]), P(items[2]), nitems, ipre.data_ptr(),
                          nlb32.data_ptr(), s)
+        t0 = tick("partition", t0) if prof else None
         flags = dec[:ncur, 0]
         excl = (torch.cumsum(flags, 0, dtype=torch.int32) - flags).contiguous()
         total = int((excl[ncur - 1] + flags[ncur - 1]).item())
         _native.call("ate_lv_children", ctypes.addressof(h), ncur, excl.data_ptr(),
                      brank.data_ptr(), next_id.data_ptr(), nxt.data_ptr(), s)
+        if prof:
+            tick("children", t0)
         cur, nxt = nxt, cur
         idx, idx2 = idx2, idx
         ncur = 2 * total
         depth += 1
+    if prof:
+        import sys
+        tot = time.perf_counter() - t_all
+        top = sorted(lv_rows, key=lambda r: -r[-1])[:6]
+        print(f"[forest_level] T={T} n={n} levels={depth} {tot:.3f}s "
+              + " ".join(f"{k}={v:.3f}" for k, v in tp.items())
+              + " slowest decide levels (depth,ncur,small,mid,big,items,s): "
+              + "; ".join(f"{r[0]},{r[1]},{r[2]},{r[3]},{r[4]},{r[5]},{r[6]:.3f}" for r in top),
+              file=sys.stderr, flush=True)
     return cap, feat, thr, left, val, next_id, inbag

@@ -170,7 +170,7 @@ __device__ __forceinline__ bool lv_accept(double best, double parent) {
 
 struct LvArgs {
   ForestParams fp;
-  const uint8_t* Xb;      // [p][n] bins (column-major)
+  const uint8_t* Xb;      // bins: element (feature f, row i) at f * fst + i * rst
   const uint8_t* ycls;    // kind 0: [n] class
   const int64_t* r1;      // kind 1: [n] response, 2^-32 fixed point
   const int32_t* w;       // [T][n] bootstrap counts
@@ -185,6 +185,7 @@ struct LvArgs {
   int32_t* left;
   double* val;
   int depth;
+  int64_t fst, rst;       // column-major [p][n]: (n, 1); row-major [n][p]: (1, p)
 };
 
 
@@ -213,7 +214,7 @@ __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __
       yv[u] = kind == 0 ? a.ycls[i] : 0;
       rv[u] = kind == 0 ? 0 : a.r1[i];
 #pragma unroll
-      for (int k = 0; k < LV_FG; ++k) bins[u][k] = xf[k][i];
+      for (int k = 0; k < LV_FG; ++k) bins[u][k] = xf[k][(int64_t)i * a.rst];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   const uint8_t* xf[LV_FG];
 #pragma unroll
   for (int k = 0; k < LV_FG; ++k)
-    xf[k] = a.Xb + (int64_t)drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)] * n;
+    xf[k] = a.Xb + (int64_t)drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)] * a.fst;
   __syncthreads();
   lv_accumulate(a, wt, xf, nk, item_q0[it], item_q1[it], sh);
   __syncthreads();
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __
     for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
     const uint8_t* xf[LV_FG];
 #pragma unroll
-    for (int k = 0; k < LV_FG; ++k) xf[k] = a.Xb + (int64_t)perm[k0 + min(k, nk - 1)] * n;
+    for (int k = 0; k < LV_FG; ++k) xf[k] = a.Xb + (int64_t)perm[k0 + min(k, nk - 1)] * a.fst;
     __syncthreads();
     lv_accumulate(a, wt, xf, nk, nd.lo, nd.hi, sh);
     __syncthreads();
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(256) void lv_small_kernel(LvArgs a, const int32_t* 
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int k = k0 + u;
-      bins[u] = (valid && k < nf) ? (int)a.Xb[(int64_t)perm[wid][k] * n + ci] : 0;
+      bins[u] = (valid && k < nf) ? (int)a.Xb[(int64_t)perm[wid][k] * a.fst + (int64_t)ci * a.rst] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(256) void lv_part_wave_kernel(LvArgs a, const int32
   const int4 d = a.dec[j];
   if (!d.x) return;
   const LNode nd = a.cur[j];
-  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fp.n;
+  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fst;
   const int m = nd.hi - nd.lo;
   const int nblk = (m + 63) / 64;
   if (nblk > LV_PART_BLK) {                                 // (not reached: mid <= LV_BIG)
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(256) void lv_part_wave_kernel(LvArgs a, const int32
     }
     int bv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) bv[u] = ii[u] < 0 ? 0 : xf[ii[u]];
+    for (int u = 0; u < 4; ++u) bv[u] = ii[u] < 0 ? 0 : xf[(int64_t)ii[u] * a.rst];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (b0 + u >= nblk) break;
@@ -623,9 +624,10 @@ __global__ __launch_bounds__(256) void lv_part_count_kernel(LvArgs a, const int3
     if (threadIdx.x == 0) icnt[it] = 0;
     return;
   }
-  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fp.n;
+  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fst;
   int c = 0;
-  for (int q = item_q0[it] + threadIdx.x; q < item_q1[it]; q += 256) c += xf[a.idx[q]] <= d.z;
+  for (int q = item_q0[it] + threadIdx.x; q < item_q1[it]; q += 256)
+    c += xf[(int64_t)a.idx[q] * a.rst] <= d.z;
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
   __syncthreads();
@@ -647,7 +649,7 @@ __global__ __launch_bounds__(256) void lv_part_scatter_kernel(LvArgs a, const in
   const int4 d = a.dec[j];
   if (!d.x) return;
   const LNode nd = a.cur[j];
-  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fp.n;
+  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fst;
   const int nlt = nlb[slot];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int run = ipre[it];                                       // lefts before this tile
@@ -658,7 +660,7 @@ __global__ __launch_bounds__(256) void lv_part_scatter_kernel(LvArgs a, const in
     bool gl = false;
     if (q < q1) {
       i = a.idx[q];
-      gl = xf[i] <= d.z;
+      gl = xf[(int64_t)i * a.rst] <= d.z;
     }
     const uint64_t bl = __ballot(gl);
     const int wl = __popcll(bl);
@@ -736,6 +738,7 @@ struct LvHost {
   int cap;
   void *feat, *thr, *left, *val;
   int depth;
+  int64_t fst, rst;
 };
 
 static LvArgs lv_args(const LvHost& h) {
@@ -756,6 +759,8 @@ static LvArgs lv_args(const LvHost& h) {
   a.left = (int32_t*)h.left;
   a.val = (double*)h.val;
   a.depth = h.depth;
+  a.fst = h.fst;
+  a.rst = h.rst;
   return a;
 }
 

@@ -104,9 +104,10 @@ def test_aipw_rf_crossfit_panel_matches_host_engine(gpu):
     assert c.diagnostics["trees_this_device"] == 8
 
 
+@pytest.mark.parametrize("layout", ["row", "col"])
 @pytest.mark.parametrize("big,chunk", [(8192, 4096), (300, 128), (65, 64)])
 @pytest.mark.parametrize("case", ["rf_class", "rf_reg"])
-def test_level_engine_bit_identical_to_host(gpu, case, big, chunk, monkeypatch):
+def test_level_engine_bit_identical_to_host(gpu, case, big, chunk, layout, monkeypatch):
     """The level-synchronous engine (csrc/forest_level.hip: all trees level by level, big
     nodes over many workgroups, mid nodes a workgroup, small nodes a wave) grows the host
     engine's trees bit for bit. Small thresholds push most nodes through the big /
@@ -114,6 +115,8 @@ def test_level_engine_bit_identical_to_host(gpu, case, big, chunk, monkeypatch):
     monkeypatch.setenv("ATE_FOREST_ENGINE", "level")
     monkeypatch.setenv("ATE_FOREST_LV_BIG", str(big))
     monkeypatch.setenv("ATE_FOREST_LV_CH", str(chunk))
+    monkeypatch.setenv("ATE_FOREST_LV_ITEMS", "100000")   # keep the small chunks
+    monkeypatch.setenv("ATE_FOREST_LV_LAYOUT", layout)
     X, W, Y = _data(6000)
     kw = dict(ntree=12, seed=23)
     if case == "rf_class":

@@ -51,6 +51,9 @@ def main():
                          "aipw_rf_crossfit_panel; use --n3 10000000 --p3 500 --shard3 0/8 for "
                          "the per-GPU work of the 8-GPU config)")
     ap.add_argument("--shard3", default=None, help="rank/world tree shard on this device")
+    ap.add_argument("--serial3", action="store_true",
+                    help="config 3: grow the 15 forests one after another (each fills the GPU "
+                         "on the level engine) instead of concurrently on streams")
     ap.add_argument("--panel5", action="store_true",
                     help="config 5 from a device-generated bf16 panel (use --n5 12500000 "
                          "--p5 2000 for the per-GPU shard of N=1e8)")
@@ -76,12 +79,14 @@ def main():
         from ate_replication_causalml_amd.estimators.crossfit import aipw_rf_crossfit_panel
         pan = synthetic_panel(a.n3, p=a.p3, folds=5, seed=11, dtype="bf16", device=dev)
         shard = tuple(int(v) for v in a.shard3.split("/")) if a.shard3 else None
-        r, s = timed(lambda: aipw_rf_crossfit_panel(pan, num_trees=a.trees3, tree_shard=shard),
+        r, s = timed(lambda: aipw_rf_crossfit_panel(pan, num_trees=a.trees3, tree_shard=shard,
+                                                    concurrent=not a.serial3),
                      warm=a.n3 <= 2_000_000)
         out.append({"config": 3, "estimator": "AIPW 5-fold cross-fit, RF nuisances (3 forests/"
                     "fold), HBM panel, device binning", "rows": a.n3, "p": a.p3,
                     "trees_per_forest": a.trees3, "tree_shard": a.shard3,
                     "trees_this_device": r.diagnostics.get("trees_this_device"),
+                    "serial": a.serial3,
                     "seconds": s, "rows_per_s": a.n3 / s, "ate": r.ate, "se": r.se})
         print(json.dumps(out[-1]), flush=True)
         del pan
