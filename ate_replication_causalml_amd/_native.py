@@ -66,10 +66,10 @@ _SIGS = {
     "ate_select_compact": "plppddpppp" + "p",
     "ate_gbdt_run": "ppp",
     "ate_lv_boot": "ppp",
-    "ate_lv_classify": "piippp",
-    "ate_lv_decide": "ppiiiipppppiipip",
-    "ate_lv_partition": "ppiiiipppipp",
-    "ate_lv_scatter": "ppipppippp",
+    "ate_lv_classify": "piiippp",
+    "ate_lv_decide": "ppipipipippppp" + "iipip",
+    "ate_lv_partition": "ppipippppipp",
+    "ate_lv_scatter": "pppppippp",
     "ate_lv_children": "pippppp",
     "ate_gbdt_bin_panel": "pilpipppilpppl" + "p",
     "ate_gbdt_slab_entries": "liii",

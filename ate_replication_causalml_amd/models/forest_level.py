@@ -32,7 +32,7 @@ class LvHost(ctypes.Structure):
     _fields_ = [("fp", F.ForestParams), ("Xb", P), ("ycls", P), ("r1", P), ("w", P), ("idx", P),
                 ("idx2", P), ("cur", P), ("dec", P), ("nl", P), ("cap", ctypes.c_int),
                 ("feat", P), ("thr", P), ("left", P), ("val", P), ("depth", ctypes.c_int),
-                ("fst", ctypes.c_int64), ("rst", ctypes.c_int64)]
+                ("fst", ctypes.c_int64), ("rst", ctypes.c_int64), ("Xc", P)]
 
 
 def supported(fp: F.ForestParams) -> bool:
@@ -45,15 +45,33 @@ def _env_int(name, default):
     return int(v) if v else default
 
 
+def _items(cur, sel, chunk, target, dev):
+    """Work items (slot, q0, q1) cutting the nodes cur[sel] into position chunks of
+    max(chunk, total / target) rows; also each slot's first item index."""
+    lohi = cur.index_select(0, sel)[:, 1:3].cpu().numpy().astype(np.int64)
+    lens = lohi[:, 1] - lohi[:, 0]
+    ch = max(chunk, -(-int(lens.sum()) // target) // 256 * 256 + 256)
+    per = -(-lens // ch)
+    slot = np.repeat(np.arange(len(lens)), per)
+    firsts = np.concatenate([[0], np.cumsum(per)[:-1]])
+    q0 = lohi[slot, 0] + (np.arange(len(slot)) - np.repeat(firsts, per)) * ch
+    q1 = np.minimum(q0 + ch, lohi[slot, 1])
+    t = tuple(torch.as_tensor(a.astype(np.int32), device=dev) for a in (slot, q0, q1))
+    return t, len(slot), torch.as_tensor(firsts, device=dev)
+
+
 def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chunk=None,
          stream=None):
     """Grow fp.ntree trees on the device. Xb: [p][n] uint8 (cuda), yt: [n] uint8 (kind 0),
     r1t: [n] int64 fixed point (kind 1). Returns (cap, feat, thr, left, val, nnodes, inbag)."""
     dev = Xb.device
     T, n, p = fp.ntree, fp.n, fp.p
-    big = min(big or _env_int("ATE_FOREST_LV_BIG", 8192), 8192)   # mid partition: <= 8192 rows
+    # node classes: <= 64 rows a wave; <= t2 a workgroup + wave partition; <= t3 a
+    # workgroup + chunked partition; above, many workgroups per node
+    t2 = max(64, min(8192, _env_int("ATE_FOREST_LV_T2", 8192)))
+    t3 = max(t2, big or _env_int("ATE_FOREST_LV_BIG", 65536))
     chunk = chunk or _env_int("ATE_FOREST_LV_CH", 4096)
-    items_target = _env_int("ATE_FOREST_LV_ITEMS", 2048)
+    items_target = _env_int("ATE_FOREST_LV_ITEMS", 1024)
     s = (stream or torch.cuda.current_stream(dev)).cuda_stream
     i32 = dict(dtype=torch.int32, device=dev)
     cap = 2 * n + 1
@@ -91,7 +109,7 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     dec = torch.zeros((lcap, 4), **i32)
     nl = torch.zeros(lcap, **i32)
     brank = torch.zeros(T, **i32)
-    counts = torch.zeros(3, **i32)
+    counts = torch.zeros(4, **i32)
     nf_max = min(fp.mtry, p)
     ngroups = -(-nf_max // LV_FG)
     hist = None
@@ -104,7 +122,8 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         fst, rst = 1, p
     else:
         Xg, fst, rst = Xb, n, 1
-    h = LvHost(fp=fp, Xb=Xg.data_ptr(), ycls=yt.data_ptr() if yt is not None else None,
+    h = LvHost(fp=fp, Xb=Xg.data_ptr(), Xc=Xb.data_ptr(),
+               ycls=yt.data_ptr() if yt is not None else None,
                r1=r1t.data_ptr() if r1t is not None else None, w=w.data_ptr(), cap=cap,
                feat=feat.data_ptr(), thr=thr.data_ptr(), left=left.data_ptr(),
                val=val.data_ptr(), fst=fst, rst=rst)
@@ -130,58 +149,48 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         h.idx, h.idx2 = idx.data_ptr(), idx2.data_ptr()
         h.cur, h.dec, h.nl = cur.data_ptr(), dec.data_ptr(), nl.data_ptr()
         h.depth = depth
-        lists = torch.empty(3 * ncur, **i32)
+        lists = torch.empty(4 * ncur, **i32)
         counts.zero_()
-        _native.call("ate_lv_classify", cur.data_ptr(), ncur, big, lists.data_ptr(),
+        _native.call("ate_lv_classify", cur.data_ptr(), ncur, t2, t3, lists.data_ptr(),
                      counts.data_ptr(), s)
-        nsmall, nmid, nbig = (int(v) for v in counts.cpu())
+        nsmall, nmid, nmid2, nbig = (int(v) for v in counts.cpu())
         t0 = tick("classify", t0) if prof else None
-        items = (None, None, None)
-        nitems = 0
-        drawn = nfo = None
+        L = [lists[k * ncur:k * ncur + c] for k, c in enumerate((nsmall, nmid, nmid2, nbig))]
+        P = lambda t: t.data_ptr() if t is not None else None
+        items, nitems, drawn, nfo = (None, None, None), 0, None, None
         if nbig:
-            bl = lists[2 * ncur:2 * ncur + nbig].long()
-            lohi = cur.index_select(0, bl)[:, 1:3].cpu().numpy().astype(np.int64)
-            lens = lohi[:, 1] - lohi[:, 0]
-            # items: ~ITEMS per level (every item's histogram is added to its node's with
-            # global atomics, so many small items of one node contend on the same lines)
-            ch = max(chunk, -(-int(lens.sum()) // items_target) // 256 * 256 + 256)
-            per = -(-lens // ch)
-            slot = np.repeat(np.arange(nbig), per)
-            first = np.repeat(np.concatenate([[0], np.cumsum(per)[:-1]]), per)
-            q0 = lohi[slot, 0] + (np.arange(len(slot)) - first) * ch
-            q1 = np.minimum(q0 + ch, lohi[slot, 1])
-            nitems = len(slot)
-            items = tuple(torch.as_tensor(a.astype(np.int32), device=dev) for a in (slot, q0, q1))
+            items, nitems, _ = _items(cur, L[3].long(), chunk, items_target, dev)
             drawn = torch.empty(nbig * LV_MAXF, dtype=torch.int16, device=dev)
             nfo = torch.empty(nbig, **i32)
             need = nbig * nf_max * 2 * F.MAX_BINS
             if hist is None or hist.numel() < need:
                 hist = torch.empty(need, dtype=torch.int64, device=dev)
             hist[:need].zero_()
-        P = lambda t: t.data_ptr() if t is not None else None
-        _native.call("ate_lv_decide", ctypes.addressof(h), lists.data_ptr(), ncur, nsmall, nmid,
-                     nbig, P(drawn), P(nfo), P(items[0]), P(items[1]), P(items[2]), nitems,
-                     ngroups, P(hist), nf_max, s)
+        _native.call("ate_lv_decide", ctypes.addressof(h), P(L[0]), nsmall, P(L[1]), nmid,
+                     P(L[2]), nmid2, P(L[3]), nbig, P(drawn), P(nfo), P(items[0]), P(items[1]),
+                     P(items[2]), nitems, ngroups, P(hist), nf_max, s)
         if prof:
             td = tick("decide", t0)
-            lv_rows.append((depth, ncur, nsmall, nmid, nbig, nitems, td - t0))
+            lv_rows.append((depth, ncur, nsmall, nmid, nmid2, nbig, td - t0))
             t0 = td
-        icnt = torch.empty(max(nitems, 1), **i32)
-        _native.call("ate_lv_partition", ctypes.addressof(h), lists.data_ptr(), ncur, nsmall, nmid,
-                     nbig, P(items[0]), P(items[1]), P(items[2]), nitems, icnt.data_ptr(), s)
-        if nbig:
-            ic = icnt[:nitems].long()
-            slot_t = items[0].long()
+        # partition: small + mid by waves, mid-large + big by position chunks
+        plist = torch.cat([L[2], L[3]]) if nmid2 + nbig else None
+        pitems, npit, firsts = (None, None, None), 0, None
+        if plist is not None:
+            pitems, npit, firsts = _items(cur, plist.long(), chunk, 4 * items_target, dev)
+        icnt = torch.empty(max(npit, 1), **i32)
+        _native.call("ate_lv_partition", ctypes.addressof(h), P(L[0]), nsmall, P(L[1]), nmid,
+                     P(plist), P(pitems[0]), P(pitems[1]), P(pitems[2]), npit, icnt.data_ptr(), s)
+        if npit:
+            ic = icnt[:npit].long()
+            slot_t = pitems[0].long()
             csum = torch.cumsum(ic, 0) - ic                                   # exclusive
-            firsts = torch.as_tensor(np.concatenate([[0], np.cumsum(per)[:-1]]), device=dev)
             ipre = (csum - csum.index_select(0, firsts).index_select(0, slot_t)).to(torch.int32)
-            nlb = torch.zeros(nbig, dtype=torch.int64, device=dev).index_add_(0, slot_t, ic)
+            nlb = torch.zeros(plist.numel(), dtype=torch.int64, device=dev).index_add_(0, slot_t, ic)
             nlb32 = nlb.to(torch.int32)
-            nl.index_copy_(0, bl, nlb32)
-            _native.call("ate_lv_scatter", ctypes.addressof(h), lists.data_ptr(), ncur,
-                         P(items[0]), P(items[1]), P(items[2]), nitems, ipre.data_ptr(),
-                         nlb32.data_ptr(), s)
+            nl.index_copy_(0, plist.long(), nlb32)
+            _native.call("ate_lv_scatter", ctypes.addressof(h), P(plist), P(pitems[0]),
+                         P(pitems[1]), P(pitems[2]), npit, ipre.data_ptr(), nlb32.data_ptr(), s)
         t0 = tick("partition", t0) if prof else None
         flags = dec[:ncur, 0]
         excl = (torch.cumsum(flags, 0, dtype=torch.int32) - flags).contiguous()
@@ -200,7 +209,7 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         top = sorted(lv_rows, key=lambda r: -r[-1])[:6]
         print(f"[forest_level] T={T} n={n} levels={depth} {tot:.3f}s "
               + " ".join(f"{k}={v:.3f}" for k, v in tp.items())
-              + " slowest decide levels (depth,ncur,small,mid,big,items,s): "
+              + " slowest decide levels (depth,ncur,small,mid,mid2,big,s): "
               + "; ".join(f"{r[0]},{r[1]},{r[2]},{r[3]},{r[4]},{r[5]},{r[6]:.3f}" for r in top),
               file=sys.stderr, flush=True)
     return cap, feat, thr, left, val, next_id, inbag

@@ -171,6 +171,7 @@ __device__ __forceinline__ bool lv_accept(double best, double parent) {
 struct LvArgs {
   ForestParams fp;
   const uint8_t* Xb;      // bins: element (feature f, row i) at f * fst + i * rst
+  const uint8_t* Xc;      // the same bins column-major [p][n] (dense big-node streams)
   const uint8_t* ycls;    // kind 0: [n] class
   const int64_t* r1;      // kind 1: [n] response, 2^-32 fixed point
   const int32_t* w;       // [T][n] bootstrap counts
@@ -193,8 +194,8 @@ struct LvArgs {
 // loads, then every row's weight / label / LV_FG bins, then the LDS atomics) into the LDS
 // histograms sh[k][c][bin] of the nk features xf[0..nk)
 __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __restrict__ wt,
-                                              const uint8_t* const* xf, int nk, int q0, int q1,
-                                              int64_t (*sh)[2][NBINS]) {
+                                              const uint8_t* const* xf, int64_t rst, int nk,
+                                              int q0, int q1, int64_t (*sh)[2][NBINS]) {
   constexpr int U = 4;
   const int kind = a.fp.kind;
   for (int base = q0 + threadIdx.x; base < q1; base += 256 * U) {
@@ -214,7 +215,7 @@ __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __
       yv[u] = kind == 0 ? a.ycls[i] : 0;
       rv[u] = kind == 0 ? 0 : a.r1[i];
 #pragma unroll
-      for (int k = 0; k < LV_FG; ++k) bins[u][k] = xf[k][(int64_t)i * a.rst];
+      for (int k = 0; k < LV_FG; ++k) bins[u][k] = xf[k][(int64_t)i * rst];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -244,16 +245,29 @@ __global__ __launch_bounds__(256) void lv_boot_kernel(ForestParams fp, int32_t* 
 }
 
 // ------------------------------------------------------------------ node classes
+// classes: 0 small (<= 64 rows: wave decide, wave partition), 1 mid (<= t2 rows: workgroup
+// decide, wave partition), 2 mid-large (<= t3: workgroup decide, chunked partition), 3 big
+// (> t3: multi-workgroup decide, chunked partition). One atomic per wave and class.
 __global__ __launch_bounds__(256) void lv_classify_kernel(const LNode* __restrict__ cur, int ncur,
-                                                          int big, int32_t* __restrict__ lists,
+                                                          int t2, int t3, int32_t* __restrict__ lists,
                                                           int32_t* __restrict__ counts) {
-  // lists: [3][ncur] (small, mid, big); counts[3]
   const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= ncur) return;
-  const int m = cur[j].hi - cur[j].lo;
-  const int c = m <= 64 ? 0 : (m <= big ? 1 : 2);
-  const int pos = atomicAdd(&counts[c], 1);
-  lists[(int64_t)c * ncur + pos] = j;
+  const int lane = threadIdx.x & 63;
+  int c = -1;
+  if (j < ncur) {
+    const int m = cur[j].hi - cur[j].lo;
+    c = m <= 64 ? 0 : (m <= t2 ? 1 : (m <= t3 ? 2 : 3));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t mk = __ballot(c == k);
+    if (!mk) continue;
+    const int leader = __ffsll((long long)mk) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&counts[k], __popcll(mk));
+    base = __shfl(base, leader, 64);
+    if (c == k) lists[(int64_t)k * ncur + base + __popcll(mk & ((1ull << lane) - 1ull))] = j;
+  }
 }
 
 // ------------------------------------------------------------------ BIG nodes
@@ -296,9 +310,10 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   const uint8_t* xf[LV_FG];
 #pragma unroll
   for (int k = 0; k < LV_FG; ++k)
-    xf[k] = a.Xb + (int64_t)drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)] * a.fst;
+    xf[k] = a.Xc + (int64_t)drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)] * n;
   __syncthreads();
-  lv_accumulate(a, wt, xf, nk, item_q0[it], item_q1[it], sh);
+  // big nodes hold dense runs of ascending positions: the column-major bins stream
+  lv_accumulate(a, wt, xf, 1, nk, item_q0[it], item_q1[it], sh);
   __syncthreads();
   int64_t* hs = hist + ((int64_t)slot * fs + k0) * 2 * NBINS;
   for (int e = threadIdx.x; e < nk * 2 * NBINS; e += 256) {
@@ -402,7 +417,7 @@ __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __
 #pragma unroll
     for (int k = 0; k < LV_FG; ++k) xf[k] = a.Xb + (int64_t)perm[k0 + min(k, nk - 1)] * a.fst;
     __syncthreads();
-    lv_accumulate(a, wt, xf, nk, nd.lo, nd.hi, sh);
+    lv_accumulate(a, wt, xf, a.rst, nk, nd.lo, nd.hi, sh);
     __syncthreads();
     if (k0 == 0) {
       if (wid == 0) {
@@ -624,10 +639,9 @@ __global__ __launch_bounds__(256) void lv_part_count_kernel(LvArgs a, const int3
     if (threadIdx.x == 0) icnt[it] = 0;
     return;
   }
-  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fst;
+  const uint8_t* xf = a.Xc + (int64_t)d.y * a.fp.n;
   int c = 0;
-  for (int q = item_q0[it] + threadIdx.x; q < item_q1[it]; q += 256)
-    c += xf[(int64_t)a.idx[q] * a.rst] <= d.z;
+  for (int q = item_q0[it] + threadIdx.x; q < item_q1[it]; q += 256) c += xf[a.idx[q]] <= d.z;
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
   __syncthreads();
@@ -649,7 +663,7 @@ __global__ __launch_bounds__(256) void lv_part_scatter_kernel(LvArgs a, const in
   const int4 d = a.dec[j];
   if (!d.x) return;
   const LNode nd = a.cur[j];
-  const uint8_t* xf = a.Xb + (int64_t)d.y * a.fst;
+  const uint8_t* xf = a.Xc + (int64_t)d.y * a.fp.n;
   const int nlt = nlb[slot];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int run = ipre[it];                                       // lefts before this tile
@@ -660,7 +674,7 @@ __global__ __launch_bounds__(256) void lv_part_scatter_kernel(LvArgs a, const in
     bool gl = false;
     if (q < q1) {
       i = a.idx[q];
-      gl = xf[(int64_t)i * a.rst] <= d.z;
+      gl = xf[i] <= d.z;
     }
     const uint64_t bl = __ballot(gl);
     const int wl = __popcll(bl);
@@ -739,6 +753,7 @@ struct LvHost {
   void *feat, *thr, *left, *val;
   int depth;
   int64_t fst, rst;
+  const void* Xc;
 };
 
 static LvArgs lv_args(const LvHost& h) {
@@ -761,6 +776,7 @@ static LvArgs lv_args(const LvHost& h) {
   a.depth = h.depth;
   a.fst = h.fst;
   a.rst = h.rst;
+  a.Xc = (const uint8_t*)h.Xc;
   return a;
 }
 
@@ -773,34 +789,36 @@ ATE_API int ate_lv_boot(const void* fpp, void* w, void* stream) {
   return 0;
 }
 
-ATE_API int ate_lv_classify(const void* cur, int ncur, int big, void* lists, void* counts,
+ATE_API int ate_lv_classify(const void* cur, int ncur, int t2, int t3, void* lists, void* counts,
                             void* stream) {
   if (ncur <= 0) return 0;
   hipLaunchKernelGGL(lv_classify_kernel, dim3((ncur + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, (const LNode*)cur, ncur, big, (int32_t*)lists,
+                     (hipStream_t)stream, (const LNode*)cur, ncur, t2, t3, (int32_t*)lists,
                      (int32_t*)counts);
   ATE_CHECK_LAUNCH();
   return 0;
 }
 
-// phase 1: decisions of every node of the level
-ATE_API int ate_lv_decide(const void* hp, const void* lists, int ncur, int nsmall, int nmid,
-                          int nbig, void* drawn, void* nfo, const void* item_slot,
-                          const void* item_q0, const void* item_q1, int nitems, int ngroups,
-                          void* hist, int fs, void* stream) {
+// phase 1: decisions of every node of the level (class lists from ate_lv_classify)
+ATE_API int ate_lv_decide(const void* hp, const void* small, int nsmall, const void* mid, int nmid,
+                          const void* mid2, int nmid2, const void* big, int nbig, void* drawn,
+                          void* nfo, const void* item_slot, const void* item_q0,
+                          const void* item_q1, int nitems, int ngroups, void* hist, int fs,
+                          void* stream) {
   const LvHost& h = *(const LvHost*)hp;
   if (h.fp.kind > 1 || h.fp.sampling != 0 || h.fp.mtry_poisson || h.fp.p > LV_PMAX ||
       h.fp.mtry > LV_MAXF || fs < h.fp.mtry || ngroups * LV_FG < h.fp.mtry)
     return -1;
   const LvArgs a = lv_args(h);
   hipStream_t st = (hipStream_t)stream;
-  const int32_t* L = (const int32_t*)lists;
   if (nsmall)
-    hipLaunchKernelGGL(lv_small_kernel, dim3((nsmall + 3) / 4), dim3(256), 0, st, a, L, nsmall);
-  if (nmid)
-    hipLaunchKernelGGL(lv_mid_kernel, dim3(nmid), dim3(256), 0, st, a, L + ncur);
+    hipLaunchKernelGGL(lv_small_kernel, dim3((nsmall + 3) / 4), dim3(256), 0, st, a,
+                       (const int32_t*)small, nsmall);
+  if (nmid) hipLaunchKernelGGL(lv_mid_kernel, dim3(nmid), dim3(256), 0, st, a, (const int32_t*)mid);
+  if (nmid2)
+    hipLaunchKernelGGL(lv_mid_kernel, dim3(nmid2), dim3(256), 0, st, a, (const int32_t*)mid2);
   if (nbig) {
-    const int32_t* B = L + 2 * (int64_t)ncur;
+    const int32_t* B = (const int32_t*)big;
     hipLaunchKernelGGL(lv_big_draw_kernel, dim3((nbig + 3) / 4), dim3(256), 0, st, a, B, nbig,
                        (int16_t*)drawn, (int32_t*)nfo);
     hipLaunchKernelGGL(lv_big_hist_kernel, dim3(nitems, ngroups), dim3(256), 0, st, a,
@@ -814,29 +832,30 @@ ATE_API int ate_lv_decide(const void* hp, const void* lists, int ncur, int nsmal
   return 0;
 }
 
-// phase 2a: partition of the small / mid split nodes, left counts of the big items
-ATE_API int ate_lv_partition(const void* hp, const void* lists, int ncur, int nsmall, int nmid,
-                             int nbig, const void* item_slot, const void* item_q0,
+// phase 2a: partition of the wave-partitioned split nodes (two lists), left counts of the
+// chunked list's items
+ATE_API int ate_lv_partition(const void* hp, const void* l1, int n1, const void* l2, int n2,
+                             const void* plist, const void* item_slot, const void* item_q0,
                              const void* item_q1, int nitems, void* icnt, void* stream) {
   const LvHost& h = *(const LvHost*)hp;
   const LvArgs a = lv_args(h);
   hipStream_t st = (hipStream_t)stream;
-  const int32_t* L = (const int32_t*)lists;
-  if (nsmall)
-    hipLaunchKernelGGL(lv_part_wave_kernel, dim3((nsmall + 3) / 4), dim3(256), 0, st, a, L, nsmall);
-  if (nmid)
-    hipLaunchKernelGGL(lv_part_wave_kernel, dim3((nmid + 3) / 4), dim3(256), 0, st, a, L + ncur,
-                       nmid);
-  if (nbig)
+  if (n1)
+    hipLaunchKernelGGL(lv_part_wave_kernel, dim3((n1 + 3) / 4), dim3(256), 0, st, a,
+                       (const int32_t*)l1, n1);
+  if (n2)
+    hipLaunchKernelGGL(lv_part_wave_kernel, dim3((n2 + 3) / 4), dim3(256), 0, st, a,
+                       (const int32_t*)l2, n2);
+  if (nitems)
     hipLaunchKernelGGL(lv_part_count_kernel, dim3(nitems), dim3(256), 0, st, a,
                        (const int32_t*)item_slot, (const int32_t*)item_q0,
-                       (const int32_t*)item_q1, L + 2 * (int64_t)ncur, (int32_t*)icnt);
+                       (const int32_t*)item_q1, (const int32_t*)plist, (int32_t*)icnt);
   ATE_CHECK_LAUNCH();
   return 0;
 }
 
-// phase 2b: scatter of the big split nodes (ipre / nlb from the item counts)
-ATE_API int ate_lv_scatter(const void* hp, const void* lists, int ncur, const void* item_slot,
+// phase 2b: stable scatter of the chunked list (ipre / nlb from the item counts)
+ATE_API int ate_lv_scatter(const void* hp, const void* plist, const void* item_slot,
                            const void* item_q0, const void* item_q1, int nitems, const void* ipre,
                            const void* nlb, void* stream) {
   const LvHost& h = *(const LvHost*)hp;
@@ -844,8 +863,8 @@ ATE_API int ate_lv_scatter(const void* hp, const void* lists, int ncur, const vo
   if (nitems)
     hipLaunchKernelGGL(lv_part_scatter_kernel, dim3(nitems), dim3(256), 0, (hipStream_t)stream, a,
                        (const int32_t*)item_slot, (const int32_t*)item_q0,
-                       (const int32_t*)item_q1, (const int32_t*)lists + 2 * (int64_t)ncur,
-                       (const int32_t*)ipre, (const int32_t*)nlb);
+                       (const int32_t*)item_q1, (const int32_t*)plist, (const int32_t*)ipre,
+                       (const int32_t*)nlb);
   ATE_CHECK_LAUNCH();
   return 0;
 }

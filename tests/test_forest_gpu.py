@@ -105,17 +105,19 @@ def test_aipw_rf_crossfit_panel_matches_host_engine(gpu):
 
 
 @pytest.mark.parametrize("layout", ["row", "col"])
-@pytest.mark.parametrize("big,chunk", [(8192, 4096), (300, 128), (65, 64)])
+@pytest.mark.parametrize("big,chunk", [(65536, 4096), (8192, 4096), (300, 128), (65, 64)])
 @pytest.mark.parametrize("case", ["rf_class", "rf_reg"])
 def test_level_engine_bit_identical_to_host(gpu, case, big, chunk, layout, monkeypatch):
     """The level-synchronous engine (csrc/forest_level.hip: all trees level by level, big
     nodes over many workgroups, mid nodes a workgroup, small nodes a wave) grows the host
     engine's trees bit for bit. Small thresholds push most nodes through the big /
-    chunked-partition path."""
+    chunked-partition paths (every node class and both partition paths are exercised);
+    both layouts of the growth copy (row-major, column-major)."""
     monkeypatch.setenv("ATE_FOREST_ENGINE", "level")
     monkeypatch.setenv("ATE_FOREST_LV_BIG", str(big))
     monkeypatch.setenv("ATE_FOREST_LV_CH", str(chunk))
     monkeypatch.setenv("ATE_FOREST_LV_ITEMS", "100000")   # keep the small chunks
+    monkeypatch.setenv("ATE_FOREST_LV_T2", str(max(65, big // 2)))
     monkeypatch.setenv("ATE_FOREST_LV_LAYOUT", layout)
     X, W, Y = _data(6000)
     kw = dict(ntree=12, seed=23)
