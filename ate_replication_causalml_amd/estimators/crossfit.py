@@ -36,110 +36,135 @@ def _backend(dev):
 
 
 def _binary(y):
-    return bool(np.all((y == 0) | (y == 1)))
+    y = torch.as_tensor(y)
+    return bool(torch.all((y == 0) | (y == 1)))
 
 
-def _rf_fit_predict(Xtr, ytr, Xho, num_trees, seed, dev, comm, edges):
+def _rf_fit_predict(Xb, tr_idx, ytr, ho_idx, num_trees, seed, dev, comm, edges):
+    """Forest on the training columns of the binned matrix ``Xb`` [p][n] (gathered where
+    it lives: no host slicing of X), predictions for the held-out columns -> tensor on
+    ``dev``."""
     kind = F.KIND_CLASS if _binary(ytr) else F.KIND_REG
-    kw = dict(y=ytr) if kind == F.KIND_CLASS else dict(r1=ytr, min_node=5,
-                                                        mtry=max(1, Xtr.shape[1] // 3))
+    p = Xb.shape[0]
+    kw = dict(y=ytr) if kind == F.KIND_CLASS else dict(r1=ytr, min_node=5, mtry=max(1, p // 3))
+    Xt = Xb.index_select(1, tr_idx)
+    Xho = Xb.index_select(1, ho_idx)
     if comm is not None and comm.world_size > 1:
-        fr = F.fit_forest_sharded(Xtr, kind, num_trees, comm, seed=seed, backend=_backend(dev),
-                                  edges=edges, **kw)
-        return F.predict_tree_parallel(fr, comm, X=Xho)
-    fr = F.fit_forest(Xtr, kind, ntree=num_trees, seed=seed, backend=_backend(dev), edges=edges,
-                      **kw)
-    return fr.predict_proba(Xho)
+        t0, cnt = F.tree_shard(num_trees, 1, comm.rank, comm.world_size)
+        fr = F.fit_forest_binned(Xt, edges, kind, ntree=cnt, seed=seed, tree_offset=t0, **kw)
+        out = F.predict_tree_parallel(fr, comm, Xb=Xho, host=False)
+    else:
+        fr = F.fit_forest_binned(Xt, edges, kind, ntree=num_trees, seed=seed, **kw)
+        out = fr.predict_binned(Xho, host=False)
+    return torch.as_tensor(out, dtype=torch.float64, device=dev)
 
 
-def _glm_fit_predict(Xtr, ytr, Xho, dev):
-    pan = build_panel(Xtr, None, ytr, dtype="f64", device=dev, extra_cols=("z",))
+def _glm_fit_predict(Xd, tr_idx, ytr_host, ho_idx, dev):
+    """Logistic IRLS on the training rows (panel assembled from the device X), fitted
+    probabilities of the held-out rows on the device."""
+    pan = build_panel(Xd.index_select(0, tr_idx), None, ytr_host, dtype="f64", device=dev,
+                      extra_cols=("z",))
     cols = [pan.cols["one"], *pan.xcols]
     fit = logistic_irls(pan, cols, pan.cols["Y"], pan.cols["z"])
-    beta = torch.nan_to_num(fit.beta.double(), nan=0.0).cpu().numpy()
-    eta = beta[0] + Xho @ beta[1:]
-    return 1.0 / (1.0 + np.exp(-eta))
+    beta = torch.nan_to_num(fit.beta.double(), nan=0.0).to(dev)
+    eta = beta[0] + Xd.index_select(0, ho_idx) @ beta[1:]
+    return torch.sigmoid(eta)
 
 
 def _gbdt_fit_predict(y, train, ho, Xb, edges, dev, seed, gbdt_kw):
     """Trees learn from ``train`` rows of the shared binned panel; the held-out
-    predictions are the trainer's final scores of the ``ho`` rows."""
+    predictions are the trainer's final scores of the ``ho`` rows (device tensors)."""
     from ..models import gbdt as G
     loss = "logistic" if _binary(y[train]) else "squared"
-    m = G.fit_gbdt(None, y, loss=loss, train=train, seed=seed, backend=_backend(dev),
+    be = _backend(dev)
+    m = G.fit_gbdt(None, y if be == "gpu" else y.cpu().numpy(), loss=loss,
+                   train=train if be == "gpu" else train.cpu().numpy(), seed=seed, backend=be,
                    edges=edges, Xb=Xb, **(gbdt_kw or {}))
-    f = m.scores.cpu().numpy() if isinstance(m.scores, torch.Tensor) else m.scores
-    f = f[ho]
-    return 1.0 / (1.0 + np.exp(-f)) if loss == "logistic" else f
+    f = torch.as_tensor(m.scores, dtype=torch.float64).to(dev)[ho]
+    return torch.sigmoid(f) if loss == "logistic" else f
+
+
+def aipw_score(Y, W, e, mu1, mu0, clip=0.01):
+    """Textbook AIPW score on the device: Gamma = mu1 - mu0 + W (Y - mu1) / e
+    - (1 - W) (Y - mu0) / (1 - e), e clipped to [clip, 1 - clip]; -> (tau, se, e)."""
+    e = e.clamp(clip, 1 - clip)
+    gamma = mu1 - mu0 + W * (Y - mu1) / e - (1 - W) * (Y - mu0) / (1 - e)
+    n = gamma.numel()
+    return gamma.mean(), gamma.std() / math.sqrt(n), e
 
 
 def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold_stream=11,
                   clip=0.01, method=None, device=None, comm=None, gbdt_kw=None) -> AteResult:
+    """K-fold cross-fitted AIPW. X moves to ``device`` once (and is binned there for the
+    tree learners); every training / held-out set is gathered on the device, every
+    nuisance prediction stays there, and the score, its mean and SE are computed on the
+    device (one read-back of the result)."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
     n = len(Yn)
-    fid = rng.fold_ids(n, folds, seed, fold_stream)
-    e = np.empty(n)
-    mu1 = np.empty(n)
-    mu0 = np.empty(n)
-    edges = F.bin_edges(Xn) if learner == "rf" else None
-    if learner == "gbdt":
+    fid = torch.as_tensor(rng.fold_ids(n, folds, seed, fold_stream), device=dev)
+    Yd = torch.as_tensor(Yn, dtype=torch.float64, device=dev)
+    Wd = torch.as_tensor(Wn, dtype=torch.float64, device=dev)
+    e = torch.empty(n, dtype=torch.float64, device=dev)
+    mu1 = torch.empty_like(e)
+    mu0 = torch.empty_like(e)
+    Xd = Xb = edges = None
+    if learner == "rf":
+        edges = F.bin_edges(Xn)
+        Xb = F.bin_matrix(Xn, edges[0], edges[1], dev if dev.type == "cuda" else None)
+    elif learner == "gbdt":
         from ..models import gbdt as G
         edges = G.sample_bin_edges(Xn, device=dev)
         Xb = G.binned(Xn, edges, dev)
+    elif learner == "glm":
+        Xd = torch.as_tensor(Xn, dtype=torch.float64, device=dev)
+    else:
+        raise ValueError(learner)
+    jobs = []
+    for k in range(folds):
+        ho = fid == k
+        tr = ~ho
+        t1, t0 = tr & (Wd == 1), tr & (Wd == 0)
+        sd = seed + 1000 * (k + 1)
+        jobs += [(e, ho, tr, Wd, sd), (mu1, ho, t1, Yd, sd + 1), (mu0, ho, t0, Yd, sd + 2)]
+
+    def run(job):
+        out, ho, rows, target, sd = job
+        hoi = ho.nonzero().squeeze(1)
+        if learner == "rf":
+            ri = rows.nonzero().squeeze(1)
+            r = _rf_fit_predict(Xb, ri, target.index_select(0, ri), hoi, num_trees, sd, dev,
+                                comm, edges)
+        elif learner == "glm":
+            ri = rows.nonzero().squeeze(1)
+            r = _glm_fit_predict(Xd, ri, target.index_select(0, ri).cpu().numpy(), hoi, dev)
+        else:
+            r = _gbdt_fit_predict(target, rows, ho, Xb, edges, dev, sd, gbdt_kw)
+        out.index_copy_(0, hoi, r)
+
     concurrent = learner == "rf" and dev.type == "cuda" and (comm is None or comm.world_size == 1)
     if concurrent:
         # the 3K forests are independent: grow them concurrently, one HIP stream per host
         # thread, so a 100-tree forest (100 workgroups) does not leave most CUs idle;
         # every forest is a deterministic function of its inputs (same trees as serially)
-        jobs = []
-        for k in range(folds):
-            ho = fid == k
-            tr = ~ho
-            t1, t0 = tr & (Wn == 1), tr & (Wn == 0)
-            s = seed + 1000 * (k + 1)
-            jobs += [(e, ho, tr, Wn, s), (mu1, ho, t1, Yn, s + 1), (mu0, ho, t0, Yn, s + 2)]
+        main = torch.cuda.current_stream(dev)
 
-        def run(job):
-            out, ho, rows, target, sd = job
+        def run_on(job):
             st = torch.cuda.Stream(device=dev)
+            st.wait_stream(main)
             with torch.cuda.device(dev), torch.cuda.stream(st):
-                r = _rf_fit_predict(Xn[rows], target[rows], Xn[ho], num_trees, sd, dev, None,
-                                    edges)
+                run(job)
             st.synchronize()
-            return r
 
         with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
-            for (out, ho, _, _, _), r in zip(jobs, ex.map(run, jobs)):
-                out[ho] = r
-    for k in range(folds):
-        if concurrent:
-            break
-        ho = fid == k
-        tr = ~ho
-        t1, t0 = tr & (Wn == 1), tr & (Wn == 0)
-        Xho = Xn[ho]
-        s = seed + 1000 * (k + 1)
-        if learner == "rf":
-            e[ho] = _rf_fit_predict(Xn[tr], Wn[tr], Xho, num_trees, s, dev, comm, edges)
-            mu1[ho] = _rf_fit_predict(Xn[t1], Yn[t1], Xho, num_trees, s + 1, dev, comm, edges)
-            mu0[ho] = _rf_fit_predict(Xn[t0], Yn[t0], Xho, num_trees, s + 2, dev, comm, edges)
-        elif learner == "glm":
-            e[ho] = _glm_fit_predict(Xn[tr], Wn[tr], Xho, dev)
-            mu1[ho] = _glm_fit_predict(Xn[t1], Yn[t1], Xho, dev)
-            mu0[ho] = _glm_fit_predict(Xn[t0], Yn[t0], Xho, dev)
-        elif learner == "gbdt":
-            e[ho] = _gbdt_fit_predict(Wn, tr, ho, Xb, edges, dev, s, gbdt_kw)
-            mu1[ho] = _gbdt_fit_predict(Yn, t1, ho, Xb, edges, dev, s + 1, gbdt_kw)
-            mu0[ho] = _gbdt_fit_predict(Yn, t0, ho, Xb, edges, dev, s + 2, gbdt_kw)
-        else:
-            raise ValueError(learner)
-    e = np.clip(e, clip, 1 - clip)
-    gamma = mu1 - mu0 + Wn * (Yn - mu1) / e - (1 - Wn) * (Yn - mu0) / (1 - e)
-    tau = float(gamma.mean())
-    se = float(gamma.std(ddof=1) / math.sqrt(n))
-    return AteResult.make(method or f"AIPW cross-fit ({learner}, K={folds})", tau, se,
-                          e_min=float(e.min()), e_max=float(e.max()))
+            list(ex.map(run_on, jobs))
+    else:
+        for job in jobs:
+            run(job)
+    tau, se, ec = aipw_score(Yd, Wd, e, mu1, mu0, clip)
+    v = torch.stack([tau, se, ec.min(), ec.max()]).cpu().numpy()
+    return AteResult.make(method or f"AIPW cross-fit ({learner}, K={folds})", float(v[0]),
+                          float(v[1]), e_min=float(v[2]), e_max=float(v[3]), device_scores=True)
 
 
 def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
@@ -206,8 +231,8 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
                                  ntree=cnt, seed=sd, tree_offset=t0, **kw)
         del Xt
         Xho = Xb[:, a:b].contiguous()
-        pred = F.predict_tree_parallel(fr, pcomm, Xb=Xho) if pcomm is not None else \
-            fr.predict_binned(Xho)
+        pred = F.predict_tree_parallel(fr, pcomm, Xb=Xho, host=False) if pcomm is not None \
+            else fr.predict_binned(Xho, host=False)
         out[a:b] = torch.as_tensor(pred, device=dev)
 
     if concurrent and dev.type == "cuda" and pcomm is None and engine == "gpu":
@@ -246,12 +271,10 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     else:
         for job in jobs:
             run(job)
-    e = e.clamp(clip, 1 - clip)
-    gamma = mu1 - mu0 + W * (Y - mu1) / e - (1 - W) * (Y - mu0) / (1 - e)
-    tau = float(gamma.mean())
-    se = float(gamma.std() / math.sqrt(n))
-    return AteResult.make(method, tau, se, n=n, trees=num_trees, trees_this_device=cnt,
-                          e_min=float(e.min()), e_max=float(e.max()))
+    tau, se, ec = aipw_score(Y, W, e, mu1, mu0, clip)
+    v = torch.stack([tau, se, ec.min(), ec.max()]).cpu().numpy()
+    return AteResult.make(method, float(v[0]), float(v[1]), n=n, trees=num_trees,
+                          trees_this_device=cnt, e_min=float(v[2]), e_max=float(v[3]))
 
 
 def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_seed=1991,

@@ -212,12 +212,13 @@ class Forest:
                 return None
         return res.reshape(n2, width) if width > 1 else res
 
-    def predict_binned(self, Xb):
+    def predict_binned(self, Xb, host=True):
         """Predictions for already binned rows (column-major uint8 [p][n2], a device tensor
-        for GPU forests, host array/tensor for CPU forests)."""
+        for GPU forests, host array/tensor for CPU forests); ``host=False`` keeps a GPU
+        forest's predictions on the device."""
         if self.backend == "cpu" and isinstance(Xb, torch.Tensor):
             Xb = Xb.cpu().numpy()
-        return self.predict_state(Xb, False, self.new_state(Xb.shape[1]), phases=7)
+        return self.predict_state(Xb, False, self.new_state(Xb.shape[1]), phases=7, host=host)
 
     # randomForest-style accessors
     def oob_proba(self):
@@ -474,10 +475,11 @@ def fit_forest_sharded(X, kind, ntree, comm, group=1, **kw) -> Forest:
     return fit_forest(X, kind, ntree=max(cnt, 0), group=group, tree_offset=t0, **kw)
 
 
-def predict_tree_parallel(forest: Forest, comm, X=None, oob=False, Xb=None):
+def predict_tree_parallel(forest: Forest, comm, X=None, oob=False, Xb=None, host=True):
     """Forest prediction with trees sharded over ranks: all-reduce the per-tree sums
     (C05), then (causal forests) the little-bag group sums, then finalise locally.
-    ``Xb``: already binned rows (column-major uint8 [p][n2]) instead of ``X``."""
+    ``Xb``: already binned rows (column-major uint8 [p][n2]) instead of ``X``.
+    ``host=False`` (GPU forests): the predictions stay a device tensor."""
     if Xb is None:
         Xb = forest._bins(X)
     n2 = Xb.shape[1]
@@ -491,4 +493,4 @@ def predict_tree_parallel(forest: Forest, comm, X=None, oob=False, Xb=None):
         forest.predict_state(Xb, oob, st, phases=2)
         if comm.world_size > 1:
             comm.all_reduce_(t[5 * n2:])
-    return forest.predict_state(Xb, oob, st, phases=4)
+    return forest.predict_state(Xb, oob, st, phases=4, host=host)

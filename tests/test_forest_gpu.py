@@ -84,6 +84,11 @@ def test_crossfit_and_cf_bootstrap_gpu_match_host(gpu):
     a = CF.aipw_crossfit(Yb, W, X, learner="rf", num_trees=20, device=gpu)
     b = CF.aipw_crossfit(Yb, W, X, learner="rf", num_trees=20, device="cpu")
     assert a.ate == pytest.approx(b.ate, rel=1e-10) and a.se == pytest.approx(b.se, rel=1e-10)
+    assert a.diagnostics["device_scores"]        # nuisances + score stayed on the GPU
+    for learner in ("glm", "gbdt"):
+        g = CF.aipw_crossfit(Yb, W, X, learner=learner, device=gpu, gbdt_kw={"n_trees": 8})
+        h = CF.aipw_crossfit(Yb, W, X, learner=learner, device="cpu", gbdt_kw={"n_trees": 8})
+        assert g.ate == pytest.approx(h.ate, abs=5e-3) and g.se == pytest.approx(h.se, rel=0.05)
     c = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64, device=gpu)
     d = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64, device="cpu")
     assert c.ate == pytest.approx(d.ate, rel=1e-9) and c.se == pytest.approx(d.se, rel=1e-8)
