@@ -84,6 +84,40 @@ def _gbdt_fit_predict(y, train, ho, Xb, edges, dev, seed, gbdt_kw):
     return torch.sigmoid(f) if loss == "logistic" else f
 
 
+_NAMES = ("e", "mu1", "mu0")
+
+
+class _JobCache:
+    """Per-job checkpoint of held-out nuisance predictions: job j of a
+    cross-fit (fold j // 3, nuisance _NAMES[j % 3]) saves its predictions once computed;
+    a resumed run loads finished jobs instead of refitting them. Every rank decides from
+    the same all-reduced flags (tree-parallel ranks must skip the same forests)."""
+
+    def __init__(self, ck, key, tag, comm, dev):
+        self.ck, self.key, self.tag = ck, key, tag
+        self.done = set()
+        if ck is None:
+            return
+        n = 3 * 64
+        flags = torch.tensor([float(ck.has(self.stage(j), key)) for j in range(n)],
+                             dtype=torch.float64)
+        if comm is not None and comm.world_size > 1:
+            fd = flags.to(dev) if getattr(comm, "capturable", False) else flags
+            comm.all_reduce_min_(fd)
+            flags = fd.cpu()
+        self.done = {j for j in range(n) if flags[j] > 0}
+
+    def stage(self, j):
+        return f"aipw_fold{j // 3}_{_NAMES[j % 3]}{self.tag}"
+
+    def load(self, j, dev):
+        return torch.as_tensor(self.ck.load(self.stage(j), self.key)["pred"], device=dev)
+
+    def save(self, j, pred):
+        if self.ck is not None:
+            self.ck.save(self.stage(j), self.key, pred=pred.detach().cpu().numpy())
+
+
 def aipw_score(Y, W, e, mu1, mu0, clip=0.01):
     """Textbook AIPW score on the device: Gamma = mu1 - mu0 + W (Y - mu1) / e
     - (1 - W) (Y - mu0) / (1 - e), e clipped to [clip, 1 - clip]; -> (tau, se, e)."""
@@ -94,11 +128,13 @@ def aipw_score(Y, W, e, mu1, mu0, clip=0.01):
 
 
 def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold_stream=11,
-                  clip=0.01, method=None, device=None, comm=None, gbdt_kw=None) -> AteResult:
+                  clip=0.01, method=None, device=None, comm=None, gbdt_kw=None,
+                  checkpoint=None) -> AteResult:
     """K-fold cross-fitted AIPW. X moves to ``device`` once (and is binned there for the
     tree learners); every training / held-out set is gathered on the device, every
     nuisance prediction stays there, and the score, its mean and SE are computed on the
-    device (one read-back of the result)."""
+    device (one read-back of the result). ``checkpoint`` (utils/checkpoint.Checkpoint):
+    finished (fold, nuisance) predictions are saved and reloaded on a rerun."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
     n = len(Yn)
@@ -120,17 +156,28 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
         Xd = torch.as_tensor(Xn, dtype=torch.float64, device=dev)
     else:
         raise ValueError(learner)
+    key = ""
+    if checkpoint is not None:
+        from ..utils.checkpoint import fingerprint
+        key = fingerprint(Yn, Wn, Xn, np.array([folds, num_trees, seed, fold_stream]),
+                          np.frombuffer(learner.encode(), dtype=np.uint8))
+    tag = "" if comm is None or comm.world_size == 1 else f".r{comm.rank}of{comm.world_size}"
+    cache = _JobCache(checkpoint, key, tag, comm, dev)
     jobs = []
     for k in range(folds):
         ho = fid == k
         tr = ~ho
         t1, t0 = tr & (Wd == 1), tr & (Wd == 0)
         sd = seed + 1000 * (k + 1)
-        jobs += [(e, ho, tr, Wd, sd), (mu1, ho, t1, Yd, sd + 1), (mu0, ho, t0, Yd, sd + 2)]
+        jobs += [(e, ho, tr, Wd, sd, 3 * k), (mu1, ho, t1, Yd, sd + 1, 3 * k + 1),
+                 (mu0, ho, t0, Yd, sd + 2, 3 * k + 2)]
 
     def run(job):
-        out, ho, rows, target, sd = job
+        out, ho, rows, target, sd, j = job
         hoi = ho.nonzero().squeeze(1)
+        if j in cache.done:
+            out.index_copy_(0, hoi, cache.load(j, dev))
+            return
         if learner == "rf":
             ri = rows.nonzero().squeeze(1)
             r = _rf_fit_predict(Xb, ri, target.index_select(0, ri), hoi, num_trees, sd, dev,
@@ -141,6 +188,7 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
         else:
             r = _gbdt_fit_predict(target, rows, ho, Xb, edges, dev, sd, gbdt_kw)
         out.index_copy_(0, hoi, r)
+        cache.save(j, r)
 
     concurrent = learner == "rf" and dev.type == "cuda" and (comm is None or comm.world_size == 1)
     if concurrent:
@@ -169,7 +217,8 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
 
 def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
                            tree_shard=None, concurrent=True, engine="gpu",
-                           method="AIPW cross-fit (rf, HBM panel)") -> AteResult:
+                           method="AIPW cross-fit (rf, HBM panel)", checkpoint=None,
+                           data_key="") -> AteResult:
     """Config 3 on an HBM-resident panel (data/device_dgp.synthetic_panel, segment k =
     fold k): the panel's feature columns are binned on the device (``bin_panel``, no host
     copy of X) into the forest engine's column-major uint8 layout; per fold, the
@@ -185,7 +234,8 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     by side on separate streams, in batches that fit free HBM (a forest of T trees fills
     only T CUs).
     ``engine="cpu"`` grows the same forests on the host engine from the same device bins
-    (bit-identical trees; the parity test)."""
+    (bit-identical trees; the parity test). ``checkpoint`` + ``data_key`` (a name of the
+    panel's data): per (fold, nuisance) held-out predictions saved / resumed."""
     from .boosting import bin_panel
     dev = pan.device
     K = pan.nseg
@@ -210,16 +260,26 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     mu1 = torch.empty_like(e)
     mu0 = torch.empty_like(e)
     ar = torch.arange(n, device=dev)
+    tag = "" if pcomm is None else f".r{rank}of{world}"
+    key = f"{data_key}.{n}.{p}.{num_trees}.{seed}.{t0}.{cnt}" if checkpoint is not None else ""
+    cache = _JobCache(checkpoint, key, tag, pcomm, dev)
     jobs = []
     for k in range(K):
         a, b = int(c0[k]), int(c0[k + 1])
         tr = (ar < a) | (ar >= b)
         sd = seed + 1000 * (k + 1)
-        jobs += [(e, tr, W, sd, a, b), (mu1, tr & (W == 1), Y, sd + 1, a, b),
-                 (mu0, tr & (W == 0), Y, sd + 2, a, b)]
+        jobs += [(e, tr, W, sd, a, b, 3 * k), (mu1, tr & (W == 1), Y, sd + 1, a, b, 3 * k + 1),
+                 (mu0, tr & (W == 0), Y, sd + 2, a, b, 3 * k + 2)]
+    todo = []
+    for jb in jobs:                          # finished jobs of an earlier run: load them
+        if jb[-1] in cache.done:
+            jb[0][jb[4]:jb[5]] = cache.load(jb[-1], dev)
+        else:
+            todo.append(jb)
+    jobs = todo
 
     def run(job):
-        out, mask, target, sd, a, b = job
+        out, mask, target, sd, a, b, j = job
         idx = mask.nonzero().squeeze(1)
         yt = target.index_select(0, idx)
         binary = bool(((yt == 0) | (yt == 1)).all())
@@ -234,6 +294,7 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
         pred = F.predict_tree_parallel(fr, pcomm, Xb=Xho, host=False) if pcomm is not None \
             else fr.predict_binned(Xho, host=False)
         out[a:b] = torch.as_tensor(pred, device=dev)
+        cache.save(j, out[a:b])
 
     if concurrent and dev.type == "cuda" and pcomm is None and engine == "gpu":
         # the 3K forests are independent: grow them side by side (one stream per host
@@ -279,19 +340,52 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
 
 def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_seed=1991,
                             method="Causal Forest(GRF) + bootstrap SE", device=None, comm=None,
-                            nuisance_trees=None) -> AteResult:
+                            nuisance_trees=None, checkpoint=None, boot_chunk=250) -> AteResult:
     """Config 4: grf-style causal forest (trees sharded over ``comm``), AIPW scores
     Gamma_i from the OOB CATEs, and B multinomial bootstrap replicates of mean(Gamma)
-    sharded over the ranks (C07); SE = sd of the replicates."""
+    sharded over the ranks (C07); SE = sd of the replicates. The scores are formed and
+    resampled on the device. ``checkpoint``: the forest outputs and every range of
+    ``boot_chunk`` replicates are saved once computed; a rerun resumes from them with
+    identical results (every draw is keyed by (seed, replicate, row))."""
     from .linear import bootstrap_replicates
     dev = resolve_device(device)
-    cf = F.causal_forest(as_np(X), as_np(Y), as_np(W), num_trees=num_trees, seed=seed,
-                         nuisance_trees=nuisance_trees, backend=_backend(dev), comm=comm)
-    est, se_aipw = F.average_treatment_effect(cf)
-    w_res = cf.W - cf.w_hat
-    tau = np.where(np.isnan(cf.tau_oob), np.nanmean(cf.tau_oob), cf.tau_oob)
-    what = np.clip(cf.w_hat, 1e-6, 1 - 1e-6)
-    gamma = tau + w_res / (what * (1 - what)) * (cf.Y - cf.y_hat - tau * w_res)
-    g = torch.as_tensor(gamma, device=dev)
-    taus = bootstrap_replicates(g, torch.zeros_like(g), B, boot_seed, comm)
-    return AteResult.make(method, est, float(taus.std(unbiased=True)), se_aipw=se_aipw, B=B)
+    Xn, Yn, Wn = as_np(X), as_np(Y), as_np(W)
+    key, tag = "", ""
+    if checkpoint is not None:
+        from ..utils.checkpoint import fingerprint
+        key = fingerprint(Yn, Wn, Xn, np.array([num_trees, seed, nuisance_trees or 0]))
+        tag = "" if comm is None or comm.world_size == 1 else f".r{comm.rank}of{comm.world_size}"
+    stage = f"cf_fit{tag}"
+    if checkpoint is not None and checkpoint.has(stage, key):
+        z = checkpoint.load(stage, key)
+        y_hat, w_hat, tau_oob = z["y_hat"], z["w_hat"], z["tau_oob"]
+    else:
+        cf = F.causal_forest(Xn, Yn, Wn, num_trees=num_trees, seed=seed,
+                             nuisance_trees=nuisance_trees, backend=_backend(dev), comm=comm)
+        y_hat, w_hat, tau_oob = cf.y_hat, cf.w_hat, cf.tau_oob
+        if checkpoint is not None:
+            checkpoint.save(stage, key, y_hat=y_hat, w_hat=w_hat, tau_oob=tau_oob,
+                            var_oob=cf.var_oob)
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)
+    Yd, Wd, yh, wh, to = t(Yn), t(Wn), t(y_hat), t(w_hat), t(tau_oob)
+    w_res = Wd - wh
+    tau = torch.where(torch.isnan(to), torch.nanmean(to), to)
+    what = wh.clamp(1e-6, 1 - 1e-6)
+    g = tau + w_res / (what * (1 - what)) * (Yd - yh - tau * w_res)
+    n = g.numel()
+    est, se_aipw = g.mean(), g.std() / math.sqrt(n)      # models/forest.average_treatment_effect
+    zeros = torch.zeros_like(g)
+    parts = []
+    for b0 in range(0, B, boot_chunk):
+        nb = min(boot_chunk, B - b0)
+        bst = f"cf_boot_{b0}_{b0 + nb}{tag}"
+        if checkpoint is not None and checkpoint.has(bst, key + f".{boot_seed}"):
+            parts.append(t(checkpoint.load(bst, key + f".{boot_seed}")["taus"]))
+            continue
+        tb = bootstrap_replicates(g, zeros, nb, boot_seed, comm, b_start=b0)
+        if checkpoint is not None:
+            checkpoint.save(bst, key + f".{boot_seed}", taus=tb.cpu().numpy())
+        parts.append(tb.to(dev))
+    taus = torch.cat(parts)
+    v = torch.stack([est, taus.std(unbiased=True), se_aipw]).cpu().numpy()
+    return AteResult.make(method, float(v[0]), float(v[1]), se_aipw=float(v[2]), B=B)

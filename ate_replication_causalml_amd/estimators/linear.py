@@ -256,14 +256,16 @@ def bootstrap_sharded(e1, e2, B, seed, dist):
     return bootstrap_replicates(e1f, e2f, B, seed, dist.comm)
 
 
-def bootstrap_replicates(e1, e2, B, seed, comm=None):
-    """tau_b for b < B with the replicates sharded over ``comm`` (rows replicated on
-    every rank): rank r evaluates [b0, b0+B_r) with the same global-index Philox draws
-    as one device, then the estimates are all-gathered in rank order (C07)."""
+def bootstrap_replicates(e1, e2, B, seed, comm=None, b_start=0):
+    """tau_b for b_start <= b < b_start + B with the replicates sharded over ``comm``
+    (rows replicated on every rank): rank r evaluates its slice with the same
+    global-index Philox draws as one device, then the estimates are all-gathered in rank
+    order (C07). ``b_start`` lets a long run resample in checkpointed ranges."""
     from ..parallel.dist import shard_range
     world = comm.world_size if comm is not None else 1
     rank = comm.rank if comm is not None else 0
     b0, nb = shard_range(B, rank, world)
+    b0 += b_start
     mine = S.bootstrap_multinomial(e1.contiguous(), e2.contiguous(), nb, seed, b0=b0) \
         if nb else torch.empty(0, dtype=torch.float64, device=e1.device)
     if world == 1:

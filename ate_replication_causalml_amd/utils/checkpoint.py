@@ -1,7 +1,17 @@
 """Checkpoint / resume of long runs.
 
 Nuisance predictions per fold and bootstrap replicate ranges are cached as ``.npz``
-files keyed by a hash of (stage name, configuration, data fingerprint). Because all
+files keyed by a hash of (stage name, configuration, data fingerprint). Users:
+
+* ``estimators/boosting.py`` (config 5 DML-GBDT, host arrays and HBM panel): the
+  held-out E[Y|X], E[W|X] predictions of every finished fold (per rank);
+* ``estimators/crossfit.py``: the held-out predictions of every (fold, nuisance) of the
+  AIPW cross-fits (config 3, host arrays and HBM panel), and for the causal-forest
+  bootstrap (config 4) the forest outputs and each range of bootstrap replicates;
+* ``api.replicate``: every finished row of the 14-estimator driver.
+
+Tests kill each of these mid-run and resume to bitwise-identical results
+(tests/test_gbdt.py, tests/test_crossfit.py, tests/test_robustness.py). Because all
 randomness is counter-based Philox keyed by (seed, purpose, stream, index), a resumed
 run reproduces the uninterrupted one bit for bit: completed stages are loaded, the
 rest recomputed. Files are written atomically (tmp + rename) and loaded with

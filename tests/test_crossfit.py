@@ -59,3 +59,64 @@ def test_crossfit_and_cf_bootstrap_tree_parallel():
     for a, b in run_simulated(2, fn):
         assert a.ate == pytest.approx(a1.ate, rel=1e-10) and a.se == pytest.approx(a1.se, rel=1e-9)
         assert b.ate == pytest.approx(b1.ate, rel=1e-9) and b.se == pytest.approx(b1.se, rel=1e-7)
+
+
+class _Killed(RuntimeError):
+    pass
+
+
+@pytest.mark.parametrize("learner", ["rf", "glm"])
+def test_aipw_crossfit_checkpoint_resume(learner, tmp_path, monkeypatch):
+    """A cross-fit killed after fold 2 resumes from its per-(fold, nuisance) checkpoints:
+    only the missing nuisances are refit and the ATE / SE are bitwise identical."""
+    from ate_replication_causalml_amd.utils.checkpoint import Checkpoint
+    X, W, Y, _ = _toy(1500, 4)
+    kw = dict(learner=learner, num_trees=12, device="cpu")
+    want = CF.aipw_crossfit(Y, W, X, **kw)
+    name = "_rf_fit_predict" if learner == "rf" else "_glm_fit_predict"
+    real = getattr(CF, name)
+    calls = {"n": 0, "die": 9}                  # folds 0-2 = 9 nuisance fits
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        if calls["n"] > calls["die"]:
+            raise _Killed()
+        return real(*a, **k)
+    monkeypatch.setattr(CF, name, counted)
+    ck = Checkpoint(tmp_path, {"cfg": "aipw"})
+    with pytest.raises(_Killed):
+        CF.aipw_crossfit(Y, W, X, checkpoint=ck, **kw)
+    assert len(list(tmp_path.glob("aipw_fold*.npz"))) == 9
+    calls.update(n=0, die=10 ** 9)
+    got = CF.aipw_crossfit(Y, W, X, checkpoint=ck, **kw)
+    assert calls["n"] == 6                      # folds 3 and 4 only
+    assert got.ate == want.ate and got.se == want.se
+
+
+def test_cf_bootstrap_checkpoint_resume(tmp_path, monkeypatch):
+    """Config 4: the forest outputs and the bootstrap ranges are checkpointed; a run
+    killed after the first replicate range resumes to the identical SE."""
+    from ate_replication_causalml_amd.estimators import linear as L
+    from ate_replication_causalml_amd.utils.checkpoint import Checkpoint
+    X, W, Y, _ = _toy(800, 5)
+    kw = dict(num_trees=16, nuisance_trees=8, B=60, device="cpu", boot_chunk=20)
+    want = CF.causal_forest_bootstrap(Y, W, X, **kw)
+    real = L.bootstrap_replicates
+    calls = {"n": 0, "die": 1}
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        if calls["n"] > calls["die"]:
+            raise _Killed()
+        return real(*a, **k)
+    monkeypatch.setattr(L, "bootstrap_replicates", counted)
+    ck = Checkpoint(tmp_path, {"cfg": 4})
+    with pytest.raises(_Killed):
+        CF.causal_forest_bootstrap(Y, W, X, checkpoint=ck, **kw)
+    calls.update(n=0, die=10 ** 9)
+    from ate_replication_causalml_amd.models import forest as F
+    monkeypatch.setattr(F, "causal_forest", lambda *a, **k: (_ for _ in ()).throw(
+        AssertionError("the forest must come from the checkpoint")))
+    got = CF.causal_forest_bootstrap(Y, W, X, checkpoint=ck, **kw)
+    assert calls["n"] == 2                       # replicate ranges 2 and 3 only
+    assert got.ate == want.ate and got.se == want.se
