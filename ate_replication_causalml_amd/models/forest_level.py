@@ -32,7 +32,7 @@ class LvHost(ctypes.Structure):
     _fields_ = [("fp", F.ForestParams), ("Xb", P), ("ycls", P), ("r1", P), ("w", P), ("idx", P),
                 ("idx2", P), ("cur", P), ("dec", P), ("nl", P), ("cap", ctypes.c_int),
                 ("feat", P), ("thr", P), ("left", P), ("val", P), ("depth", ctypes.c_int),
-                ("fst", ctypes.c_int64), ("rst", ctypes.c_int64), ("Xc", P)]
+                ("fst", ctypes.c_int64), ("rst", ctypes.c_int64), ("Xc", P), ("nbin", P)]
 
 
 def supported(fp: F.ForestParams) -> bool:
@@ -122,7 +122,10 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         fst, rst = 1, p
     else:
         Xg, fst, rst = Xb, n, 1
-    h = LvHost(fp=fp, Xb=Xg.data_ptr(), Xc=Xb.data_ptr(),
+    # bins per feature (max bin + 1 over the training rows): few-bin features spread their
+    # LDS histograms over the 256 slots (csrc/forest_level.hip lv_spread)
+    nbin = (Xb.amax(dim=1).to(torch.int32) + 1).to(torch.int16).contiguous()
+    h = LvHost(fp=fp, Xb=Xg.data_ptr(), Xc=Xb.data_ptr(), nbin=nbin.data_ptr(),
                ycls=yt.data_ptr() if yt is not None else None,
                r1=r1t.data_ptr() if r1t is not None else None, w=w.data_ptr(), cap=cap,
                feat=feat.data_ptr(), thr=thr.data_ptr(), left=left.data_ptr(),

@@ -100,6 +100,54 @@ __device__ __forceinline__ void lv_scan(const int64_t* h0, const int64_t* h1, in
   *bin = lbin;
 }
 
+// LDS atomics of few-bin features (binary covariates: 64 lanes on 2 x 2 addresses) serialise
+// in the LDS. A feature with nb bins therefore SPREADS its histogram over the same 256 slots:
+// slot = bin * S + (lane & (S - 1)), S = the largest power of two <= 64 with nb * S <= 256,
+// so lanes of a wave hit different slots; lv_collapse folds the S copies back into bins
+// [0, nb) (exact integer sums) before a scan reads them.
+__device__ __forceinline__ int lv_spread(int nb) {
+  int S = 1;
+  while (S < 64 && nb * (S * 2) <= NBINS) S *= 2;
+  return S;
+}
+
+// one wave folds a spread two-channel histogram in place (slots >= nb end up zero)
+__device__ void lv_collapse(int64_t* h0, int64_t* h1, int S) {
+  if (S == 1) return;
+  const int lane = threadIdx.x & 63;
+  int64_t a[4], b[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { a[e] = h0[4 * lane + e]; b[e] = h1[4 * lane + e]; }
+  int64_t p0, p1, q0 = 0, q1 = 0;
+  if (S == 2) {                                   // lane holds bins 2L (slots 0,1), 2L+1 (2,3)
+    p0 = a[0] + a[1]; q0 = a[2] + a[3];
+    p1 = b[0] + b[1]; q1 = b[2] + b[3];
+  } else {                                        // lane holds part of bin 4L / S
+    p0 = a[0] + a[1] + a[2] + a[3];
+    p1 = b[0] + b[1] + b[2] + b[3];
+    for (int o = 1; o < S / 4; o <<= 1) {
+      p0 += __shfl_xor(p0, o, 64);
+      p1 += __shfl_xor(p1, o, 64);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { h0[4 * lane + e] = 0; h1[4 * lane + e] = 0; }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  if (S == 2) {
+    h0[2 * lane] = p0; h0[2 * lane + 1] = q0;
+    h1[2 * lane] = p1; h1[2 * lane + 1] = q1;
+  } else if ((lane & (S / 4 - 1)) == 0) {
+    const int bin = lane / (S / 4);
+    h0[bin] = p0;
+    h1[bin] = p1;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+}
+
 // the partial Fisher-Yates draw of a node's candidate features (forest.hip / host order):
 // perm[0..nf) in a per-wave LDS buffer of p int16
 __device__ void lv_draw(const ForestParams& fp, int tg, int v, int nf, int16_t* perm) {
@@ -172,6 +220,7 @@ struct LvArgs {
   ForestParams fp;
   const uint8_t* Xb;      // bins: element (feature f, row i) at f * fst + i * rst
   const uint8_t* Xc;      // the same bins column-major [p][n] (dense big-node streams)
+  const int16_t* nbin;    // [p] bins per feature (edges + 1)
   const uint8_t* ycls;    // kind 0: [n] class
   const int64_t* r1;      // kind 1: [n] response, 2^-32 fixed point
   const int32_t* w;       // [T][n] bootstrap counts
@@ -194,10 +243,12 @@ struct LvArgs {
 // loads, then every row's weight / label / LV_FG bins, then the LDS atomics) into the LDS
 // histograms sh[k][c][bin] of the nk features xf[0..nk)
 __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __restrict__ wt,
-                                              const uint8_t* const* xf, int64_t rst, int nk,
-                                              int q0, int q1, int64_t (*sh)[2][NBINS]) {
+                                              const uint8_t* const* xf, const int* sp,
+                                              int64_t rst, int nk, int q0, int q1,
+                                              int64_t (*sh)[2][NBINS]) {
   constexpr int U = 4;
   const int kind = a.fp.kind;
+  const int lane = threadIdx.x & 63;
   for (int base = q0 + threadIdx.x; base < q1; base += 256 * U) {
     int ii[U];
 #pragma unroll
@@ -223,12 +274,12 @@ __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __
 #pragma unroll
       for (int k = 0; k < LV_FG; ++k) {
         if (k >= nk) break;
+        const int slot = bins[u][k] * sp[k] + (lane & (sp[k] - 1));
         if (kind == 0) {
-          atomicAdd((unsigned long long*)&sh[k][yv[u]][bins[u][k]], (unsigned long long)wv[u]);
+          atomicAdd((unsigned long long*)&sh[k][yv[u]][slot], (unsigned long long)wv[u]);
         } else {
-          atomicAdd((unsigned long long*)&sh[k][0][bins[u][k]], (unsigned long long)wv[u]);
-          atomicAdd((unsigned long long*)&sh[k][1][bins[u][k]],
-                    (unsigned long long)(wv[u] * rv[u]));
+          atomicAdd((unsigned long long*)&sh[k][0][slot], (unsigned long long)wv[u]);
+          atomicAdd((unsigned long long*)&sh[k][1][slot], (unsigned long long)(wv[u] * rv[u]));
         }
       }
     }
@@ -308,12 +359,18 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   const int32_t* wt = a.w + (int64_t)nd.tree * n;
   for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
   const uint8_t* xf[LV_FG];
+  int sp[LV_FG];
 #pragma unroll
-  for (int k = 0; k < LV_FG; ++k)
-    xf[k] = a.Xc + (int64_t)drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)] * n;
+  for (int k = 0; k < LV_FG; ++k) {
+    const int f = drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)];
+    xf[k] = a.Xc + (int64_t)f * n;
+    sp[k] = lv_spread(a.nbin[f]);
+  }
   __syncthreads();
   // big nodes hold dense runs of ascending positions: the column-major bins stream
-  lv_accumulate(a, wt, xf, 1, nk, item_q0[it], item_q1[it], sh);
+  lv_accumulate(a, wt, xf, sp, 1, nk, item_q0[it], item_q1[it], sh);
+  __syncthreads();
+  for (int k = threadIdx.x >> 6; k < nk; k += 4) lv_collapse(sh[k][0], sh[k][1], sp[k]);
   __syncthreads();
   int64_t* hs = hist + ((int64_t)slot * fs + k0) * 2 * NBINS;
   for (int e = threadIdx.x; e < nk * 2 * NBINS; e += 256) {
@@ -414,10 +471,17 @@ __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __
     const int nk = min(LV_FG, nf - k0);
     for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
     const uint8_t* xf[LV_FG];
+    int sp[LV_FG];
 #pragma unroll
-    for (int k = 0; k < LV_FG; ++k) xf[k] = a.Xb + (int64_t)perm[k0 + min(k, nk - 1)] * a.fst;
+    for (int k = 0; k < LV_FG; ++k) {
+      const int f = perm[k0 + min(k, nk - 1)];
+      xf[k] = a.Xb + (int64_t)f * a.fst;
+      sp[k] = lv_spread(a.nbin[f]);
+    }
     __syncthreads();
-    lv_accumulate(a, wt, xf, a.rst, nk, nd.lo, nd.hi, sh);
+    lv_accumulate(a, wt, xf, sp, a.rst, nk, nd.lo, nd.hi, sh);
+    __syncthreads();
+    for (int k = wid; k < nk; k += 4) lv_collapse(sh[k][0], sh[k][1], sp[k]);
     __syncthreads();
     if (k0 == 0) {
       if (wid == 0) {
@@ -546,12 +610,15 @@ __global__ __launch_bounds__(256) void lv_small_kernel(LvArgs a, const int32_t* 
         for (int b = lane; b < NBINS; b += 64) { hist[wid][0][b] = 0; hist[wid][1][b] = 0; }
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
+        const int S = lv_spread(a.nbin[f]);
         if (valid) {
-          atomicAdd((unsigned long long*)&hist[wid][0][bins[u]], (unsigned long long)v0);
-          atomicAdd((unsigned long long*)&hist[wid][1][bins[u]], (unsigned long long)v1);
+          const int slot = bins[u] * S + (lane & (S - 1));
+          atomicAdd((unsigned long long*)&hist[wid][0][slot], (unsigned long long)v0);
+          atomicAdd((unsigned long long*)&hist[wid][1][slot], (unsigned long long)v1);
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
+        lv_collapse(hist[wid][0], hist[wid][1], S);
         lv_scan(hist[wid][0], hist[wid][1], kind, nw, n1, s1, minc, &lbest, &lbin);
         __builtin_amdgcn_wave_barrier();
       }
@@ -754,6 +821,7 @@ struct LvHost {
   int depth;
   int64_t fst, rst;
   const void* Xc;
+  const void* nbin;
 };
 
 static LvArgs lv_args(const LvHost& h) {
@@ -777,6 +845,7 @@ static LvArgs lv_args(const LvHost& h) {
   a.fst = h.fst;
   a.rst = h.rst;
   a.Xc = (const uint8_t*)h.Xc;
+  a.nbin = (const int16_t*)h.nbin;
   return a;
 }
 
