@@ -61,7 +61,8 @@ __device__ __forceinline__ double lv_crit(int kind, int64_t L0, int64_t L1, int6
 
 // one wave scans a feature's two-channel histogram (h0, h1: 256 bins each, any memory):
 // max criterion, lowest bin on ties (bin NBINS when nothing is admissible)
-__device__ __forceinline__ void lv_scan(const int64_t* h0, const int64_t* h1, int kind, int64_t nw,
+template <typename HT>
+__device__ __forceinline__ void lv_scan(const HT* h0, const HT* h1, int kind, int64_t nw,
                                         int64_t n1, int64_t s1, int minc, double* best,
                                         int* bin) {
   const int lane = threadIdx.x & 63;
@@ -69,8 +70,8 @@ __device__ __forceinline__ void lv_scan(const int64_t* h0, const int64_t* h1, in
   int64_t a0 = 0, a1 = 0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    a0 += h0[4 * lane + e];
-    a1 += h1[4 * lane + e];
+    a0 += (int64_t)h0[4 * lane + e];
+    a1 += (int64_t)h1[4 * lane + e];
     c0[e] = a0;
     c1[e] = a1;
   }
@@ -112,13 +113,14 @@ __device__ __forceinline__ int lv_spread(int nb) {
 }
 
 // one wave folds a spread two-channel histogram in place (slots >= nb end up zero)
-__device__ void lv_collapse(int64_t* h0, int64_t* h1, int S) {
+template <typename HT>
+__device__ void lv_collapse(HT* h0, HT* h1, int S) {
   if (S == 1) return;
   const int lane = threadIdx.x & 63;
-  int64_t a[4], b[4];
+  HT a[4], b[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) { a[e] = h0[4 * lane + e]; b[e] = h1[4 * lane + e]; }
-  int64_t p0, p1, q0 = 0, q1 = 0;
+  HT p0, p1, q0 = 0, q1 = 0;
   if (S == 2) {                                   // lane holds bins 2L (slots 0,1), 2L+1 (2,3)
     p0 = a[0] + a[1]; q0 = a[2] + a[3];
     p1 = b[0] + b[1]; q1 = b[2] + b[3];
@@ -242,11 +244,13 @@ struct LvArgs {
 // accumulate rows [q0, q1) (stride 256 per thread, 4 rows per thread in flight: the idx
 // loads, then every row's weight / label / LV_FG bins, then the LDS atomics) into the LDS
 // histograms sh[k][c][bin] of the nk features xf[0..nk)
+// HT: LDS histogram element (uint32 for kind 0: integer weights; int64 for kind 1),
+// FG: features per pass, U: rows in flight per thread
+template <typename HT, int FG, int U>
 __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __restrict__ wt,
-                                              const uint8_t* const* xf, const int* sp,
-                                              int64_t rst, int nk, int q0, int q1,
-                                              int64_t (*sh)[2][NBINS]) {
-  constexpr int U = 4;
+                                              const uint8_t* X, const int* fi, int64_t fst,
+                                              const int* sp, int64_t rst, int nk, int q0, int q1,
+                                              HT (*sh)[2][NBINS]) {
   const int kind = a.fp.kind;
   const int lane = threadIdx.x & 63;
   for (int base = q0 + threadIdx.x; base < q1; base += 256 * U) {
@@ -258,7 +262,7 @@ __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __
     }
     int64_t wv[U], rv[U];
     int yv[U];
-    int bins[U][LV_FG];
+    int bins[U][FG];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = ii[u] < 0 ? 0 : ii[u];
@@ -266,16 +270,18 @@ __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __
       yv[u] = kind == 0 ? a.ycls[i] : 0;
       rv[u] = kind == 0 ? 0 : a.r1[i];
 #pragma unroll
-      for (int k = 0; k < LV_FG; ++k) bins[u][k] = xf[k][(int64_t)i * rst];
+      for (int k = 0; k < FG; ++k) bins[u][k] = X[(int64_t)fi[k] * fst + (int64_t)i * rst];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (ii[u] < 0) continue;
 #pragma unroll
-      for (int k = 0; k < LV_FG; ++k) {
+      for (int k = 0; k < FG; ++k) {
         if (k >= nk) break;
         const int slot = bins[u][k] * sp[k] + (lane & (sp[k] - 1));
-        if (kind == 0) {
+        if constexpr (sizeof(HT) == 4) {                    // kind 0: class weights
+          atomicAdd((unsigned int*)&sh[k][yv[u]][slot], (unsigned int)wv[u]);
+        } else if (kind == 0) {
           atomicAdd((unsigned long long*)&sh[k][yv[u]][slot], (unsigned long long)wv[u]);
         } else {
           atomicAdd((unsigned long long*)&sh[k][0][slot], (unsigned long long)wv[u]);
@@ -358,17 +364,15 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   const int n = a.fp.n;
   const int32_t* wt = a.w + (int64_t)nd.tree * n;
   for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
-  const uint8_t* xf[LV_FG];
-  int sp[LV_FG];
+  int fi[LV_FG], sp[LV_FG];
 #pragma unroll
   for (int k = 0; k < LV_FG; ++k) {
-    const int f = drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)];
-    xf[k] = a.Xc + (int64_t)f * n;
-    sp[k] = lv_spread(a.nbin[f]);
+    fi[k] = drawn[(int64_t)slot * LV_MAXF + k0 + min(k, nk - 1)];
+    sp[k] = lv_spread(a.nbin[fi[k]]);
   }
   __syncthreads();
   // big nodes hold dense runs of ascending positions: the column-major bins stream
-  lv_accumulate(a, wt, xf, sp, 1, nk, item_q0[it], item_q1[it], sh);
+  lv_accumulate<int64_t, LV_FG, 4>(a, wt, a.Xc, fi, n, sp, 1, nk, item_q0[it], item_q1[it], sh);
   __syncthreads();
   for (int k = threadIdx.x >> 6; k < nk; k += 4) lv_collapse(sh[k][0], sh[k][1], sp[k]);
   __syncthreads();
@@ -443,9 +447,14 @@ __global__ __launch_bounds__(256) void lv_big_split_kernel(LvArgs a, const int32
 }
 
 // ------------------------------------------------------------------ MID nodes
-// one workgroup (4 waves) per node with 65 .. LV_BIG rows
+// one workgroup (4 waves) per node with 65 .. t3 rows. Kind 0 (class weights) keeps
+// uint32 histograms of 24 features in LDS (48 KB), so mtry <= 24 candidates take ONE pass
+// over the node's rows: a row's drawn bins (row-major: its few cache lines) are fetched
+// once, not once per feature group (the groups' re-reads were the HBM traffic of the
+// deep levels). Kind 1 (int64 sums) takes groups of 8.
+template <typename HT, int FG, int U>
 __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __restrict__ mlist) {
-  __shared__ int64_t sh[LV_FG][2][NBINS];
+  __shared__ HT sh[FG][2][NBINS];
   __shared__ int16_t perm[LV_PMAX];
   __shared__ double rbest[LV_MAXF];
   __shared__ int rbin[LV_MAXF];
@@ -467,26 +476,24 @@ __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __
   const int nf = snf;
   int64_t nw = 0, n1 = 0, s1 = 0;
   int minc = 1;
-  for (int k0 = 0; k0 < nf; k0 += LV_FG) {
-    const int nk = min(LV_FG, nf - k0);
-    for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
-    const uint8_t* xf[LV_FG];
-    int sp[LV_FG];
+  for (int k0 = 0; k0 < nf; k0 += FG) {
+    const int nk = min(FG, nf - k0);
+    for (int e = threadIdx.x; e < FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
+    int fi[FG], sp[FG];
 #pragma unroll
-    for (int k = 0; k < LV_FG; ++k) {
-      const int f = perm[k0 + min(k, nk - 1)];
-      xf[k] = a.Xb + (int64_t)f * a.fst;
-      sp[k] = lv_spread(a.nbin[f]);
+    for (int k = 0; k < FG; ++k) {
+      fi[k] = perm[k0 + min(k, nk - 1)];
+      sp[k] = lv_spread(a.nbin[fi[k]]);
     }
     __syncthreads();
-    lv_accumulate(a, wt, xf, sp, a.rst, nk, nd.lo, nd.hi, sh);
+    lv_accumulate<HT, FG, U>(a, wt, a.Xb, fi, a.fst, sp, a.rst, nk, nd.lo, nd.hi, sh);
     __syncthreads();
     for (int k = wid; k < nk; k += 4) lv_collapse(sh[k][0], sh[k][1], sp[k]);
     __syncthreads();
     if (k0 == 0) {
       if (wid == 0) {
         int64_t c0 = 0, c1 = 0;
-        for (int e = lane; e < NBINS; e += 64) { c0 += sh[0][0][e]; c1 += sh[0][1][e]; }
+        for (int e = lane; e < NBINS; e += 64) { c0 += (int64_t)sh[0][0][e]; c1 += (int64_t)sh[0][1][e]; }
         c0 = lv_wsum(c0);
         c1 = lv_wsum(c1);
         if (lane == 0) {
@@ -883,9 +890,15 @@ ATE_API int ate_lv_decide(const void* hp, const void* small, int nsmall, const v
   if (nsmall)
     hipLaunchKernelGGL(lv_small_kernel, dim3((nsmall + 3) / 4), dim3(256), 0, st, a,
                        (const int32_t*)small, nsmall);
-  if (nmid) hipLaunchKernelGGL(lv_mid_kernel, dim3(nmid), dim3(256), 0, st, a, (const int32_t*)mid);
-  if (nmid2)
-    hipLaunchKernelGGL(lv_mid_kernel, dim3(nmid2), dim3(256), 0, st, a, (const int32_t*)mid2);
+  for (int c = 0; c < 2; ++c) {
+    const int cnt = c == 0 ? nmid : nmid2;
+    const int32_t* L = (const int32_t*)(c == 0 ? mid : mid2);
+    if (!cnt) continue;
+    if (h.fp.kind == 0)
+      hipLaunchKernelGGL((lv_mid_kernel<uint32_t, 24, 1>), dim3(cnt), dim3(256), 0, st, a, L);
+    else
+      hipLaunchKernelGGL((lv_mid_kernel<int64_t, LV_FG, 4>), dim3(cnt), dim3(256), 0, st, a, L);
+  }
   if (nbig) {
     const int32_t* B = (const int32_t*)big;
     hipLaunchKernelGGL(lv_big_draw_kernel, dim3((nbig + 3) / 4), dim3(256), 0, st, a, B, nbig,
