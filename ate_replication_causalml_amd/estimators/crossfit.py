@@ -17,6 +17,7 @@ Learners: ``"rf"`` (histogram forests; ``comm`` shards the trees over ranks, C05
 from __future__ import annotations
 
 import math
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -308,10 +309,13 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
             return (p * nt + cnt * (2 * nt + 1) * 20 + cnt * nt
                     + int(lib.ate_forest_scratch_bytes(nt, cnt)))
 
+        # forests on the level engine fill the GPU by themselves: a few side by side only
+        # hide each other's per-level host syncs (ATE_CF_CONCURRENT caps the batch)
+        cap_b = int(os.environ.get("ATE_CF_CONCURRENT", "0")) or len(jobs)
         batches, cur_b, used = [], [], 0
         for job in jobs:
             m = need(job)
-            if cur_b and used + m > 0.6 * free:
+            if cur_b and (used + m > 0.6 * free or len(cur_b) >= cap_b):
                 batches.append(cur_b)
                 cur_b, used = [], 0
             cur_b.append(job)
