@@ -71,6 +71,7 @@ _SIGS = {
     "ate_lv_partition": "ppipippppipp",
     "ate_lv_scatter": "pppppippp",
     "ate_lv_children": "pippppp",
+    "ate_lv_transpose": "piipip",
     "ate_gbdt_bin_panel": "pilpipppilpppl" + "p",
     "ate_gbdt_slab_entries": "liii",
     "ate_gbdt_apply": "plliipppp" + "p",

@@ -306,12 +306,17 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
 
         def need(job):
             nt = int(job[1].sum())
-            return (p * nt + cnt * (2 * nt + 1) * 20 + cnt * nt
-                    + int(lib.ate_forest_scratch_bytes(nt, cnt)))
+            base = p * nt + cnt * (2 * nt + 1) * 20 + cnt * nt      # bins, trees, in-bag
+            if F.LEVEL_MIN_ROWS <= nt:
+                # level engine: row-major copy, weights / positions, level lists
+                return base + p * nt + cnt * nt * 12 + cnt * nt * 56
+            return base + int(lib.ate_forest_scratch_bytes(nt, cnt))
 
         # forests on the level engine fill the GPU by themselves: a few side by side only
-        # hide each other's per-level host syncs (ATE_CF_CONCURRENT caps the batch)
-        cap_b = int(os.environ.get("ATE_CF_CONCURRENT", "0")) or len(jobs)
+        # hide each other's per-level host syncs (ATE_CF_CONCURRENT caps the batch;
+        # profiles/r03_forest: 1 -> 10.3 s, 2 -> 9.4, 3 -> 8.7, 5 -> 8.4 for the config-3
+        # per-GPU shard)
+        cap_b = int(os.environ.get("ATE_CF_CONCURRENT", "5")) or len(jobs)
         batches, cur_b, used = [], [], 0
         for job in jobs:
             m = need(job)

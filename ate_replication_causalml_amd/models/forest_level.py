@@ -118,8 +118,10 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     # line; in a row-major [n][p] copy a row's drawn features share that row's few lines
     # (22 of 500 bytes: ~4 lines instead of 22). One transpose (n x p bytes) per forest.
     if os.environ.get("ATE_FOREST_LV_LAYOUT", "row") == "row":
-        Xg = Xb.t().contiguous()
-        fst, rst = 1, p
+        ldr = -(-p // 16) * 16
+        Xg = torch.empty((n, ldr), dtype=torch.uint8, device=dev)
+        _native.call("ate_lv_transpose", Xb.data_ptr(), p, n, Xg.data_ptr(), ldr, s)
+        fst, rst = 1, ldr
     else:
         Xg, fst, rst = Xb, n, 1
     # bins per feature (max bin + 1 over the training rows): few-bin features spread their

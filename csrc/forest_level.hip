@@ -812,6 +812,52 @@ __global__ __launch_bounds__(256) void lv_next_id_kernel(const LNode* __restrict
   if (j == ncur - 1 || cur[j + 1].tree != t) next_id[t] += 2 * (excl[j] + dec[j].x - brank[t]);
 }
 
+// ------------------------------------------------------------------ layout copy
+// column-major bins [p][n] -> row-major [n][ldr] (ldr % 16 == 0): a workgroup moves a
+// 64-feature x 256-row tile through LDS, reading 4-byte words along the rows and writing
+// each row's 64 bytes as four aligned 16-byte stores
+__global__ __launch_bounds__(256) void lv_transpose_kernel(const uint8_t* __restrict__ src, int p,
+                                                           int n, uint8_t* __restrict__ dst,
+                                                           int ldr) {
+  __shared__ uint8_t tile[64][256 + 4];
+  const int f0 = blockIdx.y * 64;
+  const int r0 = blockIdx.x * 256;
+  const int t = threadIdx.x;
+  const bool full = r0 + 256 <= n && (n & 3) == 0;
+  for (int fl = t >> 6; fl < 64; fl += 4) {
+    const int f = f0 + fl;
+    const int c = (t & 63) * 4;                             // row offset within the tile
+    uint32_t v = 0;
+    if (f < p) {
+      const uint8_t* row = src + (int64_t)f * n + r0 + c;
+      if (full) {
+        v = *reinterpret_cast<const uint32_t*>(row);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (r0 + c + e < n) v |= (uint32_t)row[e] << (8 * e);
+      }
+    }
+    *reinterpret_cast<uint32_t*>(&tile[fl][c]) = v;
+  }
+  __syncthreads();
+  const int r = r0 + t;
+  if (r >= n) return;
+  uint8_t* out = dst + (int64_t)r * ldr + f0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (f0 + 16 * q >= ldr) break;
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int fl = 16 * q + 4 * e;
+      w[e] = (uint32_t)tile[fl][t] | ((uint32_t)tile[fl + 1][t] << 8) |
+             ((uint32_t)tile[fl + 2][t] << 16) | ((uint32_t)tile[fl + 3][t] << 24);
+    }
+    *reinterpret_cast<uint4*>(out + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 }  // namespace
 
 // --------------------------------------------------------------------- host entry points
@@ -964,6 +1010,15 @@ ATE_API int ate_lv_children(const void* hp, int ncur, const void* excl, void* br
                      (const int32_t*)brank, (int32_t*)next_id, (LNode*)nxt);
   hipLaunchKernelGGL(lv_next_id_kernel, dim3(g), dim3(256), 0, st, a.cur, ncur,
                      (const int32_t*)excl, a.dec, (const int32_t*)brank, (int32_t*)next_id);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
+ATE_API int ate_lv_transpose(const void* src, int p, int n, void* dst, int ldr, void* stream) {
+  if (ldr % 16 || ldr < p) return -1;
+  dim3 grid((n + 255) / 256, (p + 63) / 64);
+  hipLaunchKernelGGL(lv_transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)src, p, n, (uint8_t*)dst, ldr);
   ATE_CHECK_LAUNCH();
   return 0;
 }
