@@ -234,18 +234,41 @@ def ipm_balance_panel(pan, masks, target, zeta=0.5, tol=1e-11, maxit=100, seg_ar
     return gam * lf, iters
 
 
-def _arb_body(pan, target, zeta, alpha, K, seg_arm, allow_negative=False):
+class _Budget:
+    """Interior-point iteration budget of one panel layout's captured graph (identity-
+    hashed: the same object is the GraphCache static argument on every call)."""
+
+    def __init__(self):
+        self.value = None
+
+
+_budgets: dict = {}
+
+
+def _arb_body(pan, target, zeta, alpha, K, seg_arm, allow_negative=False, budget=None):
     """E14 as one device function (utils/graphs.GraphCache): per-arm CV elastic net, the
-    balancing QPs at a fixed interior-point budget (converged arms frozen on the device),
-    and the residual-balancing estimate. Returns [mu1, mu0, var1, var0, iters1, iters0,
-    min fold passes]."""
+    balancing QPs and the residual-balancing estimate. Returns [mu1, mu0, var1, var0,
+    iters1, iters0, min fold passes].
+
+    The interior point of a captured graph runs a FIXED budget of iterations (converged
+    arms frozen on the device: the same result as stopping). The budget is learned: the
+    first call of a layout (eager, the GraphCache warm-up) stops at convergence and sets
+    ``budget.value`` to its iteration count plus a margin, so a replay costs about the
+    converged iterations, not the 100-iteration worst case."""
     G = gram(pan).clone()
     cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],
                           full_sets=[list(range(K)), list(range(K, 2 * K))], alpha=alpha)
     masks = _arm_masks(pan, K)
     tg = target.to(pan.device, torch.float64)
-    gam, iters = ipm_balance_panel(pan, masks, tg, zeta, seg_arm=seg_arm, fixed=True,
-                                   allow_negative=allow_negative)
+    if budget is not None and budget.value is None and not torch.cuda.is_current_stream_capturing():
+        gam, it_h = ipm_balance_panel(pan, masks, tg, zeta, seg_arm=seg_arm,
+                                      allow_negative=allow_negative)
+        budget.value = int(max(it_h)) + max(4, int(max(it_h)) // 2)
+        iters = torch.as_tensor(np.asarray(it_h, dtype=np.int64), device=pan.device)
+    else:
+        maxit = budget.value if budget is not None and budget.value else 100
+        gam, iters = ipm_balance_panel(pan, masks, tg, zeta, seg_arm=seg_arm, fixed=True,
+                                       maxit=maxit, allow_negative=allow_negative)
     b = cv.coef_1se.to(torch.float64)
     Xd = pan.data.double()
     fit = b[:, :1] + b[:, 1:] @ Xd.index_select(0, const(pan.xcols, torch.int64, pan.device))
@@ -260,14 +283,15 @@ def _arb_body(pan, target, zeta, alpha, K, seg_arm, allow_negative=False):
 
 def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 11), nfolds=10,
                      scale_x=True, method="residual_balancing", device=None, dtype="f64",
-                     graph=False, allow_negative=False):
+                     graph=True, allow_negative=False):
     """E14 on the device; matches reference.balance.residual_balance_ate.
 
-    graph=True (GPU): one hipGraph launch per call after the first of a panel layout
-    (utils/graphs.GraphCache over _arb_body, the interior point at a fixed budget of 100
-    iterations with converged arms frozen on the device; equal to the eager solver to
-    1e-12). Off by default: the eager solver stops at convergence (~14 iterations on the
-    tutorial data), which is cheaper than replaying the fixed budget."""
+    graph=True (default, GPU): one hipGraph launch per call after the first of a panel
+    layout (utils/graphs.GraphCache over _arb_body). The captured interior point runs the
+    budget learned by the layout's first call (its converged iteration count plus a
+    margin), converged arms frozen on the device, so it equals the stopping solver; a
+    replay whose arms did not converge within the budget is redone eagerly and the budget
+    raised (the next call recaptures)."""
     dev = resolve_device(device)
     Yn, Wn = as_np(Y), as_np(W)
     Xs = scale_columns(as_np(X))[0] if scale_x else as_np(X)
@@ -278,18 +302,30 @@ def residual_balance(Y, W, X, zeta=0.5, alpha=0.9, seed=1991, fold_streams=(10, 
     seg[~arm] = nfolds + rng.fold_ids(int((~arm).sum()), nfolds, seed, fold_streams[1])
     pan = build_panel(Xs, None, Yn, folds=seg, dtype=dtype, device=dev)
     if graph and pan.data.is_cuda:
+        from ..utils.graphs import layout_key
         K = nfolds
         nr = np.asarray(pan.seg_nreal)
         seg_arm = tuple(int(s // K) if nr[s] > 0 else -1 for s in range(pan.nseg))
-        out, g = estimator_graphs.run("arb", _arb_body, (pan, target.to(dev)), float(zeta),
-                                      float(alpha), K, seg_arm, bool(allow_negative))
+        statics = (float(zeta), float(alpha), K, seg_arm, bool(allow_negative))
+        bkey = (layout_key(pan), statics)
+        budget = _budgets.setdefault(bkey, _Budget())
+        out, g = estimator_graphs.run("arb", _arb_body, (pan, target.to(dev)), *statics, budget)
         v = out.cpu().numpy()
         if v[6] < 0:
             from ..utils.guards import NumericalError
             raise NumericalError("CV fold path timed out waiting for its full-data lambda "
                                  "sequence; selection is invalid")
+        if budget.value is not None and max(v[4], v[5]) >= budget.value:
+            # an arm did not converge within the captured budget: redo this call with the
+            # stopping solver and recapture next time with a larger budget
+            estimator_graphs.drop("arb", (pan, target.to(dev)), *statics, budget)
+            budget.value = None
+            return residual_balance(Y, W, X, zeta, alpha, seed, fold_streams, nfolds, scale_x,
+                                    method, device, dtype, graph=False,
+                                    allow_negative=allow_negative)
         return AteResult.make(method, v[0] - v[1], float(np.sqrt(v[2] + v[3])), mu1=float(v[0]),
-                              mu0=float(v[1]), ipm_iters=(int(v[4]), int(v[5])), hipgraph=g)
+                              mu0=float(v[1]), ipm_iters=(int(v[4]), int(v[5])), hipgraph=g,
+                              ipm_budget=budget.value)
     G = gram(pan).clone()
     K = nfolds
     cv = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]],

@@ -363,6 +363,13 @@ class GraphCache:
         self.sizes[key] = nb
         return g(inputs), True
 
+    def drop(self, name, inputs, *static_args):
+        """Forget the entry of (name, static args, input layout): its next call starts over."""
+        key = (name, static_args, layout_key(*inputs))
+        self.entries.pop(key, None)
+        self.sizes.pop(key, None)
+        self.eager.discard(key)
+
     def clear(self):
         self.entries.clear()
         self.sizes.clear()
