@@ -29,10 +29,10 @@ c_double = ctypes.c_double
 
 # name -> argtypes (restype int). 'p' pointer, 'i' int32, 'l' int64, 'u' uint64, 'd' double
 _SIGS = {
-    "ate_gram_bf16": "pliipipipippp",
-    "ate_gram_bf16_pair": "pllipippipippip",
-    "ate_gram_f32": "plippipipipppp",
-    "ate_gram_f64": "plippipipipppp",
+    "ate_gram_bf16": "pliipipipipppp",
+    "ate_gram_bf16_pair": "pllipippipippipp",
+    "ate_gram_f32": "plippipipippppp",
+    "ate_gram_f64": "plippipipippppp",
     "ate_gram_tile_sizes": "pppp",
     "ate_chol_solve": "pipiipdpppppp",
     "ate_chol_solve_k": "pipipidppppp",

@@ -17,25 +17,34 @@ from . import dgp as host_dgp
 N_TUTORIAL_COLS = 21
 
 
-def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1):
-    """[(global_start, count)] of this rank's slice of each fold."""
+def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1, align: int = 0):
+    """[(global_start, count)] of this rank's slice of each fold. ``align`` > 0: slices are
+    cut at multiples of ``align`` rows from the fold start (whole blocks per rank), the
+    layout of the world-size-invariant exact reduction mode (ops/gram.py ``exact``)."""
     out = []
     for k in range(folds):
         f0, f1 = k * n_total // folds, (k + 1) * n_total // folds
         m = f1 - f0
-        a = f0 + rank * m // world
-        b = f0 + (rank + 1) * m // world
+        if align:
+            nb = -(-m // align)
+            a = min(f1, f0 + (rank * nb // world) * align)
+            b = min(f1, f0 + ((rank + 1) * nb // world) * align)
+        else:
+            a = f0 + rank * m // world
+            b = f0 + (rank + 1) * m // world
         out.append((a, b - a))
     return out
 
 
 def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991,
                     dtype: str = "bf16", device="cpu", rank: int = 0, world: int = 1,
-                    blocked: bool = False) -> DevicePanel:
+                    blocked: bool = False, align: int = 0) -> DevicePanel:
+    """``align`` > 0: block-aligned rank slices (fold_slices); the panel then records
+    ``exact_block`` = align, the row block of the exact (world-size-invariant) Gram."""
     if p < N_TUTORIAL_COLS:
         raise ValueError("p must be >= 21 (tutorial columns)")
     p_extra = p - N_TUTORIAL_COLS
-    slices = fold_slices(n_total, folds, rank, world)
+    slices = fold_slices(n_total, folds, rank, world, align)
     hi_lo = dtype == "bf16"
     names = ["one"] + [f"x{j}" for j in range(p)] + ["W", "Y"]
     if hi_lo:
@@ -68,4 +77,5 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
         if blocked:
             pan.data.copy_(cm.reshape(pan.P, -1, 64).permute(1, 0, 2))
     pan.n = sum(c for _, c in slices)
+    pan.exact_block = int(align)
     return pan

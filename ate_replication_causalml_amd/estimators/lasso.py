@@ -256,8 +256,41 @@ def global_seg_counts(pan, comm):
     return c.numpy()
 
 
+EXACT_BLOCK = 8192   # rows per Gram chunk in exact mode (synthetic_panel(align=EXACT_BLOCK))
+
+
+def dml_residual_terms(pan, coef: torch.Tensor, rows: int = 1 << 20) -> torch.Tensor:
+    """Per-row orthogonal-score terms [ld, 7] of the held-out residuals (the summands of
+    dml_moments; padding rows all zero), computed with torch in row blocks (exact mode:
+    the terms, not their order-dependent sums, are reduced)."""
+    K = coef.shape[0]
+    Xc = pan.colmajor()
+    dev = Xc.device
+    bf = pan.dtype == torch.bfloat16
+    xc = torch.as_tensor(pan.xcols, dtype=torch.long, device=dev)
+    out = []
+    for k in range(K):
+        r0, r1 = (int(v) for v in pan.seg_bounds[k])
+        for a in range(r0, r1, rows):
+            b = min(r1, a + rows)
+            blk = Xc[:, a:b]
+            valid = (blk[pan.cols["one"]] != 0).double()    # padding rows: all terms 0
+            xs = blk.index_select(0, xc).double()
+            y = blk[pan.cols["Y_hi"]].double() + blk[pan.cols["Y_lo"]].double() if bf else \
+                blk[pan.cols["Y"]].double()
+            w = blk[pan.cols["W_hi"]].double() + blk[pan.cols["W_lo"]].double() if bf else \
+                blk[pan.cols["W"]].double()
+            yr = y - (coef[k, 0, 0] + coef[k, 0, 1:].double() @ xs)
+            wr = w - (coef[k, 1, 0] + coef[k, 1, 1:].double() @ xs)
+            yr, wr = yr * valid, wr * valid         # (no boolean indexing: capturable)
+            w2 = wr * wr
+            out.append(torch.stack([wr * yr, w2, yr * yr * w2, yr * w2 * wr, w2 * w2,
+                                    valid, yr * yr], 1))
+    return torch.cat(out)
+
+
 def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G=None,
-               shard_paths=True):
+               shard_paths=True, exact=False):
     """The cross-fit DML-PLR step as phases for utils.graphs.SegmentedStep:
 
     A  per-fold Gram stack (K01): tile kernel, then slab reduce     device (two phases)
@@ -280,7 +313,12 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     holds a fifth (or less) of the CUs it would, and the Gram beside it runs faster.
 
     Every phase maps a state dict to a state dict; device phases touch only tensors
-    whose storage is static across calls, so the whole step can be captured."""
+    whose storage is static across calls, so the whole step can be captured.
+
+    exact (block-aligned panels, synthetic_panel(align=EXACT_BLOCK)): the fold Gram stack
+    is reduced as int64 limbs of per-block partials and all-reduced as integers, and the
+    score moments are exact sums of per-row terms (ops/exact.py): ATE and SE are the SAME
+    BITS at every world size, at the cost of a residual pass in torch."""
     from ..utils.graphs import Collective
     dist = comm is not None and comm.world_size > 1
     if dist and seg_counts is None:
@@ -293,10 +331,33 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     p1 = len(pan.xcols) + 1
 
     def phase_gram(_):
+        if exact:
+            return {"GX": gram(pan, stage="tiles", exact=True)}
         return {"G": gram(pan, stage="tiles") if G is None else G}
 
     def phase_gram_reduce(st):
+        if exact:
+            return {"GX": gram(pan, stage="reduce", exact=True)}
         return st if G is not None else {"G": gram(pan, stage="reduce", out=st["G"])}
+
+    def phase_from_limbs(st):
+        from ..ops.exact import from_limbs
+        return {**st, "G": from_limbs(st["GX"])}
+
+    n_rows = int(np.asarray(seg_counts if seg_counts is not None else pan.seg_nreal).sum())
+
+    def phase_terms(st):
+        from ..ops.exact import column_amax
+        terms = dml_residual_terms(pan, st["coef"])
+        return {**st, "terms": terms, "amax": column_amax(terms)}
+
+    def phase_limbs(st):
+        from ..ops.exact import sum_limbs
+        return {**st, "limbs": sum_limbs(st["terms"], st["amax"], n_rows)}
+
+    def phase_mom_exact(st):
+        from ..ops.exact import finish_limbs
+        return {**st, "mom": finish_limbs(st["limbs"], st["amax"], n_rows)}
 
     def fit(st):
         if not mine:
@@ -329,12 +390,32 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
 
     cap = bool(getattr(comm, "capturable", False))
 
-    def reduce(name):
+    def reduce(name, op="sum"):
         def f(st):
-            comm.all_reduce_(st[name])
+            (comm.all_reduce_ if op == "sum" else comm.all_reduce_max_)(st[name])
             return st
         return Collective(f, capturable=cap)     # RCCL: captured inside the step's graph
 
+    if exact:
+        phases = [phase_gram, phase_gram_reduce]
+        if dist:
+            phases.append(reduce("GX"))
+        phases.append(phase_from_limbs)
+        if sharded:
+            phases += [phase_fit_sharded, reduce("coef")]
+        else:
+            def phase_fit_coef(st):
+                cv = fit(st)
+                return {**st, "cv": cv, "coef": pick(cv).double()}
+            phases.append(phase_fit_coef)
+        phases.append(phase_terms)
+        if dist:
+            phases.append(reduce("amax", "max"))
+        phases.append(phase_limbs)
+        if dist:
+            phases.append(reduce("limbs"))
+        phases += [phase_mom_exact, phase_final]
+        return phases
     phases = [phase_gram, phase_gram_reduce]
     if dist:
         phases.append(reduce("G"))
@@ -348,7 +429,8 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     return phases
 
 
-def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, seg_counts=None):
+def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, seg_counts=None,
+                       exact=False):
     """DML-PLR on a fold-segmented panel (segment k = fold k). Returns (res[2], moments[7], cv).
 
     comm: optional parallel.comm.Communicator — each rank holds a row shard of every
@@ -356,9 +438,9 @@ def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, se
     seg_counts: global rows per fold (computed with one all-reduce when omitted).
     A truncated CV fold path NaN-poisons res (ops/enet.poison_if_truncated)."""
     st = None
-    for ph in dml_phases(pan, folds, lambda_rule, comm, seg_counts, G):
+    for ph in dml_phases(pan, folds, lambda_rule, comm, seg_counts, G, exact=exact):
         st = ph(st)
-    return st["res"], st["mom"], st["cv"]
+    return st["res"], st["mom"], st.get("cv")
 
 
 def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:

@@ -53,7 +53,7 @@ def _stream():
 
 
 class GramPlan:
-    def __init__(self, panel: DevicePanel, weighted: bool):
+    def __init__(self, panel: DevicePanel, weighted: bool, exact: bool = False):
         bf16 = panel.dtype == torch.bfloat16
         if bf16 and weighted:
             raise ValueError("weighted Gram needs an fp32/fp64 panel")
@@ -89,7 +89,21 @@ class GramPlan:
         nchunk_target = max(1, target // ntiles)
         chunks = []
         seg_chunk0 = [0]
-        if self.pair:
+        if exact:
+            # one chunk per row block of the segment (blocks counted from the segment start:
+            # the same global blocks at every world size, data/device_dgp.fold_slices(align))
+            B = int(panel.exact_block)
+            if B <= 0 or B % K:
+                raise ValueError("exact Gram needs a block-aligned panel (synthetic_panel("
+                                 f"align=B) with B a multiple of {K})")
+            for s_, (r0, r1) in enumerate(panel.seg_bounds):
+                r = int(r0)
+                while r < r1:
+                    e = min(int(r1), r + B)
+                    chunks.append((r, e, s_, 0))
+                    r = e
+                seg_chunk0.append(len(chunks))
+        elif self.pair:
             # equal chunks, the same count in every segment, total workgroups <= target: a
             # launch of 2 x nseg x k near-equal workgroups fills whole rounds of CUs instead of
             # leaving a few stragglers of a ~0.3 ms workgroup to run alone at the end (2060 WGs
@@ -120,6 +134,8 @@ class GramPlan:
         per_tile = PAIR_SLOTS * 256 if self.pair else T * T
         self.slab = torch.empty(self.nchunks * ntiles * per_tile, dtype=slab_dtype, device=dev)
         self.G = torch.empty((panel.nseg, P, P), dtype=torch.float64, device=dev)
+        self.Gx = torch.empty((2, panel.nseg, P, P), dtype=torch.int64, device=dev) \
+            if exact else None
 
 
 def pair_chunks(seg_bounds, K: int, ntiles: int, target: int, ncu: int = 0):
@@ -202,19 +218,19 @@ def _pair_tiles(nt: int):
     return tiles, blocks
 
 
-def plan_for(panel: DevicePanel, weighted=False) -> GramPlan:
+def plan_for(panel: DevicePanel, weighted=False, exact=False) -> GramPlan:
     """Cached launch plan + workspace. The cache is an LRU of ``PLAN_CACHE_MAX`` entries
     (a bf16 plan at N=1e7 holds ~0.5 GB of slab): evicting drops only the cache's
     reference, and a hipGraph that captured the plan keeps it alive (utils/graphs.pin).
     Keyed by the panel's address too: the plan owns the returned Gram buffer, and two
     live panels of one shape must not share it."""
     key = (panel.data.data_ptr(), tuple(panel.data.shape), panel.data.dtype, weighted,
-           tuple(map(tuple, panel.seg_bounds)), _slot)
+           tuple(map(tuple, panel.seg_bounds)), _slot, exact)
     pl = _plan_cache.pop(key, None)
     if pl is None:
         while len(_plan_cache) >= PLAN_CACHE_MAX:
             _plan_cache.pop(next(iter(_plan_cache)))
-        pl = GramPlan(panel, weighted)
+        pl = GramPlan(panel, weighted, exact)
     _plan_cache[key] = pl          # most recently used last
     return pin(pl)
 
@@ -228,32 +244,40 @@ _STAGES = {"all": 3, "tiles": 1, "reduce": 2}
 
 
 def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor | None = None,
-         out: torch.Tensor | None = None, stage: str = "all") -> torch.Tensor:
+         out: torch.Tensor | None = None, stage: str = "all", exact: bool = False) -> torch.Tensor:
     """Per-segment Gram stack [nseg, P, P] (fp64). ``w``: optional row weights (panel order).
 
     stage (paired-tile bf16 Gram): "tiles" launches only the tile kernel (slab partials),
     "reduce" only the fixed-order slab reduce into the returned buffer, "all" both. Split,
     the reduce can run on another stream than the next Gram (bench.py --stagger 2). Other
-    kernels do everything at "tiles" and nothing at "reduce"."""
+    kernels do everything at "tiles" and nothing at "reduce".
+
+    ``exact``: world-size-invariant mode for block-aligned panels (panel.exact_block): one
+    row block per chunk and the chunk partials summed as int64 limbs (ops/exact.py);
+    returns the limb stack [2, nseg, P, P] (int64): all-reduce it over row shards, then
+    ops.exact.from_limbs gives the same fp64 Gram at every world size."""
     X = panel.data
     if not X.is_cuda:
+        if exact:
+            return _gram_cpu_exact(panel, w)
         return _gram_cpu(panel, w, out) if stage != "reduce" else out
-    pl = plan_for(panel, weighted=w is not None)
+    pl = plan_for(panel, weighted=w is not None, exact=exact)
     G = pl.G if out is None else out
+    Gx = pl.Gx.data_ptr() if exact else None
     s = _stream()
     if X.dtype == torch.bfloat16 and pl.pair:
         cs, bs = panel.strides()
         _native.call("ate_gram_bf16_pair", X.data_ptr(), cs, bs, panel.P, pl.tiles.data_ptr(),
                      pl.ntiles, pl.blocks.data_ptr(), pl.chunks.data_ptr(), pl.nchunks,
                      pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(),
-                     _STAGES[stage], s)
-        return G
+                     _STAGES[stage], Gx, s)
+        return pl.Gx if exact else G
     if stage == "reduce":
-        return G
+        return pl.Gx if exact else G
     if X.dtype == torch.bfloat16:
         _native.call("ate_gram_bf16", X.data_ptr(), panel.cm_ld, panel.P, pl.T, pl.tiles.data_ptr(),
                      pl.ntiles, pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(),
-                     panel.nseg, pl.slab.data_ptr(), G.data_ptr(), s)
+                     panel.nseg, pl.slab.data_ptr(), G.data_ptr(), Gx, s)
     else:
         name = "ate_gram_f64" if X.dtype == torch.float64 else "ate_gram_f32"
         if w is not None:
@@ -261,8 +285,8 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
         _native.call(name, X.data_ptr(), panel.cm_ld, panel.P, 0 if w is None else w.data_ptr(),
                      pl.tiles.data_ptr(), pl.ntiles, pl.chunks.data_ptr(), pl.nchunks,
                      pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(),
-                     0 if done is None else done.data_ptr(), s)
-    return G
+                     0 if done is None else done.data_ptr(), Gx, s)
+    return pl.Gx if exact else G
 
 
 def _gram_cpu(panel, w, out):
@@ -277,6 +301,24 @@ def _gram_cpu(panel, w, out):
         out.copy_(G)
         return out
     return G
+
+
+def _gram_cpu_exact(panel, w):
+    """CPU twin of the exact mode: per (segment, row block) fp64 partial Grams, summed as
+    int64 limbs (same block decomposition as the GPU plan)."""
+    from .exact import to_limbs
+    B = int(panel.exact_block)
+    if B <= 0:
+        raise ValueError("exact Gram needs a block-aligned panel (synthetic_panel(align=B))")
+    X = panel.colmajor().double()
+    out = torch.zeros((2, panel.nseg, panel.P, panel.P), dtype=torch.int64)
+    for s_, (r0, r1) in enumerate(panel.seg_bounds):
+        for r in range(int(r0), int(r1), B):
+            e = min(int(r1), r + B)
+            Xs = X[:, r:e]
+            A = Xs if w is None else Xs * w[r:e].double()
+            out[:, s_] += to_limbs(A @ Xs.T)
+    return out
 
 
 def gram_reference(panel: DevicePanel, w=None) -> torch.Tensor:

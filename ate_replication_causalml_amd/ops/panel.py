@@ -46,6 +46,10 @@ class DevicePanel:
     # (profiles/r01_pmc/gram_diag.txt). Kernels that take (cs, bs) strides read both
     # layouts; the others require column-major (``cm_ld`` raises).
     blocked: bool = False
+    # exact (world-size-invariant) Gram: rows of every segment form blocks of this many
+    # rows counted from the segment start, the same blocks at every world size
+    # (data/device_dgp.fold_slices(align=...)); 0 = not block-aligned
+    exact_block: int = 0
 
     @property
     def P(self):

@@ -83,6 +83,10 @@ def main():
                          "instead of both Grams, then both paths, running together; 2: the "
                          "Grams of all fits run on one low-priority stream and the rest of "
                          "each fit on its own high-priority stream")
+    ap.add_argument("--exact", type=int, default=0,
+                    help="1: world-size-invariant exact reduction mode (block-aligned row "
+                         "shards, int64-limb Gram all-reduce, exact score moments: the same "
+                         "ATE / SE bits at every world size; estimators/lasso.dml_phases)")
     ap.add_argument("--inflight", type=int, default=-1,
                     help="independent cross-fits in flight (one hipGraph + stream + Gram "
                          "workspace each); every timed step is still one complete DML-ATE")
@@ -111,9 +115,11 @@ def main():
     else:
         device = torch.device("cpu")
     n_total = int(args.rows) * (world if args.scaling == "weak" else 1)
+    from ate_replication_causalml_amd.estimators.lasso import EXACT_BLOCK
     pan = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed, dtype=args.dtype,
                           blocked=bool(args.blocked) and args.dtype == "bf16",
-                          device=device, rank=rank, world=world)
+                          device=device, rank=rank, world=world,
+                          align=EXACT_BLOCK if args.exact else 0)
 
     def sync():
         if device.type == "cuda":
@@ -211,7 +217,8 @@ def main():
         # hooks of the stagger stay eager between the Gram graph and the rest
         with plan_slot(i):      # private Gram workspace per in-flight fit
             phases = [in_slot(ph, i) for ph in staggered(
-                dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts), i)]
+                dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts,
+                           exact=bool(args.exact)), i)]
             try:
                 return SegmentedStep(phases, graph=use_graph), None
             except Exception as e:  # noqa: BLE001 - reported, then every rank goes eager
@@ -237,7 +244,8 @@ def main():
               flush=True)
         with plan_slot(0):
             runs = [SegmentedStep(dml_phases(pan, args.folds, "min", comm=comm,
-                                             seg_counts=seg_counts), graph=False, warmup=0)]
+                                             seg_counts=seg_counts, exact=bool(args.exact)),
+                                  graph=False, warmup=0)]
     graphs_per_fit = runs[0].graph_count
     # world 1 has no collectives; at world > 1: whether every rank captured them
     collectives_captured = bool(cc.item()) if world > 1 and graphed else None
@@ -341,12 +349,15 @@ def main():
             },
             "ate": ate,
             "se": se,
+            "ate_hex": ate.hex(),
+            "se_hex": se.hex(),
             "hipgraph": graphed,
             "inflight": n_inflight,
             "single_fit_ms": lat * 1e3,
             "single_fit_ms_all": [round(v * 1e3, 4) for v in lats],
             "single_fit_rows_per_s": n_total / lat,
             "graphs_per_fit": graphs_per_fit,
+            "exact": bool(args.exact),
             "collectives_captured": collectives_captured,
             "parity": parity,
         }

@@ -366,12 +366,23 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
     pair_wave<false>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
 }
 
+// Exact (world-size-invariant) reduction: a chunk partial v is split into two int64 limbs
+// of fixed scale, hi = floor(v 2^24), lo = rint((v 2^24 - hi) 2^32) (both exact in fp64),
+// and the limbs of all chunks are summed as integers -- associative, so the rank that
+// reduces a chunk and the all-reduce order cannot change a bit (ops/exact.py from_limbs).
+__device__ __forceinline__ void gram_limbs(double v, long long& hi, long long& lo) {
+  const double x = v * 16777216.0;                      // 2^24
+  const double h = floor(x);
+  hi = (long long)h;
+  lo = (long long)rint((x - h) * 4294967296.0);         // 2^32
+}
+
 // blocks: [ntiles][PAIR_SLOTS] int2 (I, J) = 16-column block coordinates of the Gram (I: A
 // side = row), (-1, -1) = unused slot. Blocks with I == J are full 16x16 diagonal blocks: only
 // their r <= c entries are written (plus mirror), so every Gram entry has ONE writer.
 __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const int2* __restrict__ blocks,
                                         int ntiles, const int* __restrict__ seg_chunk0, int nseg,
-                                        int P, double* __restrict__ G) {
+                                        int P, double* __restrict__ G, long long* __restrict__ Gx) {
   const int64_t per = (int64_t)ntiles * PAIR_SLOTS * 256;
   const int64_t total = (int64_t)nseg * per;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
@@ -387,6 +398,23 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
     // fixed chunk order; 8 independent loads in flight per batch
     const int c0 = seg_chunk0[s], c1 = seg_chunk0[s + 1];
     const float* src = slab + rem;
+    const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
+    if (Gx) {                                       // exact mode: int64 limbs
+      long long hs = 0, ls = 0;
+      for (int ci = c0; ci < c1; ++ci) {
+        long long h, l;
+        gram_limbs((double)src[(int64_t)ci * per], h, l);
+        hs += h;
+        ls += l;
+      }
+      const int64_t PP = (int64_t)nseg * P * P;
+      long long* Xs = Gx + (int64_t)s * P * P;
+      Xs[(int64_t)a * P + b] = hs;
+      Xs[(int64_t)b * P + a] = hs;
+      Xs[PP + (int64_t)a * P + b] = ls;
+      Xs[PP + (int64_t)b * P + a] = ls;
+      continue;
+    }
     double acc = 0.0;
     int ci = c0;
     for (; ci + 8 <= c1; ci += 8) {
@@ -397,7 +425,6 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
       for (int u = 0; u < 8; ++u) acc += (double)v[u];
     }
     for (; ci < c1; ++ci) acc += (double)src[(int64_t)ci * per];
-    const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
     double* Gs = G + (int64_t)s * P * P;
     Gs[(int64_t)a * P + b] = acc;
     Gs[(int64_t)b * P + a] = acc;
@@ -409,7 +436,7 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
 ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, const void* tiles, int ntiles,
                                const void* blocks, const void* chunks, int nchunks,
                                const void* seg_chunk0, int nseg, void* slab, void* G, int what,
-                               void* stream) {
+                               void* Gx, void* stream) {
   if (P % (2 * GT) || what < 1 || what > 3) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (what & 1) {
@@ -422,7 +449,7 @@ ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, con
     const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
     hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                        (const float*)slab, (const int2*)blocks, ntiles, (const int*)seg_chunk0,
-                       nseg, P, (double*)G);
+                       nseg, P, (double*)G, (long long*)Gx);
     ATE_CHECK_LAUNCH();
   }
   return 0;
@@ -512,7 +539,8 @@ __global__ __launch_bounds__(256) void gram_small_kernel(
 template <typename S>
 __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2* __restrict__ tiles,
                                    int ntiles, const int* __restrict__ seg_chunk0, int nseg, int P,
-                                   double* __restrict__ G, const int* __restrict__ done) {
+                                   double* __restrict__ G, const int* __restrict__ done,
+                                   long long* __restrict__ Gx) {
   if (done && *done) return;
   const int tt = T * T;
   const int64_t total = (int64_t)nseg * ntiles * tt;
@@ -526,6 +554,23 @@ __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2
     // tile's (i, j) and (j, i) partials round differently, (x_i w) x_j vs (x_j w) x_i, and
     // two writers made the weighted Gram differ run to run at rounding level.)
     if (tiles[t].x == tiles[t].y && ij / T > ij % T) continue;
+    if (Gx) {                                       // exact mode: int64 limbs
+      long long hs = 0, ls = 0;
+      for (int c = seg_chunk0[s]; c < seg_chunk0[s + 1]; ++c) {
+        long long h, l;
+        gram_limbs((double)slab[((int64_t)c * ntiles + t) * tt + ij], h, l);
+        hs += h;
+        ls += l;
+      }
+      const int a = tiles[t].x * T + ij / T, b = tiles[t].y * T + ij % T;
+      const int64_t PP = (int64_t)nseg * P * P;
+      long long* Xs = Gx + (int64_t)s * P * P;
+      Xs[(int64_t)a * P + b] = hs;
+      Xs[(int64_t)b * P + a] = hs;
+      Xs[PP + (int64_t)a * P + b] = ls;
+      Xs[PP + (int64_t)b * P + a] = ls;
+      continue;
+    }
     double acc = 0.0;
     for (int c = seg_chunk0[s]; c < seg_chunk0[s + 1]; ++c)
       acc += (double)slab[((int64_t)c * ntiles + t) * tt + ij];
@@ -542,7 +587,8 @@ __global__ void gram_reduce_kernel(const S* __restrict__ slab, int T, const int2
 // tile table and chunk plan must use the same tile size.
 ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile,
                           const void* tiles, int ntiles, const void* chunks, int nchunks,
-                          const void* seg_chunk0, int nseg, void* slab, void* G, void* stream) {
+                          const void* seg_chunk0, int nseg, void* slab, void* G, void* Gx,
+                          void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int nwg = nchunks * ntiles;
   if (tile == GT) {
@@ -560,7 +606,7 @@ ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile,
   int64_t total = (int64_t)nseg * ntiles * tile * tile;
   hipLaunchKernelGGL(gram_reduce_kernel<float>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                      (const float*)slab, tile, (const int2*)tiles, ntiles, (const int*)seg_chunk0,
-                     nseg, P, (double*)G, (const int*)nullptr);
+                     nseg, P, (double*)G, (const int*)nullptr, (long long*)Gx);
   ATE_CHECK_LAUNCH();
   return 0;
 }
@@ -568,7 +614,7 @@ ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile,
 template <typename T>
 static int gram_small(const void* X, int64_t ld, int P, const void* w, const void* tiles,
                       int ntiles, const void* chunks, int nchunks, const void* seg_chunk0,
-                      int nseg, void* slab, void* G, const void* done, void* stream) {
+                      int nseg, void* slab, void* G, const void* done, void* Gx, void* stream) {
   if (P % FT) return -1;
   hipStream_t s = (hipStream_t)stream;
   int nwg = nchunks * ntiles;
@@ -579,23 +625,23 @@ static int gram_small(const void* X, int64_t ld, int P, const void* w, const voi
   int64_t total = (int64_t)nseg * ntiles * FT * FT;
   hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                      (const T*)slab, FT, (const int2*)tiles, ntiles, (const int*)seg_chunk0,
-                     nseg, P, (double*)G, (const int*)done);
+                     nseg, P, (double*)G, (const int*)done, (long long*)Gx);
   ATE_CHECK_LAUNCH();
   return 0;
 }
 
 ATE_API int ate_gram_f32(const void* X, int64_t ld, int P, const void* w, const void* tiles,
                          int ntiles, const void* chunks, int nchunks, const void* seg_chunk0,
-                         int nseg, void* slab, void* G, const void* done, void* stream) {
+                         int nseg, void* slab, void* G, const void* done, void* Gx, void* stream) {
   return gram_small<float>(X, ld, P, w, tiles, ntiles, chunks, nchunks, seg_chunk0, nseg, slab, G,
-                           done, stream);
+                        done, Gx, stream);
 }
 
 ATE_API int ate_gram_f64(const void* X, int64_t ld, int P, const void* w, const void* tiles,
                          int ntiles, const void* chunks, int nchunks, const void* seg_chunk0,
-                         int nseg, void* slab, void* G, const void* done, void* stream) {
+                         int nseg, void* slab, void* G, const void* done, void* Gx, void* stream) {
   return gram_small<double>(X, ld, P, w, tiles, ntiles, chunks, nchunks, seg_chunk0, nseg, slab, G,
-                            done, stream);
+                        done, Gx, stream);
 }
 
 ATE_API int ate_gram_tile_sizes(int* bf16_tile, int* bf16_kstep, int* f32_tile, int* f32_kstep) {

@@ -54,3 +54,24 @@ def test_cfg5_gbdt_two_ranks_on_one_gpu_bitwise(gpu):
     ref = _json(one.stdout)
     assert two["world"] == 2 and ref["world"] == 1
     assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)
+
+
+def test_exact_mode_two_ranks_on_one_gpu_bitwise(gpu):
+    """bench.py --exact (int64-limb Gram all-reduce of block partials, exact moments) with
+    two ranks sharing the GPU gives the SAME BITS as one process holding all rows; the
+    default mode agrees with exact mode to rounding."""
+    bench = os.path.join(ROOT, "bench.py")
+    args = ["--steps", "2", "--warmup", "1", "--parity", "0", "--exact", "1"]
+    env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29659",
+                        bench, "--gpus", "2", "--rows", "500000", *args],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = _json(r.stdout)
+    one = subprocess.run([sys.executable, bench, "--rows", "1000000", *args],
+                         capture_output=True, text=True, timeout=240)
+    assert one.returncode == 0, one.stderr[-3000:]
+    ref = _json(one.stdout)
+    assert two["exact"] and ref["exact"] and two["n_gpus"] == 2
+    assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)

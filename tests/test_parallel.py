@@ -207,3 +207,67 @@ dist.destroy_process_group()
     ref = dml_plr_gbdt(m.Y, m.W, m.X, n_trees=5, depth=3, device="cpu")
     for a, s in got:                               # every rank, every bit
         assert float.fromhex(a) == ref.ate and float.fromhex(s) == ref.se
+
+
+def _dml_exact(world, rank, comm, n=1500, p=24, block=64):
+    pan = synthetic_panel(n, p=p, folds=5, seed=3, dtype="f64", device="cpu", rank=rank,
+                          world=world, align=block)
+    res, mom, _ = dml_crossfit_panel(pan, 5, comm=comm, exact=True)
+    return res.numpy(), mom.numpy()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_exact_mode_dml_bitwise_world_invariant(world):
+    """Exact reduction mode: block-aligned shards, the fold Gram stack
+    all-reduced as int64 limbs of per-block partials, exact score moments -> the DML ATE,
+    SE and moments are the SAME BITS at world 1, 2 and 4 (rtol=0)."""
+    ref, mref = _dml_exact(1, 0, LocalComm())
+    outs = run_simulated(world, lambda c: _dml_exact(world, c.rank, c))
+    for res, mom in outs:
+        np.testing.assert_array_equal(res, ref)
+        np.testing.assert_array_equal(mom, mref)
+    # the exact mode estimates the same quantity as the default mode (rounding only)
+    plain, _ = _dml(1, 0, LocalComm())
+    np.testing.assert_allclose(ref, plain, rtol=1e-9)
+
+
+def test_gloo_exact_mode_dml_bitwise():
+    """The same on real gloo processes (world 2 and 4 in one launcher call each)."""
+    script = r"""
+import os, sys, json
+sys.path.insert(0, %r)
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+from ate_replication_causalml_amd.parallel.comm import TorchComm
+from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+c = TorchComm()
+pan = synthetic_panel(1500, p=24, folds=5, seed=3, dtype="f64", device="cpu", rank=c.rank,
+                      world=c.world_size, align=64)
+res, mom, _ = dml_crossfit_panel(pan, 5, comm=c, exact=True)
+allv = [None] * c.world_size
+dist.all_gather_object(allv, [float(v).hex() for v in res.tolist()])
+if c.rank == 0:
+    print("RESULT", json.dumps(allv), flush=True)
+dist.destroy_process_group()
+""" % ROOT
+    import json
+    import tempfile
+    ref, _ = _dml_exact(1, 0, LocalComm())
+    want = [float(v).hex() for v in ref.tolist()]
+    with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
+        f.write(script)
+        path = f.name
+    try:
+        for world in (2, 4):
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+                   f"--master-port={29581 + world}", path]
+            r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+            assert r.returncode == 0, r.stderr[-3000:]
+            got = json.loads([l for l in r.stdout.splitlines()
+                              if l.startswith("RESULT")][0].split(" ", 1)[1])
+            assert all(g == want for g in got), (world, got, want)
+    finally:
+        os.unlink(path)

@@ -15,7 +15,7 @@ from ate_replication_causalml_amd.estimators.balance import residual_balance  # 
 d = make_tutorial_data(50000, 1991)
 m, _ = apply_selection_bias(d, 0.85, 0.85, "reference")
 graph = len(sys.argv) < 2 or sys.argv[1] != "eager"
-for i in range(4):
+for i in range(int(os.environ.get("REPS", "4"))):
     t0 = time.perf_counter()
     r = residual_balance(m.Y, m.W, m.X, device=torch.device("cuda", 0), graph=graph)
     torch.cuda.synchronize()
