@@ -54,6 +54,7 @@ _SIGS = {
     "ate_cv_select": "pppiipipppp",
     "ate_enet_pick": "ppiiiipp",
     "ate_dml_resid_moments": "ipllpipipiiiiiippp",
+    "ate_dml_resid_exact": "pllpipipiiiiiiippp",
     "ate_lognet_path": "iplpiipipipdddippippppppppp",
     "ate_lognet_cvloss": "iplpiippipppipp",
     "ate_dgp_fill": "iplllllu" + "iip",

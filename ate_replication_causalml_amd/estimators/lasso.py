@@ -346,13 +346,22 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
 
     n_rows = int(np.asarray(seg_counts if seg_counts is not None else pan.seg_nreal).sum())
 
+    native_exact = pan.data.is_cuda and pan.dtype == torch.bfloat16
+
     def phase_terms(st):
         from ..ops.exact import column_amax
+        if native_exact:       # csrc/dml.hip exact mode 1: per-block max |term|, no row buffer
+            part = _exact_resid(pan, st["coef"], 1, None)
+            return {**st, "amax": part.view(-1, 7).amax(0)}
         terms = dml_residual_terms(pan, st["coef"])
         return {**st, "terms": terms, "amax": column_amax(terms)}
 
     def phase_limbs(st):
-        from ..ops.exact import sum_limbs
+        from ..ops.exact import _scale_exp, sum_limbs
+        if native_exact:       # mode 2: per-block int64 limb sums at the global scale
+            sh = _scale_exp(st["amax"], n_rows).contiguous()
+            part = _exact_resid(pan, st["coef"], 2, sh).view(torch.int64).view(-1, 14).sum(0)
+            return {**st, "limbs": torch.stack([part[:7], part[7:]])}
         return {**st, "limbs": sum_limbs(st["terms"], st["amax"], n_rows)}
 
     def phase_mom_exact(st):
@@ -441,6 +450,26 @@ def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, se
     for ph in dml_phases(pan, folds, lambda_rule, comm, seg_counts, G, exact=exact):
         st = ph(st)
     return st["res"], st["mom"], st.get("cv")
+
+
+def _exact_resid(pan, coef: torch.Tensor, mode: int, sh) -> torch.Tensor:
+    """Exact-mode passes of the fused bf16 residual kernel (csrc/dml.hip): mode 1 ->
+    per-block max |term| [blocks * 7] fp64; mode 2 -> per-block int64 limb sums
+    [blocks * 14] (returned in an fp64-typed buffer of the same bytes)."""
+    K = coef.shape[0]
+    dev = pan.device
+    xc = const(pan.xcols, torch.int32, dev)
+    segs = const(np.asarray(pan.seg_bounds[:K], dtype=np.int64), torch.int64, dev)
+    nbx = 512
+    part = torch.empty(K * nbx * (7 if mode == 1 else 14), dtype=torch.float64, device=dev)
+    cs, bs = pan.strides()
+    c = coef.double().contiguous()
+    _native.call("ate_dml_resid_exact", pan.data.data_ptr(), cs, bs, xc.data_ptr(), len(pan.xcols),
+                 segs.data_ptr(), K, c.data_ptr(), pan.cols["Y_hi"], pan.cols["Y_lo"],
+                 pan.cols["W_hi"], pan.cols["W_lo"], pan.cols["one"], nbx, mode,
+                 None if sh is None else sh.data_ptr(), part.data_ptr(),
+                 torch.cuda.current_stream().cuda_stream)
+    return part
 
 
 def dml_residual_moments(pan, coef: torch.Tensor) -> torch.Tensor:

@@ -148,10 +148,16 @@ static int dml_resid_t(const void* X, int64_t ld, const void* xcols, int p, cons
 // bf16 panels: each thread owns 8 CONSECUTIVE rows, so every column read is one 16-byte
 // load (a wave reads 1 KB contiguous per column -- Guideline 13); dot products in fp32
 // (bf16 values are exact in fp32; coefficients rounded to fp32), moments in fp64.
+// mode 0: fp64 moments (partial [blocks][7] double); exact mode (world-size-invariant,
+// ops/exact.py): 1 = per-term max |t| (partial [blocks][7] double, reduced with max),
+// 2 = per-term int64 limb sums at the shifts sh[7] derived from the global max
+// (partial [blocks][14] int64: hi limbs, then lo limbs) -- integer sums, so the block and
+// the rank that own a row cannot change the result.
 __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
     const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const int* __restrict__ xcols, int p,
     const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
-    int y0, int y1, int w0, int w1, int vcol, double* __restrict__ partial) {
+    int y0, int y1, int w0, int w1, int vcol, double* __restrict__ partial, int mode,
+    const int64_t* __restrict__ sh) {
   extern __shared__ __attribute__((aligned(16))) float shf[];
   float* cy = shf;                 // [p+1]
   float* cw = shf + (p + 1);       // [p+1]
@@ -167,6 +173,10 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
   __syncthreads();
   p = compact_support(cy, cw, xc, p, wcnt);
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  long long lh[7] = {0, 0, 0, 0, 0, 0, 0}, ll[7] = {0, 0, 0, 0, 0, 0, 0};
+  double scale[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) scale[q] = mode == 2 ? ldexp(1.0, (int)sh[q]) : 1.0;
   const Seg sg = segs[k];
   auto ld8 = [&](int c, int64_t i, float (&o)[8]) {
     // (c, i) at c*cs + (i/64)*bs + i%64: column-major (cs = ld, bs = 64) or 64-row blocked
@@ -204,15 +214,71 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
       const double yr = ((double)ya[r] + (double)yb[r]) - (double)py[r];
       const double wr = ((double)wa[r] + (double)wb[r]) - (double)pw[r];
       const double w2 = wr * wr;
-      v[0] += wr * yr; v[1] += w2; v[2] += yr * yr * w2; v[3] += yr * w2 * wr; v[4] += w2 * w2;
-      v[5] += 1.0; v[6] += yr * yr;
+      if (mode == 0) {
+        v[0] += wr * yr; v[1] += w2; v[2] += yr * yr * w2; v[3] += yr * w2 * wr; v[4] += w2 * w2;
+        v[5] += 1.0; v[6] += yr * yr;
+        continue;
+      }
+      const double t[7] = {wr * yr, w2, yr * yr * w2, yr * w2 * wr, w2 * w2, 1.0, yr * yr};
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        if (mode == 1) {
+          v[q] = fmax(v[q], fabs(t[q]));
+        } else {
+          const double x = t[q] * scale[q];                 // exact (power of two)
+          const double h = floor(x);
+          lh[q] += (long long)h;
+          ll[q] += (long long)rint((x - h) * 4294967296.0);
+        }
+      }
     }
   }
-  block_sum<7>(v, red);
-  if (threadIdx.x == 0) {
-    double* out = partial + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 7;
+  const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if (mode == 0) {
+    block_sum<7>(v, red);
+    if (threadIdx.x == 0) {
+      double* out = partial + blk * 7;
 #pragma unroll
-    for (int q = 0; q < 7; ++q) out[q] = v[q];
+      for (int q = 0; q < 7; ++q) out[q] = v[q];
+    }
+    return;
+  }
+  // exact modes: wave reduction (max or integer sum, both order-free), then one atomic-free
+  // LDS pass over the 4 waves
+  __shared__ long long xr[4][14];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    for (int o = 32; o > 0; o >>= 1) {
+      if (mode == 1) {
+        v[q] = fmax(v[q], __shfl_xor(v[q], o, 64));
+      } else {
+        lh[q] += __shfl_xor(lh[q], o, 64);
+        ll[q] += __shfl_xor(ll[q], o, 64);
+      }
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      xr[wid][q] = mode == 1 ? __double_as_longlong(v[q]) : lh[q];
+      xr[wid][7 + q] = ll[q];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 14) {
+    const int q = threadIdx.x;
+    if (mode == 1) {
+      if (q < 7) {
+        double m = 0.0;
+        for (int w = 0; w < 4; ++w) m = fmax(m, __longlong_as_double(xr[w][q]));
+        partial[blk * 7 + q] = m;
+      }
+    } else {
+      long long a = 0;
+      for (int w = 0; w < 4; ++w) a += xr[w][q];
+      reinterpret_cast<long long*>(partial)[blk * 14 + q] = a;
+    }
   }
 }
 
@@ -237,7 +303,7 @@ ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t cs, int64_t 
     dim3 grid(nbx, nseg);
     hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), sh, s, (const bf16_t*)X, cs, bs,
                        (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
-                       w0, w1, vcol, (double*)partial);
+                       w0, w1, vcol, (double*)partial, 0, (const int64_t*)nullptr);
     ATE_CHECK_LAUNCH();
     hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
                        (double*)moments);
@@ -245,4 +311,22 @@ ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t cs, int64_t 
     return 0;
   }
   return -1;
+}
+
+// exact-mode passes of the bf16 residual kernel (mode 1: per-block max |term| into
+// partial [nseg*nbx][7] double; mode 2: per-block int64 limb sums into partial
+// [nseg*nbx][14] at the shifts sh[7]); the caller reduces the blocks (max / integer sum)
+ATE_API int ate_dml_resid_exact(const void* X, int64_t cs, int64_t bs, const void* xcols, int p,
+                                const void* segs, int nseg, const void* coef, int y0, int y1,
+                                int w0, int w1, int vcol, int nbx, int mode, const void* sh,
+                                void* partial, void* stream) {
+  if (mode < 1 || mode > 2) return -1;
+  size_t shm = (size_t)2 * (p + 1) * sizeof(float) + (size_t)p * sizeof(int);
+  dim3 grid(nbx, nseg);
+  hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), shm, (hipStream_t)stream,
+                     (const bf16_t*)X, cs, bs, (const int*)xcols, p, (const Seg*)segs, nseg,
+                     (const double*)coef, y0, y1, w0, w1, vcol, (double*)partial, mode,
+                     (const int64_t*)sh);
+  ATE_CHECK_LAUNCH();
+  return 0;
 }
