@@ -49,8 +49,8 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
     names = ["one"] + [f"x{j}" for j in range(p)] + ["W", "Y"]
     if hi_lo:
         names += ["W_hi", "W_lo", "Y_hi", "Y_lo"]
-    align = 128 if dtype == "bf16" else 64
-    P = (len(names) + align - 1) // align * align
+    cpad = 128 if dtype == "bf16" else 64
+    P = (len(names) + cpad - 1) // cpad * cpad
     pan = empty_panel([c for _, c in slices], P, dtype=dtype, device=device, blocked=blocked)
     pan.cols = {nm: i for i, nm in enumerate(names)}
     pan.xcols = [pan.cols[f"x{j}"] for j in range(p)]

@@ -256,7 +256,7 @@ def global_seg_counts(pan, comm):
     return c.numpy()
 
 
-EXACT_BLOCK = 8192   # rows per Gram chunk in exact mode (synthetic_panel(align=EXACT_BLOCK))
+EXACT_BLOCK = 16384  # rows per Gram chunk in exact mode (synthetic_panel(align=EXACT_BLOCK))
 
 
 def dml_residual_terms(pan, coef: torch.Tensor, rows: int = 1 << 20) -> torch.Tensor:

@@ -401,7 +401,20 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
     const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
     if (Gx) {                                       // exact mode: int64 limbs
       long long hs = 0, ls = 0;
-      for (int ci = c0; ci < c1; ++ci) {
+      int ci = c0;
+      for (; ci + 8 <= c1; ci += 8) {               // 8 independent loads in flight
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(ci + u) * per];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          long long h, l;
+          gram_limbs((double)v[u], h, l);
+          hs += h;
+          ls += l;
+        }
+      }
+      for (; ci < c1; ++ci) {
         long long h, l;
         gram_limbs((double)src[(int64_t)ci * per], h, l);
         hs += h;
