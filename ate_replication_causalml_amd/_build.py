@@ -25,7 +25,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-ffp-contract=fast-honor-pragmas", "-Wno-unused-result"]
-NO_CONTRACT = {"forest.hip", "forest_level.hip", "gbdt.hip"}
+NO_CONTRACT = {"forest.hip", "forest_level.hip", "forest_exact.hip", "gbdt.hip"}
 CPU_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-march=x86-64-v2"]
 
 

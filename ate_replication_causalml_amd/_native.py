@@ -62,6 +62,9 @@ _SIGS = {
     "ate_forest_predict": "ppiiipppppippip",
     "ate_forest_pack": "pippppppp",
     "ate_forest_scratch_bytes": "ii",
+    "ate_forest_exact_scratch_bytes": "ii",
+    "ate_forest_fit_exact": "piippipppipppppppp",
+    "ate_forest_predict16": "ppiiippppppippip",
     "ate_bin_matrix": "plipppp",
     "ate_panel_xtv": "iplpipplipp",
     "ate_select_compact": "plppddpppp" + "p",
@@ -81,7 +84,8 @@ _SIGS = {
     "ate_standardize": "pllippp",
     "ate_interactions": "pllipl" + "p",
 }
-_RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64}
+_RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64,
+            "ate_forest_exact_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}
 
 

@@ -15,6 +15,12 @@ Backends: ``"gpu"`` (csrc/forest.hip, one workgroup per tree) and ``"cpu"``
 csrc/forest_common.hpp and grow bit-identical trees from the same Philox streams.
 Continuous covariates are quantile-binned to <= 256 bins (exact for <= 256 distinct
 values); splits are at bin boundaries.
+
+Exact-split mode (``splits="exact"``, randomForest kinds 0/1 with bootstrap sampling):
+bins are the ranks of every feature's distinct values (uint16, <= 65536 rows), splits
+can fall between any two consecutive distinct in-node values and sit at their midpoint
+(randomForest's ``findbestsplit``). GPU: csrc/forest_exact.hip, host twin
+grow_tree_exact in csrc/cpu/forest_cpu.cpp -- the same trees bit for bit.
 """
 from __future__ import annotations
 
@@ -121,6 +127,52 @@ def bin_matrix(X, edges, ne, device=None) -> torch.Tensor:
     return torch.from_numpy(out)
 
 
+EXACT_MAX_ROWS = 65536
+
+
+@dataclass
+class ExactBins:
+    """Value-rank binning of the exact-split mode: vals [p][ldv] sorted distinct values
+    (+inf padded), nval [p] their counts, mids [p][ldv-1] midpoints between consecutive
+    values (bin(x) = #{mids < x}: the rank of x when x is in the table)."""
+    vals: np.ndarray
+    nval: np.ndarray
+    mids: np.ndarray
+
+    @property
+    def ldv(self):
+        return self.vals.shape[1]
+
+    def bin(self, X) -> np.ndarray:
+        """uint16 [p][n] column-major bins of X (host)."""
+        Xh = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X,
+                        dtype=np.float64)
+        p = self.vals.shape[0]
+        out = np.empty((p, Xh.shape[0]), dtype=np.uint16)
+        for j in range(p):
+            out[j] = np.searchsorted(self.mids[j, :self.nval[j] - 1], Xh[:, j], side="left")
+        return out
+
+
+def exact_bins(X) -> ExactBins:
+    """Distinct values of every feature of X (n <= 65536 rows)."""
+    X = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X,
+                   dtype=np.float64)
+    n, p = X.shape
+    if n > EXACT_MAX_ROWS:
+        raise ValueError(f"exact-split forests take at most {EXACT_MAX_ROWS} rows (got {n})")
+    us = [np.unique(X[:, j]) for j in range(p)]
+    ldv = max(2, max(len(u) for u in us))
+    vals = np.full((p, ldv), np.inf)
+    mids = np.full((p, ldv - 1), np.inf)
+    nval = np.zeros(p, dtype=np.int32)
+    for j, u in enumerate(us):
+        vals[j, :len(u)] = u
+        mids[j, :len(u) - 1] = (u[:-1] + u[1:]) / 2.0
+        nval[j] = len(u)
+    return ExactBins(vals, nval, mids)
+
+
 # ------------------------------------------------------------------ forest object
 def _nthreads():
     return int(os.environ.get("ATE_CPU_THREADS", os.cpu_count() or 1))
@@ -142,6 +194,7 @@ class Forest:
     nedges: np.ndarray
     Xb_train: object = None
     packed: object = None        # GPU: int2 per node (see csrc/forest.hip forest_pack_kernel)
+    exact: ExactBins | None = None   # exact-split forests: uint16 value-rank bins
 
     @property
     def device(self):
@@ -151,6 +204,9 @@ class Forest:
     def _bins(self, X):
         if X is None:
             return self.Xb_train
+        if self.exact is not None:
+            b = torch.from_numpy(self.exact.bin(X))
+            return b.to(self.device) if self.backend == "gpu" else b
         return bin_matrix(X, self.edges, self.nedges, self.device if self.backend == "gpu" else None)
 
     def predict_raw(self, X=None, oob=False) -> np.ndarray:
@@ -175,6 +231,18 @@ class Forest:
         if self.backend == "gpu":
             dev = self.device
             s = torch.cuda.current_stream().cuda_stream
+            if self.exact is not None:
+                tchunk = max(1, min(self.params.ntree, (1 << 28) // max(n2, 1)))
+                leaves = torch.empty(tchunk * n2, dtype=torch.int32, device=dev)
+                out = torch.empty(n2 * width, dtype=torch.float64, device=dev)
+                _native.call("ate_forest_predict16", ctypes.addressof(self.params),
+                             Xb.data_ptr(), n2, int(oob), self.cap, self.feat.data_ptr(),
+                             self.thr.data_ptr(), self.left.data_ptr(), self.val.data_ptr(),
+                             self.inbag.data_ptr(), leaves.data_ptr(), tchunk, state.data_ptr(),
+                             out.data_ptr(), phases, s)
+                if not phases & 4:
+                    return None
+                return out if not host else out.cpu().numpy()
             if self.packed is None:
                 self.packed = torch.zeros(self.params.ntree * self.cap * 2, dtype=torch.int32,
                                           device=dev)
@@ -201,7 +269,8 @@ class Forest:
             res = np.empty(n2 * width)
             Xbn = np.ascontiguousarray(Xb.numpy() if isinstance(Xb, torch.Tensor) else Xb)
             lib = _native.cpu()
-            rc = lib.atecpu_forest_predict(
+            fn = lib.atecpu_forest_predict16 if self.exact is not None else lib.atecpu_forest_predict
+            rc = fn(
                 ctypes.byref(self.params), _ptr(Xbn), ctypes.c_int(n2), ctypes.c_int(int(oob)),
                 ctypes.c_int(self.cap), _ptr(self.feat), _ptr(self.thr), _ptr(self.left),
                 _ptr(self.val), _ptr(self.inbag), _ptr(self.est) if self.est is not None else None,
@@ -241,13 +310,26 @@ def _ptr(a):
 
 def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min_node=1,
                sampling=0, honesty=False, group=1, mtry_poisson=False, alpha=0.0,
-               sample_fraction=0.5, seed=1, backend=None, edges=None, tree_offset=0) -> Forest:
+               sample_fraction=0.5, seed=1, backend=None, edges=None, tree_offset=0,
+               splits="binned") -> Forest:
     """Grow a forest. X: (n, p) float; kind 0 needs y in {0,1}; kind 1 needs r1 (response);
-    kind 2 needs r1 = W~ and r2 = Y~ (centred treatment / outcome)."""
+    kind 2 needs r1 = W~ and r2 = Y~ (centred treatment / outcome).
+    ``splits="exact"``: randomForest split semantics (every distinct value a candidate,
+    midpoint thresholds); ``edges`` is then an ExactBins (default: from X)."""
     X = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X, dtype=np.float64)
     if backend is None:
         backend = "gpu" if torch.cuda.is_available() else "cpu"
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "gpu" else None
+    if splits == "exact":
+        eb = edges if isinstance(edges, ExactBins) else exact_bins(X)
+        Xb = torch.from_numpy(eb.bin(X))
+        if dev is not None:
+            Xb = Xb.to(dev)
+        return fit_forest_exact(Xb, eb, kind, y=y, r1=r1, ntree=ntree, mtry=mtry,
+                                min_node=min_node, sampling=sampling, seed=seed,
+                                tree_offset=tree_offset)
+    if splits != "binned":
+        raise ValueError(f"splits must be 'binned' or 'exact', got {splits!r}")
     Xsrc = X
     if edges is None:
         if dev is not None and X.size >= DEVICE_EDGES_MIN:
@@ -361,18 +443,88 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
     return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xbn)
 
 
+def fit_forest_exact(Xb, eb: ExactBins, kind: int, y=None, r1=None, ntree=500, mtry=None,
+                     min_node=1, sampling=0, seed=1, tree_offset=0) -> Forest:
+    """Exact-split forest on value-rank bins ``Xb`` (uint16 [p][n]; a device tensor grows on
+    the GPU, csrc/forest_exact.hip, a host one on the CPU twin). randomForest sampling,
+    kinds 0/1."""
+    if sampling != 0 or kind not in (KIND_CLASS, KIND_REG):
+        raise ValueError("exact-split forests: randomForest sampling, classification or "
+                         "regression")
+    gpu = isinstance(Xb, torch.Tensor) and Xb.is_cuda
+    p, n = Xb.shape
+    if n > EXACT_MAX_ROWS:
+        raise ValueError(f"exact-split forests take at most {EXACT_MAX_ROWS} rows (got {n})")
+    if mtry is None:
+        mtry = max(1, int(math.floor(math.sqrt(p))))
+    fp = ForestParams(kind=kind, sampling=0, ntree=ntree, mtry=min(mtry, p), min_node=min_node,
+                      honesty=0, group=1, mtry_poisson=0, alpha=0.0, sample_fraction=0.5,
+                      pois0=math.exp(-min(mtry, p)), seed=seed, p=p, n=n, t0=tree_offset)
+    cap = 2 * n + 1
+    h = lambda a: None if a is None else (a.cpu().numpy() if isinstance(a, torch.Tensor) else
+                                           np.asarray(a))
+    if gpu:
+        dev = Xb.device
+        yt = None if y is None else torch.as_tensor(h(y).astype(np.uint8), device=dev)
+        r1t = None if r1 is None else torch.as_tensor(to_fix(h(r1)), device=dev)
+        vals = torch.as_tensor(eb.vals, device=dev)
+        nval = torch.as_tensor(eb.nval, device=dev)
+        feat = torch.empty(ntree * cap, dtype=torch.int32, device=dev)
+        thr = torch.empty_like(feat)
+        left = torch.empty_like(feat)
+        val = torch.zeros(ntree * cap, dtype=torch.float64, device=dev)
+        nnodes = torch.empty(ntree, dtype=torch.int32, device=dev)
+        inbag = torch.empty(ntree * n, dtype=torch.uint8, device=dev)
+        per = _native.hip().ate_forest_exact_scratch_bytes(n, 1)
+        chunk = max(1, min(ntree, (1 << 30) // per))       # scratch <= ~1 GiB
+        scratch = torch.empty(per * chunk, dtype=torch.uint8, device=dev)
+        Xb = Xb.contiguous()
+        p_ = lambda a: 0 if a is None else a.data_ptr()
+        s = torch.cuda.current_stream().cuda_stream
+        for t0 in range(0, ntree, chunk):
+            _native.call("ate_forest_fit_exact", ctypes.addressof(fp), t0, min(chunk, ntree - t0),
+                         Xb.data_ptr(), vals.data_ptr(), eb.ldv, nval.data_ptr(), p_(yt), p_(r1t),
+                         cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(), val.data_ptr(),
+                         nnodes.data_ptr(), inbag.data_ptr(), scratch.data_ptr(), s)
+        del scratch
+        return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, None, None, None, Xb,
+                      exact=eb)
+    Xbn = np.ascontiguousarray(h(Xb), dtype=np.uint16)
+    ycls = None if y is None else h(y).astype(np.uint8)
+    r1f = None if r1 is None else to_fix(h(r1))
+    feat = np.empty(ntree * cap, dtype=np.int32)
+    thr = np.empty_like(feat)
+    left = np.empty_like(feat)
+    val = np.zeros(ntree * cap)
+    nnodes = np.empty(ntree, dtype=np.int32)
+    inbag = np.empty(ntree * n, dtype=np.uint8)
+    vals = np.ascontiguousarray(eb.vals)
+    nval = np.ascontiguousarray(eb.nval, dtype=np.int32)
+    rc = _native.cpu().atecpu_forest_fit_exact(
+        ctypes.byref(fp), _ptr(Xbn), _ptr(vals), ctypes.c_int(eb.ldv), _ptr(nval), _ptr(ycls),
+        _ptr(r1f), ctypes.c_int(cap), _ptr(feat), _ptr(thr), _ptr(left), _ptr(val), _ptr(nnodes),
+        _ptr(inbag), ctypes.c_int(_nthreads()))
+    if rc != 0:
+        raise RuntimeError("atecpu_forest_fit_exact failed")
+    return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, None, None, None, Xbn,
+                  exact=eb)
+
+
 # ------------------------------------------------------------------ public learners
-def rf_classifier(X, y, num_trees=500, mtry=None, nodesize=1, seed=1, backend=None) -> Forest:
-    """randomForest(factor(y) ~ X, ntree, type="classification") (ate_functions.R:169)."""
+def rf_classifier(X, y, num_trees=500, mtry=None, nodesize=1, seed=1, backend=None,
+                  splits="binned") -> Forest:
+    """randomForest(factor(y) ~ X, ntree, type="classification") (ate_functions.R:169).
+    ``splits="exact"``: randomForest's split semantics on continuous covariates."""
     return fit_forest(X, KIND_CLASS, y=y, ntree=num_trees, mtry=mtry, min_node=nodesize,
-                      seed=seed, backend=backend)
+                      seed=seed, backend=backend, splits=splits)
 
 
-def rf_regressor(X, y, num_trees=500, mtry=None, nodesize=5, seed=1, backend=None) -> Forest:
+def rf_regressor(X, y, num_trees=500, mtry=None, nodesize=5, seed=1, backend=None,
+                 splits="binned") -> Forest:
     """Breiman regression forest (bootstrap, variance-reduction splits)."""
     p = np.asarray(X).shape[1]
-    return fit_forest(X, KIND_REG, r1=y, ntree=num_trees,
-                      mtry=mtry or max(1, p // 3), min_node=nodesize, seed=seed, backend=backend)
+    return fit_forest(X, KIND_REG, r1=y, ntree=num_trees, mtry=mtry or max(1, p // 3),
+                      min_node=nodesize, seed=seed, backend=backend, splits=splits)
 
 
 def grf_mtry(p):

@@ -257,7 +257,152 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
   }
 }
 
+// Exact-split mode (forest_common.hpp::exact_threshold_bin; GPU twin csrc/forest_exact.hip):
+// uint16 value-rank bins, randomForest sampling (bootstrap), kinds 0/1. A node's candidate
+// feature is scanned over its rows sorted by (bin, row); the criterion is evaluated at every
+// boundary between two consecutive DISTINCT in-node values, in ascending order, with the same
+// integer statistics, formulas and (feature slot, position) tie-break as the binned engine.
+static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, const double* vals,
+                            int ldv, const int32_t* nval, const uint8_t* ycls, const int64_t* r1,
+                            const Out& o) {
+  const int n = fp.n, p = fp.p;
+  std::vector<int32_t> w(n, 0);
+  const int tg = fp.t0 + t;
+  uint8_t* inb = o.inbag + (int64_t)t * n;
+  for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)]++;
+  for (int i = 0; i < n; ++i) inb[i] = w[i] > 0;
+  std::vector<int> idx;
+  for (int i = 0; i < n; ++i)
+    if (w[i] > 0) idx.push_back(i);
+  const int m = (int)idx.size();
+  const int64_t base = (int64_t)t * o.cap;
+  int32_t* feat = o.feat + base;
+  int32_t* thr = o.thr + base;
+  int32_t* left = o.left + base;
+  double* val = o.val + base;
+  std::vector<Rng> cur{{0, m, 0}};
+  int next_id = 1;
+  std::vector<int> tmp(m);
+  std::vector<uint64_t> keys(m);
+  std::vector<int> perm(p);
+  for (int depth = 0; !cur.empty(); ++depth) {
+    std::vector<Rng> nxt;
+    for (const Rng& nd : cur) {
+      const int v = nd.id;
+      int64_t nw = 0, n1 = 0, s1 = 0;
+      for (int q = nd.lo; q < nd.hi; ++q) {
+        const int i = idx[q];
+        nw += w[i];
+        if (fp.kind == 0) n1 += (int64_t)w[i] * ycls[i];
+        else s1 += (int64_t)w[i] * r1[i];
+      }
+      const double dn = (double)nw;
+      bool terminal = nw <= fp.min_node || depth >= MAX_DEPTH - 1;
+      if (fp.kind == 0 && (n1 == 0 || n1 == nw)) terminal = true;
+      int bf = -1, blo = -1, bhi = -1;
+      if (!terminal) {
+        double parent;
+        if (fp.kind == 0) {
+          double a = (double)(nw - n1), b = (double)n1;
+          parent = (a * a + b * b) / dn;
+        } else {
+          double sd = from_fix(s1);
+          parent = (sd * sd) / dn;
+        }
+        const int minc = min_child(fp, dn);
+        const int nf = draw_num_features(fp, tg, v);
+        std::iota(perm.begin(), perm.end(), 0);
+        for (int k = 0; k < nf; ++k) {
+          uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, k), (uint32_t)(p - k));
+          std::swap(perm[k], perm[k + r]);
+        }
+        double best = -INFINITY;
+        const int cnt = nd.hi - nd.lo;
+        for (int k = 0; k < nf; ++k) {
+          const int f = perm[k];
+          const uint16_t* xf = Xb + (int64_t)f * n;
+          for (int q = 0; q < cnt; ++q)
+            keys[q] = ((uint64_t)xf[idx[nd.lo + q]] << 32) | (uint32_t)idx[nd.lo + q];
+          std::sort(keys.begin(), keys.begin() + cnt);
+          int64_t c0 = 0, c1 = 0;
+          for (int s = 0; s + 1 < cnt; ++s) {
+            const int i = (int)(uint32_t)keys[s];
+            if (fp.kind == 0) {
+              c0 += (int64_t)w[i] * (1 - ycls[i]);
+              c1 += (int64_t)w[i] * ycls[i];
+            } else {
+              c0 += w[i];
+              c1 += (int64_t)w[i] * r1[i];
+            }
+            const int b = (int)(keys[s] >> 32), bn = (int)(keys[s + 1] >> 32);
+            if (b == bn) continue;
+            const int64_t nl = fp.kind == 0 ? c0 + c1 : c0;
+            const int64_t nr = nw - nl;
+            if (nl < minc || nr < minc) continue;
+            const double crit = fp.kind == 0
+                ? gini_crit((double)c0, (double)c1, (double)(nw - n1 - c0), (double)(n1 - c1))
+                : mse_crit(from_fix(c1), (double)nl, from_fix(s1 - c1), (double)nr);
+            if (crit > best) {
+              best = crit;
+              bf = f;
+              blo = b;
+              bhi = bn;
+            }
+          }
+        }
+        if (!(bf >= 0 && best > parent + 1e-12 * std::max(1.0, std::fabs(parent)))) bf = -1;
+      }
+      if (bf < 0) {
+        feat[v] = -1;
+        thr[v] = -1;
+        left[v] = -1;
+        if (fp.kind == 0) {
+          int vote;
+          if (2 * n1 > nw) vote = 1;
+          else if (2 * n1 < nw) vote = 0;
+          else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, 4095)) & 1u);
+          val[v] = vote;
+        } else {
+          val[v] = from_fix(s1) / dn;
+        }
+        continue;
+      }
+      const int tb = exact_threshold_bin(vals + (int64_t)bf * ldv, nval[bf], blo, bhi);
+      const uint16_t* xf = Xb + (int64_t)bf * n;
+      int nl = 0;
+      for (int q = nd.lo; q < nd.hi; ++q)
+        if (xf[idx[q]] <= tb) tmp[nd.lo + nl++] = idx[q];
+      int nr = 0;
+      for (int q = nd.lo; q < nd.hi; ++q)
+        if (xf[idx[q]] > tb) tmp[nd.lo + nl + nr++] = idx[q];
+      for (int q = nd.lo; q < nd.hi; ++q) idx[q] = tmp[q];
+      feat[v] = bf;
+      thr[v] = tb;
+      left[v] = next_id;
+      val[v] = 0.0;
+      nxt.push_back({nd.lo, nd.lo + nl, next_id});
+      nxt.push_back({nd.lo + nl, nd.hi, next_id + 1});
+      next_id += 2;
+    }
+    cur.swap(nxt);
+  }
+  o.nnodes[t] = next_id;
+}
+
 }  // namespace
+
+ATECPU_API int atecpu_forest_fit_exact(const ForestParams* fpp, const uint16_t* Xb, const double* vals,
+                                       int ldv, const int32_t* nval, const uint8_t* ycls,
+                                       const int64_t* r1, int cap, int32_t* feat, int32_t* thr,
+                                       int32_t* left, double* val, int32_t* nnodes, uint8_t* inbag,
+                                       int nthreads) {
+  const ForestParams fp = *fpp;
+  if (fp.p >= 4094 || fp.n <= 0 || fp.sampling != 0 || fp.kind == 2) return -1;
+  Out o{cap, feat, thr, left, val, nnodes, inbag, nullptr};
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int t = 0; t < fp.ntree; ++t) grow_tree_exact(fp, t, Xb, vals, ldv, nval, ycls, r1, o);
+  return 0;
+}
 
 ATECPU_API int atecpu_forest_fit(const ForestParams* fpp, const uint8_t* Xb, const uint8_t* ycls,
                                  const int64_t* r1, const int64_t* r2, int cap, int32_t* feat,
@@ -276,11 +421,11 @@ ATECPU_API int atecpu_forest_fit(const ForestParams* fpp, const uint8_t* Xb, con
 //  out (kind 0): [n2] vote share (NaN if no tree used); (kind 1): [n2] mean of tree
 //  predictions; (kind 2): [n2][4] = tau, var (little bags), trees used, groups used.
 // Regression/causal grf trees predict from the deepest node on the path with J2 rows.
-ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb, int n2, int oob,
-                                     int cap, const int32_t* feat, const int32_t* thr,
-                                     const int32_t* left, const double* val,
-                                     const uint8_t* inbag, const int64_t* est, double* state,
-                                     int phases, double* out, int nthreads) {
+template <typename BT>
+static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, int cap,
+                        const int32_t* feat, const int32_t* thr, const int32_t* left,
+                        const double* val, const uint8_t* inbag, const int64_t* est, double* state,
+                        int phases, double* out, int nthreads) {
   // state: [10][n2] accumulators, same protocol as csrc/forest.hip ate_forest_predict
   // (1 = per-tree sums, 2 = kind-2 little-bag group sums, 4 = finalise).
   const ForestParams fp = *fpp;
@@ -387,4 +532,23 @@ ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb,
     }
   }
   return 0;
+}
+
+ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb, int n2, int oob,
+                                     int cap, const int32_t* feat, const int32_t* thr,
+                                     const int32_t* left, const double* val,
+                                     const uint8_t* inbag, const int64_t* est, double* state,
+                                     int phases, double* out, int nthreads) {
+  return predict_impl(fpp, Xb, n2, oob, cap, feat, thr, left, val, inbag, est, state, phases, out,
+                      nthreads);
+}
+
+// exact-split forests: uint16 value-rank bins
+ATECPU_API int atecpu_forest_predict16(const ForestParams* fpp, const uint16_t* Xb, int n2, int oob,
+                                       int cap, const int32_t* feat, const int32_t* thr,
+                                       const int32_t* left, const double* val,
+                                       const uint8_t* inbag, const int64_t* est, double* state,
+                                       int phases, double* out, int nthreads) {
+  return predict_impl(fpp, Xb, n2, oob, cap, feat, thr, left, val, inbag, est, state, phases, out,
+                      nthreads);
 }

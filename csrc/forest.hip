@@ -749,6 +749,27 @@ __global__ __launch_bounds__(256) void forest_leaf_kernel(ForestParams fp,
   *out = honest ? last_ok : v;
 }
 
+// exact-split forests (csrc/forest_exact.hip): uint16 value-rank bins, unpacked node arrays
+__global__ __launch_bounds__(256) void forest_leaf16_kernel(ForestParams fp,
+                                                            const uint16_t* __restrict__ Xb, int n2,
+                                                            int oob, int cap, int t0,
+                                                            const int32_t* __restrict__ feat,
+                                                            const int32_t* __restrict__ thr,
+                                                            const int32_t* __restrict__ left,
+                                                            const uint8_t* __restrict__ inbag,
+                                                            int32_t* __restrict__ leaves) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int t = t0 + blockIdx.y;
+  if (i >= n2) return;
+  int32_t* out = leaves + (int64_t)blockIdx.y * n2 + i;
+  if (oob && inbag[(int64_t)t * fp.n + i]) { *out = -1; return; }
+  const int64_t b = (int64_t)t * cap;
+  int v = 0;
+  while (feat[b + v] >= 0)
+    v = Xb[(int64_t)feat[b + v] * n2 + i] <= thr[b + v] ? left[b + v] : left[b + v] + 1;
+  *out = v;
+}
+
 // kind 0/1: running (sum, count) per row over trees in ascending order
 __global__ __launch_bounds__(256) void forest_vote_kernel(ForestParams fp, int n2, int cap, int t0,
                                                           int nt, const int32_t* __restrict__ leaves,
@@ -881,21 +902,17 @@ ATE_API int ate_forest_pack(const void* fpp, int cap, const void* feat, const vo
 // 2 = kind-2 little-bag group sums (needs the COMPLETE phase-1 sums in state),
 // 4 = finalise state -> out. A tree-parallel forest runs 1, all-reduce(state[0:5n2]),
 // 2, all-reduce(state[5n2:10n2]), 4 (models/forest.py::predict_tree_parallel).
-ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob, int cap,
-                               const void* packed, const void* val, const void* inbag,
+template <typename LeafFn>
+static int forest_predict_impl(const ForestParams& fp, int n2, int cap, const void* val,
                                const void* est, void* leaves, int tchunk, void* state, void* out,
-                               int phases, void* stream) {
-  const ForestParams fp = *(const ForestParams*)fpp;
-  hipStream_t st = (hipStream_t)stream;
+                               int phases, hipStream_t st, LeafFn leaf) {
   if (tchunk < 1 || (fp.kind == 2 && tchunk % fp.group)) return -1;
   const int rb = (n2 + 255) / 256;
   for (int pass = 0; pass < 2; ++pass) {
     if (!(phases & (1 << pass)) || (pass == 1 && fp.kind != 2)) continue;
     for (int t0 = 0; t0 < fp.ntree; t0 += tchunk) {
       const int nt = min(tchunk, fp.ntree - t0);
-      hipLaunchKernelGGL(forest_leaf_kernel, dim3(rb, nt), dim3(256), 0, st, fp,
-                         (const uint8_t*)Xb, n2, oob, cap, t0, (const int2*)packed,
-                         (const uint8_t*)inbag, (int32_t*)leaves);
+      leaf(dim3(rb, nt), t0);
       if (fp.kind != 2)
         hipLaunchKernelGGL(forest_vote_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
                            (const int32_t*)leaves, (const double*)val, (const int64_t*)est,
@@ -913,6 +930,34 @@ ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob,
                        (const double*)state, (double*)out);
   ATE_CHECK_LAUNCH();
   return 0;
+}
+
+ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob, int cap,
+                               const void* packed, const void* val, const void* inbag,
+                               const void* est, void* leaves, int tchunk, void* state, void* out,
+                               int phases, void* stream) {
+  const ForestParams fp = *(const ForestParams*)fpp;
+  hipStream_t st = (hipStream_t)stream;
+  return forest_predict_impl(fp, n2, cap, val, est, leaves, tchunk, state, out, phases, st,
+                             [&](dim3 g, int t0) {
+    hipLaunchKernelGGL(forest_leaf_kernel, g, dim3(256), 0, st, fp, (const uint8_t*)Xb, n2, oob,
+                       cap, t0, (const int2*)packed, (const uint8_t*)inbag, (int32_t*)leaves);
+  });
+}
+
+// exact-split forests: uint16 bins and the unpacked (feat, thr, left) arrays
+ATE_API int ate_forest_predict16(const void* fpp, const void* Xb, int n2, int oob, int cap,
+                                 const void* feat, const void* thr, const void* left,
+                                 const void* val, const void* inbag, void* leaves, int tchunk,
+                                 void* state, void* out, int phases, void* stream) {
+  const ForestParams fp = *(const ForestParams*)fpp;
+  hipStream_t st = (hipStream_t)stream;
+  return forest_predict_impl(fp, n2, cap, val, nullptr, leaves, tchunk, state, out, phases, st,
+                             [&](dim3 g, int t0) {
+    hipLaunchKernelGGL(forest_leaf16_kernel, g, dim3(256), 0, st, fp, (const uint16_t*)Xb, n2, oob,
+                       cap, t0, (const int32_t*)feat, (const int32_t*)thr, (const int32_t*)left,
+                       (const uint8_t*)inbag, (int32_t*)leaves);
+  });
 }
 
 // ------------------------------------------------------------ K11 binning

@@ -141,6 +141,26 @@ ATE_HD int min_child(const ForestParams& fp, double n_node) {
   return c < 1.0 ? 1 : (int)c;
 }
 
+// Exact-split mode (randomForest split semantics, csrc/forest_exact.hip and its host twin):
+// bins are the ranks of a feature's distinct values (uint16, <= 65536 distinct values,
+// vals = the sorted distinct values); a split between the node's consecutive distinct
+// values u[blo] < u[bhi] is placed at their midpoint like randomForest's findbestsplit, and
+// stored as the largest global bin whose value is <= the midpoint (clamped to [blo, bhi-1]
+// so the node's own partition cannot change when the fp64 midpoint rounds onto u[bhi]).
+// Any row whose value is in the table goes left iff value <= midpoint.
+ATE_HD int exact_threshold_bin(const double* v, int nv, int blo, int bhi) {
+  const double mid = (v[blo] + v[bhi]) / 2.0;
+  int lo = 0, hi = nv;                 // first index with v > mid
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (v[m] <= mid) lo = m + 1; else hi = m;
+  }
+  int t = lo - 1;
+  if (t < blo) t = blo;
+  if (t > bhi - 1) t = bhi - 1;
+  return t;
+}
+
 // causal node constants from exact fixed-point sums over the node's J1 rows:
 // n, SW = sum W~, SY = sum Y~, SWW, SWY (products in fixed point as well)
 struct CausalNode { double wbar, ybar, tau, varw; };

@@ -136,7 +136,8 @@ def test_causal_forest_heterogeneous_effect():
     assert 0.01 < np.sqrt(np.nanmean(cf.var_oob)) < 2.0
 
 
-def test_rf_oob_propensity_matches_sklearn_statistically():
+@pytest.mark.parametrize("splits", ["binned", "exact"])
+def test_rf_oob_propensity_matches_sklearn_statistically(splits):
     """Independent cross-check of the randomForest semantics (ate_functions.R:169-174:
     bootstrap, mtry = floor(sqrt(p)), Gini, fully grown, OOB vote shares) against
     scikit-learn's RandomForestClassifier with the same settings on the tutorial DGP's
@@ -149,7 +150,7 @@ def test_rf_oob_propensity_matches_sklearn_statistically():
     from ate_replication_causalml_amd.data.selection import apply_selection_bias
     m, _ = apply_selection_bias(make_tutorial_data(30000, seed=1991))
     X, W = m.X, m.W
-    ours = F.rf_classifier(X, W, num_trees=500, seed=7, backend="cpu").oob_proba()
+    ours = F.rf_classifier(X, W, num_trees=500, seed=7, backend="cpu", splits=splits).oob_proba()
     sk = RandomForestClassifier(n_estimators=500, max_features="sqrt", bootstrap=True,
                                 min_samples_leaf=1, oob_score=True, random_state=0,
                                 n_jobs=4).fit(X, W).oob_decision_function_[:, 1]
@@ -181,3 +182,81 @@ def test_rf_regressor_matches_sklearn_statistically():
     r2 = lambda f: 1 - np.mean((f - yt) ** 2) / np.var(yt)
     assert abs(r2(ours) - r2(sk)) < 0.03 and r2(ours) > 0.7
     assert np.corrcoef(ours, sk)[0, 1] > 0.97
+
+
+# ------------------------------------------------------------------ exact-split mode
+def _exact_data(n=3000, p=6, seed=0, rounded=False):
+    r = np.random.default_rng(seed)
+    X = r.normal(size=(n, p))
+    if rounded:
+        X = np.round(X, 1)          # < 256 distinct values per feature
+    W = (r.uniform(size=n) < 1 / (1 + np.exp(-X[:, 0] - X[:, 1] * X[:, 2]))).astype(float)
+    Y = X[:, 1] + W * (1 + X[:, 0]) + 0.5 * r.normal(size=n)
+    return X, W, Y
+
+
+@pytest.mark.parametrize("kind", [F.KIND_CLASS, F.KIND_REG])
+def test_exact_splits_equal_binned_engine_on_few_distinct_values(kind):
+    """With <= 256 distinct values per feature the binned engine's bins are already the value
+    ranks, so the sort-based exact engine must grow the same tree shapes (features, children,
+    leaf values, in-bag rows); only thresholds may move inside the gap between a node's
+    neighbouring values (binned: at the left value, exact: at the midpoint)."""
+    X, W, Y = _exact_data(rounded=True)
+    kw = dict(ntree=12, seed=5, backend="cpu")
+    kw.update(y=W) if kind == F.KIND_CLASS else kw.update(r1=Y, min_node=5)
+    a = F.fit_forest(X, kind, splits="exact", **kw)
+    b = F.fit_forest(X, kind, **kw)
+    fa, ta, la, va, na = a.tree_arrays()
+    fb, tb, lb, vb, nb = b.tree_arrays()
+    np.testing.assert_array_equal(na, nb)
+    for t in range(12):
+        s = slice(t * a.cap, t * a.cap + na[t])
+        np.testing.assert_array_equal(fa[s], fb[s])
+        np.testing.assert_array_equal(la[s], lb[s])
+        np.testing.assert_array_equal(va[s], vb[s])
+        assert (ta[s] >= tb[s]).all()
+    np.testing.assert_array_equal(np.asarray(a.inbag), np.asarray(b.inbag))
+
+
+def test_exact_split_thresholds_are_randomforest_midpoints():
+    """Every split of an exact forest on continuous covariates sits at the midpoint of the
+    node's two neighbouring in-bag values (randomForest findbestsplit): routing the in-bag
+    rows down each tree, max(left values) <= thr value and the stored bin is the last table
+    value <= (max left + min right) / 2."""
+    X, W, _ = _exact_data(n=1500, p=5, seed=2)
+    fr = F.fit_forest(X, F.KIND_CLASS, y=W, ntree=6, seed=9, backend="cpu", splits="exact")
+    eb = fr.exact
+    feat, thr, left, _, nn = fr.tree_arrays()
+    inbag = np.asarray(fr.inbag).reshape(6, -1)
+    checked = 0
+    for t in range(6):
+        base = t * fr.cap
+        stack = [(0, np.flatnonzero(inbag[t]))]
+        while stack:
+            v, rows = stack.pop()
+            f = feat[base + v]
+            if f < 0:
+                continue
+            x = X[rows, f]
+            go = fr.exact.bin(X[rows])[f] <= thr[base + v]
+            lmax, rmin = x[go].max(), x[~go].min()
+            mid = (lmax + rmin) / 2.0
+            u = eb.vals[f, :eb.nval[f]]
+            want = max(np.searchsorted(u, lmax), min(np.searchsorted(u, mid, side="right") - 1,
+                                                     np.searchsorted(u, rmin) - 1))
+            assert thr[base + v] == want
+            checked += 1
+            stack += [(left[base + v], rows[go]), (left[base + v] + 1, rows[~go])]
+    assert checked > 500
+
+
+def test_exact_splits_new_data_prediction_uses_midpoints():
+    """Prediction on rows of the training table goes left iff value <= midpoint: a tree
+    with one split on a single feature classifies a grid of table values accordingly."""
+    x = np.array([0.0, 1.0, 4.0, 5.0] * 50)[:, None]
+    y = (x[:, 0] > 2).astype(float)
+    fr = F.fit_forest(x, F.KIND_CLASS, y=y, ntree=3, seed=1, backend="cpu", splits="exact")
+    feat, thr, _, _, nn = fr.tree_arrays()
+    assert (nn == 3).all() and (thr[::fr.cap] == 1).all()     # bins 0,1 | 2,3: at 2.5
+    np.testing.assert_array_equal(fr.predict_proba(np.array([[0.0], [1.0], [4.0], [5.0]])),
+                                  [0, 0, 1, 1])

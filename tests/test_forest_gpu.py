@@ -153,3 +153,27 @@ def test_level_engine_wide_many_features(gpu, monkeypatch):
     monkeypatch.setenv("ATE_FOREST_ENGINE", "tree")
     t = F.fit_forest(X, backend="gpu", **kw)
     assert_same_forest(g, t)
+
+
+@pytest.mark.parametrize("n", [3000, 20000])
+@pytest.mark.parametrize("case", ["rf_class", "rf_reg"])
+def test_exact_split_engine_bit_identical_to_host(gpu, case, n):
+    """csrc/forest_exact.hip (sort-based splits on uint16 value ranks: wave-level nodes <= 64
+    rows, workgroup bitonic sorts in LDS <= 8192 rows and in global scratch above -- the
+    n = 20000 root) grows the host twin's trees bit for bit; OOB and new-row predictions
+    match."""
+    r = np.random.default_rng(11)
+    X = r.normal(size=(n, 7))
+    X[:, 3] = np.round(X[:, 3])                 # a few ties / repeated values
+    W = (r.uniform(size=n) < 1 / (1 + np.exp(-X[:, 0] - X[:, 1] * X[:, 2]))).astype(float)
+    Y = X[:, 1] + W * (1 + X[:, 0]) + 0.5 * r.normal(size=n)
+    kw = dict(ntree=10, seed=13, splits="exact")
+    if case == "rf_class":
+        kw.update(kind=F.KIND_CLASS, y=W)
+    else:
+        kw.update(kind=F.KIND_REG, r1=Y, min_node=5, mtry=3)
+    g = F.fit_forest(X, backend="gpu", **kw)
+    c = F.fit_forest(X, backend="cpu", **kw)
+    assert_same_forest(g, c)
+    np.testing.assert_array_equal(g.oob_proba(), c.oob_proba())
+    np.testing.assert_array_equal(g.predict_proba(X[:700]), c.predict_proba(X[:700]))
