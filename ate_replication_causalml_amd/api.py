@@ -146,17 +146,21 @@ def ate_lasso(Y, W, X, nfolds=10, method="Usual LASSO", run=None) -> AteResult:
 
 
 def ate_aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000,
-                method="Doubly Robust with Random Forest PS", run=None) -> AteResult:
-    """E8 doubly_robust (ate_functions.R:149-207)."""
+                method="Doubly Robust with Random Forest PS", run=None,
+                splits="auto") -> AteResult:
+    """E8 doubly_robust (ate_functions.R:149-207). ``splits``: "exact" = randomForest split
+    semantics (every distinct value, midpoint thresholds), "binned" = 256-bin histograms,
+    "auto" = exact up to 65536 rows (the tutorial's df_mod)."""
     run = _run(run)
     with trace("ate_aipw_rf", trees=num_trees):
         if _ref(run):
             from .reference import estimators as R
             return R.aipw_rf(Y, W, X, num_trees=num_trees, bootstrap_se=bootstrap_se, B=B,
-                             seed=run.seed, compat=run.compat, method=method)
+                             seed=run.seed, compat=run.compat, method=method, splits=splits)
         from .estimators import forest as DF
         return DF.aipw_rf(Y, W, X, num_trees=num_trees, bootstrap_se=bootstrap_se, B=B,
-                          seed=run.seed, compat=run.compat, method=method, device=run.device())
+                          seed=run.seed, compat=run.compat, method=method, device=run.device(),
+                          splits=splits)
 
 
 def ate_aipw_glm(Y, W, X, bootstrap_se=False, B=1000,
@@ -187,15 +191,18 @@ def ate_belloni(Y, W, X, nfolds=10, method="Belloni et.al", run=None) -> AteResu
                           method=method, device=run.device(), dtype=run.dtype)
 
 
-def ate_double_ml(Y, W, X, num_trees=100, method="Double Machine Learning", run=None) -> AteResult:
-    """E12/E13 double_ml (ate_functions.R:332-389): two-half RF cross-fitting."""
+def ate_double_ml(Y, W, X, num_trees=100, method="Double Machine Learning", run=None,
+                  splits="auto") -> AteResult:
+    """E12/E13 double_ml (ate_functions.R:332-389): two-half RF cross-fitting; ``splits``
+    as in ate_aipw_rf."""
     run = _run(run)
     with trace("ate_double_ml", trees=num_trees):
         if _ref(run):
             from .reference import estimators as R
-            return R.double_ml(Y, W, X, num_trees=num_trees, method=method)
+            return R.double_ml(Y, W, X, num_trees=num_trees, method=method, splits=splits)
         from .estimators import forest as DF
-        return DF.double_ml(Y, W, X, num_trees=num_trees, method=method, device=run.device())
+        return DF.double_ml(Y, W, X, num_trees=num_trees, method=method, device=run.device(),
+                            splits=splits)
 
 
 def ate_dml(Y, W, X, folds=5, lambda_rule="min", method="DML cross-fit (LASSO)",

@@ -143,6 +143,11 @@ class ExactBins:
     def ldv(self):
         return self.vals.shape[1]
 
+    def on(self, dev) -> "DeviceExactBins":
+        """The value table as device tensors (inputs of a captured estimator graph)."""
+        return DeviceExactBins(torch.as_tensor(self.vals, device=dev),
+                               torch.as_tensor(self.nval, device=dev))
+
     def bin(self, X) -> np.ndarray:
         """uint16 [p][n] column-major bins of X (host)."""
         Xh = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X,
@@ -152,6 +157,30 @@ class ExactBins:
         for j in range(p):
             out[j] = np.searchsorted(self.mids[j, :self.nval[j] - 1], Xh[:, j], side="left")
         return out
+
+
+@dataclass
+class DeviceExactBins:
+    """ExactBins.vals / nval resident on the device (no host data: rows must come binned)."""
+    vals: torch.Tensor
+    nval: torch.Tensor
+
+    @property
+    def ldv(self):
+        return self.vals.shape[1]
+
+    def bin(self, X):
+        raise ValueError("a device-only exact bin table cannot bin new rows; pass binned rows")
+
+
+def resolve_splits(splits: str, n: int) -> str:
+    """"auto": randomForest's exact splits when the rows fit the uint16 value ranks
+    (n <= 65536, the tutorial scale), else the 256-bin histogram engine."""
+    if splits == "auto":
+        return "exact" if n <= EXACT_MAX_ROWS else "binned"
+    if splits not in ("binned", "exact"):
+        raise ValueError(f"splits must be 'auto', 'binned' or 'exact', got {splits!r}")
+    return splits
 
 
 def exact_bins(X) -> ExactBins:
@@ -207,7 +236,8 @@ class Forest:
         if self.exact is not None:
             b = torch.from_numpy(self.exact.bin(X))
             return b.to(self.device) if self.backend == "gpu" else b
-        return bin_matrix(X, self.edges, self.nedges, self.device if self.backend == "gpu" else None)
+        dev = self.device if self.backend == "gpu" else None
+        return bin_matrix(X, self.edges, self.nedges, dev)
 
     def predict_raw(self, X=None, oob=False) -> np.ndarray:
         """kind 0/1: [n] predictions; kind 2: [n, 4] (tau, var, trees used, groups used)."""
@@ -269,7 +299,8 @@ class Forest:
             res = np.empty(n2 * width)
             Xbn = np.ascontiguousarray(Xb.numpy() if isinstance(Xb, torch.Tensor) else Xb)
             lib = _native.cpu()
-            fn = lib.atecpu_forest_predict16 if self.exact is not None else lib.atecpu_forest_predict
+            fn = lib.atecpu_forest_predict16 if self.exact is not None else \
+                lib.atecpu_forest_predict
             rc = fn(
                 ctypes.byref(self.params), _ptr(Xbn), ctypes.c_int(n2), ctypes.c_int(int(oob)),
                 ctypes.c_int(self.cap), _ptr(self.feat), _ptr(self.thr), _ptr(self.left),
@@ -443,11 +474,11 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
     return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xbn)
 
 
-def fit_forest_exact(Xb, eb: ExactBins, kind: int, y=None, r1=None, ntree=500, mtry=None,
+def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, ntree=500, mtry=None,
                      min_node=1, sampling=0, seed=1, tree_offset=0) -> Forest:
     """Exact-split forest on value-rank bins ``Xb`` (uint16 [p][n]; a device tensor grows on
     the GPU, csrc/forest_exact.hip, a host one on the CPU twin). randomForest sampling,
-    kinds 0/1."""
+    kinds 0/1. ``eb``: ExactBins (or, on the GPU, its DeviceExactBins)."""
     if sampling != 0 or kind not in (KIND_CLASS, KIND_REG):
         raise ValueError("exact-split forests: randomForest sampling, classification or "
                          "regression")
@@ -465,10 +496,18 @@ def fit_forest_exact(Xb, eb: ExactBins, kind: int, y=None, r1=None, ntree=500, m
                                            np.asarray(a))
     if gpu:
         dev = Xb.device
-        yt = None if y is None else torch.as_tensor(h(y).astype(np.uint8), device=dev)
-        r1t = None if r1 is None else torch.as_tensor(to_fix(h(r1)), device=dev)
-        vals = torch.as_tensor(eb.vals, device=dev)
-        nval = torch.as_tensor(eb.nval, device=dev)
+        # device responses stay on the device (capturable estimator bodies)
+        if isinstance(y, torch.Tensor):
+            yt = y.to(dev, torch.uint8)
+        else:
+            yt = None if y is None else torch.as_tensor(h(y).astype(np.uint8), device=dev)
+        if isinstance(r1, torch.Tensor):
+            v = r1.to(dev, torch.float64) * FIX
+            r1t = torch.where(v >= 0, torch.floor(v + 0.5), torch.ceil(v - 0.5)).to(torch.int64)
+        else:
+            r1t = None if r1 is None else torch.as_tensor(to_fix(h(r1)), device=dev)
+        de = eb.on(dev) if isinstance(eb, ExactBins) else eb
+        vals, nval = de.vals, de.nval
         feat = torch.empty(ntree * cap, dtype=torch.int32, device=dev)
         thr = torch.empty_like(feat)
         left = torch.empty_like(feat)
@@ -483,7 +522,7 @@ def fit_forest_exact(Xb, eb: ExactBins, kind: int, y=None, r1=None, ntree=500, m
         s = torch.cuda.current_stream().cuda_stream
         for t0 in range(0, ntree, chunk):
             _native.call("ate_forest_fit_exact", ctypes.addressof(fp), t0, min(chunk, ntree - t0),
-                         Xb.data_ptr(), vals.data_ptr(), eb.ldv, nval.data_ptr(), p_(yt), p_(r1t),
+                         Xb.data_ptr(), vals.data_ptr(), de.ldv, nval.data_ptr(), p_(yt), p_(r1t),
                          cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(), val.data_ptr(),
                          nnodes.data_ptr(), inbag.data_ptr(), scratch.data_ptr(), s)
         del scratch

@@ -195,14 +195,16 @@ def aipw_glm(Y, W, X, bootstrap_se=False, B=1000, seed=1991, compat="reference",
 
 
 def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, forest_seed=12325,
-            compat="reference", method="Doubly Robust with Random Forest PS"):
+            compat="reference", method="Doubly Robust with Random Forest PS", splits="auto"):
     """``doubly_robust`` (ate_functions.R:149-207): logistic outcome model,
     random-forest OOB propensity (clipped, Q9), counterfactual quirk Q6 under
-    ``compat="reference"``."""
+    ``compat="reference"``. ``splits``: models/forest.resolve_splits."""
+    from ..models.forest import resolve_splits
     from .forest import rf_classifier_fit
     Y, W, X = _arr(Y), _arr(W), _arr(X)
     mu0, mu1 = outcome_logit_mu(Y, W, X, counterfactual_quirk=(compat == "reference"))
-    rf = rf_classifier_fit(X, W, num_trees=num_trees, seed=forest_seed)
+    rf = rf_classifier_fit(X, W, num_trees=num_trees, seed=forest_seed,
+                           splits=resolve_splits(splits, len(Y)))
     p = clip_propensity(rf.oob_proba())
     return _aipw_result(method, W, Y, p, mu0, mu1, bootstrap_se, B, seed, compat,
                         n_oob_nan=int(np.isnan(rf.oob_proba()).sum()))
@@ -272,15 +274,16 @@ def belloni(Y, W, X, seed=1991, nfolds=10, compat="reference", method="Belloni e
 
 
 # ---------------------------------------------------------------- E12/E13 DML (compat)
-def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123):
-    """One DML half (ate_functions.R:332-369, Q14/Q15)."""
+def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, splits="auto"):
+    """One DML half (ate_functions.R:332-369, Q14/Q15); bins from all rows."""
     from ..models import forest as F
     Y, W, X = _arr(Y), _arr(W), _arr(X)
-    edges = F.bin_edges(X)
+    splits = F.resolve_splits(splits, len(Y))
+    edges = F.exact_bins(X) if splits == "exact" else F.bin_edges(X)
     rf1 = F.fit_forest(X[idx1], F.KIND_CLASS, y=W[idx1], ntree=num_trees, seed=seed,
-                       backend="cpu", edges=edges)
+                       backend="cpu", edges=edges, splits=splits)
     rf2 = F.fit_forest(X[idx2], F.KIND_CLASS, y=Y[idx2], ntree=num_trees, seed=seed + 1,
-                       backend="cpu", edges=edges)
+                       backend="cpu", edges=edges, splits=splits)
     ew = rf1.predict_proba(X)
     ey = rf2.predict_proba(X)
     return resid_on_resid(Y - ey, W - ew)
@@ -295,13 +298,14 @@ def resid_on_resid(yr, wr):
     return tau, se
 
 
-def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning"):
+def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning",
+              splits="auto"):
     """``double_ml`` (ate_functions.R:372-389): positional 2-way split, average tau and SE."""
     n = len(Y)
     h = n // 2
     idx1, idx2 = np.arange(h), np.arange(h, n)
-    t1, s1 = chernozhukov(Y, W, X, idx1, idx2, num_trees, seed)
-    t2, s2 = chernozhukov(Y, W, X, idx2, idx1, num_trees, seed + 2)
+    t1, s1 = chernozhukov(Y, W, X, idx1, idx2, num_trees, seed, splits)
+    t2, s2 = chernozhukov(Y, W, X, idx2, idx1, num_trees, seed + 2, splits)
     return AteResult.make(method, (t1 + t2) / 2, (s1 + s2) / 2)
 
 

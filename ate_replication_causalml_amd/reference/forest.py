@@ -5,6 +5,6 @@ from ..models.forest import (average_treatment_effect, causal_forest, fit_forest
                              regression_forest, rf_classifier)
 
 
-def rf_classifier_fit(X, y, num_trees=500, seed=1, mtry=None, nodesize=1):
+def rf_classifier_fit(X, y, num_trees=500, seed=1, mtry=None, nodesize=1, splits="binned"):
     return rf_classifier(X, y, num_trees=num_trees, mtry=mtry, nodesize=nodesize, seed=seed,
-                         backend="cpu")
+                         backend="cpu", splits=splits)

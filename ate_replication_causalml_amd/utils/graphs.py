@@ -232,6 +232,9 @@ def layout_key(*inputs):
     devices and, for panels, the column map, fold segments and real-row counts."""
     key = []
     for x in inputs:
+        if x is None:                 # optional input (e.g. no exact-split value table)
+            key.append(None)
+            continue
         t = _data(x)
         k = (tuple(t.shape), t.dtype, str(t.device))
         if not isinstance(x, torch.Tensor):
@@ -253,7 +256,7 @@ class _Captured:
 
     def load(self, inputs):
         for s, x in zip(self.inputs, inputs):
-            if x is not s:
+            if x is not s and x is not None:
                 _data(s).copy_(_data(x))
 
     def __call__(self, inputs):
@@ -274,6 +277,8 @@ class _Seen:
 def _nbytes(inputs):
     tot = 0
     for x in inputs:
+        if x is None:
+            continue
         t = _data(x)
         tot += t.numel() * t.element_size()
     return tot
@@ -351,7 +356,7 @@ class GraphCache:
             try:
                 torch.cuda.synchronize()
                 for s, x in zip(static, inputs):
-                    if x is not s:
+                    if x is not s and x is not None:
                         _data(s).copy_(_data(x))
                 g = _Captured(body, static, static_args, warmup=1)
             except Exception as e:  # noqa: BLE001 - fall back to eager, but say why
