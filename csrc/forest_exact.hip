@@ -9,32 +9,56 @@
 // prefix-summed in that order; the criterion is evaluated at every boundary between two
 // distinct values, ties broken by (feature slot, position) as on the host.
 //
-// Decomposition: ONE workgroup (4 waves) per tree, level by level.
-//  * nodes of <= 64 rows are decided and partitioned by ONE WAVE each (the 4 waves take
-//    them round-robin): a row per lane, ranks by 64 lane compares, the sorted order built
-//    with ds_permute (no LDS round trip), prefix sums by lane shuffles;
-//  * larger nodes are decided by the whole workgroup, one at a time: a bitonic sort of the
-//    32-bit keys in LDS (<= 8192 rows) or in the tree's global scratch (larger nodes),
-//    chunked prefix sums with a workgroup scan, an argmax reduction;
-//  * child ids are assigned after the level in list order (thread 0), so numbering
-//    equals the host engine's.
+// Decomposition: ONE workgroup (8 waves) per tree, level by level.
+//  * nodes of <= 512 rows are decided and partitioned by ONE WAVE each, without workgroup
+//    barriers (node j goes to wave j mod 8). <= 64 rows: a row per lane, ranks by 64
+//    lane compares, the sorted order built with ds_permute, prefix sums by lane shuffles;
+//    65..512 rows: a wave-synchronous bitonic sort of the 32-bit keys in the wave's LDS
+//    slice, the per-position statistics staged beside them, chunk sums and a wave scan;
+//  * larger nodes are decided by the whole workgroup, one at a time: a bitonic sort in LDS
+//    (<= 16384 rows) or in the tree's global scratch, chunked prefix sums with a workgroup
+//    scan, an argmax reduction;
+//  * child ids are assigned after the level in list order (a workgroup scan of the split
+//    flags), so numbering equals the host engine's.
 // Only randomForest sampling (bootstrap) and kinds 0/1 (classification, regression).
 #include "common.hpp"
 #include "forest_common.hpp"
 
 using namespace atef;
 
+#ifdef EXACT_PROF
+// per-phase wall_clock64 ticks of tree 0 (tools/exact_forest_prof.py): [0] setup, [1] big-node
+// list, [2] workgroup decisions, [3] wave decisions, [4] ids, [5] workgroup partitions,
+// [6] wave partitions, [7] levels, [8..15] per-wave busy ticks in the wave decisions,
+// workgroup decisions split: [16] statistics + draws, [17] key fill, [18] sort, [19] walk +
+// argmax, [20] threshold, [21] workgroup-level nodes decided
+__device__ unsigned long long exact_prof[24];
+#define XPROF_T(v) const unsigned long long v = wall_clock64()
+#define XPROF_ADD(k, d) do { if (blockIdx.x == 0 && threadIdx.x == 0) exact_prof[k] += (d); } while (0)
+#else
+#define XPROF_T(v)
+#define XPROF_ADD(k, d) do { } while (0)
+#endif
+
 namespace {
 
-constexpr int XT = 256;            // threads per tree
+constexpr int XT = 512;            // threads per tree
 constexpr int XW = XT / 64;        // waves per tree
-constexpr int XLDS = 8192;         // node keys sorted in LDS up to this many rows
+constexpr int XLDS = 16384;        // workgroup-level node keys sorted in LDS up to this many rows
+constexpr int WCAP = 512;          // nodes up to this many rows: one wave each
+// one LDS arena: the workgroup-level key buffer (XLDS keys) or, per wave, WCAP keys and the
+// WCAP per-position statistics (2 x int64) of the wave's node
+constexpr int WSLICE = WCAP * 4 + WCAP * 16;
+constexpr int XBIG = 65536 / WCAP + 1;     // > WCAP-row nodes of one level (n <= 65536)
+constexpr int ARENA = (XLDS * 4 > XW * WSLICE) ? XLDS * 4 : XW * WSLICE;
 constexpr int XPMAX = 512;         // max features
 
 struct XRng { int lo, hi, id; };
 struct XDec { int split, feat, thr, nl; double val; };
 
 struct XScratch {
+  int64_t* sx0;     // [n] per-position statistics of the workgroup-level node being decided
+  int64_t* sx1;     // [n]
   int32_t* w;       // [n] bootstrap weights
   int32_t* idx;     // [n] rows of the growing nodes (node = contiguous range)
   uint32_t* keys;   // [np2] global sort keys / partition staging
@@ -52,13 +76,15 @@ __host__ __device__ inline int np2(int n) {
 __host__ __device__ inline int64_t align16(int64_t b) { return (b + 15) & ~(int64_t)15; }
 
 __host__ __device__ inline int64_t tree_bytes(int n) {
-  return align16(4ll * n) * 2 + align16(4ll * np2(n)) + align16(12ll * (n + 1)) * 2 +
-         align16((int64_t)sizeof(XDec) * (n + 1));
+  return align16(8ll * n) * 2 + align16(4ll * n) * 2 + align16(4ll * np2(n)) +
+         align16(12ll * (n + 1)) * 2 + align16((int64_t)sizeof(XDec) * (n + 1));
 }
 
 __device__ XScratch scratch_at(char* base, int n) {
   XScratch s;
   char* p = base;
+  s.sx0 = (int64_t*)p; p += align16(8ll * n);
+  s.sx1 = (int64_t*)p; p += align16(8ll * n);
   s.w = (int32_t*)p; p += align16(4ll * n);
   s.idx = (int32_t*)p; p += align16(4ll * n);
   s.keys = (uint32_t*)p; p += align16(4ll * np2(n));
@@ -164,20 +190,89 @@ __device__ int draw_features(const ForestParams& fp, int tg, int v, int* perm) {
   return nf;
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int64_t wave_excl_scan64(int64_t v, int lane) {
+  int64_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(x, o, 64);
+    if (lane >= o) x += u;
+  }
+  return x - v;
+}
+
+// Workgroup exclusive count of `f` over threads (thread order); returns the total.
+// scnt: XW ints of LDS. Two barriers.
+__device__ __forceinline__ int block_flag_scan(bool f, int* scnt, int& before) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t b = __ballot(f);
+  if (lane == 0) scnt[wid] = __popcll(b);
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int w = 0; w < XW; ++w) {
+    if (w < wid) off += scnt[w];
+    tot += scnt[w];
+  }
+  before = off + __popcll(b & ((1ull << lane) - 1ull));
+  __syncthreads();
+  return tot;
+}
+
+// forest_common.hpp::exact_threshold_bin by a whole wave (uniform arguments): the largest
+// index t in [blo, bhi) with v[t] <= (v[blo] + v[bhi]) / 2, by a 64-ary search (one memory
+// latency per 64x narrowing instead of one per halving).
+__device__ int wave_threshold(const double* __restrict__ v, int blo, int bhi, int lane) {
+  const double mid = (v[blo] + v[bhi]) / 2.0;
+  int lo = blo, hi = bhi;                     // answer in [lo, hi); v[lo] <= mid
+  while (hi - lo > 1) {
+    const int step = (hi - lo + 63) / 64;
+    const int x = lo + lane * step;
+    const bool ok = x < hi && v[x] <= mid;
+    const uint64_t b = __ballot(ok);           // a prefix of lanes (v is sorted)
+    const int L = 63 - __clzll(b);
+    lo = lo + L * step;
+    hi = min(hi, lo + step);
+  }
+  return lo;
+}
+
+// Ascending bitonic sort of K[0..N2) (N2 a power of two) by ONE wave (wave-synchronous LDS).
+__device__ void wave_bitonic(uint32_t* K, int N2, int lane) {
+  for (int kk = 2; kk <= N2; kk <<= 1)
+    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+      for (int s = lane; s < N2; s += 64) {
+        const int o = s ^ jj;
+        if (o > s) {
+          const uint32_t x = K[s], y = K[o];
+          if ((x > y) == ((s & kk) == 0)) { K[s] = y; K[o] = x; }
+        }
+      }
+      wave_sync();
+    }
+}
+
 __global__ __launch_bounds__(XT) void forest_exact_kernel(
     ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const double* __restrict__ vals,
     int ldv, const int32_t* __restrict__ nval, const uint8_t* __restrict__ ycls,
     const int64_t* __restrict__ r1, int cap, int32_t* __restrict__ feat, int32_t* __restrict__ thr,
     int32_t* __restrict__ left, double* __restrict__ val, int32_t* __restrict__ nnodes,
     uint8_t* __restrict__ inbag, char* __restrict__ scratch) {
-  __shared__ uint32_t skeys[XLDS];
-  __shared__ int64_t sc0[XT], sc1[XT];
+  // one LDS key buffer: the whole of it for a workgroup-level node, a quarter (WCAP keys)
+  // per wave for the wave-level nodes (the two phases never overlap)
+  __shared__ __attribute__((aligned(16))) char sarena[ARENA];
+  __shared__ int64_t sw0[XW], sw1[XW];
   __shared__ int sperm[XW][XPMAX];
   __shared__ double sredc[XW];
   __shared__ int sreds[XW];
   __shared__ int64_t sred64[3][XW];
   __shared__ int scnt[XW + 1];
-  __shared__ int sncur, snext_id, sm;
+  __shared__ int sncur, snext_id, sm, snbig;
+  __shared__ int sbig[XBIG];                  // this level's workgroup-level nodes
   const int t = tbeg + blockIdx.x;            // tree within this forest
   const int tg = fp.t0 + t;                   // global tree id (RNG key)
   const int n = fp.n, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -188,6 +283,11 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
   int32_t* tleft = left + base;
   double* tval = val + base;
   uint8_t* inb = inbag + (int64_t)t * n;
+  uint32_t* skeys = (uint32_t*)sarena;
+  char* wsl = sarena + wid * WSLICE;          // this wave's slice: keys, then statistics
+  uint32_t* Kw = (uint32_t*)wsl;
+  int64_t* Xw0 = (int64_t*)(wsl + WCAP * 4);
+  int64_t* Xw1 = Xw0 + WCAP;
 
   // ---- bootstrap weights (integer atomics: order-free), in-bag mask, row list
   for (int i = tid; i < n; i += XT) S.w[i] = 0;
@@ -217,16 +317,45 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
     snext_id = 1;
   }
   __syncthreads();
+#ifdef EXACT_PROF
+  unsigned long long tp = wall_clock64();
+  XPROF_ADD(0, 0ull);
+#define XPHASE(k) do { __syncthreads(); const unsigned long long tn_ = wall_clock64(); \
+    XPROF_ADD(k, tn_ - tp); tp = tn_; } while (0)
+#else
+#define XPHASE(k) do { } while (0)
+#endif
 
   for (int depth = 0;; ++depth) {
     const int ncur = sncur;
     if (ncur == 0) break;
+    // this level's workgroup-level nodes, in list order
+    {
+      int nb = 0;
+      for (int c0 = 0; c0 < ncur; c0 += XT) {
+        const int j = c0 + tid;
+        bool big = false;
+        if (j < ncur) {
+          const XRng nd = S.cur[j];
+          big = nd.hi - nd.lo > WCAP;
+        }
+        int before;
+        const int tot = block_flag_scan(big, scnt, before);
+        if (big) sbig[nb + before] = j;
+        nb += tot;
+      }
+      if (tid == 0) snbig = nb;
+      __syncthreads();
+    }
+    const int nbig = snbig;
+    XPHASE(1);
+    XPROF_ADD(7, 1ull);
 
-    // ================= decisions: nodes > 64 rows, whole workgroup, one at a time
-    for (int j = 0; j < ncur; ++j) {
+    // ================= decisions: nodes > WCAP rows, whole workgroup, one at a time
+    for (int jb = 0; jb < nbig; ++jb) {
+      const int j = sbig[jb];
       const XRng nd = S.cur[j];
       const int cnt = nd.hi - nd.lo;
-      if (cnt <= 64) continue;
       // node statistics
       int64_t a = 0, b1 = 0, c = 0;
       for (int q = nd.lo + tid; q < nd.hi; q += XT) {
@@ -249,21 +378,58 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
       }
       if (tid == 0) scnt[XW] = draw_features(fp, tg, nd.id, sperm[0]);
       __syncthreads();
+#ifdef EXACT_PROF
+      unsigned long long tq = wall_clock64();
+#define XSUB(k) do { __syncthreads(); const unsigned long long tn_ = wall_clock64(); \
+    XPROF_ADD(k, tn_ - tq); tq = tn_; } while (0)
+      XPROF_ADD(21, 1ull);
+#else
+#define XSUB(k) do { } while (0)
+#endif
       const int nf = scnt[XW];
       const int minc = min_child(fp, (double)st.nw);
       const int N2 = np2(cnt);
       uint32_t* K = N2 <= XLDS ? skeys : S.keys;
+      // per-position statistics once per node (the feature loop reads them by sorted key)
+      for (int qb = tid; qb < cnt; qb += XT * 8) {
+        int iv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) iv[u] = qb + u * XT < cnt ? S.idx[nd.lo + qb + u * XT] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (qb + u * XT < cnt)
+            row_stats(fp, S.w, ycls, r1, iv[u], S.sx0[nd.lo + qb + u * XT], S.sx1[nd.lo + qb + u * XT]);
+      }
       double best = -INFINITY;                // thread 0's running best over features
       int bf = -1, blo = -1, bhi = -1, bnl = 0;
       for (int k = 0; k < nf; ++k) {
         const int f = sperm[0][k];
         const uint16_t* xf = Xb + (int64_t)f * n;
-        for (int s = tid; s < N2; s += XT)
-          K[s] = s < cnt ? (((uint32_t)xf[S.idx[nd.lo + s]] << 16) | (uint32_t)s) : 0xFFFFFFFFu;
+        // 8 positions per batch: their row ids, then the bins, then the key stores (the
+        // loads of a batch are in flight together)
+        for (int sb = tid; sb < N2; sb += XT * 8) {
+          int iv[8];
+          uint32_t bv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) iv[u] = sb + u * XT < cnt ? S.idx[nd.lo + sb + u * XT] : 0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) bv[u] = sb + u * XT < cnt ? (uint32_t)xf[iv[u]] : 0u;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int s = sb + u * XT;
+            if (s < N2) K[s] = s < cnt ? ((bv[u] << 16) | (uint32_t)s) : 0xFFFFFFFFu;
+          }
+        }
         __syncthreads();
-        // bitonic sort, ascending
-        for (int kk = 2; kk <= N2; kk <<= 1)
-          for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        XSUB(17);
+        // bitonic sort, ascending. In LDS, wave w owns the contiguous chunk [w C, (w+1) C):
+        // stages with partner distance jj < C stay inside a chunk and need only the wave's
+        // own ordering (no workgroup barrier); the few with jj >= C run workgroup-wide.
+        const int C = N2 / XW;
+        const bool local = K == skeys && C >= 64;
+        for (int kk = 2; kk <= N2; kk <<= 1) {
+          int jj = kk >> 1;
+          for (; jj > 0 && (!local || jj >= C); jj >>= 1) {
             for (int s = tid; s < N2; s += XT) {
               const int o = s ^ jj;
               if (o > s) {
@@ -274,28 +440,67 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
             }
             __syncthreads();
           }
+          for (; jj > 0; jj >>= 1) {            // local stages (only when `local`)
+            for (int s = wid * C + lane; s < (wid + 1) * C; s += 64) {
+              const int o = s ^ jj;
+              if (o > s) {
+                const uint32_t x = K[s], y = K[o];
+                const bool up = (s & kk) == 0;
+                if ((x > y) == up) { K[s] = y; K[o] = x; }
+              }
+            }
+            wave_sync();
+          }
+          if (local && kk >= C) __syncthreads();   // the next stage may cross chunks
+        }
+        __syncthreads();
+        XSUB(18);
         // chunked prefix sums: thread tid owns positions [s0, s1)
         const int ch = (cnt + XT - 1) / XT;
         const int s0 = min(cnt, tid * ch), s1 = min(cnt, s0 + ch);
+        const int64_t* g0 = S.sx0 + nd.lo;
+        const int64_t* g1 = S.sx1 + nd.lo;
         int64_t l0 = 0, l1 = 0;
-        for (int s = s0; s < s1; ++s) {
-          int64_t x0, x1;
-          row_stats(fp, S.w, ycls, r1, S.idx[nd.lo + (int)(K[s] & 0xFFFFu)], x0, x1);
-          l0 += x0; l1 += x1;
+        for (int sb = s0; sb < s1; sb += 8) {
+          int qv[8];
+          int64_t a0[8], a1[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) qv[u] = sb + u < s1 ? (int)(K[sb + u] & 0xFFFFu) : 0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            a0[u] = sb + u < s1 ? g0[qv[u]] : 0;
+            a1[u] = sb + u < s1 ? g1[qv[u]] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) { l0 += a0[u]; l1 += a1[u]; }
         }
-        sc0[tid] = l0; sc1[tid] = l1;
+        // workgroup exclusive scan of the chunk sums: wave scan + wave totals
+        int64_t p0 = wave_excl_scan64(l0, lane), p1 = wave_excl_scan64(l1, lane);
+        if (lane == 63) { sw0[wid] = p0 + l0; sw1[wid] = p1 + l1; }
         __syncthreads();
-        int64_t p0 = 0, p1 = 0;
-        for (int q = 0; q < tid; ++q) { p0 += sc0[q]; p1 += sc1[q]; }
+        for (int q = 0; q < wid; ++q) { p0 += sw0[q]; p1 += sw1[q]; }
         double bc = -INFINITY;
         int bs = 0x7FFFFFFF;
-        for (int s = s0; s < s1; ++s) {
-          int64_t x0, x1;
-          row_stats(fp, S.w, ycls, r1, S.idx[nd.lo + (int)(K[s] & 0xFFFFu)], x0, x1);
-          p0 += x0; p1 += x1;
-          if (s + 1 < cnt && (K[s] >> 16) != (K[s + 1] >> 16)) {
-            const double cr = boundary_crit(fp, st, minc, p0, p1);
-            if (cr > bc) { bc = cr; bs = s; }
+        for (int sb = s0; sb < s1; sb += 8) {
+          uint32_t kv[9];
+          int64_t a0[8], a1[8];
+#pragma unroll
+          for (int u = 0; u < 9; ++u) kv[u] = sb + u < cnt ? K[sb + u] : 0xFFFFFFFFu;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int q = (int)(kv[u] & 0xFFFFu);
+            a0[u] = sb + u < s1 ? g0[q] : 0;
+            a1[u] = sb + u < s1 ? g1[q] : 0;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int s = sb + u;
+            if (s >= s1) break;
+            p0 += a0[u]; p1 += a1[u];
+            if (s + 1 < cnt && (kv[u] >> 16) != (kv[u + 1] >> 16)) {
+              const double cr = boundary_crit(fp, st, minc, p0, p1);
+              if (cr > bc) { bc = cr; bs = s; }
+            }
           }
         }
         wave_argmax(bc, bs);
@@ -313,7 +518,8 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
             bnl = s2 + 1;
           }
         }
-        __syncthreads();                      // K, sc*, sred* reused by the next feature
+        __syncthreads();                      // K, sw*, sred* reused by the next feature
+        XSUB(19);
       }
       if (tid == 0) {
         const double parent = parent_crit(fp, st);
@@ -324,30 +530,119 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
           S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
       }
     }
+    __syncthreads();                          // the LDS key buffer changes owners
+    XPHASE(2);
+#ifdef EXACT_PROF
+    const unsigned long long tw0_ = wall_clock64();
+#endif
 
-    // ================= decisions: nodes <= 64 rows, one wave each
+    // ================= decisions: nodes <= WCAP rows, one wave each (round-robin)
     {
-      int r = 0;                              // rank among small nodes (uniform)
       int* perm = sperm[wid];
-      for (int j = 0; j < ncur; ++j) {
-        const XRng nd = S.cur[j];
+      XRng ndn = wid < ncur ? S.cur[wid] : XRng{0, 0, 0};
+      for (int j = wid; j < ncur; j += XW) {   // node j -> wave j % XW
+        const XRng nd = ndn;
+        if (j + XW < ncur) ndn = S.cur[j + XW];   // next node's range, in flight meanwhile
         const int cnt = nd.hi - nd.lo;
-        if (cnt > 64) continue;
-        if ((r++ % XW) != wid) continue;
-        const bool live = lane < cnt;
-        const int i = live ? S.idx[nd.lo + lane] : 0;
-        int64_t x0 = 0, x1 = 0;
-        if (live) row_stats(fp, S.w, ycls, r1, i, x0, x1);
-        NodeStats st;
-        if (fp.kind == 0) {
-          st.nw = wave_sum64(x0 + x1);
-          st.n1 = wave_sum64(x1);
-          st.s1 = 0;
-        } else {
-          st.nw = wave_sum64(x0);
-          st.n1 = 0;
-          st.s1 = wave_sum64(x1);
+        if (cnt > WCAP) continue;
+        if (cnt <= 64) {
+          // ---- a row per lane: ranks by lane compares, sorted order by ds_permute
+          const bool live = lane < cnt;
+          const int i = live ? S.idx[nd.lo + lane] : 0;
+          int64_t x0 = 0, x1 = 0;
+          if (live) row_stats(fp, S.w, ycls, r1, i, x0, x1);
+          NodeStats st;
+          if (fp.kind == 0) {
+            st.nw = wave_sum64(x0 + x1);
+            st.n1 = wave_sum64(x1);
+            st.s1 = 0;
+          } else {
+            st.nw = wave_sum64(x0);
+            st.n1 = 0;
+            st.s1 = wave_sum64(x1);
+          }
+          if (is_terminal(fp, st, depth)) {
+            if (lane == 0) S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
+            continue;
+          }
+          int nf = 0;
+          if (lane == 0) nf = draw_features(fp, tg, nd.id, perm);
+          nf = __shfl(nf, 0, 64);
+          wave_sync();
+          const int minc = min_child(fp, (double)st.nw);
+          double best = -INFINITY;
+          int bf = -1, blo = -1, bhi = -1, bnl = 0;
+          // the row's bins of up to 8 candidate features fetched together (one memory
+          // latency per 8 features instead of one per feature)
+          constexpr int PF = 8;
+          uint32_t bins[PF];
+          for (int k = 0; k < nf; ++k) {
+            const int f = perm[k];
+            if ((k % PF) == 0) {
+#pragma unroll
+              for (int u = 0; u < PF; ++u)
+                bins[u] = (live && k + u < nf) ? (uint32_t)Xb[(int64_t)perm[k + u] * n + i] : 0u;
+            }
+            uint32_t bk = bins[0];
+#pragma unroll
+            for (int u = 1; u < PF; ++u) bk = (k % PF) == u ? bins[u] : bk;
+            // idle lanes sort last with distinct keys (ranks cnt..63: ds_permute is a bijection)
+            const uint32_t key = live ? ((bk << 16) | (uint32_t)lane) : (0xFFFF0000u | (uint32_t)lane);
+            int rank = 0;
+            for (int q = 0; q < 64; ++q) rank += (uint32_t)__builtin_amdgcn_readlane((int)key, q) < key;
+            // lane s receives the key and statistics of the row ranked s
+            const uint32_t ks = permute_u32(rank, key);
+            int64_t c0 = permute_i64(rank, x0), c1 = permute_i64(rank, x1);
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+              const int64_t u0 = __shfl_up(c0, o, 64), u1 = __shfl_up(c1, o, 64);
+              if (lane >= o) { c0 += u0; c1 += u1; }
+            }
+            const uint32_t kn = __shfl_down(ks, 1, 64);
+            double cr = -INFINITY;
+            int s = 0x7FFFFFFF;
+            if (lane + 1 < cnt && (ks >> 16) != (kn >> 16)) {
+              cr = boundary_crit(fp, st, minc, c0, c1);
+              s = lane;
+            }
+            wave_argmax(cr, s);
+            if (cr > best) {                  // uniform
+              best = cr;
+              bf = f;
+              blo = (int)(__shfl(ks, s, 64) >> 16);
+              bhi = (int)(__shfl(kn, s, 64) >> 16);
+              bnl = s + 1;
+            }
+          }
+          const double parent = parent_crit(fp, st);
+          const bool split = bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent));
+          const int tb = split ? wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane) : -1;
+          if (lane == 0)
+            S.dec[j] = split ? XDec{1, bf, tb, bnl, 0.0}
+                             : XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
+          continue;
         }
+        // ---- 64 < cnt <= WCAP: wave bitonic sort of the keys in this wave's LDS slice, the
+        // per-position statistics staged beside them
+        static_assert(WCAP <= 64 * 8, "one 8-row batch per lane");
+        int iv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) iv[u] = lane + 64 * u < cnt ? S.idx[nd.lo + lane + 64 * u] : 0;
+        int64_t a = 0, b1 = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = lane + 64 * u;
+          if (q < cnt) {
+            int64_t x0, x1;
+            row_stats(fp, S.w, ycls, r1, iv[u], x0, x1);
+            Xw0[q] = x0; Xw1[q] = x1;
+            a += x0; b1 += x1;
+          }
+        }
+        a = wave_sum64(a); b1 = wave_sum64(b1);
+        NodeStats st;
+        if (fp.kind == 0) { st.nw = a + b1; st.n1 = b1; st.s1 = 0; }
+        else { st.nw = a; st.n1 = 0; st.s1 = b1; }
         if (is_terminal(fp, st, depth)) {
           if (lane == 0) S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
           continue;
@@ -355,80 +650,103 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
         int nf = 0;
         if (lane == 0) nf = draw_features(fp, tg, nd.id, perm);
         nf = __shfl(nf, 0, 64);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
         const int minc = min_child(fp, (double)st.nw);
+        const int N2 = np2(cnt);
+        const int ch = (cnt + 63) / 64;
+        const int s0 = min(cnt, lane * ch), s1 = min(cnt, s0 + ch);
         double best = -INFINITY;
         int bf = -1, blo = -1, bhi = -1, bnl = 0;
         for (int k = 0; k < nf; ++k) {
           const int f = perm[k];
-          // idle lanes sort last with distinct keys (ranks cnt..63, so ds_permute is a bijection)
-          const uint32_t key = live ? (((uint32_t)Xb[(int64_t)f * n + i] << 16) | (uint32_t)lane)
-                                    : (0xFFFF0000u | (uint32_t)lane);
-          int rank = 0;
-          for (int q = 0; q < 64; ++q) rank += (uint32_t)__builtin_amdgcn_readlane((int)key, q) < key;
-          // lane s receives the key and statistics of the row ranked s
-          const uint32_t ks = permute_u32(rank, key);
-          int64_t c0 = permute_i64(rank, x0), c1 = permute_i64(rank, x1);
+          const uint16_t* xf = Xb + (int64_t)f * n;
+          uint32_t bv[8];
 #pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const int64_t u0 = __shfl_up(c0, o, 64), u1 = __shfl_up(c1, o, 64);
-            if (lane >= o) { c0 += u0; c1 += u1; }
+          for (int u = 0; u < 8; ++u) bv[u] = lane + 64 * u < cnt ? (uint32_t)xf[iv[u]] : 0u;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int q = lane + 64 * u;
+            if (q < N2) Kw[q] = q < cnt ? ((bv[u] << 16) | (uint32_t)q) : 0xFFFFFFFFu;
           }
-          const uint32_t kn = __shfl_down(ks, 1, 64);
-          double cr = -INFINITY;
-          int s = 0x7FFFFFFF;
-          if (lane + 1 < cnt && (ks >> 16) != (kn >> 16)) {
-            cr = boundary_crit(fp, st, minc, c0, c1);
-            s = lane;
+          wave_sync();
+          wave_bitonic(Kw, N2, lane);
+          // lane owns sorted positions [s0, s1): local sums, wave exclusive scan, walk
+          int64_t l0 = 0, l1 = 0;
+          for (int s = s0; s < s1; ++s) {
+            const int q = (int)(Kw[s] & 0xFFFFu);
+            l0 += Xw0[q]; l1 += Xw1[q];
           }
-          wave_argmax(cr, s);
-          if (cr > best) {                    // uniform
-            best = cr;
+          int64_t p0 = wave_excl_scan64(l0, lane), p1 = wave_excl_scan64(l1, lane);
+          double bc = -INFINITY;
+          int bs = 0x7FFFFFFF;
+          for (int s = s0; s < s1; ++s) {
+            const int q = (int)(Kw[s] & 0xFFFFu);
+            p0 += Xw0[q]; p1 += Xw1[q];
+            if (s + 1 < cnt && (Kw[s] >> 16) != (Kw[s + 1] >> 16)) {
+              const double cr = boundary_crit(fp, st, minc, p0, p1);
+              if (cr > bc) { bc = cr; bs = s; }
+            }
+          }
+          wave_argmax(bc, bs);
+          if (bc > best) {                    // uniform
+            best = bc;
             bf = f;
-            blo = (int)(__shfl(ks, s, 64) >> 16);
-            bhi = (int)(__shfl(kn, s, 64) >> 16);
-            bnl = s + 1;
+            blo = (int)(Kw[bs] >> 16);
+            bhi = (int)(Kw[bs + 1] >> 16);
+            bnl = bs + 1;
           }
+          wave_sync();                        // Kw reused by the next feature
         }
         const double parent = parent_crit(fp, st);
-        if (lane == 0) {
-          if (bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent)))
-            S.dec[j] = XDec{1, bf, exact_threshold_bin(vals + (int64_t)bf * ldv, nval[bf], blo, bhi),
-                            bnl, 0.0};
-          else
-            S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
-        }
+        const bool split = bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent));
+        const int tb = split ? wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane) : -1;
+        if (lane == 0)
+          S.dec[j] = split ? XDec{1, bf, tb, bnl, 0.0}
+                           : XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
       }
     }
+#ifdef EXACT_PROF
+    if (blockIdx.x == 0 && lane == 0) exact_prof[8 + wid] += wall_clock64() - tw0_;
+#endif
     __syncthreads();
+    XPHASE(3);
 
     // ================= child ids in list order (host numbering), node arrays
-    if (tid == 0) {
-      int nid = snext_id, nn = 0;
-      for (int j = 0; j < ncur; ++j) {
-        const XRng nd = S.cur[j];
-        const XDec d = S.dec[j];
-        if (!d.split) {
-          tfeat[nd.id] = -1; tthr[nd.id] = -1; tleft[nd.id] = -1; tval[nd.id] = d.val;
-          continue;
+    {
+      const int nid0 = snext_id;
+      int ns = 0;                             // split nodes before this chunk (uniform)
+      for (int c0 = 0; c0 < ncur; c0 += XT) {
+        const int j = c0 + tid;
+        XRng nd{0, 0, 0};
+        XDec d{0, -1, -1, 0, 0.0};
+        if (j < ncur) { nd = S.cur[j]; d = S.dec[j]; }
+        int before;
+        const int tot = block_flag_scan(j < ncur && d.split, scnt, before);
+        if (j < ncur) {
+          if (!d.split) {
+            tfeat[nd.id] = -1; tthr[nd.id] = -1; tleft[nd.id] = -1; tval[nd.id] = d.val;
+          } else {
+            const int k = ns + before, nid = nid0 + 2 * k;
+            tfeat[nd.id] = d.feat; tthr[nd.id] = d.thr; tleft[nd.id] = nid; tval[nd.id] = 0.0;
+            S.nxt[2 * k] = XRng{nd.lo, nd.lo + d.nl, nid};
+            S.nxt[2 * k + 1] = XRng{nd.lo + d.nl, nd.hi, nid + 1};
+          }
         }
-        tfeat[nd.id] = d.feat; tthr[nd.id] = d.thr; tleft[nd.id] = nid; tval[nd.id] = 0.0;
-        S.nxt[nn++] = XRng{nd.lo, nd.lo + d.nl, nid};
-        S.nxt[nn++] = XRng{nd.lo + d.nl, nd.hi, nid + 1};
-        nid += 2;
+        ns += tot;
       }
-      snext_id = nid;
-      sm = nn;
+      if (tid == 0) {
+        snext_id = nid0 + 2 * ns;
+        sm = 2 * ns;
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    XPHASE(4);
 
     // ================= stable partitions by bin <= thr
-    for (int j = 0; j < ncur; ++j) {          // large nodes: whole workgroup
+    for (int jb = 0; jb < nbig; ++jb) {       // large nodes: whole workgroup
+      const int j = sbig[jb];
       const XRng nd = S.cur[j];
       const int cnt = nd.hi - nd.lo;
-      if (cnt <= 64) continue;
       const XDec d = S.dec[j];
       if (!d.split) continue;
       const uint16_t* xf = Xb + (int64_t)d.feat * n;
@@ -454,27 +772,36 @@ __global__ __launch_bounds__(XT) void forest_exact_kernel(
       for (int q = tid; q < cnt; q += XT) S.idx[nd.lo + q] = (int32_t)S.keys[nd.lo + q];
       __syncthreads();
     }
-    {                                          // small nodes: one wave each, in registers
-      int r = 0;
-      for (int j = 0; j < ncur; ++j) {
+    XPHASE(5);
+    {                                          // wave-level nodes, staged in the wave's LDS
+      for (int j = wid; j < ncur; j += XW) {
         const XRng nd = S.cur[j];
         const int cnt = nd.hi - nd.lo;
-        if (cnt > 64) continue;
-        if ((r++ % XW) != wid) continue;
+        if (cnt > WCAP) continue;
         const XDec d = S.dec[j];
         if (!d.split) continue;
-        const bool in = lane < cnt;
-        const int i = in ? S.idx[nd.lo + lane] : 0;
-        const bool l = in && Xb[(int64_t)d.feat * n + i] <= d.thr;
-        const uint64_t bl = __ballot(l), br = __ballot(in && !l);
+        const uint16_t* xf = Xb + (int64_t)d.feat * n;
+        int lo_l = 0, lo_r = d.nl;
         const uint64_t below = (1ull << lane) - 1ull;
-        if (in) S.idx[nd.lo + (l ? __popcll(bl & below) : d.nl + __popcll(br & below))] = i;
+        for (int c0 = 0; c0 < cnt; c0 += 64) {
+          const int q = c0 + lane;
+          const bool in = q < cnt;
+          const int i = in ? S.idx[nd.lo + q] : 0;
+          const bool l = in && xf[i] <= d.thr;
+          const uint64_t bl = __ballot(l), br = __ballot(in && !l);
+          if (in) Kw[l ? lo_l + __popcll(bl & below) : lo_r + __popcll(br & below)] = (uint32_t)i;
+          lo_l += __popcll(bl);
+          lo_r += __popcll(br);
+        }
+        wave_sync();
+        for (int q = lane; q < cnt; q += 64) S.idx[nd.lo + q] = (int32_t)Kw[q];
+        wave_sync();
       }
     }
     __syncthreads();
+    XPHASE(6);
     if (tid == 0) sncur = sm;
-    // next level reads the children list: swap the roles of cur / nxt
-    {
+    {                                         // the children list becomes the current list
       XRng* tmp = S.cur;
       S.cur = S.nxt;
       S.nxt = tmp;
@@ -506,3 +833,13 @@ ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, const vo
   ATE_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef EXACT_PROF
+extern "C" __attribute__((visibility("default"))) int ate_exact_prof_read(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(exact_prof), sizeof(exact_prof));
+}
+extern "C" __attribute__((visibility("default"))) int ate_exact_prof_reset() {
+  static unsigned long long z[24];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(exact_prof), z, sizeof(z));
+}
+#endif
