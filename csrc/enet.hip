@@ -16,6 +16,8 @@
 //            Gram: sum (y - a0 - x b)^2 = y'y - 2 a0 S_y - 2 b'X'y + n a0^2 + 2 a0 b'S_x
 //            + b'X'X b -- no pass over the data.
 //  select:   cvm, cvsd, lambda.min, lambda.1se with glmnet's rules.
+#include <cstdlib>
+
 #include "common.hpp"
 
 #include <type_traits>
@@ -243,7 +245,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     const double* __restrict__ vp_in, const EnetProblem* __restrict__ probs, int nprob,
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
-    int* __restrict__ nlam_out, int* __restrict__ npass_out, int L, int* __restrict__ progress) {
+    int* __restrict__ nlam_out, int* __restrict__ npass_out, int L, int* __restrict__ progress,
+    long spin_max) {
   constexpr int TMAX = PMAX / 64;
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
   __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
@@ -937,7 +940,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         for (long spin = 0;; ++spin) {
           v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (v > m) break;
-          if (spin > (1l << 26)) { v = -1; break; }
+          if (spin > spin_max) { v = -1; break; }
           __builtin_amdgcn_s_sleep(2);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -1043,12 +1046,16 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
   hipStream_t s = (hipStream_t)stream;
   // grid rounded up to a multiple of 8 so the XCD remap is a bijection onto [0, nwg)
   const int nwg = (nprob + 7) / 8 * 8;
+  // bound of a fold problem's wait for its source's next lambda (polls of ~2 s_sleep);
+  // ATE_ENET_SPIN_MAX overrides it (tests force the timeout path with 0)
+  const char* sm = getenv("ATE_ENET_SPIN_MAX");
+  const long spin_max = sm ? atol(sm) : (1l << 26);
 #define LAUNCH_C(CTT)                                                                          \
   hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(NTH), 0, s, (const CTT*)C,       \
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
-                     (int*)npass_out, L, (int*)progress)
+                     (int*)npass_out, L, (int*)progress, spin_max)
   if (c_f32) LAUNCH_C(float);
   else LAUNCH_C(double);
 #undef LAUNCH_C

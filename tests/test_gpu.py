@@ -175,6 +175,34 @@ def test_enet_cv_kernels_vs_cpu(gpu):
     assert np.allclose(rg.cvm[0, :nl].cpu().numpy(), rc.cvm[0, :nl].numpy(), rtol=1e-6)
 
 
+def test_enet_fold_wait_timeout_poisons_and_raises(gpu, monkeypatch):
+    """The CV fold problems spin (bounded) on their full-data problem's lambda progress
+    (csrc/enet.hip). Forcing the bound to zero polls makes fold waits time out: the launch
+    must come back (no hang), flag the folds (npass < 0), NaN-poison the CV curve and the
+    selection, and EnetCvResult.check() must raise; with the default bound the same call
+    is clean again."""
+    from ate_replication_causalml_amd.ops.enet import cv_enet_gaussian
+    from ate_replication_causalml_amd.parallel import rng
+    from ate_replication_causalml_amd.utils.guards import NumericalError
+    rs = np.random.RandomState(7)
+    n, p = 4000, 120
+    X = rs.randn(n, p)
+    y = X[:, :6] @ [1.0, -1.0, 0.5, 0.25, 0.2, -0.3] + rs.randn(n)
+    pan = build_panel(X, None, y, folds=rng.fold_ids(n, 10, 1), dtype="f64", device=gpu)
+    G = gram_op.gram(pan)
+    monkeypatch.setenv("ATE_ENET_SPIN_MAX", "0")
+    r = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]])
+    torch.cuda.synchronize()
+    bad = (r.fold_npass < 0).cpu().numpy()
+    assert bad.any(), "no fold wait timed out with a zero spin bound"
+    assert torch.isnan(r.cvm).all() and torch.isnan(r.coef_min).all()
+    with pytest.raises(NumericalError):
+        r.check()
+    monkeypatch.delenv("ATE_ENET_SPIN_MAX")
+    ok = cv_enet_gaussian(G, pan, pan.xcols, [pan.cols["Y"]]).check()
+    assert (ok.fold_npass >= 0).all() and torch.isfinite(ok.coef_min).all()
+
+
 def test_device_estimators_vs_reference(gpu, tutorial):
     from ate_replication_causalml_amd.estimators import lasso as DL
     from ate_replication_causalml_amd.estimators import linear as D
