@@ -241,6 +241,9 @@ static_assert(NW >= 3, "phase B uses wave 1 for block tn and waves 2.. for snaps
 // the fp32 pulls give ONE 64-column block to each pull wave (jb = wid + (wid >= t)), so
 // every block of a PMAX-column problem needs its own wave
 static_assert(NW >= PMAX / 64, "one pull wave per 64-column block: NW >= PMAX / 64");
+#ifndef ENET_SETPRIO
+#define ENET_SETPRIO 0       // A/B: 1 = recurrence wave at issue priority 3, 2 = every wave
+#endif
 #ifndef ENET_BALLOT_ONLY
 #define ENET_BALLOT_ONLY 0   // 1: every pass uses the ballot recurrence (A/B timing)
 #endif
@@ -304,6 +307,10 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   const EnetProblem pr = probs[q];
   if (pr.ulam_src < -1) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#if ENET_SETPRIO
+  // issue priority of the recurrence wave (or all waves) over co-resident Gram waves
+  if (ENET_SETPRIO == 2 || wid == 0) __builtin_amdgcn_s_setprio(3);
+#endif
   const int T = (p + 63) >> 6;
   const int ldc = T * 64;
   const int cw = ldc / NW;                 // columns per wave in the pull (multiple of 8)

@@ -248,7 +248,11 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
           const uint32_t bin = (bA[u] >> (8 * q)) & 255;
           u64* e0 = sh + bin * FB + (q << 2 | l4);
           atomicAdd(e0, gA[u]);
-          atomicAdd(e0 + 256 * FB, hA[u]);
+          if (mode & 8) continue;                             // ablation: G only
+          if (mode & 16)                                      // ablation: H as a u32 add
+            atomicAdd(reinterpret_cast<unsigned*>(e0 + 256 * FB), (unsigned)hA[u]);
+          else
+            atomicAdd(e0 + 256 * FB, hA[u]);
         }
       }
     }
@@ -719,7 +723,9 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
   const int M = (1 << (a.depth + 1)) - 1;
   const int ydim = (a.p + FB - 1) / FB, ydim_s = (a.p + SFB - 1) / SFB;
   const int64_t per = 512LL * a.p;
-  const char* hm = getenv("ATE_GBDT_HIST_MODE");          // ablation switch (profiling only)
+  // ablation switch (profiling only): 1 no LDS atomics, 2 no bin gather, 4 no slab store,
+  // 8 G atomics only, 16 H atomics as u32
+  const char* hm = getenv("ATE_GBDT_HIST_MODE");
   const int hmode = hm ? atoi(hm) : 0;
   for (; s.t < a.n_trees; ++s.t, s.d = 0) {
     int32_t* ft = a.feat + (int64_t)s.t * M;
