@@ -686,12 +686,19 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
   const int ydim = (p + FB - 1) / FB;
   // rows histogrammed: all of them at the root, at most half (count rule) or all
   // (hessian rule) of them below; `target` workgroups of full chunks (two resident per
-  // CU; each pays a fixed 64-KB LDS clear + slab store, so not too many)
+  // CU; each pays a fixed 64-KB LDS clear + slab store)
   const int64_t rows = (d == 0 || rule == 1) ? n_train : (n_train + 1) / 2;
-  static const int target = [] {
+  // Chunks of ~32k rows: the ydim workgroups of a chunk read 16-byte slices of the same
+  // row-major lines, and they only share them through L2 while they run close together --
+  // short chunks keep them so (config-5 shard, 3 trees: 512 workgroups 4.46 s, 8192-65536
+  // workgroups 2.7-3.2 s, the same bits; profiles/r03_cfg5). ATE_GBDT_HIST_TARGET = fixed
+  // workgroup count.
+  static const int64_t env_target = [] {
     const char* e = getenv("ATE_GBDT_HIST_TARGET");
-    return e ? std::max(64, atoi(e)) : 512;
+    return e ? (int64_t)std::max(64, atoi(e)) : (int64_t)0;
   }();
+  const int64_t target = env_target ? env_target
+                                    : std::max<int64_t>(512, (rows * ydim + 32767) / 32768);
   int64_t ch = (rows * ydim + target - 1) / target;
   ch = std::max<int64_t>(1024, (ch + 255) / 256 * 256);
   const int64_t wg = (((n_train + ch - 1) / ch + (1 << d)) * ydim + 7) / 8 * 8;
