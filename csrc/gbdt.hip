@@ -41,8 +41,16 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int NTH = 512;             // histogram workgroup (two per CU: 2 x 64-KB LDS images)
-constexpr int FB = 16;               // features per histogram workgroup
+#ifndef GBDT_FB
+#define GBDT_FB 16
+#endif
+// features per histogram workgroup: 16 (512 threads, 64-KB LDS image, two workgroups per
+// CU) or 32 (1024 threads, one 128-KB image per CU: half the workgroups per row chunk share
+// each 128-B bin line, and idx / gh are loaded half as often)
+constexpr int FB = GBDT_FB;
+static_assert(FB == 16 || FB == 32, "GBDT_FB: 16 or 32");
+constexpr int NTH = FB * 32;         // histogram workgroup: FB / 4 lanes per row, 16 waves per CU
+constexpr int FQ = FB / 4;           // dwords (lanes) per row
 constexpr int SFB = 8;               // features per split-search workgroup (one per wave)
 constexpr int HS = 257;              // padded bins per (feature, channel) in LDS
 constexpr int MAXB = 65;             // partition buckets: 2 * 32 children + retired
@@ -193,12 +201,12 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
     for (int t = threadIdx.x; t < SLAB / 2; t += NTH) z[t] = make_ulonglong2(0, 0);
   }
   __syncthreads();
-  // lane = (row r16 of 16, word l4 of 4): the lane reads the dword of features
-  // 4*l4..+3 of its row. LDS slot of local feature f: (f & 3) << 2 | f >> 2, so feature
-  // 4*l4 + q sits on bank pair 4*q + l4; row r walks q in the order rotated by r & 3, so
-  // the four rows of every 16-lane LDS group use 16 distinct bank pairs: the int64
-  // atomics are conflict-free whatever the bins are.
-  const int l4 = threadIdx.x & 3, r16 = (threadIdx.x >> 2) & 15, w = threadIdx.x >> 6;
+  // lane = (row r16 of 64 / FQ, word l4 of FQ): the lane reads the dword of features
+  // 4*l4..+3 of its row. LDS slot of local feature f: (f & 3) * FQ + (f >> 2), so feature
+  // 4*l4 + q sits on bank pair FQ*q + l4; row r walks q in the order rotated by r & 3, so
+  // the four consecutive rows of a lane group use distinct bank pairs: the int64 atomics
+  // are conflict-free whatever the bins are.
+  const int l4 = threadIdx.x % FQ, r16 = (threadIdx.x / FQ) % (64 / FQ), w = threadIdx.x >> 6;
   const int rot = r16 & 3;
   const uint32_t* xw = reinterpret_cast<const uint32_t*>(Xr + j0) + l4;   // in the row
   const int64_t ldw = ldr >> 2;
@@ -206,13 +214,13 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   // iteration i+2 and (g, h, bins) of iteration i+1 are in flight while iteration i's
   // atomics run. Loads are unconditional (positions past the segment are clamped to its
   // last row; words past p read row padding), so no branch forces a vmcnt(0) per row.
-  constexpr int U = 8, RPI = U * (NTH / 4);
+  constexpr int U = 8, RPI = U * (NTH / FQ);
   int32_t iiA[U], iiB[U];
   u64 gA[U], hA[U];
   uint32_t bA[U];
   const int64_t last = e - 1;
   const bool wok = 4 * l4 < nf;
-  auto pos = [&](int64_t base, int u) { return base + (u * (NTH / 64) + w) * 16 + r16; };
+  auto pos = [&](int64_t base, int u) { return base + (u * (NTH / 64) + w) * (64 / FQ) + r16; };
 #pragma unroll
   for (int u = 0; u < U; ++u) iiA[u] = idx[min(pos(s, u), last)];
 #pragma unroll
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
         for (int k = 0; k < 4; ++k) {
           const int q = (k + rot) & 3;
           const uint32_t bin = (bA[u] >> (8 * q)) & 255;
-          u64* e0 = sh + bin * FB + (q << 2 | l4);
+          u64* e0 = sh + bin * FB + (q * FQ + l4);
           atomicAdd(e0, gA[u]);
           if (mode & 8) continue;                             // ablation: G only
           if (mode & 16)                                      // ablation: H as a u32 add
@@ -292,7 +300,7 @@ __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
     const int cb = (int)(t / p), j = (int)(t - (int64_t)cb * p);
     const int yb = j / FB, fl = j - yb * FB;
-    const u64* sp = slab + ((int64_t)a * ydim + yb) * SLAB + cb * FB + ((fl & 3) << 2 | fl >> 2);
+    const u64* sp = slab + ((int64_t)a * ydim + yb) * SLAB + cb * FB + ((fl & 3) * FQ + (fl >> 2));
     const int64_t stride = (int64_t)ydim * SLAB;
     u64 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
     int i = 0;
