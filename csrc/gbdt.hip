@@ -13,9 +13,11 @@
 //   "segments"), with the fixed-point gradient pair (packed into one int64) stored in
 //   the same order. After each level's split a three-kernel partition (count / scan /
 //   scatter) moves (idx, gh) into child buckets — 12 B per row, bins never move;
-// * a histogram workgroup = (node segment chunk, 16-feature block): 16 features x 256
-//   bins x (G, H) int64 live in 64 KB of LDS (two workgroups per CU), feature-minor so
-//   the int64 LDS atomics are bank-conflict-free; partial images go to slabs (plain stores) and a reduce kernel
+// * a histogram workgroup = (node segment chunk, 32-feature block): 32 features x 256
+//   bins x (G, H) int64 live in 128 KB of LDS (one 1024-thread workgroup per CU; GBDT_FB=16
+//   builds two 64-KB workgroups per CU), feature-minor so the int64 LDS atomics are
+//   bank-conflict-free; chunk c runs on XCD c % 8 with its feature blocks back to back;
+//   partial images go to slabs (plain stores) and a reduce kernel
 //   sums each node's slabs into H[node][c][bin][feature] — no global atomics. Only the
 //   SMALLER child of each split parent is histogrammed — the sibling is parent - child
 //   (histogram subtraction), so levels >= 1 touch at most half of the rows;
@@ -42,7 +44,7 @@ namespace {
 
 constexpr int NT = 256;
 #ifndef GBDT_FB
-#define GBDT_FB 16
+#define GBDT_FB 32
 #endif
 // features per histogram workgroup: 16 (512 threads, 64-KB LDS image, two workgroups per
 // CU) or 32 (1024 threads, one 128-KB image per CU: half the workgroups per row chunk share
@@ -167,7 +169,7 @@ constexpr int SLAB = 2 * 256 * FB;   // one workgroup's histogram image, u64 ent
 // LDS image [c][bin][slot(f)] (feature-minor, see the lane map below: the int64 LDS
 // atomics are bank-conflict-free whatever the bins are). The image goes to slab
 // `logical` with plain 16-B stores; gbdt_hist_reduce_kernel sums a node's slabs.
-// 1-D grid, XCD-remapped so the feature blocks of one chunk share an XCD's L2.
+// 1-D grid, chunk-to-XCD mapped (below) so the feature blocks of one chunk share an XCD's L2.
 __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
     const uint8_t* __restrict__ Xr, int64_t ldr, const int32_t* __restrict__ idx,
     const int64_t* __restrict__ gh, const int32_t* __restrict__ seg, const int64_t* tot,
@@ -176,10 +178,17 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   __shared__ u64 sh[SLAB];
   __shared__ int sseg[33], sacc[33], snch[32];
   __shared__ int64_t wk[3];
-  const int G = gridDim.x;
   const int bid = blockIdx.x;
-  const int logical = (bid & 7) * (G >> 3) + (bid >> 3);   // G % 8 == 0
-  const int chunk = logical / ydim, yb = logical - chunk * ydim;
+  // Chunk c runs on XCD c % 8 (dispatch sends block b to XCD b % 8), its ydim feature
+  // blocks back to back there (they share the chunk's bin lines through that XCD's L2).
+  // Chunks are numbered over the level's histogrammed nodes only, so the spare
+  // workgroups of an upper-bound grid are the highest chunks of EVERY XCD: a level that
+  // histograms half of the rows keeps all 8 XCDs busy (a chunk-major order put all the
+  // spare workgroups, half the grid below the root, on XCDs 4-7).
+  // G == 8 * ceil(chunks / 8) * ydim (gbdt_hist_geom).
+  const int xq = bid >> 3;
+  const int chunk = (xq / ydim) * 8 + (bid & 7), yb = xq % ydim;
+  const int logical = chunk * ydim + yb;
   if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -709,7 +718,7 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
                                     : std::max<int64_t>(512, (rows * ydim + 32767) / 32768);
   int64_t ch = (rows * ydim + target - 1) / target;
   ch = std::max<int64_t>(1024, (ch + 255) / 256 * 256);
-  const int64_t wg = (((n_train + ch - 1) / ch + (1 << d)) * ydim + 7) / 8 * 8;
+  const int64_t wg = (((n_train + ch - 1) / ch + (1 << d)) + 7) / 8 * 8 * ydim;
   *CH = ch;
   *nwg = wg;
 }

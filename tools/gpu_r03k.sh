@@ -1,5 +1,5 @@
 #!/bin/bash
-# GBDT ~32k-row histogram chunks: bit-identity tests, config-5 shard at 100 trees
+# GBDT histograms: bit-identity tests, config-5 shard at 100 trees
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gbdt_gpu.py tests/test_gpu_multirank.py tests/test_forest_gpu.py -k "gbdt or cfg5 or multirank or crossfit" > gpurun_out/gbdt_tests.log 2>&1
