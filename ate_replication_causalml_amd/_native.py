@@ -83,9 +83,13 @@ _SIGS = {
     "ate_col_moments": "pllipppp",
     "ate_standardize": "pllippp",
     "ate_interactions": "pllipl" + "p",
+    "ate_scan_parts": "l",
+    "ate_excl_scan_i32": "plpppp",
+    "ate_excl_scan_i64": "plpppp",
 }
 _RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64,
-            "ate_forest_exact_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64}
+            "ate_forest_exact_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64,
+            "ate_scan_parts": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}
 
 

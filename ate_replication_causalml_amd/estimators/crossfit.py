@@ -27,6 +27,7 @@ from .. import _native
 from ..models import forest as F
 from ..ops.linalg import logistic_irls
 from ..ops.panel import build_panel
+from ..ops.scan import compact_rows
 from ..parallel import rng
 from ..result import AteResult
 from .common import as_np, resolve_device
@@ -165,26 +166,28 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
     tag = "" if comm is None or comm.world_size == 1 else f".r{comm.rank}of{comm.world_size}"
     cache = _JobCache(checkpoint, key, tag, comm, dev)
     jobs = []
+    # row lists by a lookback-free compaction on this stream, before the jobs run side by
+    # side on their own streams (ops/scan.py: torch.nonzero there stalled config 3)
     for k in range(folds):
         ho = fid == k
         tr = ~ho
         t1, t0 = tr & (Wd == 1), tr & (Wd == 0)
         sd = seed + 1000 * (k + 1)
-        jobs += [(e, ho, tr, Wd, sd, 3 * k), (mu1, ho, t1, Yd, sd + 1, 3 * k + 1),
-                 (mu0, ho, t0, Yd, sd + 2, 3 * k + 2)]
+        hoi = compact_rows(ho)
+        rl = (lambda m: compact_rows(m)) if learner in ("rf", "glm") else (lambda m: None)
+        jobs += [(e, ho, tr, Wd, sd, 3 * k, hoi, rl(tr)),
+                 (mu1, ho, t1, Yd, sd + 1, 3 * k + 1, hoi, rl(t1)),
+                 (mu0, ho, t0, Yd, sd + 2, 3 * k + 2, hoi, rl(t0))]
 
     def run(job):
-        out, ho, rows, target, sd, j = job
-        hoi = ho.nonzero().squeeze(1)
+        out, ho, rows, target, sd, j, hoi, ri = job
         if j in cache.done:
             out.index_copy_(0, hoi, cache.load(j, dev))
             return
         if learner == "rf":
-            ri = rows.nonzero().squeeze(1)
             r = _rf_fit_predict(Xb, ri, target.index_select(0, ri), hoi, num_trees, sd, dev,
                                 comm, edges)
         elif learner == "glm":
-            ri = rows.nonzero().squeeze(1)
             r = _glm_fit_predict(Xd, ri, target.index_select(0, ri).cpu().numpy(), hoi, dev)
         else:
             r = _gbdt_fit_predict(target, rows, ho, Xb, edges, dev, sd, gbdt_kw)
@@ -279,9 +282,14 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
             todo.append(jb)
     jobs = todo
 
+    # training rows of every job, computed here on the caller's stream: a lookback-free
+    # compaction (ops/scan.py) and never inside the side-by-side forests below, where
+    # torch.nonzero's spinning workgroups stalled the shard (profiles/r03_cfg3b)
+    jobs = [(out, compact_rows(mask), target, sd, a, b, j)
+            for out, mask, target, sd, a, b, j in jobs]
+
     def run(job):
-        out, mask, target, sd, a, b, j = job
-        idx = mask.nonzero().squeeze(1)
+        out, idx, target, sd, a, b, j = job
         yt = target.index_select(0, idx)
         binary = bool(((yt == 0) | (yt == 1)).all())
         kw = dict(y=yt) if binary else dict(r1=yt, min_node=5, mtry=max(1, p // 3))
@@ -305,7 +313,7 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
         lib = _native.hip()
 
         def need(job):
-            nt = int(job[1].sum())
+            nt = job[1].numel()
             base = p * nt + cnt * (2 * nt + 1) * 20 + cnt * nt      # bins, trees, in-bag
             if F.LEVEL_MIN_ROWS <= nt:
                 # level engine: row-major copy, weights / positions, level lists
@@ -314,8 +322,8 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
 
         # forests on the level engine fill the GPU by themselves: a few side by side only
         # hide each other's per-level host syncs (ATE_CF_CONCURRENT caps the batch;
-        # profiles/r03_forest: 1 -> 10.3 s, 2 -> 9.4, 3 -> 8.7, 5 -> 8.4 for the config-3
-        # per-GPU shard)
+        # profiles/r03_cfg3: 1 -> 10.3 s, 2 -> 9.4, 3 -> 8.7, 5 -> 8.4 for the config-3
+        # per-GPU shard; r03_cfg3b, lookback-free scans: 3 -> 8.0 s, 5 -> 7.7 s)
         cap_b = int(os.environ.get("ATE_CF_CONCURRENT", "5")) or len(jobs)
         batches, cur_b, used = [], [], 0
         for job in jobs:

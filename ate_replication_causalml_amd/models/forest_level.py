@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from ..ops.scan import exclusive_cumsum
 from . import forest as F
 
 LV_FG = 8
@@ -82,14 +83,19 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     inb = wv > 0
     inbag = inb.to(torch.uint8).reshape(-1)
     m = inb.sum(1)                                           # in-bag rows per tree
-    nz = torch.nonzero(inb)                                  # (t, i), t-major, i ascending
     m_h = m.cpu().numpy().astype(np.int64)
-    start = torch.as_tensor(np.concatenate([[0], np.cumsum(m_h)[:-1]]), device=dev)
-    dest = nz[:, 0] * n + (torch.arange(nz.shape[0], device=dev) - start[nz[:, 0]])
-    idx = torch.zeros(T * n, **i32)
-    idx[dest] = nz[:, 1].to(torch.int32)
+    # in-bag rows of tree t, ascending, at idx[t*n ...]: rank within the tree from a
+    # lookback-free exclusive scan (ops/scan.py: this runs beside other forests' streams)
+    rank = exclusive_cumsum(inb.reshape(-1).to(torch.int32)).view(T, n)
+    rank = rank - rank[:, :1]
+    tn = (torch.arange(T, device=dev, dtype=torch.int64) * n)[:, None]
+    dest = torch.where(inb, rank.long() + tn, torch.full_like(tn, T * n))
+    del rank
+    idx = torch.zeros(T * n + 1, **i32)
+    idx.scatter_(0, dest.reshape(-1), torch.arange(n, **i32).expand(T, n).reshape(-1))
+    idx = idx[:T * n]
     idx2 = torch.zeros_like(idx)
-    del nz, dest
+    del dest
     # ---- outputs
     feat = torch.zeros(T * cap, **i32)
     thr = torch.zeros(T * cap, **i32)
@@ -102,8 +108,9 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     nxt = torch.zeros((lcap, 4), **i32)
     tt = torch.arange(T, **i32)
     root = torch.stack([tt, tt * n, tt * n + m.to(torch.int32), torch.zeros_like(tt)], 1)
-    keep = m > 0
-    root = root[keep]
+    keep = np.flatnonzero(m_h > 0)
+    if len(keep) < T:
+        root = root.index_select(0, torch.as_tensor(keep, device=dev))
     ncur = int(root.shape[0])
     cur[:ncur] = root
     dec = torch.zeros((lcap, 4), **i32)
@@ -189,7 +196,7 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
         if npit:
             ic = icnt[:npit].long()
             slot_t = pitems[0].long()
-            csum = torch.cumsum(ic, 0) - ic                                   # exclusive
+            csum = exclusive_cumsum(ic)
             ipre = (csum - csum.index_select(0, firsts).index_select(0, slot_t)).to(torch.int32)
             nlb = torch.zeros(plist.numel(), dtype=torch.int64, device=dev).index_add_(0, slot_t, ic)
             nlb32 = nlb.to(torch.int32)
@@ -198,8 +205,8 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
                          P(pitems[1]), P(pitems[2]), npit, ipre.data_ptr(), nlb32.data_ptr(), s)
         t0 = tick("partition", t0) if prof else None
         flags = dec[:ncur, 0]
-        excl = (torch.cumsum(flags, 0, dtype=torch.int32) - flags).contiguous()
-        total = int((excl[ncur - 1] + flags[ncur - 1]).item())
+        excl, tot = exclusive_cumsum(flags.contiguous(), total=True)
+        total = int(tot.item())
         _native.call("ate_lv_children", ctypes.addressof(h), ncur, excl.data_ptr(),
                      brank.data_ptr(), next_id.data_ptr(), nxt.data_ptr(), s)
         if prof:
