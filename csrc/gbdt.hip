@@ -166,15 +166,20 @@ __device__ void gbdt_plan(const int* sseg, const int64_t* tot, int rule, int nn,
 constexpr int SLAB = 2 * 256 * FB;   // one workgroup's histogram image, u64 entries
 
 // Partial histograms: workgroup = (chunk of a computed node's segment, 32-feature block),
-// LDS image [c][bin][slot(f)] (feature-minor, see the lane map below: the int64 LDS
+// LDS image [bin][c][slot(f)] (feature-minor, see the lane map below: the int64 LDS
 // atomics are bank-conflict-free whatever the bins are). The image goes to slab
 // `logical` with plain 16-B stores; gbdt_hist_reduce_kernel sums a node's slabs.
 // 1-D grid, chunk-to-XCD mapped (below) so the feature blocks of one chunk share an XCD's L2.
+// ABL: the profiling ablation build (ATE_GBDT_HIST_MODE != 0); the production
+// instantiation compiles the mode tests out of the atomic loop (they were uniform branches
+// plus scalar bookkeeping around every LDS atomic).
+template <bool ABL>
 __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
     const uint8_t* __restrict__ Xr, int64_t ldr, const int32_t* __restrict__ idx,
     const int64_t* __restrict__ gh, const int32_t* __restrict__ seg, const int64_t* tot,
-    int rule, int nn, int p, int d, int64_t CH, int ydim, u64* __restrict__ slab, int mode,
+    int rule, int nn, int p, int d, int64_t CH, int ydim, u64* __restrict__ slab, int mode_in,
     int loss) {
+  const int mode = ABL ? mode_in : 0;
   __shared__ u64 sh[SLAB];
   __shared__ int sseg[33], sacc[33], snch[32];
   __shared__ int64_t wk[3];
@@ -223,9 +228,14 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   // iteration i+2 and (g, h, bins) of iteration i+1 are in flight while iteration i's
   // atomics run. Loads are unconditional (positions past the segment are clamped to its
   // last row; words past p read row padding), so no branch forces a vmcnt(0) per row.
-  constexpr int U = 8, RPI = U * (NTH / FQ);
+#ifndef GBDT_U
+#define GBDT_U 8
+#endif
+  constexpr int U = GBDT_U, RPI = U * (NTH / FQ);
+  // (g, h) stay packed (one int64 per row) until the atomics: half the VGPRs of two
+  // unpacked u64 per row (U = 12 fits without spills but was not faster)
   int32_t iiA[U], iiB[U];
-  u64 gA[U], hA[U];
+  int64_t gA[U];
   uint32_t bA[U];
   const int64_t last = e - 1;
   const bool wok = 4 * l4 < nf;
@@ -236,40 +246,44 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   for (int u = 0; u < U; ++u) iiB[u] = idx[min(pos(s + RPI, u), last)];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    gbdt_unpack(loss, gh[min(pos(s, u), last)], gA[u], hA[u]);
+    gA[u] = gh[min(pos(s, u), last)];
     bA[u] = (mode & 2) ? (uint32_t)iiA[u] * 0x9E3779B1u : xw[(int64_t)iiA[u] * ldw];
   }
   u64 dummy = 0;
   for (int64_t base = s; base < e; base += RPI) {
-    u64 gB[U], hB[U];
+    int64_t gB[U];
     uint32_t bB[U];
     int32_t iiC[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      gbdt_unpack(loss, gh[min(pos(base + RPI, u), last)], gB[u], hB[u]);
+      gB[u] = gh[min(pos(base + RPI, u), last)];
       bB[u] = (mode & 2) ? (uint32_t)iiB[u] * 0x9E3779B1u : xw[(int64_t)iiB[u] * ldw];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) iiC[u] = idx[min(pos(base + 2 * RPI, u), last)];
     if (mode & 1) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) dummy += gA[u] * bA[u] + hA[u];
+      for (int u = 0; u < U; ++u) dummy += (u64)gA[u] * bA[u];
     } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         // padding words and rows past the segment add nothing: their lanes stay idle
         if (!wok || pos(base, u) > last) continue;
+        u64 gu, hu;
+        gbdt_unpack(loss, gA[u], gu, hu);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int q = (k + rot) & 3;
-          const uint32_t bin = (bA[u] >> (8 * q)) & 255;
-          u64* e0 = sh + bin * FB + (q * FQ + l4);
-          atomicAdd(e0, gA[u]);
+          // bit-field extract + shift-or: 2 VALU per byte for the address (was 3)
+          const uint32_t bin = __builtin_amdgcn_ubfe(bA[u], 8 * q, 8);
+          // image [bin][G, H][slot]: H sits 8 * FB bytes after G, inside the DS offset field
+          u64* e0 = sh + ((bin * 2 * FB) | (q * FQ + l4));
+          atomicAdd(e0, gu);
           if (mode & 8) continue;                             // ablation: G only
           if (mode & 16)                                      // ablation: H as a u32 add
-            atomicAdd(reinterpret_cast<unsigned*>(e0 + 256 * FB), (unsigned)hA[u]);
+            atomicAdd(reinterpret_cast<unsigned*>(e0 + FB), (unsigned)hu);
           else
-            atomicAdd(e0 + 256 * FB, hA[u]);
+            atomicAdd(e0 + FB, hu);
         }
       }
     }
@@ -277,7 +291,6 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
     for (int u = 0; u < U; ++u) {
       iiA[u] = iiB[u];
       gA[u] = gB[u];
-      hA[u] = hB[u];
       bA[u] = bB[u];
       iiB[u] = iiC[u];
     }
@@ -309,7 +322,9 @@ __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
     const int cb = (int)(t / p), j = (int)(t - (int64_t)cb * p);
     const int yb = j / FB, fl = j - yb * FB;
-    const u64* sp = slab + ((int64_t)a * ydim + yb) * SLAB + cb * FB + ((fl & 3) * FQ + (fl >> 2));
+    // slab image [bin][channel][slot] (gbdt_hist_kernel); Hs is [channel][bin][feature]
+    const int bc = ((cb & 255) << 1) | (cb >> 8);
+    const u64* sp = slab + ((int64_t)a * ydim + yb) * SLAB + bc * FB + ((fl & 3) * FQ + (fl >> 2));
     const int64_t stride = (int64_t)ydim * SLAB;
     u64 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
     int i = 0;
@@ -820,7 +835,8 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
         if (!s.resume) {
           int64_t CH, nwg;
           gbdt_hist_geom(a.n_train, a.p, d, a.rule, &CH, &nwg);
-          hipLaunchKernelGGL(gbdt_hist_kernel, dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr,
+          hipLaunchKernelGGL(hmode ? gbdt_hist_kernel<true> : gbdt_hist_kernel<false>,
+                             dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr,
                              a.ldr, a.idx[cur], a.gh[cur], a.seg[cur], a.tot, a.rule, nn, a.p, d,
                              CH, ydim, a.slab, hmode, a.loss);
           hipLaunchKernelGGL(gbdt_hist_reduce_kernel,
