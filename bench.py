@@ -21,7 +21,9 @@ RCCL the all-reduces (C01 Gram stack, C08 coefficients, C06 moments) are capture
 the fit's graph (utils/graphs.SegmentedStep), so a fit is the same two graph launches
 (Gram tiles on the Gram stream; everything else on the fit's stream) at every world
 size; if capture of the collectives fails they run eagerly between graph segments and
-the JSON says so (``collectives_captured``).
+the JSON says so (``collectives_captured``). Each in-flight fit owns an RCCL communicator
+(``communicators`` in the JSON): the fits' graphs replay concurrently on their own
+streams, and no two of them may run collectives of one communicator at the same time.
 
 Latency (SURVEY.md §7.5 protocol): ``single_fit_ms`` is the MEDIAN of >= 5 single-call
 replays, each bracketed by device syncs (``single_fit_ms_all`` lists them).
@@ -135,6 +137,19 @@ def main():
     # 1/2/4/8 curve): the CV path solve is a latency-bound serial recurrence that fills few
     # CUs, so another fit's HBM-bound Gram runs beside it on its own stream.
     inflight = 3 if args.inflight < 0 else max(1, args.inflight)
+    # One RCCL communicator per in-flight fit. The fits' graphs replay side by side on their
+    # own streams; collectives of ONE communicator must never run concurrently (their
+    # kernels share the communicator's channel buffers, and captured graphs replayed on
+    # different streams carry no order between them), while each fit's own collectives
+    # stay in stream order on its private communicator. gloo (CPU) ops are synchronous
+    # calls: one communicator serves every slot.
+    slot_comms = [comm] * inflight
+    if world > 1 and inflight > 1 and isinstance(comm, C.TorchComm) and comm.capturable:
+        import torch.distributed as tdist
+        slot_comms = [comm] + [C.TorchComm(tdist.new_group(list(range(world))))
+                               for _ in range(inflight - 1)]
+        for c in slot_comms[1:]:
+            c.barrier()             # create each communicator now, outside any capture
     if inflight > 1:
         # Gram workgroup count beside another fit's path solve: 1024 for two fits in
         # lockstep (profiles/r01_bench/wg_inflight.log); staggered, 824-4096 are within 3 %
@@ -217,7 +232,7 @@ def main():
         # hooks of the stagger stay eager between the Gram graph and the rest
         with plan_slot(i):      # private Gram workspace per in-flight fit
             phases = [in_slot(ph, i) for ph in staggered(
-                dml_phases(pan, args.folds, "min", comm=comm, seg_counts=seg_counts,
+                dml_phases(pan, args.folds, "min", comm=slot_comms[i], seg_counts=seg_counts,
                            exact=bool(args.exact)), i)]
             try:
                 return SegmentedStep(phases, graph=use_graph), None
@@ -359,6 +374,7 @@ def main():
             "graphs_per_fit": graphs_per_fit,
             "exact": bool(args.exact),
             "collectives_captured": collectives_captured,
+            "communicators": len({id(c) for c in slot_comms}),
             "parity": parity,
         }
         if emulate > 1:

@@ -45,8 +45,8 @@ def rccl(gpu):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("capture_cc", [True, False])
-def test_segmented_graphs_with_rccl_match_eager(gpu, rccl, capture_cc):
+@pytest.mark.parametrize("capture_cc,slot_comms", [(True, False), (False, False), (True, True)])
+def test_segmented_graphs_with_rccl_match_eager(gpu, rccl, capture_cc, slot_comms):
     from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
     from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel, dml_phases
     from ate_replication_causalml_amd.ops import gram as gram_op
@@ -57,10 +57,18 @@ def test_segmented_graphs_with_rccl_match_eager(gpu, rccl, capture_cc):
     seg = np.asarray(pan.seg_nreal, dtype=np.float64)
     want = dml_crossfit_panel(pan, 5, "min")[0].clone()
     runs = []
+    comms = [rccl, rccl]
+    if slot_comms:
+        # bench.py at world > 1: one RCCL communicator per in-flight fit (dist.new_group),
+        # so two fits' captured collectives never share a communicator
+        import torch.distributed as dist
+        from ate_replication_causalml_amd.parallel.comm import TorchComm
+        comms = [rccl, _WideComm(TorchComm(dist.new_group([0])))]
+        comms[1].barrier()
     for i in range(2):
         with gram_op.plan_slot(i):
             # the real group has one rank: every fold's paths must be solved here
-            ph = dml_phases(pan, 5, "min", comm=rccl, seg_counts=seg, shard_paths=False)
+            ph = dml_phases(pan, 5, "min", comm=comms[i], seg_counts=seg, shard_paths=False)
             assert sum(isinstance(p, Collective) and p.capturable for p in ph) == 2
             runs.append(SegmentedStep(ph, graph=True, capture_collectives=capture_cc))
     assert all(r.graphed for r in runs)
