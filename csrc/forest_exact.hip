@@ -44,8 +44,22 @@ namespace {
 
 constexpr int XT = 512;            // threads per tree
 constexpr int XW = XT / 64;        // waves per tree
-constexpr int XLDS = 16384;        // workgroup-level node keys sorted in LDS up to this many rows
-constexpr int WCAP = 512;          // nodes up to this many rows: one wave each
+// Two trees per CU: 58 KB of LDS and <= 128 VGPRs per lane (__launch_bounds__ minimum of 4
+// waves per SIMD; the compiler spills ~60 VGPRs to scratch) instead of one tree per CU at
+// 99 KB / 228 VGPRs. On the tutorial's forests (df_mod, 2500 / 4 x 2000 trees) the many
+// trees in flight outweigh the spills and the smaller per-wave node cap: aipw_rf 188 -> 125
+// ms, double_ml 294 -> 177 ms, the same trees (profiles/r03_forest_exact/occupancy_ab.txt).
+#ifndef EXACT_XLDS
+#define EXACT_XLDS 8192        // workgroup-level nodes above this many rows sort in global scratch
+#endif
+#ifndef EXACT_WCAP
+#define EXACT_WCAP 256
+#endif
+#ifndef EXACT_MINWG
+#define EXACT_MINWG 4          // __launch_bounds__ minimum waves per SIMD
+#endif
+constexpr int XLDS = EXACT_XLDS;   // workgroup-level node keys sorted in LDS up to this many rows
+constexpr int WCAP = EXACT_WCAP;   // nodes up to this many rows: one wave each
 // one LDS arena: the workgroup-level key buffer (XLDS keys) or, per wave, WCAP keys and the
 // WCAP per-position statistics (2 x int64) of the wave's node
 constexpr int WSLICE = WCAP * 4 + WCAP * 16;
@@ -256,7 +270,7 @@ __device__ void wave_bitonic(uint32_t* K, int N2, int lane) {
     }
 }
 
-__global__ __launch_bounds__(XT) void forest_exact_kernel(
+__global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const double* __restrict__ vals,
     int ldv, const int32_t* __restrict__ nval, const uint8_t* __restrict__ ycls,
     const int64_t* __restrict__ r1, int cap, int32_t* __restrict__ feat, int32_t* __restrict__ thr,

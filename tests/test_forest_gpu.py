@@ -155,13 +155,14 @@ def test_level_engine_wide_many_features(gpu, monkeypatch):
     assert_same_forest(g, t)
 
 
-@pytest.mark.parametrize("n", [3000, 20000, 40000])
+@pytest.mark.parametrize("n", [3000, 7000, 20000, 40000])
 @pytest.mark.parametrize("case", ["rf_class", "rf_reg"])
 def test_exact_split_engine_bit_identical_to_host(gpu, case, n):
     """csrc/forest_exact.hip (sort-based splits on uint16 value ranks: lane-per-row nodes
-    <= 64 rows, wave bitonic sorts in LDS <= 4096 rows, workgroup bitonic sorts in LDS
-    <= 16384 rows -- the n = 20000 root -- and in global scratch above -- n = 40000) grows
-    the host twin's trees bit for bit; OOB and new-row predictions match."""
+    <= 64 rows, wave bitonic sorts in LDS <= 256 rows (EXACT_WCAP), workgroup bitonic sorts
+    in LDS <= 8192 rows (EXACT_XLDS) -- the n = 3000 / 7000 roots -- and in global scratch
+    above -- n = 20000 / 40000) grows the host twin's trees bit for bit; OOB and new-row
+    predictions match."""
     r = np.random.default_rng(11)
     X = r.normal(size=(n, 7))
     X[:, 3] = np.round(X[:, 3])                 # a few ties / repeated values
