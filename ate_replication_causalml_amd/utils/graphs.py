@@ -303,14 +303,16 @@ class GraphCache:
       evicted in between), captures it and replays it;
     * later calls: copy + ONE graph launch.
 
-    LRU bounded by ``maxsize`` entries and ``max_bytes`` of retained input buffers
+    LRU bounded by ``maxsize`` entries (32: the 14-row tutorial pass alone keeps more than
+    8 estimator layouts, and an LRU of 8 recaptured several of them on every pass) and
+    ``max_bytes`` of retained input buffers
     (``ATE_GRAPH_CACHE_BYTES``, default 24 GiB; each entry also holds its graph's memory
     pool). A body that cannot be captured is remembered and runs eagerly from then on
     (the reason is printed). Outputs of a replay are the graph's static tensors: read them
     before the next call. ``clear()`` drops every entry (and its HBM).
     Returns (output, replayed: bool)."""
 
-    def __init__(self, maxsize: int = 8, max_bytes: int | None = None,
+    def __init__(self, maxsize: int = 32, max_bytes: int | None = None,
                  retain_bytes: int | None = None):
         self.maxsize = maxsize
         self.max_bytes = max_bytes if max_bytes is not None else \
