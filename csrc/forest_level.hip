@@ -292,6 +292,49 @@ __device__ __forceinline__ void lv_accumulate(const LvArgs& a, const int32_t* __
   }
 }
 
+#ifndef LV_MID_RK
+#define LV_MID_RK 1
+#endif
+// Kind-0 mid nodes, lanes = (row, feature): lane l of a wave takes drawn feature l & 31 of
+// row l >> 5, so one wave instruction gathers the drawn bins of TWO rows (their few cache
+// lines, coalesced) instead of one bin of 64 rows (64 lines, one byte each); the row's
+// index, weight and class are one broadcast load per 32 lanes. Same integer sums as
+// lv_accumulate, in any order. U rows per lane in flight.
+template <int FG, int U>
+__device__ __forceinline__ void lv_accumulate_rk(const LvArgs& a, const int32_t* __restrict__ wt,
+                                                 const uint8_t* X, int fik, int64_t fst,
+                                                 int spk, int64_t rst, int nk, int q0, int q1,
+                                                 uint32_t (*sh)[2][NBINS]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane >> 5, k = lane & 31;
+  const bool kon = k < nk;
+  const int kk = kon ? k : 0;
+  const int64_t fo = (int64_t)fik * fst;
+  const int spread = lane & (spk - 1);
+  // rows of step s: q0 + ((s * U + u) * 4 + wid) * 2 + r
+  for (int base = q0 + wid * 2 + r; base < q1; base += 8 * U) {
+    int ii[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = base + u * 8;
+      ii[u] = q < q1 ? a.idx[q] : -1;
+    }
+    uint32_t wv[U];
+    int yv[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = ii[u] < 0 ? 0 : ii[u];
+      wv[u] = ii[u] < 0 ? 0u : (uint32_t)wt[i];
+      yv[u] = a.ycls[i];
+      bv[u] = X[fo + (int64_t)i * rst];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (ii[u] >= 0 && kon)
+        atomicAdd(&sh[kk][yv[u]][bv[u] * spk + spread], wv[u]);
+  }
+}
+
 // ------------------------------------------------------------------ sampling (K10)
 __global__ __launch_bounds__(256) void lv_boot_kernel(ForestParams fp, int32_t* __restrict__ w) {
   const int t = blockIdx.y;
@@ -486,7 +529,14 @@ __global__ __launch_bounds__(256) void lv_mid_kernel(LvArgs a, const int32_t* __
       sp[k] = lv_spread(a.nbin[fi[k]]);
     }
     __syncthreads();
-    lv_accumulate<HT, FG, U>(a, wt, a.Xb, fi, a.fst, sp, a.rst, nk, nd.lo, nd.hi, sh);
+    if constexpr (LV_MID_RK && sizeof(HT) == 4 && FG <= 32) {
+      const int k = threadIdx.x & 31;
+      const int fik = perm[k0 + min(k, nk - 1)];
+      lv_accumulate_rk<FG, 8>(a, wt, a.Xb, fik, a.fst, lv_spread(a.nbin[fik]), a.rst, nk,
+                              nd.lo, nd.hi, reinterpret_cast<uint32_t (*)[2][NBINS]>(sh));
+    } else {
+      lv_accumulate<HT, FG, U>(a, wt, a.Xb, fi, a.fst, sp, a.rst, nk, nd.lo, nd.hi, sh);
+    }
     __syncthreads();
     for (int k = wid; k < nk; k += 4) lv_collapse(sh[k][0], sh[k][1], sp[k]);
     __syncthreads();
@@ -542,6 +592,7 @@ __global__ __launch_bounds__(256) void lv_small_kernel(LvArgs a, const int32_t* 
                                                        int nsmall) {
   __shared__ int16_t perm[4][LV_PMAX];
   __shared__ int64_t hist[4][2][NBINS];
+  __shared__ uint8_t sbin[4][16][64];                       // [wave][drawn feature][row]
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int s = blockIdx.x * 4 + wid;
   if (s >= nsmall) return;                                  // uniform per wave
@@ -579,12 +630,28 @@ __global__ __launch_bounds__(256) void lv_small_kernel(LvArgs a, const int32_t* 
   double best = -INFINITY;
   int bf = -1, bb = -1;
   for (int k0 = 0; k0 < nf; k0 += 16) {
+    // Gather the batch's bins with lanes = (row, feature): one wave instruction covers 4
+    // rows x 16 drawn features (those rows' few lines) instead of one feature of 64 rows
+    // (64 lines, a byte each), and ceil(m / 4) instructions instead of 16 for m rows; the
+    // bins pass through LDS back to a row per lane.
+    {
+      const int kq = lane & 15, kf = k0 + kq;
+      const int64_t fo = kf < nf ? (int64_t)perm[wid][kf] * a.fst : 0;
+      for (int r0 = 0; r0 < m; r0 += 4) {                   // uniform: m is the node's
+        const int r = r0 + (lane >> 4);
+        const int cir = __shfl(ci, r & 63, 64);
+        if (r < m && kf < nf) sbin[wid][kq][r] = a.Xb[fo + (int64_t)cir * a.rst];
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);                   // lgkmcnt(0): LDS stores done
+      __builtin_amdgcn_wave_barrier();
+    }
     int bins[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int k = k0 + u;
-      bins[u] = (valid && k < nf) ? (int)a.Xb[(int64_t)perm[wid][k] * a.fst + (int64_t)ci * a.rst] : 0;
+      bins[u] = (valid && k < nf) ? (int)sbin[wid][u][lane] : 0;
     }
+    __builtin_amdgcn_wave_barrier();                        // reads done before the next batch
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int k = k0 + u;
