@@ -295,14 +295,33 @@ def main():
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.all_reduce_max_(el)
     elapsed = float(el.item())
-    # latency of ONE cross-fit alone (no overlap), SURVEY.md §7.5: median of >= 5 replays
+    # latency of ONE cross-fit alone (no overlap), SURVEY.md §7.5: median of >= 5 replays of
+    # one ate_dml call as the library runs it -- its own captured step on one stream with the
+    # default Gram plan (whole rounds of workgroups), not the throughput fits' split-stream
+    # graphs and their overlap-tuned plan
+    lat_step, lat_kind = None, "throughput fit 0"
+    if device.type == "cuda" and graphed:
+        saved = os.environ.pop("ATE_GRAM_PAIR_WG", None)
+        try:
+            with plan_slot(len(runs)):
+                lat_step = SegmentedStep(
+                    [in_slot(ph, len(runs)) for ph in dml_phases(
+                        pan, args.folds, "min", comm=comm, seg_counts=seg_counts,
+                        exact=bool(args.exact))], graph=True)
+            lat_kind = f"own step ({lat_step.graph_count} graph(s), default Gram plan)"
+        finally:
+            if saved is not None:
+                os.environ["ATE_GRAM_PAIR_WG"] = saved
     nlat = max(5, min(args.steps, 11))
     lats = []
     for k in range(nlat):
         sync()
         comm.barrier()
         t1 = time.perf_counter()
-        run_step(0)
+        if lat_step is not None:
+            lat_step()
+        else:
+            run_step(0)
         sync()
         lats.append(time.perf_counter() - t1)
     lat_t = torch.tensor(lats, dtype=torch.float64, device=device)
@@ -370,6 +389,7 @@ def main():
             "inflight": n_inflight,
             "single_fit_ms": lat * 1e3,
             "single_fit_ms_all": [round(v * 1e3, 4) for v in lats],
+            "single_fit_step": lat_kind,
             "single_fit_rows_per_s": n_total / lat,
             "graphs_per_fit": graphs_per_fit,
             "exact": bool(args.exact),
