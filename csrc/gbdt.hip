@@ -36,6 +36,7 @@
 //   again. A single-device fit runs to completion in one call. Root totals come from
 //   the (reduced) level-0 histogram.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -237,38 +238,43 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   int32_t iiA[U], iiB[U];
   int64_t gA[U];
   uint32_t bA[U];
-  const int64_t last = e - 1;
+  // positions are int32 (a fit holds < 2^31 training rows): half the address VALU of int64
+  const int s32 = (int)s, e32 = (int)e, last = e32 - 1;
   const bool wok = 4 * l4 < nf;
-  auto pos = [&](int64_t base, int u) { return base + (u * (NTH / 64) + w) * (64 / FQ) + r16; };
+  auto pos = [&](int base, int u) { return base + (u * (NTH / 64) + w) * (64 / FQ) + r16; };
 #pragma unroll
-  for (int u = 0; u < U; ++u) iiA[u] = idx[min(pos(s, u), last)];
+  for (int u = 0; u < U; ++u) iiA[u] = idx[min(pos(s32, u), last)];
 #pragma unroll
-  for (int u = 0; u < U; ++u) iiB[u] = idx[min(pos(s + RPI, u), last)];
+  for (int u = 0; u < U; ++u) iiB[u] = idx[min(pos(s32 + RPI, u), last)];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    gA[u] = gh[min(pos(s, u), last)];
+    gA[u] = gh[min(pos(s32, u), last)];
     bA[u] = (mode & 2) ? (uint32_t)iiA[u] * 0x9E3779B1u : xw[(int64_t)iiA[u] * ldw];
   }
   u64 dummy = 0;
-  for (int64_t base = s; base < e; base += RPI) {
+  // One pipelined iteration. TAIL: positions may pass the segment end (clamped loads, rows
+  // past it skipped); the main loop runs only while iterations i .. i+2 lie inside it, so it
+  // carries no clamps and no per-row range test.
+  auto step = [&](int base, auto tail_tag) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    auto at = [&](int q) { return TAIL ? min(q, last) : q; };
     int64_t gB[U];
     uint32_t bB[U];
     int32_t iiC[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      gB[u] = gh[min(pos(base + RPI, u), last)];
+      gB[u] = gh[at(pos(base + RPI, u))];
       bB[u] = (mode & 2) ? (uint32_t)iiB[u] * 0x9E3779B1u : xw[(int64_t)iiB[u] * ldw];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) iiC[u] = idx[min(pos(base + 2 * RPI, u), last)];
+    for (int u = 0; u < U; ++u) iiC[u] = idx[at(pos(base + 2 * RPI, u))];
     if (mode & 1) {
 #pragma unroll
       for (int u = 0; u < U; ++u) dummy += (u64)gA[u] * bA[u];
-    } else {
+    } else if (wok) {                                       // padding words add nothing
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        // padding words and rows past the segment add nothing: their lanes stay idle
-        if (!wok || pos(base, u) > last) continue;
+        if (TAIL && pos(base, u) > last) continue;          // rows past the segment
         u64 gu, hu;
         gbdt_unpack(loss, gA[u], gu, hu);
 #pragma unroll
@@ -294,7 +300,10 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
       bA[u] = bB[u];
       iiB[u] = iiC[u];
     }
-  }
+  };
+  int base = s32;
+  for (; base + 3 * RPI <= e32; base += RPI) step(base, std::false_type{});
+  for (; base < e32; base += RPI) step(base, std::true_type{});
   if (dummy == 0x123456789ull) sh[0] = dummy;
   __syncthreads();
   if (mode & 4) return;
