@@ -155,8 +155,9 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
         n = len(y)
         p = Xb[0].shape[0] if isinstance(Xb[0], np.ndarray) or Xb[0].device.type == "cpu" \
             else len(edges[0])
-    if depth < 1 or depth > 6:
-        raise ValueError("depth must be in [1, 6] (<= 32 nodes per level histogram)")
+    if depth < 1 or depth > MAX_DEPTH:
+        raise ValueError(f"depth must be in [1, {MAX_DEPTH}] (<= {2 ** (MAX_DEPTH - 1)} nodes "
+                         "per level histogram, csrc/gbdt.hip MAXD)")
     if backend is None:
         backend = "gpu" if torch.cuda.is_available() else "cpu"
     if edges is None:
@@ -188,6 +189,9 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
                     edges, dist, dev)
 
 
+MAX_DEPTH = 8      # csrc/gbdt.hip MAXD
+
+
 class FitArgs(ctypes.Structure):
     """Mirror of csrc/gbdt.hip::GbdtFitArgs."""
     P = ctypes.c_void_p
@@ -208,7 +212,7 @@ class RunState(ctypes.Structure):
                 ("resume", ctypes.c_int), ("red_count", ctypes.c_int64)]
 
 
-MAXB = 65
+MAXB = 2 ** (MAX_DEPTH - 1) + 1    # csrc/gbdt.hip MAXB: partition buckets + retired
 
 
 def exact_base(y_train, n_train, loss, dist=None):
@@ -266,7 +270,7 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
     rule = 0 if dist is None else 1
     cap = int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule))
     slab = torch.empty(cap, **i64)
-    cand = torch.empty(32 * (-(-p // 8)) * 4, **i64)
+    cand = torch.empty((1 << max(depth - 1, 0)) * (-(-p // 8)) * 4, **i64)   # 32-B Cand
     P = ctypes.c_void_p
     a = FitArgs(Xr=Xr.data_ptr(), ldr=ldr, n=n, n_train=n_train, p=p, depth=depth,
                 n_trees=n_trees, loss=LOSS[loss], rule=rule, W=W, lam=lam,

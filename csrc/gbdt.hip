@@ -56,7 +56,11 @@ constexpr int NTH = FB * 32;         // histogram workgroup: FB / 4 lanes per ro
 constexpr int FQ = FB / 4;           // dwords (lanes) per row
 constexpr int SFB = 8;               // features per split-search workgroup (one per wave)
 constexpr int HS = 257;              // padded bins per (feature, channel) in LDS
-constexpr int MAXB = 65;             // partition buckets: 2 * 32 children + retired
+constexpr int MAXD = 8;              // max tree depth (levels 0 .. MAXD - 1 histogrammed)
+constexpr int MAXN = 1 << (MAXD - 1);  // max nodes of a histogrammed level (128)
+constexpr int MAXM = (1 << (MAXD + 1)) - 1;   // max nodes of a tree (511)
+constexpr int MAXB = MAXN + 1;       // partition buckets (partitions follow levels <= MAXD - 2:
+                                     // 2 * 64 children) + retired; fits the uint8 bucket ids
 constexpr double GFIX = 268435456.0;   // 2^28
 
 typedef unsigned long long u64;
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
     int loss) {
   const int mode = ABL ? mode_in : 0;
   __shared__ u64 sh[SLAB];
-  __shared__ int sseg[33], sacc[33], snch[32];
+  __shared__ int sseg[MAXN + 1], sacc[MAXN + 1], snch[MAXN];
   __shared__ int64_t wk[3];
   const int bid = blockIdx.x;
   // Chunk c runs on XCD c % 8 (dispatch sends block b to XCD b % 8), its ydim feature
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
 __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
     const u64* __restrict__ slab, const int32_t* __restrict__ seg, const int64_t* tot, int rule,
     int nn, int p, int d, int64_t CH, int ydim, int64_t* __restrict__ Hs) {
-  __shared__ int sseg[33], sacc[33], snch[32];
+  __shared__ int sseg[MAXN + 1], sacc[MAXN + 1], snch[MAXN];
   const int k = blockIdx.y;
   if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
   __syncthreads();
@@ -532,7 +536,7 @@ __global__ __launch_bounds__(NT) void gbdt_part_count_kernel(
     int64_t n_train, const int32_t* __restrict__ seg, int nn, int d,
     const int32_t* __restrict__ feat, const int32_t* __restrict__ thr, int64_t R, int W,
     uint8_t* __restrict__ bkt, int32_t* __restrict__ cnt) {
-  __shared__ int sseg[33], sft[32], sth[32], lc[MAXB];
+  __shared__ int sseg[MAXN / 2 + 1], sft[MAXN / 2], sth[MAXN / 2], lc[MAXB];
   if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
   if (threadIdx.x < nn) {
     sft[threadIdx.x] = feat[(1 << d) - 1 + threadIdx.x];
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(NT) void gbdt_part_scatter_kernel(
 
 // f[i] += value of the leaf row i reaches, for trees [0, ntree) (all rows). A workgroup
 // stages RW whole rows in LDS with coalesced 16-B loads (all in flight at once) and the
-// trees (M <= 127 nodes), so a row's walk is LDS-latency only.
+// trees (M <= MAXM nodes), so a row's walk is LDS-latency only.
 __global__ __launch_bounds__(NT) void gbdt_apply_kernel(const uint8_t* __restrict__ Xr, int64_t ldr,
                                                         int64_t n, int RW, int ntree, int M,
                                                         const int32_t* __restrict__ feat,
@@ -647,8 +651,8 @@ __global__ __launch_bounds__(NT) void gbdt_apply_kernel(const uint8_t* __restric
                                                         const double* __restrict__ value,
                                                         double* __restrict__ f) {
   extern __shared__ uint4 srow[];                           // [RW][ldr] bytes
-  __shared__ int sft[127], sth[127];
-  __shared__ double sv[127];
+  __shared__ int sft[MAXM], sth[MAXM];
+  __shared__ double sv[MAXM];
   const int64_t r0 = blockIdx.x * (int64_t)RW;
   const int rows = (int)min((int64_t)RW, n - r0);
   const int v16 = (int)(ldr >> 4);
@@ -658,10 +662,10 @@ __global__ __launch_bounds__(NT) void gbdt_apply_kernel(const uint8_t* __restric
   double acc = threadIdx.x < rows ? f[r0 + threadIdx.x] : 0.0;
   for (int t = 0; t < ntree; ++t) {
     __syncthreads();
-    if (threadIdx.x < M) {
-      sft[threadIdx.x] = feat[(int64_t)t * M + threadIdx.x];
-      sth[threadIdx.x] = thr[(int64_t)t * M + threadIdx.x];
-      sv[threadIdx.x] = value[(int64_t)t * M + threadIdx.x];
+    for (int m = threadIdx.x; m < M; m += NT) {
+      sft[m] = feat[(int64_t)t * M + m];
+      sth[m] = thr[(int64_t)t * M + m];
+      sv[m] = value[(int64_t)t * M + m];
     }
     __syncthreads();
     if (threadIdx.x < rows) {
@@ -685,12 +689,12 @@ __global__ __launch_bounds__(NT) void gbdt_walk_kernel(const uint8_t* __restrict
                                                        const int32_t* __restrict__ thr,
                                                        const double* __restrict__ value,
                                                        double* __restrict__ f) {
-  __shared__ int sft[127], sth[127];
-  __shared__ double sv[127];
-  if (threadIdx.x < M) {
-    sft[threadIdx.x] = feat[threadIdx.x];
-    sth[threadIdx.x] = thr[threadIdx.x];
-    sv[threadIdx.x] = value[threadIdx.x];
+  __shared__ int sft[MAXM], sth[MAXM];
+  __shared__ double sv[MAXM];
+  for (int m = threadIdx.x; m < M; m += NT) {
+    sft[m] = feat[m];
+    sth[m] = thr[m];
+    sv[m] = value[m];
   }
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * NT * WALK_U;
@@ -761,7 +765,7 @@ struct GbdtFitArgs {
   int64_t* Hs;            // [max(1, 2^(depth-2))][2][256][p] compact histogrammed nodes
   u64* slab;              // [slab_cap] partial histograms
   int64_t slab_cap;
-  Cand* cand;             // [32 * ceil(p / 8)] split candidates (32 B each)
+  Cand* cand;             // [2^(depth-1) * ceil(p / 8)] split candidates (32 B each)
 };
 
 // Resumable position of a fit (models/gbdt.py::RunState): tree t, level d, ping-pong
@@ -814,7 +818,7 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
   const GbdtFitArgs& a = *static_cast<const GbdtFitArgs*>(args);
   GbdtRunState& s = *static_cast<GbdtRunState*>(state);
   hipStream_t st = (hipStream_t)stream;
-  if (a.depth < 1 || a.depth > 6 || (a.ldr & 31) || a.n_train < 1 || a.W < 1 || a.W > 4 * NT)
+  if (a.depth < 1 || a.depth > MAXD || (a.ldr & 31) || a.n_train < 1 || a.W < 1 || a.W > 4 * NT)
     return -1;
   if ((a.n_train + a.R - 1) / a.R > a.W) return -2;
   if (a.slab_cap < ate_gbdt_slab_entries(a.n_train, a.p, a.depth, a.rule)) return -5;
@@ -902,7 +906,7 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
 ATE_API int ate_gbdt_apply(const void* Xr, int64_t ldr, int64_t n, int ntree, int M,
                            const void* feat, const void* thr, const void* value, void* f,
                            void* stream) {
-  if (M > 127 || (ldr & 15)) return -1;
+  if (M > MAXM || (ldr & 15)) return -1;
   gbdt_launch_apply((const uint8_t*)Xr, ldr, n, ntree, M, (const int32_t*)feat,
                     (const int32_t*)thr, (const double*)value, (double*)f, (hipStream_t)stream);
   ATE_CHECK_LAUNCH();

@@ -11,7 +11,7 @@ from test_gbdt import _data
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("depth", [1, 3, 6])
+@pytest.mark.parametrize("depth", [1, 3, 6, 8])
 def test_gbdt_gpu_trees_identical_squared(gpu, depth):
     X, y = _data(5000, depth)
     tr = np.arange(len(y)) % 4 != 0
@@ -54,17 +54,18 @@ def _wide(n=20000, p=70, seed=3):
     return X, y
 
 
-@pytest.mark.parametrize("sharded", [False, True])
-def test_gbdt_gpu_wide_identical(gpu, sharded):
-    """p > 32 (several 32-feature histogram blocks, a partial last block), depth 6
-    (five partitions, histogram subtraction at every level); ``sharded`` runs the
-    row-shard path (hessian child rule + reduce callback) on a one-rank context."""
+@pytest.mark.parametrize("sharded,depth", [(False, 6), (True, 6), (False, 8), (True, 8)])
+def test_gbdt_gpu_wide_identical(gpu, sharded, depth):
+    """p > 32 (several 32-feature histogram blocks, a partial last block), depth 6 / 8
+    (five / seven partitions, up to 128 histogrammed nodes, histogram subtraction at every
+    level); ``sharded`` runs the row-shard path (hessian child rule + reduce callback) on a
+    one-rank context."""
     from ate_replication_causalml_amd.parallel.comm import LocalComm
     from ate_replication_causalml_amd.parallel.dist import DistContext
     X, y = _wide()
     tr = np.arange(len(y)) % 5 != 2
     edges = G.global_bin_edges(X, None)
-    kw = dict(n_trees=4, depth=6, lr=0.3, train=tr, edges=edges)
+    kw = dict(n_trees=4, depth=depth, lr=0.3, train=tr, edges=edges)
     dist = DistContext(LocalComm(), 0, len(y)) if sharded else None
     a = G.fit_gbdt(X, y, backend="gpu", dist=dist, **kw)
     b = G.fit_gbdt(X, y, backend="cpu", **kw)
