@@ -679,7 +679,8 @@ ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, co
   // waves per tree and register budget (tools/forest_occ.sh, growth alone on MI355X):
   // <= 256 trees: 16 waves at 4 per SIMD (64 trees, n = 1e6: 1.01 s; 4 waves at 2 per
   // SIMD 1.83 s); <= 1024 trees: 8 waves at 4 per SIMD (300 trees: 2.11 s vs 2.35 s);
-  // more: 4-wave workgroups at 3 per SIMD (2500 trees, n = 1e4: 33 ms vs 42 ms).
+  // more: 4-wave workgroups at 3 per SIMD (2500 trees, n = 1e4: 33 ms vs 42 ms), round 3:
+  // at 4 per SIMD (profiles/r03_forest_exact/w4_minw4_ab.txt).
   // nw: 0 = auto, or 4 / 8 / 16 (A/B).
   int w = nw;
   if (w == 0) w = fp.ntree <= 256 ? 16 : fp.ntree <= 1024 ? 8 : 4;
@@ -690,7 +691,10 @@ ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, co
                      (const int64_t*)r2, cap, (int32_t*)feat, (int32_t*)thr, (int32_t*)left,      \
                      (double*)val, (int32_t*)nnodes, (uint8_t*)inbag, (int64_t*)est,              \
                      (char*)scratch)
-  if (w == 4) ATE_FOREST_LAUNCH(4, 3);
+#ifndef FOREST_W4_MINW
+#define FOREST_W4_MINW 4   // 4 waves/SIMD: 4 trees per CU, ~48 VGPRs spilled; vs 3: config 4
+#endif                     // 0.616 -> 0.597 s, tutorial causal forest 124 -> 114 ms, same trees
+  if (w == 4) ATE_FOREST_LAUNCH(4, FOREST_W4_MINW);
   else if (w == 8) ATE_FOREST_LAUNCH(8, 4);
   else if (w == 16) ATE_FOREST_LAUNCH(16, 4);
   else return -1;
