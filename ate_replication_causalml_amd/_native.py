@@ -84,6 +84,7 @@ _SIGS = {
     "ate_standardize": "pllippp",
     "ate_interactions": "pllipl" + "p",
     "ate_scan_parts": "l",
+    "ate_gbdt_limits": "p",
     "ate_excl_scan_i32": "plpppp",
     "ate_excl_scan_i64": "plpppp",
 }

@@ -184,12 +184,28 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
         return GbdtModel(tr.feat, tr.thr, tr.value, tr.base, loss, depth, edges, "cpu",
                          tr.predict_binned(Xbh))
     dev = torch.device("cuda", torch.cuda.current_device())
+    _check_limits()
     Xr, ldr = Xb if Xb is not None else _rowmajor_bins(X, edges, dev)
     return _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
                     edges, dist, dev)
 
 
 MAX_DEPTH = 8      # csrc/gbdt.hip MAXD
+_limits_ok = False
+
+
+def _check_limits():
+    """The buffers below are sized with MAX_DEPTH / MAXB; the kernels index them with the
+    library's own compile-time limits: refuse to run on a mismatched build."""
+    global _limits_ok
+    if _limits_ok:
+        return
+    out = (ctypes.c_int * 3)()
+    _native.call("ate_gbdt_limits", ctypes.cast(out, ctypes.c_void_p))
+    if (out[0], out[1]) != (MAX_DEPTH, MAXB):
+        raise RuntimeError(f"libatehip GBDT limits (MAXD {out[0]}, MAXB {out[1]}) differ from "
+                           f"models/gbdt.py (MAX_DEPTH {MAX_DEPTH}, MAXB {MAXB}): rebuild")
+    _limits_ok = True
 
 
 class FitArgs(ctypes.Structure):

@@ -801,6 +801,15 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
   *nwg = wg;
 }
 
+// compile-time limits the host side sizes its buffers with (models/gbdt.py checks them)
+ATE_API int ate_gbdt_limits(void* out) {
+  int* o = static_cast<int*>(out);
+  o[0] = MAXD;
+  o[1] = MAXB;
+  o[2] = FB;
+  return 0;
+}
+
 ATE_API int64_t ate_gbdt_slab_entries(int64_t n_train, int p, int depth, int rule) {
   int64_t m = 0;
   for (int d = 0; d < depth; ++d) {
