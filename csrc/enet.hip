@@ -248,8 +248,9 @@ static_assert(NW >= PMAX / 64, "one pull wave per 64-column block: NW >= PMAX / 
 #define ENET_BALLOT_ONLY 0   // 1: every pass uses the ballot recurrence (A/B timing)
 #endif
 #ifndef ENET_PULL_DENSE      // pull a whole 64-row column block when at least this many of
-#define ENET_PULL_DENSE 32   //   its coordinates are pending, else a compacted row list
-#endif
+#define ENET_PULL_DENSE 12   //   its coordinates are pending, else a compacted row list
+#endif                       //   (sweep 4..48: 12 best, CV stage 3.12 -> 2.98 ms, same bits;
+                             //   profiles/r03_enet/pull_dense_sweep.txt)
 #ifndef ENET_DENSE_MIN       // dense (all 64 lanes, static) walk of a block when at least
 #define ENET_DENSE_MIN 28    //   this many lanes move: nonzero lanes (full pass) /
 #endif                       //   eligible lanes (active pass)
