@@ -80,11 +80,13 @@ class GramPlan:
         whole_rounds = False
         if self.pair:
             # one Gram alone on the chip: 5 whole rounds of workgroups (N=1e7, p=500, 5 folds:
-            # 2.48 ms vs 2.61 at 2040 WGs and 2.70 at 2060, profiles/r02c_gram); bench.py's
+            # 2.48 ms vs 2.61 at 2040 WGs and 2.70 at 2060, profiles/r02c_gram; ATE_GRAM_ROUNDS
+            # overrides the round count for sweeps); bench.py's
             # overlapped fits set ATE_GRAM_PAIR_WG (finer workgroups share CUs with path solves)
             env = os.environ.get("ATE_GRAM_PAIR_WG")
             whole_rounds = env is None
-            target = int(env) if env is not None else 5 * _cu_count(panel.device)
+            rounds = int(os.environ.get("ATE_GRAM_ROUNDS", "5"))
+            target = int(env) if env is not None else rounds * _cu_count(panel.device)
         target = int(os.environ.get("ATE_GRAM_WG", target))
         nchunk_target = max(1, target // ntiles)
         chunks = []
