@@ -103,7 +103,8 @@ def dml_plr_gbdt(Y, W, X, folds=5, n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
         tg = target if backend == "gpu" else target.cpu().numpy()
         return G.fit_gbdt(None, tg, loss=loss, train=tr, **kw)
 
-    dkey = _data_key(checkpoint, Yn, Wn, Xn)
+    dkey = _data_key(checkpoint, Yn, Wn, Xn, np.array([folds, n_trees, depth, lr, lam,
+                                                       min_child, seed, fold_stream], float))
     ey, ew = _crossfit(y, w, fid_t, folds, fit, dev, dist, checkpoint, dkey)
     mom = S.dml_moments_exact(y - ey, w - ew, dist)
     return read_result(S.dml_finalize(mom, "plr"), method,
@@ -197,8 +198,12 @@ def dml_plr_gbdt_panel(pan, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0
     def fit(target, loss, train):
         return G.fit_gbdt(None, target, loss=loss, train=train, **kw)
 
-    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint,
-                       f"{data_key}.{pan.n}.{len(pan.xcols)}" if checkpoint is not None else "")
+    dkey = ""
+    if checkpoint is not None:
+        from .crossfit import _panel_key
+        dkey = _panel_key(pan, data_key, pan.n, len(pan.xcols), n_trees, depth, lr, lam,
+                          min_child, edge_rows)
+    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey)
     mom = S.dml_moments_exact(y - ey, w - ew, dist)
     n_all = dist.n_total if dist is not None else pan.n
     return read_result(S.dml_finalize(mom, "plr"), method, n=n_all, trees=n_trees, depth=depth)

@@ -89,25 +89,43 @@ def _gbdt_fit_predict(y, train, ho, Xb, edges, dev, seed, gbdt_kw):
 _NAMES = ("e", "mu1", "mu0")
 
 
+def _agreed_flags(have, comm, dev):
+    """Per-stage "already on disk" flags that every rank agrees on: the minimum over
+    ranks (a stage counts as done only if every rank saved it), so tree-parallel ranks
+    skip or recompute the same stages and their collectives stay paired."""
+    flags = torch.tensor([float(h) for h in have], dtype=torch.float64)
+    if comm is not None and comm.world_size > 1 and len(have):
+        fd = flags.to(dev) if getattr(comm, "capturable", False) else flags
+        comm.all_reduce_min_(fd)
+        flags = fd.cpu()
+    return [bool(f > 0) for f in flags]
+
+
+def _panel_key(pan, data_key, *params):
+    """Checkpoint key of an HBM panel run: the caller's name for the data, a content hash
+    of a strided sample of the panel's rows (two panels with the same n and p but other
+    data never share a key) and every parameter that changes the predictions."""
+    from ..utils.checkpoint import fingerprint
+    d = pan.data
+    # ~4096 rows: every k-th 64-row block of a blocked panel, every k-th row otherwise
+    samp = (d[::max(1, d.shape[0] // 64)] if pan.blocked else
+            d[:, ::max(1, d.shape[1] // 4096)]).float().cpu().numpy()
+    return f"{data_key}.{fingerprint(samp, np.asarray(params, dtype=np.float64))}"
+
+
 class _JobCache:
     """Per-job checkpoint of held-out nuisance predictions: job j of a
     cross-fit (fold j // 3, nuisance _NAMES[j % 3]) saves its predictions once computed;
     a resumed run loads finished jobs instead of refitting them. Every rank decides from
     the same all-reduced flags (tree-parallel ranks must skip the same forests)."""
 
-    def __init__(self, ck, key, tag, comm, dev):
+    def __init__(self, ck, key, tag, comm, dev, njobs):
         self.ck, self.key, self.tag = ck, key, tag
         self.done = set()
         if ck is None:
             return
-        n = 3 * 64
-        flags = torch.tensor([float(ck.has(self.stage(j), key)) for j in range(n)],
-                             dtype=torch.float64)
-        if comm is not None and comm.world_size > 1:
-            fd = flags.to(dev) if getattr(comm, "capturable", False) else flags
-            comm.all_reduce_min_(fd)
-            flags = fd.cpu()
-        self.done = {j for j in range(n) if flags[j] > 0}
+        flags = _agreed_flags([ck.has(self.stage(j), key) for j in range(njobs)], comm, dev)
+        self.done = {j for j in range(njobs) if flags[j]}
 
     def stage(self, j):
         return f"aipw_fold{j // 3}_{_NAMES[j % 3]}{self.tag}"
@@ -162,9 +180,11 @@ def aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, seed=1991, fold
     if checkpoint is not None:
         from ..utils.checkpoint import fingerprint
         key = fingerprint(Yn, Wn, Xn, np.array([folds, num_trees, seed, fold_stream]),
-                          np.frombuffer(learner.encode(), dtype=np.uint8))
+                          np.frombuffer(learner.encode(), dtype=np.uint8),
+                          np.frombuffer(repr(sorted((gbdt_kw or {}).items())).encode(),
+                                        dtype=np.uint8))
     tag = "" if comm is None or comm.world_size == 1 else f".r{comm.rank}of{comm.world_size}"
-    cache = _JobCache(checkpoint, key, tag, comm, dev)
+    cache = _JobCache(checkpoint, key, tag, comm, dev, 3 * folds)
     jobs = []
     # row lists by a lookback-free compaction on this stream, before the jobs run side by
     # side on their own streams (ops/scan.py: torch.nonzero there stalled config 3)
@@ -265,8 +285,9 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     mu0 = torch.empty_like(e)
     ar = torch.arange(n, device=dev)
     tag = "" if pcomm is None else f".r{rank}of{world}"
-    key = f"{data_key}.{n}.{p}.{num_trees}.{seed}.{t0}.{cnt}" if checkpoint is not None else ""
-    cache = _JobCache(checkpoint, key, tag, pcomm, dev)
+    key = _panel_key(pan, data_key, n, p, num_trees, seed, t0, cnt) \
+        if checkpoint is not None else ""
+    cache = _JobCache(checkpoint, key, tag, pcomm, dev, 3 * K)
     jobs = []
     for k in range(K):
         a, b = int(c0[k]), int(c0[k + 1])
@@ -373,7 +394,16 @@ def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_se
         key = fingerprint(Yn, Wn, Xn, np.array([num_trees, seed, nuisance_trees or 0]))
         tag = "" if comm is None or comm.world_size == 1 else f".r{comm.rank}of{comm.world_size}"
     stage = f"cf_fit{tag}"
-    if checkpoint is not None and checkpoint.has(stage, key):
+    ranges = [(b0, min(boot_chunk, B - b0)) for b0 in range(0, B, boot_chunk)]
+    bkey = key + f".{boot_seed}"
+    have = [False] * (1 + len(ranges))
+    if checkpoint is not None:
+        # every rank must skip / recompute the same stages: causal_forest (tree-sharded
+        # collectives) and bootstrap_replicates (all-gather) pair up across ranks
+        have = _agreed_flags([checkpoint.has(stage, key)] +
+                             [checkpoint.has(f"cf_boot_{b0}_{b0 + nb}{tag}", bkey)
+                              for b0, nb in ranges], comm, dev)
+    if have[0]:
         z = checkpoint.load(stage, key)
         y_hat, w_hat, tau_oob = z["y_hat"], z["w_hat"], z["tau_oob"]
     else:
@@ -393,15 +423,14 @@ def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_se
     est, se_aipw = g.mean(), g.std() / math.sqrt(n)      # models/forest.average_treatment_effect
     zeros = torch.zeros_like(g)
     parts = []
-    for b0 in range(0, B, boot_chunk):
-        nb = min(boot_chunk, B - b0)
+    for i, (b0, nb) in enumerate(ranges):
         bst = f"cf_boot_{b0}_{b0 + nb}{tag}"
-        if checkpoint is not None and checkpoint.has(bst, key + f".{boot_seed}"):
-            parts.append(t(checkpoint.load(bst, key + f".{boot_seed}")["taus"]))
+        if have[1 + i]:
+            parts.append(t(checkpoint.load(bst, bkey)["taus"]))
             continue
         tb = bootstrap_replicates(g, zeros, nb, boot_seed, comm, b_start=b0)
         if checkpoint is not None:
-            checkpoint.save(bst, key + f".{boot_seed}", taus=tb.cpu().numpy())
+            checkpoint.save(bst, bkey, taus=tb.cpu().numpy())
         parts.append(tb.to(dev))
     taus = torch.cat(parts)
     v = torch.stack([est, taus.std(unbiased=True), se_aipw]).cpu().numpy()

@@ -330,9 +330,11 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     mine = [k for k in range(K) if k % comm.world_size == comm.rank] if sharded else list(range(K))
     p1 = len(pan.xcols) + 1
 
+    n_rows = int(np.asarray(seg_counts if seg_counts is not None else pan.seg_nreal).sum())
+
     def phase_gram(_):
         if exact:
-            return {"GX": gram(pan, stage="tiles", exact=True)}
+            return {"GX": gram(pan, stage="tiles", exact=True, n_total=n_rows)}
         return {"G": gram(pan, stage="tiles") if G is None else G}
 
     def phase_gram_reduce(st):
@@ -343,8 +345,6 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     def phase_from_limbs(st):
         from ..ops.exact import from_limbs
         return {**st, "G": from_limbs(st["GX"])}
-
-    n_rows = int(np.asarray(seg_counts if seg_counts is not None else pan.seg_nreal).sum())
 
     native_exact = pan.data.is_cuda and pan.dtype == torch.bfloat16
 

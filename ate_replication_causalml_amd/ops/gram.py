@@ -245,8 +245,32 @@ def clear_plans():
 _STAGES = {"all": 3, "tiles": 1, "reduce": 2}
 
 
+EXACT_LIMB_BOUND = 2.0 ** 38   # |Gram entry| bound of the fixed 2^24-scale int64 limbs
+
+
+def check_exact_range(panel: DevicePanel, n_total: int | None = None, w=None):
+    """Raise if the exact mode's fixed-scale limbs could wrap: the hi limb of an entry is
+    floor(v 2^24) summed over chunks in int64, exact only while every |G_jk| < 2^38, and
+    |G_jk| <= max_i |x_ij| max_i |x_ik| * n_total (weighted: times max |w|). ``n_total``:
+    rows over ALL ranks (weak scaling grows it). One reduction over the panel; skipped
+    inside a graph capture (the guard runs on the eager first call of a layout)."""
+    X = panel.data
+    if X.is_cuda and torch.cuda.is_current_stream_capturing():
+        return
+    dims = (0, 2) if panel.blocked else 1                 # no |X| temporary of the panel
+    amax = torch.maximum(X.amax(dim=dims), -X.amin(dim=dims)).double()
+    bound = float(amax.max()) ** 2 * float(n_total or panel.n)
+    if w is not None:
+        bound *= float(w.abs().max())
+    if not bound < EXACT_LIMB_BOUND:
+        raise ValueError(f"exact Gram: entries up to {bound:.3g} exceed the int64 limb range "
+                         f"(2^38 = {EXACT_LIMB_BOUND:.3g}); rescale the columns or use the "
+                         "non-exact mode")
+
+
 def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor | None = None,
-         out: torch.Tensor | None = None, stage: str = "all", exact: bool = False) -> torch.Tensor:
+         out: torch.Tensor | None = None, stage: str = "all", exact: bool = False,
+         n_total: int | None = None) -> torch.Tensor:
     """Per-segment Gram stack [nseg, P, P] (fp64). ``w``: optional row weights (panel order).
 
     stage (paired-tile bf16 Gram): "tiles" launches only the tile kernel (slab partials),
@@ -257,8 +281,11 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     ``exact``: world-size-invariant mode for block-aligned panels (panel.exact_block): one
     row block per chunk and the chunk partials summed as int64 limbs (ops/exact.py);
     returns the limb stack [2, nseg, P, P] (int64): all-reduce it over row shards, then
-    ops.exact.from_limbs gives the same fp64 Gram at every world size."""
+    ops.exact.from_limbs gives the same fp64 Gram at every world size (``n_total``: rows
+    over all ranks, for the limb range check ``check_exact_range``)."""
     X = panel.data
+    if exact and stage != "reduce":
+        check_exact_range(panel, n_total, w)
     if not X.is_cuda:
         if exact:
             return _gram_cpu_exact(panel, w)

@@ -146,7 +146,13 @@ class SegmentedStep:
     step's result is the last phase's state. ``graph_count``: graphs replayed per call;
     ``collectives_captured``: whether collectives sit inside the graphs."""
 
-    def __init__(self, phases, graph: bool, warmup: int = 1, capture_collectives: bool = True):
+    def __init__(self, phases, graph: bool, warmup: int = 1, capture_collectives: bool = True,
+                 agree=None):
+        """``agree(ok: bool) -> bool`` (multi-rank steps): the minimum of ``ok`` over the
+        ranks. The graphs holding collectives are captured WITHOUT replaying them, every
+        rank reports whether its capture succeeded, and only when all did are they replayed;
+        otherwise every rank rebuilds with eager collectives. No collective of the attempt
+        has then run anywhere, so the ranks' collective sequences stay paired."""
         self.raw = list(phases)
         self.fallback_reason = None
         has_cc = any(isinstance(p, Collective) and p.capturable for p in self.raw)
@@ -159,19 +165,34 @@ class SegmentedStep:
         if not graph:
             return
         if capture_collectives and has_cc:
+            ok, err = True, None
             try:
-                self._capture(_fuse(self.raw, fuse_collectives=True))
+                self._capture(_fuse(self.raw, fuse_collectives=True), replay=False)
+            except Exception as e:  # noqa: BLE001 - fall back, but say why
+                ok, err = False, e
+            if agree is not None:
+                ok = bool(agree(ok))
+                if err is None and not ok:
+                    err = RuntimeError("another rank could not capture its collectives")
+            if ok:
+                self()                  # first execution: every rank, same collectives
+                torch.cuda.synchronize()
                 self.collectives_captured = True
                 return
-            except Exception as e:  # noqa: BLE001 - fall back, but say why
-                self.fallback_reason = repr(e)
-                print(f"[graphs] capturing the collectives failed, they run eagerly between "
-                      f"graph segments: {e}", flush=True)
-                torch.cuda.synchronize()
-                self.pins = []
+            self.fallback_reason = repr(err)
+            print(f"[graphs] capturing the collectives failed, they run eagerly between "
+                  f"graph segments: {err}", flush=True)
+            torch.cuda.synchronize()
+            self.phases = _fuse(self.raw)
+            self.graphs = [None] * len(self.phases)
+            self.pins = []
         self._capture(_fuse(self.raw))
 
-    def _capture(self, phases):
+    def _capture(self, phases, replay: bool = True):
+        """Capture every device run of ``phases``. ``replay``: replay each graph right
+        after its capture (capture does not execute) so later eager phases see its
+        outputs; without it, the graphs are only recorded (their outputs' storage is all
+        that later captures need) and the first call executes them."""
         global _pins
         torch.cuda.synchronize()
         graphs = [None] * len(phases)
@@ -192,7 +213,8 @@ class SegmentedStep:
                 _pins = prev
             graphs[i] = (g, out)
             torch.cuda.synchronize()
-            g.replay()          # capture does not execute: produce the state for later phases
+            if replay:
+                g.replay()      # capture does not execute: produce the state for later phases
             state = out
         torch.cuda.synchronize()
         self.phases, self.graphs, self.pins = phases, graphs, pins

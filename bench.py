@@ -234,8 +234,13 @@ def main():
             phases = [in_slot(ph, i) for ph in staggered(
                 dml_phases(pan, args.folds, "min", comm=slot_comms[i], seg_counts=seg_counts,
                            exact=bool(args.exact)), i)]
+            def agree(ok):
+                t = torch.tensor([float(ok)], device=device)
+                comm.all_reduce_min_(t)
+                return bool(t.item())
             try:
-                return SegmentedStep(phases, graph=use_graph), None
+                return SegmentedStep(phases, graph=use_graph,
+                                     agree=agree if world > 1 else None), None
             except Exception as e:  # noqa: BLE001 - reported, then every rank goes eager
                 torch.cuda.synchronize()
                 return SegmentedStep(phases, graph=False, warmup=0), repr(e)

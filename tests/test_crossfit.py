@@ -120,3 +120,26 @@ def test_cf_bootstrap_checkpoint_resume(tmp_path, monkeypatch):
     got = CF.causal_forest_bootstrap(Y, W, X, checkpoint=ck, **kw)
     assert calls["n"] == 2                       # replicate ranges 2 and 3 only
     assert got.ate == want.ate and got.se == want.se
+
+
+def test_cf_bootstrap_resume_ranks_agree(tmp_path):
+    """Two simulated ranks resume a config-4 run in which ONE rank lost its forest and one
+    of its bootstrap ranges (a kill between the ranks' saves): every rank must recompute
+    the same stages (the tree-sharded forest and the all-gathered replicates pair up
+    across ranks), so the run completes and equals the uninterrupted one bit for bit."""
+    from ate_replication_causalml_amd.utils.checkpoint import Checkpoint
+    X, W, Y, _ = _toy(600, 6)
+    kw = dict(num_trees=16, nuisance_trees=8, B=40, device="cpu", boot_chunk=20)
+
+    def fn(comm):
+        ck = Checkpoint(tmp_path, {"cfg": 4})
+        return CF.causal_forest_bootstrap(Y, W, X, checkpoint=ck, comm=comm, **kw)
+
+    want = run_simulated(2, fn)
+    gone = [*tmp_path.glob("cf_fit.r1of2.*.npz"), *tmp_path.glob("cf_boot_20_40.r1of2.*.npz")]
+    assert len(gone) == 2
+    for f in gone:
+        f.unlink()
+    got = run_simulated(2, fn)
+    for a, b in zip(got, want):
+        assert a.ate == b.ate and a.se == b.se

@@ -271,3 +271,17 @@ dist.destroy_process_group()
             assert all(g == want for g in got), (world, got, want)
     finally:
         os.unlink(path)
+
+
+def test_exact_gram_range_guard():
+    """The exact mode's fixed 2^24-scale int64 limbs are exact only while every Gram entry
+    stays below 2^38: data that could wrap them is refused instead of silently summed
+    (the guard bounds |G_jk| by amax_j * amax_k * n_total)."""
+    from ate_replication_causalml_amd.ops.gram import check_exact_range, gram
+    pan = synthetic_panel(1500, p=24, folds=5, seed=3, dtype="f64", device="cpu", align=64)
+    check_exact_range(pan, n_total=pan.n)                       # tutorial-scale data: fine
+    with pytest.raises(ValueError, match="limb range"):
+        check_exact_range(pan, n_total=10 ** 12)                # weak scaling to 1e12 rows
+    pan.data[3, 7] = 1e5                                        # one large entry
+    with pytest.raises(ValueError, match="limb range"):
+        gram(pan, exact=True)
