@@ -289,7 +289,11 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ __attribute__((aligned(16))) CT sdelta2[NP * PER];
   __shared__ int scl[64];                 // wave 0: changed coordinates of the block
   __shared__ CT scd[64];
-  __shared__ __attribute__((aligned(16))) float sCn[64 * 64];     // next block's diagonal block
+  // diagonal blocks, double-buffered: sCn2[cpar] holds the block of the visit in progress
+  // (wave 0 loads it into registers at the start of its recurrence), the pull waves DMA the
+  // next visited block's into sCn2[cpar ^ 1]. Keeping the recurrence's registers out of the
+  // loop-carried state leaves the pull waves' code the whole register budget (no spills).
+  __shared__ __attribute__((aligned(16))) float sCn2[2][64 * 64];
   __shared__ __attribute__((aligned(16))) float sCorr[64 * 64];   // C[t rows][tn cols] (fp32 C)
   __shared__ __attribute__((aligned(16))) float sdall[64];         // wave 0: block t's deltas
   __shared__ int svis[8], snv, sblk_any[8];
@@ -336,6 +340,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   typedef typename VecT<CT>::type V;
   constexpr int W = sizeof(V) / sizeof(CT);
   float dg_lo[32], dg_hi[32];
+  int cpar = 0;                            // sCn2 buffer of the current visit's block
 
   // bring block t's gradient up to date (all waves); stage its diagonal block.
   // By symmetry coordinate j's contribution is the contiguous row segment C[j][t*64 .. +63].
@@ -456,27 +461,20 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #ifdef ENET_PROF
     if (lane == 0) sprof[wid][5] += (unsigned long long)cnt;
 #endif
-    // wave 0 (the recurrence) keeps its lane's row of the 64x64 diagonal block in
-    // registers: dg_lo[i] / dg_hi[i-32] = C[t*64+lane][t*64+i] (uniform-index reads
-    // lower to s_set_gpr_idx, no LDS or memory latency on the update chain)
-    if (wid == 0) {
-      const int r = t * 64 + lane;
-      if (r < p) {
-        const V* rowv = reinterpret_cast<const V*>(Cq + (int64_t)r * ldc + t * 64);
-#pragma unroll
-        for (int c = 0; c < 32 / W; ++c) {
-          const V a = rowv[c], b = rowv[c + 32 / W];
-          const CT* ea = reinterpret_cast<const CT*>(&a);
-          const CT* eb = reinterpret_cast<const CT*>(&b);
-#pragma unroll
-          for (int e2 = 0; e2 < W; ++e2) {
-            dg_lo[c * W + e2] = (float)ea[e2];
-            dg_hi[c * W + e2] = (float)eb[e2];
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 32; ++c) { dg_lo[c] = 0.f; dg_hi[c] = 0.f; }
+    // block t's 64x64 diagonal block -> sCn2[cpar] (wave 0 moves it into registers at the
+    // start of the visit): sCn2[i * 64 + c] = C[t*64 + i][t*64 + c]. Rows >= p are clamped
+    // (fp32, finite) or zero (fp64): they only ever multiply the step of a coordinate >= p,
+    // which is 0.
+    if constexpr (sizeof(CT) == 4) {
+      for (int pc = wid; pc < 16; pc += NW) {
+        const int i = pc * 4 + (lane >> 4);
+        const int r = min(t * 64 + i, p - 1);
+        glds16f(Cq + (int64_t)r * ldc + t * 64 + (lane & 15) * 4, &sCn2[cpar][0] + pc * 256);
+      }
+    } else {
+      for (int i = wid; i < 64; i += NW) {
+        const int r = t * 64 + i;
+        sCn2[cpar][i * 64 + lane] = r < p ? (float)Cq[(int64_t)r * ldc + t * 64 + lane] : 0.f;
       }
     }
     spart2[0][wid][lane] = (double)acc;
@@ -511,7 +509,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         const int i = (pc & 15) * 4 + (lane >> 4);
         const int r = min(blk * 64 + i, p - 1);
         const CT* src = Cq + (int64_t)r * ldc + tn * 64 + (lane & 15) * 4;
-        float* dst = (pc < 16 ? sCn : sCorr) + (pc & 15) * 256;
+        float* dst = (pc < 16 ? &sCn2[cpar ^ 1][0] : sCorr) + (pc & 15) * 256;
         glds16f(src, dst);
       }
       // every column block but tn (its own changes are in g_tn already); block t's changes
@@ -575,7 +573,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #pragma unroll
     for (int ii = 0; ii < NR; ++ii) {
       const int i = my + NP * ii;
-      if (i < 64) sCn[i * 64 + lane] = dr[ii];
+      if (i < 64) sCn2[cpar ^ 1][i * 64 + lane] = dr[ii];
     }
   };
 
@@ -641,6 +639,13 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       // LDS latency hides under the recurrence
       double dc0 = 0.0, ds0 = 0.0;
       if (wid == 0) {
+        // this block's diagonal row into registers (deposited by the last visit's DMA or
+        // by pull()): dg_lo[i] / dg_hi[i-32] = C[t*64+lane][t*64+i]
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          dg_lo[i] = sCn2[cpar][i * 64 + lane];
+          dg_hi[i] = sCn2[cpar][(i + 32) * 64 + lane];
+        }
         dc0 = sdc[k];
         ds0 = sds[t][k];
         gt = sg[k];
@@ -896,13 +901,6 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           if constexpr (sizeof(CT) == 4) {
             if (lane == 0) scorr_ok[vpar] = schg;
           }
-          // rows >= p of the DMA'd block are clamped (finite) copies: dg_*[i] only ever
-          // multiplies the step of coordinate i, which is 0 for coordinates >= p
-#pragma unroll
-          for (int i = 0; i < 32; ++i) {
-            dg_lo[i] = sCn[i * 64 + lane];
-            dg_hi[i] = sCn[(i + 32) * 64 + lane];
-          }
         }
 #ifdef ENET_PROF
         if (lane == 0) sprof[wid][9] += (unsigned long long)(wall_clock64() - tb_);
@@ -931,6 +929,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #endif
       }
       __syncthreads();
+      if (tn >= 0) cpar ^= 1;              // tn's diagonal block is in the other buffer
       PROF_T(tc_);
       PROF_ADD(0, tc_ - tb_);
     }
