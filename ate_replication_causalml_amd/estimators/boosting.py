@@ -163,6 +163,14 @@ def bin_panel(pan, edges=None, edge_rows=G.EDGE_SAMPLE, dist=None):
         edges = panel_bin_edges(pan, rows, dist, edge_rows)
     ldr = -(-p // 32) * 32
     Xr = torch.zeros((n, ldr), dtype=torch.uint8, device=dev)
+    if dev.type != "cuda":
+        # host twin of gbdt_bin_panel_kernel: bin(x) = #{edges < x} (lower bound)
+        Xc = pan.colmajor()
+        for j, c in enumerate(pan.xcols):
+            e = torch.as_tensor(edges[0][j, :int(edges[1][j])], dtype=torch.float64)
+            Xr[:, j] = torch.searchsorted(e, Xc[c].index_select(0, rows).double().contiguous(),
+                                          right=False).to(torch.uint8)
+        return Xr, ldr, edges, rows
     code = {torch.bfloat16: 0, torch.float32: 1}[X.dtype]
     t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
     e, ne = t(edges[0], torch.float64), t(edges[1], torch.int32)

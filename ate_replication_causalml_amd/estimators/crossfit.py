@@ -130,12 +130,12 @@ class _JobCache:
     def stage(self, j):
         return f"aipw_fold{j // 3}_{_NAMES[j % 3]}{self.tag}"
 
-    def load(self, j, dev):
-        return torch.as_tensor(self.ck.load(self.stage(j), self.key)["pred"], device=dev)
+    def load(self, j, dev, field="pred"):
+        return torch.as_tensor(self.ck.load(self.stage(j), self.key)[field], device=dev)
 
-    def save(self, j, pred):
+    def save(self, j, arr, field="pred"):
         if self.ck is not None:
-            self.ck.save(self.stage(j), self.key, pred=pred.detach().cpu().numpy())
+            self.ck.save(self.stage(j), self.key, **{field: arr.detach().cpu().numpy()})
 
 
 def aipw_score(Y, W, e, mu1, mu0, clip=0.01):
@@ -251,15 +251,20 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     predict the held-out fold's bins; the AIPW scores and their mean / sd are computed in
     fp64 on the device.
 
-    Trees are sharded over ``comm`` (every rank holds all binned rows and grows its share
-    of every forest; the held-out vote sums are all-reduced, C05), or over a simulated
-    ``tree_shard=(rank, world)`` on one device (the per-GPU work of a multi-GPU run;
-    the ATE is then that of the shard's trees). ``concurrent``: the 3K forests grow side
-    by side on separate streams, in batches that fit free HBM (a forest of T trees fills
-    only T CUs).
-    ``engine="cpu"`` grows the same forests on the host engine from the same device bins
-    (bit-identical trees; the parity test). ``checkpoint`` + ``data_key`` (a name of the
-    panel's data): per (fold, nuisance) held-out predictions saved / resumed."""
+    Trees are sharded over ``comm`` (one rank per GPU, every rank holding all binned rows
+    and growing its share of every forest), or over a simulated ``tree_shard=(rank,
+    world)`` on one device (the per-GPU work of a multi-GPU run; the ATE is then that of
+    the shard's trees). At every world size each forest leaves only its LOCAL held-out vote
+    sums (prediction phase 1, csrc/forest.hip); after all 3K forests, the sums of every
+    job are packed into ONE buffer and all-reduced once (C05), then divided by the tree
+    counts (= forest_final_kernel). Votes are integers, so the predictions -- and the ATE
+    and SE -- are the same bits at every world size. ``concurrent``: the 3K forests grow
+    side by side on separate streams, in batches that fit free HBM (a forest of T trees
+    fills only T CUs), at every world size.
+    ``engine="cpu"`` grows the same forests on the host engine from the same bins
+    (bit-identical trees; the parity test). ``checkpoint`` (+ ``data_key``, a name of the
+    panel's data; a sample of the panel is hashed too): each job's local vote sums are
+    saved per rank; a rerun loads them and grows only the missing forests."""
     from .boosting import bin_panel
     dev = pan.device
     K = pan.nseg
@@ -280,37 +285,37 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
         rank, world = 0, 1
     t0, cnt = F.tree_shard(num_trees, 1, rank, world)
     pcomm = comm if comm is not None and comm.world_size > 1 else None
-    e = torch.empty(n, dtype=torch.float64, device=dev)
-    mu1 = torch.empty_like(e)
-    mu0 = torch.empty_like(e)
     ar = torch.arange(n, device=dev)
     tag = "" if pcomm is None else f".r{rank}of{world}"
     key = _panel_key(pan, data_key, n, p, num_trees, seed, t0, cnt) \
         if checkpoint is not None else ""
     cache = _JobCache(checkpoint, key, tag, pcomm, dev, 3 * K)
+    # job j = 3k + {0: e (W on the other folds), 1: mu1 (Y, treated), 2: mu0 (Y, control)};
+    # its local sums live at pack[off_j : off_j + 2 nho_k] (votes, then trees counted)
+    off = np.concatenate([[0], np.cumsum([2 * int(nr[j // 3]) for j in range(3 * K)])])
+    pack = torch.zeros(int(off[-1]), dtype=torch.float64, device=dev)
     jobs = []
     for k in range(K):
         a, b = int(c0[k]), int(c0[k + 1])
         tr = (ar < a) | (ar >= b)
         sd = seed + 1000 * (k + 1)
-        jobs += [(e, tr, W, sd, a, b, 3 * k), (mu1, tr & (W == 1), Y, sd + 1, a, b, 3 * k + 1),
-                 (mu0, tr & (W == 0), Y, sd + 2, a, b, 3 * k + 2)]
+        for j, (mask, target, s_) in enumerate(((tr, W, sd), (tr & (W == 1), Y, sd + 1),
+                                               (tr & (W == 0), Y, sd + 2))):
+            jobs.append((mask, target, s_, a, b, 3 * k + j))
     todo = []
-    for jb in jobs:                          # finished jobs of an earlier run: load them
-        if jb[-1] in cache.done:
-            jb[0][jb[4]:jb[5]] = cache.load(jb[-1], dev)
+    for jb in jobs:                          # finished jobs of an earlier run: their sums
+        j = jb[-1]
+        if j in cache.done:
+            pack[off[j]:off[j + 1]] = cache.load(j, dev, "sums")
         else:
             todo.append(jb)
-    jobs = todo
-
     # training rows of every job, computed here on the caller's stream: a lookback-free
     # compaction (ops/scan.py) and never inside the side-by-side forests below, where
     # torch.nonzero's spinning workgroups stalled the shard (profiles/r03_cfg3b)
-    jobs = [(out, compact_rows(mask), target, sd, a, b, j)
-            for out, mask, target, sd, a, b, j in jobs]
+    jobs = [(compact_rows(mask), target, sd, a, b, j) for mask, target, sd, a, b, j in todo]
 
     def run(job):
-        out, idx, target, sd, a, b, j = job
+        idx, target, sd, a, b, j = job
         yt = target.index_select(0, idx)
         binary = bool(((yt == 0) | (yt == 1)).all())
         kw = dict(y=yt) if binary else dict(r1=yt, min_node=5, mtry=max(1, p // 3))
@@ -321,12 +326,15 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
                                  ntree=cnt, seed=sd, tree_offset=t0, **kw)
         del Xt
         Xho = Xb[:, a:b].contiguous()
-        pred = F.predict_tree_parallel(fr, pcomm, Xb=Xho, host=False) if pcomm is not None \
-            else fr.predict_binned(Xho, host=False)
-        out[a:b] = torch.as_tensor(pred, device=dev)
-        cache.save(j, out[a:b])
+        if fr.backend == "cpu":
+            Xho = Xho.cpu().numpy()
+        st = fr.new_state(b - a)
+        fr.predict_state(Xho, False, st, phases=1)          # this rank's trees only
+        loc = torch.as_tensor(st[:2 * (b - a)], device=dev)
+        pack[off[j]:off[j + 1]] = loc
+        cache.save(j, loc, "sums")
 
-    if concurrent and dev.type == "cuda" and pcomm is None and engine == "gpu":
+    if concurrent and dev.type == "cuda" and engine == "gpu" and len(jobs) > 1:
         # the 3K forests are independent: grow them side by side (one stream per host
         # thread; a forest of T trees fills only T CUs), in batches whose working set
         # (training bins + node arrays + growth scratch) fits a share of free HBM
@@ -334,7 +342,7 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
         lib = _native.hip()
 
         def need(job):
-            nt = job[1].numel()
+            nt = job[0].numel()
             base = p * nt + cnt * (2 * nt + 1) * 20 + cnt * nt      # bins, trees, in-bag
             if F.LEVEL_MIN_ROWS <= nt:
                 # level engine: row-major copy, weights / positions, level lists
@@ -370,6 +378,19 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     else:
         for job in jobs:
             run(job)
+    if pcomm is not None:
+        pcomm.all_reduce_(pack)              # C05: every job's vote sums, one collective
+    e = torch.empty(n, dtype=torch.float64, device=dev)
+    mu1 = torch.empty_like(e)
+    mu0 = torch.empty_like(e)
+    for j in range(3 * K):
+        k = j // 3
+        a, b = int(c0[k]), int(c0[k + 1])
+        s_ = pack[off[j]:off[j + 1]]
+        votes, used = s_[:b - a], s_[b - a:]
+        # forest_final_kernel: votes / trees (NaN for a row no tree reached)
+        (e, mu1, mu0)[j % 3][a:b] = torch.where(used > 0, votes / used,
+                                                torch.full_like(votes, float("nan")))
     tau, se, ec = aipw_score(Y, W, e, mu1, mu0, clip)
     v = torch.stack([tau, se, ec.min(), ec.max()]).cpu().numpy()
     return AteResult.make(method, float(v[0]), float(v[1]), n=n, trees=num_trees,
