@@ -75,3 +75,23 @@ def test_exact_mode_two_ranks_on_one_gpu_bitwise(gpu):
     ref = _json(one.stdout)
     assert two["exact"] and ref["exact"] and two["n_gpus"] == 2
     assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)
+
+
+def test_cfg3_rf_two_ranks_on_one_gpu_bitwise(gpu):
+    """Config 3's tree-parallel RF cross-fit (tools/cfg3.py) with two ranks sharing the GPU
+    (gloo collectives): each rank grows its half of the 15 forests side by side, the local
+    vote sums are all-reduced once -> the SAME BITS as one process growing every tree."""
+    cfg3 = os.path.join(ROOT, "tools", "cfg3.py")
+    args = ["--rows", "300000", "--cols", "40", "--trees", "8"]
+    env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29661",
+                        cfg3, *args], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = _json(r.stdout)
+    one = subprocess.run([sys.executable, cfg3, *args], capture_output=True, text=True,
+                         timeout=240)
+    assert one.returncode == 0, one.stderr[-3000:]
+    ref = _json(one.stdout)
+    assert two["world"] == 2 and ref["world"] == 1 and two["trees_this_rank"] == 4
+    assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)
