@@ -293,7 +293,7 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
     # job j = 3k + {0: e (W on the other folds), 1: mu1 (Y, treated), 2: mu0 (Y, control)};
     # its local sums live at pack[off_j : off_j + 2 nho_k] (votes, then trees counted)
     off = np.concatenate([[0], np.cumsum([2 * int(nr[j // 3]) for j in range(3 * K)])])
-    pack = torch.zeros(int(off[-1]), dtype=torch.float64, device=dev)
+    pack = torch.zeros(int(off[-1]), dtype=torch.int64, device=dev)   # fixed-point sums
     jobs = []
     for k in range(K):
         a, b = int(c0[k]), int(c0[k + 1])
@@ -387,7 +387,8 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
         k = j // 3
         a, b = int(c0[k]), int(c0[k + 1])
         s_ = pack[off[j]:off[j + 1]]
-        votes, used = s_[:b - a], s_[b - a:]
+        votes = s_[:b - a].double() / F.FIX           # from_fix: 2^-32 fixed point
+        used = s_[b - a:].double()
         # forest_final_kernel: votes / trees (NaN for a row no tree reached)
         (e, mu1, mu0)[j % 3][a:b] = torch.where(used > 0, votes / used,
                                                 torch.full_like(votes, float("nan")))

@@ -246,9 +246,12 @@ class Forest:
         return self.predict_state(Xb, oob, state, phases=7)
 
     def new_state(self, n2):
+        """Prediction accumulators [10, n2]: int64 sums of per-tree terms in 2^-32 fixed
+        point (csrc/forest_common.hpp mean_fix) -- exact and order-free, so tree-parallel
+        ranks all-reduce them to the single-device bits."""
         if self.backend == "gpu":
-            return torch.zeros(10 * n2, dtype=torch.float64, device=self.device)
-        return np.zeros(10 * n2)
+            return torch.zeros(10 * n2, dtype=torch.int64, device=self.device)
+        return np.zeros(10 * n2, dtype=np.int64)
 
     def predict_state(self, Xb, oob, state, phases, host=True):
         """Run prediction phases (1: per-tree sums, 2: little-bag group sums, 4: finalise)
@@ -668,7 +671,9 @@ def fit_forest_sharded(X, kind, ntree, comm, group=1, **kw) -> Forest:
 
 def predict_tree_parallel(forest: Forest, comm, X=None, oob=False, Xb=None, host=True):
     """Forest prediction with trees sharded over ranks: all-reduce the per-tree sums
-    (C05), then (causal forests) the little-bag group sums, then finalise locally.
+    (C05), then (causal forests) the little-bag group sums, then finalise locally. The
+    sums are int64 fixed point (``Forest.new_state``): every world size gives the same
+    bits as one device growing all the trees.
     ``Xb``: already binned rows (column-major uint8 [p][n2]) instead of ``X``.
     ``host=False`` (GPU forests): the predictions stay a device tensor."""
     if Xb is None:

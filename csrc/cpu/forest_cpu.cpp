@@ -424,9 +424,10 @@ ATECPU_API int atecpu_forest_fit(const ForestParams* fpp, const uint8_t* Xb, con
 template <typename BT>
 static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, int cap,
                         const int32_t* feat, const int32_t* thr, const int32_t* left,
-                        const double* val, const uint8_t* inbag, const int64_t* est, double* state,
+                        const double* val, const uint8_t* inbag, const int64_t* est, int64_t* state,
                         int phases, double* out, int nthreads) {
-  // state: [10][n2] accumulators, same protocol as csrc/forest.hip ate_forest_predict
+  // state: [10][n2] int64 accumulators (2^-32 fixed point, forest_common.hpp mean_fix),
+  // same protocol as csrc/forest.hip ate_forest_predict
   // (1 = per-tree sums, 2 = kind-2 little-bag group sums, 4 = finalise).
   const ForestParams fp = *fpp;
 #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
@@ -443,29 +444,28 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
       }
       return base + (fp.sampling == 1 && est ? last_ok : v);
     };
-    double* st = state;
+    int64_t* st = state;
     if (phases & 1) {
       if (fp.kind != 2) {
-        double acc = st[i], used = st[n2 + i];
+        int64_t acc = st[i], used = st[n2 + i];
         for (int t = 0; t < fp.ntree; ++t) {
           const int64_t nd = leaf_of(t);
           if (nd < 0) continue;
-          used += 1.0;
-          if (fp.kind == 0 || fp.sampling == 0) acc += val[nd];
-          else acc += from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
+          used += 1;
+          if (fp.kind == 0 || fp.sampling == 0) acc += to_fix(val[nd]);
+          else acc += mean_fix(est[nd * 5 + 1], est[nd * 5]);
         }
         st[i] = acc;
         st[n2 + i] = used;
       } else {
-        double a1 = st[i], aw = st[n2 + i], ay = st[2 * n2 + i], aww = st[3 * n2 + i],
-               awy = st[4 * n2 + i];
+        int64_t a1 = st[i], aw = st[n2 + i], ay = st[2 * n2 + i], aww = st[3 * n2 + i],
+                awy = st[4 * n2 + i];
         for (int t = 0; t < fp.ntree; ++t) {
           const int64_t nd = leaf_of(t);
           if (nd < 0) continue;
           const int64_t* e = est + nd * 5;
-          const double c = (double)e[0];
-          a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
-          aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
+          a1 += 1; aw += mean_fix(e[1], e[0]); ay += mean_fix(e[2], e[0]);
+          aww += mean_fix(e[3], e[0]); awy += mean_fix(e[4], e[0]);
         }
         st[i] = a1; st[n2 + i] = aw; st[2 * n2 + i] = ay; st[3 * n2 + i] = aww;
         st[4 * n2 + i] = awy;
@@ -474,13 +474,13 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
     if ((phases & 2) && fp.kind == 2 && st[i] > 0) {
       // little bags: linearised score psi = (w - Wbar)(y - Ybar - tau (w - Wbar)) per
       // group at the full-forest tau
-      const double a1 = st[i];
-      const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
-      const double H = st[3 * n2 + i] / a1 - wb * wb;
+      const double a1 = (double)st[i];
+      const double wb = from_fix(st[n2 + i]) / a1, yb = from_fix(st[2 * n2 + i]) / a1;
+      const double H = from_fix(st[3 * n2 + i]) / a1 - wb * wb;
       if (H > 0) {
-        const double tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
-        double gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
-        double nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
+        const double tau = (from_fix(st[4 * n2 + i]) / a1 - wb * yb) / H;
+        int64_t gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
+        int64_t nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
         for (int g0 = 0; g0 < fp.ntree; g0 += fp.group) {
           double ps = 0, pss = 0;
           int nb = 0;
@@ -488,16 +488,15 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
             const int64_t nd = leaf_of(t);
             if (nd < 0) continue;
             const int64_t* e = est + nd * 5;
-            const double c = (double)e[0];
-            const double w_ = from_fix(e[1]) / c, y_ = from_fix(e[2]) / c;
-            const double ww = from_fix(e[3]) / c, wy = from_fix(e[4]) / c;
+            const double w_ = from_fix(mean_fix(e[1], e[0])), y_ = from_fix(mean_fix(e[2], e[0]));
+            const double ww = from_fix(mean_fix(e[3], e[0])), wy = from_fix(mean_fix(e[4], e[0]));
             const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
             ps += psi; pss += psi * psi; ++nb;
           }
           if (nb == 0) continue;
           const double pg = ps / nb;
-          gs += pg; gss += pg * pg; ng += 1.0;
-          if (nb >= 2) { within += pss / nb - pg * pg; nwithin += 1.0; }
+          gs += to_fix(pg); gss += to_fix(pg * pg); ng += 1;
+          if (nb >= 2) { within += to_fix(pss / nb - pg * pg); nwithin += 1; }
         }
         st[5 * n2 + i] = gs; st[6 * n2 + i] = gss; st[7 * n2 + i] = within;
         st[8 * n2 + i] = nwithin; st[9 * n2 + i] = ng;
@@ -505,22 +504,22 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
     }
     if (phases & 4) {
       if (fp.kind != 2) {
-        out[i] = st[n2 + i] > 0 ? st[i] / st[n2 + i] : NAN;
+        out[i] = st[n2 + i] > 0 ? from_fix(st[i]) / (double)st[n2 + i] : NAN;
         continue;
       }
-      const double a1 = st[i];
+      const double a1 = (double)st[i];
       double tau = NAN, var = NAN;
-      const double ng = st[9 * n2 + i];
+      const double ng = (double)st[9 * n2 + i];
       if (a1 > 0) {
-        const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
-        const double H = st[3 * n2 + i] / a1 - wb * wb;
+        const double wb = from_fix(st[n2 + i]) / a1, yb = from_fix(st[2 * n2 + i]) / a1;
+        const double H = from_fix(st[3 * n2 + i]) / a1 - wb * wb;
         if (H > 0) {
-          tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
+          tau = (from_fix(st[4 * n2 + i]) / a1 - wb * yb) / H;
           if (ng >= 2) {
-            const double mean = st[5 * n2 + i] / ng;
-            const double between = st[6 * n2 + i] / ng - mean * mean;
-            const double nw = st[8 * n2 + i];
-            const double wc = nw > 0 ? st[7 * n2 + i] / nw / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
+            const double mean = from_fix(st[5 * n2 + i]) / ng;
+            const double between = from_fix(st[6 * n2 + i]) / ng - mean * mean;
+            const double nw = (double)st[8 * n2 + i];
+            const double wc = nw > 0 ? from_fix(st[7 * n2 + i]) / nw / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
             var = std::fmax(between - wc, 0.0) / (H * H);
           }
         }
@@ -537,7 +536,7 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
 ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb, int n2, int oob,
                                      int cap, const int32_t* feat, const int32_t* thr,
                                      const int32_t* left, const double* val,
-                                     const uint8_t* inbag, const int64_t* est, double* state,
+                                     const uint8_t* inbag, const int64_t* est, int64_t* state,
                                      int phases, double* out, int nthreads) {
   return predict_impl(fpp, Xb, n2, oob, cap, feat, thr, left, val, inbag, est, state, phases, out,
                       nthreads);
@@ -547,7 +546,7 @@ ATECPU_API int atecpu_forest_predict(const ForestParams* fpp, const uint8_t* Xb,
 ATECPU_API int atecpu_forest_predict16(const ForestParams* fpp, const uint16_t* Xb, int n2, int oob,
                                        int cap, const int32_t* feat, const int32_t* thr,
                                        const int32_t* left, const double* val,
-                                       const uint8_t* inbag, const int64_t* est, double* state,
+                                       const uint8_t* inbag, const int64_t* est, int64_t* state,
                                        int phases, double* out, int nthreads) {
   return predict_impl(fpp, Xb, n2, oob, cap, feat, thr, left, val, inbag, est, state, phases, out,
                       nthreads);

@@ -774,64 +774,64 @@ __global__ __launch_bounds__(256) void forest_leaf16_kernel(ForestParams fp,
   *out = v;
 }
 
-// kind 0/1: running (sum, count) per row over trees in ascending order
+// kind 0/1: running (sum, count) per row over trees in ascending order; per-tree values
+// in 2^-32 fixed point, int64 sums (forest_common.hpp mean_fix)
 __global__ __launch_bounds__(256) void forest_vote_kernel(ForestParams fp, int n2, int cap, int t0,
                                                           int nt, const int32_t* __restrict__ leaves,
                                                           const double* __restrict__ val,
                                                           const int64_t* __restrict__ est,
-                                                          double* __restrict__ state) {
+                                                          int64_t* __restrict__ state) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n2) return;
-  double acc = state[i], used = state[n2 + i];
+  int64_t acc = state[i], used = state[n2 + i];
   const bool leafmean = fp.kind == 0 || fp.sampling == 0;
 #pragma unroll 4
   for (int tt = 0; tt < nt; ++tt) {
     const int lf = leaves[(int64_t)tt * n2 + i];
     if (lf < 0) continue;
     const int64_t nd = (int64_t)(t0 + tt) * cap + lf;
-    used += 1.0;
-    acc += leafmean ? val[nd] : from_fix(est[nd * 5 + 1]) / (double)est[nd * 5];
+    used += 1;
+    acc += leafmean ? to_fix(val[nd]) : mean_fix(est[nd * 5 + 1], est[nd * 5]);
   }
   state[i] = acc;
   state[n2 + i] = used;
 }
 
-// kind 2, pass 1: forest-weighted leaf moments (1, W, Y, WW, WY)
+// kind 2, pass 1: forest-weighted leaf moments (1, W, Y, WW, WY), fixed-point terms
 __global__ __launch_bounds__(256) void forest_cate1_kernel(int n2, int cap, int t0, int nt,
                                                            const int32_t* __restrict__ leaves,
                                                            const int64_t* __restrict__ est,
-                                                           double* __restrict__ st) {
+                                                           int64_t* __restrict__ st) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n2) return;
-  double a1 = st[i], aw = st[n2 + i], ay = st[2 * n2 + i], aww = st[3 * n2 + i],
-         awy = st[4 * n2 + i];
+  int64_t a1 = st[i], aw = st[n2 + i], ay = st[2 * n2 + i], aww = st[3 * n2 + i],
+          awy = st[4 * n2 + i];
   for (int tt = 0; tt < nt; ++tt) {
     const int lf = leaves[(int64_t)tt * n2 + i];
     if (lf < 0) continue;
     const int64_t* e = est + ((int64_t)(t0 + tt) * cap + lf) * 5;
-    const double c = (double)e[0];
-    a1 += 1; aw += from_fix(e[1]) / c; ay += from_fix(e[2]) / c;
-    aww += from_fix(e[3]) / c; awy += from_fix(e[4]) / c;
+    a1 += 1; aw += mean_fix(e[1], e[0]); ay += mean_fix(e[2], e[0]);
+    aww += mean_fix(e[3], e[0]); awy += mean_fix(e[4], e[0]);
   }
   st[i] = a1; st[n2 + i] = aw; st[2 * n2 + i] = ay; st[3 * n2 + i] = aww; st[4 * n2 + i] = awy;
 }
 
 // kind 2, pass 2: little-bag groups of the linearised score psi at the full-forest tau
-// (chunks hold whole groups). st[5..9]: gs, gss, within, nwithin, ng.
+// (chunks hold whole groups). st[5..9]: gs, gss, within (fixed point), nwithin, ng.
 __global__ __launch_bounds__(256) void forest_cate2_kernel(ForestParams fp, int n2, int cap, int t0,
                                                            int nt, const int32_t* __restrict__ leaves,
                                                            const int64_t* __restrict__ est,
-                                                           double* __restrict__ st) {
+                                                           int64_t* __restrict__ st) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n2) return;
-  const double a1 = st[i];
+  const double a1 = (double)st[i];
   if (!(a1 > 0)) return;
-  const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
-  const double H = st[3 * n2 + i] / a1 - wb * wb;
+  const double wb = from_fix(st[n2 + i]) / a1, yb = from_fix(st[2 * n2 + i]) / a1;
+  const double H = from_fix(st[3 * n2 + i]) / a1 - wb * wb;
   if (!(H > 0)) return;
-  const double tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
-  double gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
-  double nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
+  const double tau = (from_fix(st[4 * n2 + i]) / a1 - wb * yb) / H;
+  int64_t gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
+  int64_t nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
   for (int g0 = 0; g0 < nt; g0 += fp.group) {
     double ps = 0, pss = 0;
     int nb = 0;
@@ -839,43 +839,42 @@ __global__ __launch_bounds__(256) void forest_cate2_kernel(ForestParams fp, int 
       const int lf = leaves[(int64_t)tt * n2 + i];
       if (lf < 0) continue;
       const int64_t* e = est + ((int64_t)(t0 + tt) * cap + lf) * 5;
-      const double c = (double)e[0];
-      const double w_ = from_fix(e[1]) / c, y_ = from_fix(e[2]) / c;
-      const double ww = from_fix(e[3]) / c, wy = from_fix(e[4]) / c;
+      const double w_ = from_fix(mean_fix(e[1], e[0])), y_ = from_fix(mean_fix(e[2], e[0]));
+      const double ww = from_fix(mean_fix(e[3], e[0])), wy = from_fix(mean_fix(e[4], e[0]));
       const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
       ps += psi; pss += psi * psi; ++nb;
     }
     if (nb == 0) continue;
     const double pg = ps / nb;
-    gs += pg; gss += pg * pg; ng += 1.0;
-    if (nb >= 2) { within += pss / nb - pg * pg; nwithin += 1.0; }
+    gs += to_fix(pg); gss += to_fix(pg * pg); ng += 1;
+    if (nb >= 2) { within += to_fix(pss / nb - pg * pg); nwithin += 1; }
   }
   st[5 * n2 + i] = gs; st[6 * n2 + i] = gss; st[7 * n2 + i] = within;
   st[8 * n2 + i] = nwithin; st[9 * n2 + i] = ng;
 }
 
 __global__ __launch_bounds__(256) void forest_final_kernel(ForestParams fp, int n2,
-                                                           const double* __restrict__ st,
+                                                           const int64_t* __restrict__ st,
                                                            double* __restrict__ out) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n2) return;
   if (fp.kind != 2) {
-    out[i] = st[n2 + i] > 0 ? st[i] / st[n2 + i] : NAN;
+    out[i] = st[n2 + i] > 0 ? from_fix(st[i]) / (double)st[n2 + i] : NAN;
     return;
   }
-  const double a1 = st[i];
+  const double a1 = (double)st[i];
   double tau = NAN, var = NAN;
-  const double ng = st[9 * n2 + i];
+  const double ng = (double)st[9 * n2 + i];
   if (a1 > 0) {
-    const double wb = st[n2 + i] / a1, yb = st[2 * n2 + i] / a1;
-    const double H = st[3 * n2 + i] / a1 - wb * wb;
+    const double wb = from_fix(st[n2 + i]) / a1, yb = from_fix(st[2 * n2 + i]) / a1;
+    const double H = from_fix(st[3 * n2 + i]) / a1 - wb * wb;
     if (H > 0) {
-      tau = (st[4 * n2 + i] / a1 - wb * yb) / H;
+      tau = (from_fix(st[4 * n2 + i]) / a1 - wb * yb) / H;
       if (ng >= 2) {
-        const double mean = st[5 * n2 + i] / ng;
-        const double between = st[6 * n2 + i] / ng - mean * mean;
-        const double nw = st[8 * n2 + i];
-        const double wc = nw > 0 ? st[7 * n2 + i] / nw / (double)(fp.group > 1 ? fp.group - 1 : 1)
+        const double mean = from_fix(st[5 * n2 + i]) / ng;
+        const double between = from_fix(st[6 * n2 + i]) / ng - mean * mean;
+        const double nw = (double)st[8 * n2 + i];
+        const double wc = nw > 0 ? from_fix(st[7 * n2 + i]) / nw / (double)(fp.group > 1 ? fp.group - 1 : 1)
                                  : 0.0;
         var = fmax(between - wc, 0.0) / (H * H);
       }
@@ -899,7 +898,7 @@ ATE_API int ate_forest_pack(const void* fpp, int cap, const void* feat, const vo
   return 0;
 }
 
-// state: [10][n2] fp64 accumulators (zeroed by the caller before phase 1); leaves:
+// state: [10][n2] int64 accumulators (zeroed by the caller before phase 1); leaves:
 // [tchunk][n2] int32 scratch, tchunk a multiple of the little-bag group size. Trees are
 // visited in ascending order, so the sums match the host engine's sequential loop.
 // phases (bitmask): 1 = per-tree sums (kind 0/1 votes, kind 2 leaf moments),
@@ -920,18 +919,18 @@ static int forest_predict_impl(const ForestParams& fp, int n2, int cap, const vo
       if (fp.kind != 2)
         hipLaunchKernelGGL(forest_vote_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
                            (const int32_t*)leaves, (const double*)val, (const int64_t*)est,
-                           (double*)state);
+                           (int64_t*)state);
       else if (pass == 0)
         hipLaunchKernelGGL(forest_cate1_kernel, dim3(rb), dim3(256), 0, st, n2, cap, t0, nt,
-                           (const int32_t*)leaves, (const int64_t*)est, (double*)state);
+                           (const int32_t*)leaves, (const int64_t*)est, (int64_t*)state);
       else
         hipLaunchKernelGGL(forest_cate2_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
-                           (const int32_t*)leaves, (const int64_t*)est, (double*)state);
+                           (const int32_t*)leaves, (const int64_t*)est, (int64_t*)state);
     }
   }
   if (phases & 4)
     hipLaunchKernelGGL(forest_final_kernel, dim3(rb), dim3(256), 0, st, fp, n2,
-                       (const double*)state, (double*)out);
+                       (const int64_t*)state, (double*)out);
   ATE_CHECK_LAUNCH();
   return 0;
 }

@@ -94,6 +94,13 @@ ATE_HD int64_t to_fix(double v) {
 }
 ATE_HD double from_fix(int64_t v) { return (double)v / FIX_SCALE; }
 
+// Prediction accumulators (state [10][n2] int64, csrc/forest.hip ate_forest_predict and the
+// host twin): every per-tree term (a leaf mean, a leaf moment, a little-bag score) is
+// rounded to 2^-32 fixed point ONCE, with the same IEEE operations on both sides, and the
+// terms are summed as int64 -- exact and order-free, so tree-parallel ranks all-reduce
+// their partial sums to the single-device bits.
+ATE_HD int64_t mean_fix(int64_t s, int64_t c) { return to_fix(from_fix(s) / (double)c); }
+
 // Node-level random stream ids: mtry draw k uses index node*4096 + k (p < 4094), the
 // Poisson draw 4094 and the leaf-vote coin 4095.
 ATE_HD uint64_t node_index(int node, int k) { return (uint64_t)node * 4096u + (uint64_t)k; }

@@ -85,8 +85,9 @@ def test_lasso_family_sharded_equals_single(tutorial, world):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_tree_parallel_forests_equal_single(world):
-    """Trees sharded over ranks (C05): identical trees per global tree id; OOB votes and
-    causal-forest tau/variance equal the single-device forest up to summation order."""
+    """Trees sharded over ranks (C05): identical trees per global tree id; the OOB votes,
+    the nuisance predictions and the causal-forest tau / variance are the SAME BITS as the
+    single-device forest (int64 fixed-point prediction sums)."""
     from ate_replication_causalml_amd.models import forest as F
     r = np.random.default_rng(0)
     n = 1500
@@ -104,6 +105,8 @@ def test_tree_parallel_forests_equal_single(world):
         return p, cf
 
     for p, cf in _run(fn, world, n):
-        np.testing.assert_allclose(p, rf1, rtol=1e-12, atol=1e-12, equal_nan=True)
-        np.testing.assert_allclose(cf.tau_oob, cf1.tau_oob, rtol=1e-9, atol=1e-11, equal_nan=True)
-        np.testing.assert_allclose(cf.var_oob, cf1.var_oob, rtol=1e-7, atol=1e-11, equal_nan=True)
+        np.testing.assert_array_equal(p, rf1)
+        np.testing.assert_array_equal(cf.y_hat, cf1.y_hat)
+        np.testing.assert_array_equal(cf.w_hat, cf1.w_hat)
+        np.testing.assert_array_equal(cf.tau_oob, cf1.tau_oob)
+        np.testing.assert_array_equal(cf.var_oob, cf1.var_oob)

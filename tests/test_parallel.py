@@ -285,3 +285,65 @@ def test_exact_gram_range_guard():
     pan.data[3, 7] = 1e5                                        # one large entry
     with pytest.raises(ValueError, match="limb range"):
         gram(pan, exact=True)
+
+
+def test_gloo_config4_causal_forest_bootstrap_bitwise():
+    """Config 4 end to end over real gloo processes: the tree-sharded causal forest
+    (nuisance and causal forests, int64 fixed-point C05 sums) and the replicate-sharded
+    bootstrap (C07) give the SAME BITS as one process, for the forest outputs, the AIPW
+    ATE and the bootstrap SE, at world 2 and 3."""
+    script = r"""
+import os, sys, json
+sys.path.insert(0, %r)
+import numpy as np, torch, torch.distributed as dist
+dist.init_process_group("gloo")
+from ate_replication_causalml_amd.parallel.comm import TorchComm
+from ate_replication_causalml_amd.estimators import crossfit as CF
+from ate_replication_causalml_amd.models import forest as F
+c = TorchComm()
+r = np.random.default_rng(4)
+n = 1200
+X = r.normal(size=(n, 6)); W = (r.uniform(size=n) < 0.4).astype(float)
+Y = X[:, 0] + (1 + (X[:, 1] > 0)) * W + 0.3 * r.normal(size=n)
+b = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=60, device="cpu",
+                               comm=c, boot_chunk=25)
+cf = F.causal_forest(X, Y, W, num_trees=24, nuisance_trees=12, seed=12345, backend="cpu", comm=c)
+h = lambda a: __import__("hashlib").sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+out = [float(b.ate).hex(), float(b.se).hex(), h(cf.tau_oob), h(cf.var_oob), h(cf.y_hat)]
+allv = [None] * c.world_size
+dist.all_gather_object(allv, out)
+if c.rank == 0:
+    print("RESULT", json.dumps(allv), flush=True)
+dist.destroy_process_group()
+""" % ROOT
+    import hashlib
+    import json
+    import tempfile
+    from ate_replication_causalml_amd.estimators import crossfit as CF
+    from ate_replication_causalml_amd.models import forest as F
+    r = np.random.default_rng(4)
+    n = 1200
+    X = r.normal(size=(n, 6))
+    W = (r.uniform(size=n) < 0.4).astype(float)
+    Y = X[:, 0] + (1 + (X[:, 1] > 0)) * W + 0.3 * r.normal(size=n)
+    b = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=60,
+                                   device="cpu", boot_chunk=25)
+    cf = F.causal_forest(X, Y, W, num_trees=24, nuisance_trees=12, seed=12345, backend="cpu")
+    h = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
+    want = [float(b.ate).hex(), float(b.se).hex(), h(cf.tau_oob), h(cf.var_oob), h(cf.y_hat)]
+    with tempfile.NamedTemporaryFile("w", suffix=".py", delete=False) as f:
+        f.write(script)
+        path = f.name
+    try:
+        for world in (2, 3):
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+                   f"--master-port={29601 + world}", path]
+            r2 = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+            assert r2.returncode == 0, r2.stderr[-3000:]
+            got = json.loads([l for l in r2.stdout.splitlines()
+                              if l.startswith("RESULT")][0].split(" ", 1)[1])
+            assert all(g == want for g in got), (world, got, want)
+    finally:
+        os.unlink(path)
