@@ -30,8 +30,6 @@ CTS_NAMES = [
 BIN_NAMES = ["sex", "g2000", "g2002", "p2000", "p2002", "p2004"]  # ate_replication.Rmd:56
 COVARIATES = CTS_NAMES + BIN_NAMES  # ate_replication.Rmd:57
 
-# DGP constants (calibrated so that n=50,000 gives roughly the published
-# oracle ~0.096, naive ~0.003 and ~41k dropped rows).
 S_CTS = 0           # streams 0..14: continuous covariates
 S_FACTOR = 40       # shared census-block factor for the neighbourhood covariates
 S_LATENT = 41       # latent propensity to vote
@@ -41,15 +39,49 @@ S_W = 61
 S_Y = 62
 S_EXTRA = 100       # 100.. extra nuisance columns for scaled configs
 
-INTERCEPT = -1.4
-B_HIST = 0.3
-B_LATENT = 0.2
-TAU_LOGIT = 0.45
-P_TREAT = 1.0 / 6.0
-HIST_THRESH = 0.6
-HIST_LATENT = 0.5
-YOB_LATENT = 0.3
-FACTOR_LOAD = 0.6
+
+@dataclass(frozen=True)
+class DgpParams:
+    """Constants of the latent-voter model: 15 N(0,1) continuous
+    covariates (3 individual, 12 loading on a census-block factor), latent = N(0,1) +
+    yob_latent * yob, vote history k = 1[N(0,1) + hist_latent * latent > hist_thresh[k]]
+    (g2000, g2002, p2000, p2002, p2004), sex ~ Bern(0.5), W ~ Bern(p_treat) (the RCT),
+    Y ~ Bern(sigmoid(intercept + b_hist' history + b_latent * latent + tau_logit * W))."""
+    intercept: float = -1.4
+    b_hist: tuple = (0.3, 0.3, 0.3, 0.3, 0.3)
+    b_latent: float = 0.2
+    tau_logit: float = 0.45
+    p_treat: float = 1.0 / 6.0
+    hist_thresh: tuple = (0.6, 0.6, 0.6, 0.6, 0.6)
+    hist_latent: float = 0.5
+    yob_latent: float = 0.3
+    factor_load: float = 0.6
+
+
+# The scaled-config panels (data/device_dgp.synthetic_panel, the bench) and the HIP
+# generator csrc/dgp.hip: the survey's scratch constants (one history threshold).
+PANEL = DgpParams()
+# The tutorial replication (make_tutorial_data): recalibrated to the published run
+# (ate_replication.md:118 and the three plots, BASELINE.md) -- vote-history marginals
+# like the real file's (general elections ~0.8, primaries ~0.3-0.45) so the selection
+# transform drops ~41,062 of 50,000 rows, and a baseline turnout / effect profile under
+# which the published ordering holds: oracle ~0.096, naive ~0, logistic-PS IPW below the
+# oracle, LASSO-PS IPW below that, Double ML in [0.03, 0.08] (tools/dgp_calibrate.py,
+# tests/test_dgp_calibration.py).
+# Thresholds: -Phi^-1(marginal) * sd(history score), marginals (0.85, 0.80, 0.25, 0.40,
+# 0.40), sd = sqrt(1 + 0.4^2 (1 + 0.3^2)). At n = 50,000, seed 1991 (CPU reference path,
+# tools/dgp_calibrate.py): 40,584 rows dropped (published 41,062), oracle 0.0945 (0.0961),
+# naive -0.0012 (0.0028), OLS 0.0888 (0.0777), IPW logistic PS 0.0694 (0.0637), IPW
+# LASSO PS 0.0117 (0.0110), Double ML (200 trees) 0.0533 (0.0524).
+TUTORIAL = DgpParams(intercept=-1.8, b_hist=(0.35, 0.35, 0.35, 0.35, 0.35), b_latent=0.35,
+                     tau_logit=0.4, p_treat=1.0 / 6.0,
+                     hist_thresh=(-1.1232, -0.9121, 0.7309, 0.2746, 0.2746), hist_latent=0.4)
+
+# legacy names (the panel model)
+INTERCEPT, B_LATENT, TAU_LOGIT, P_TREAT = PANEL.intercept, PANEL.b_latent, PANEL.tau_logit, \
+    PANEL.p_treat
+B_HIST, HIST_THRESH = PANEL.b_hist[0], PANEL.hist_thresh[0]
+HIST_LATENT, YOB_LATENT, FACTOR_LOAD = PANEL.hist_latent, PANEL.yob_latent, PANEL.factor_load
 
 
 def _normal(seed, stream, idx):
@@ -80,30 +112,35 @@ class TutorialData:
         return df
 
 
-def raw_columns(n: int, seed: int, p_extra: int = 0, row_offset: int = 0):
-    """Unscaled draws for rows [row_offset, row_offset+n)."""
+def raw_columns(n: int, seed: int, p_extra: int = 0, row_offset: int = 0,
+                params: DgpParams = PANEL):
+    """Unscaled draws for rows [row_offset, row_offset+n) (``params``: PANEL = the model of
+    the HIP generator csrc/dgp.hip, row for row)."""
+    P = params
     idx = np.arange(row_offset, row_offset + n, dtype=np.uint64)
     f = _normal(seed, S_FACTOR, idx)
+    fl = P.factor_load
     cts = np.empty((n, 15))
     for j in range(15):
         z = _normal(seed, S_CTS + j, idx)
-        cts[:, j] = z if j < 3 else FACTOR_LOAD * f + np.sqrt(1 - FACTOR_LOAD ** 2) * z
-    latent = _normal(seed, S_LATENT, idx) + YOB_LATENT * cts[:, 0]
+        cts[:, j] = z if j < 3 else fl * f + np.sqrt(1 - fl ** 2) * z
+    latent = _normal(seed, S_LATENT, idx) + P.yob_latent * cts[:, 0]
     hist = np.empty((n, 5))
     for k in range(5):
-        hist[:, k] = (_normal(seed, S_HIST + k, idx) + HIST_LATENT * latent > HIST_THRESH)
+        hist[:, k] = (_normal(seed, S_HIST + k, idx) + P.hist_latent * latent > P.hist_thresh[k])
     sex = (_uniform(seed, S_SEX, idx) < 0.5).astype(np.float64)
-    W = (_uniform(seed, S_W, idx) < P_TREAT).astype(np.float64)
-    eta = INTERCEPT + B_HIST * hist.sum(1) + B_LATENT * latent
-    Y = (_uniform(seed, S_Y, idx) < 1.0 / (1.0 + np.exp(-(eta + TAU_LOGIT * W)))).astype(np.float64)
-    tau_i = 1 / (1 + np.exp(-(eta + TAU_LOGIT))) - 1 / (1 + np.exp(-eta))
+    W = (_uniform(seed, S_W, idx) < P.p_treat).astype(np.float64)
+    eta = P.intercept + hist @ np.asarray(P.b_hist, dtype=np.float64) + P.b_latent * latent
+    Y = (_uniform(seed, S_Y, idx) < 1.0 / (1.0 + np.exp(-(eta + P.tau_logit * W)))).astype(
+        np.float64)
+    tau_i = 1 / (1 + np.exp(-(eta + P.tau_logit))) - 1 / (1 + np.exp(-eta))
     extra = np.empty((n, p_extra))
     for j in range(p_extra):
         z = _normal(seed, S_EXTRA + j, idx)
         if j % 4 == 3:   # every 4th extra column is binary
             extra[:, j] = (z > 0).astype(np.float64)
         else:
-            extra[:, j] = FACTOR_LOAD * f + np.sqrt(1 - FACTOR_LOAD ** 2) * z
+            extra[:, j] = fl * f + np.sqrt(1 - fl ** 2) * z
     return cts, np.column_stack([sex, hist]), extra, W, Y, tau_i
 
 
@@ -115,9 +152,10 @@ def r_scale(a: np.ndarray) -> np.ndarray:
     return (a - m) / s
 
 
-def make_tutorial_data(n: int = 50_000, seed: int = 1991, p_extra: int = 0) -> TutorialData:
+def make_tutorial_data(n: int = 50_000, seed: int = 1991, p_extra: int = 0,
+                       params: DgpParams = TUTORIAL) -> TutorialData:
     """The ``df`` of ``ate_replication.Rmd:89-94`` (scaled cts + binary + Y + W)."""
-    cts, binc, extra, W, Y, tau_i = raw_columns(n, seed, p_extra)
+    cts, binc, extra, W, Y, tau_i = raw_columns(n, seed, p_extra, params=params)
     cts = r_scale(cts)
     names = list(COVARIATES)
     blocks = [cts, binc]
