@@ -47,25 +47,49 @@ def _run(cmd):
     return r
 
 
-def build_hip(verbose: bool = False) -> Path:
+DEBUG_FLAGS = ["-DATE_DEVICE_ASSERT"]   # device bounds checks (csrc/common.hpp ATE_DASSERT)
+
+
+def debug_enabled() -> bool:
+    """``ATE_DEBUG=1``: build / load the device-assertion library (libatehip_debug.so)."""
+    return os.environ.get("ATE_DEBUG", "0") not in ("", "0")
+
+
+def hip_compile_cmd(src: Path, obj: Path, debug: bool = False) -> list:
+    """hipcc command line of one kernel source (``debug``: with the device assertions)."""
+    flags = list(HIP_FLAGS)
+    if src.name in NO_CONTRACT:
+        # bit-exact parity with the host reference: no FMA contraction
+        flags = [f for f in flags if not f.startswith("-ffp-contract")] + ["-ffp-contract=off"]
+    if debug:
+        flags += DEBUG_FLAGS
+    return [HIPCC, *flags, "-I", str(CSRC), "-c", str(src), "-o", str(obj)]
+
+
+def hip_lib_name(debug: bool = False) -> str:
+    return "libatehip_debug.so" if debug else "libatehip.so"
+
+
+def build_hip(verbose: bool = False, debug: bool | None = None) -> Path:
+    """Compile every csrc/*.hip for gfx950 and link _lib/libatehip.so; ``debug`` (default:
+    ATE_DEBUG) builds the device-assertion variant into build/debug/ and
+    _lib/libatehip_debug.so instead (the production library is untouched)."""
+    debug = debug_enabled() if debug is None else debug
     srcs = sorted(CSRC.glob("*.hip"))
     hdrs = _headers(CSRC)
-    BUILD.mkdir(exist_ok=True)
+    bdir = BUILD / "debug" if debug else BUILD
+    bdir.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(exist_ok=True)
     objs = []
     jobs = []
     for s in srcs:
-        o = BUILD / (s.stem + ".hip.o")
+        o = bdir / (s.stem + ".hip.o")
         objs.append(o)
         if _stale(o, [s, *hdrs, Path(__file__)]):
-            flags = list(HIP_FLAGS)
-            if s.name in NO_CONTRACT:
-                # bit-exact parity with the host reference: no FMA contraction
-                flags = [f for f in flags if not f.startswith("-ffp-contract")] + ["-ffp-contract=off"]
-            jobs.append([HIPCC, *flags, "-I", str(CSRC), "-c", str(s), "-o", str(o)])
+            jobs.append(hip_compile_cmd(s, o, debug))
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
         list(ex.map(_run, jobs))
-    lib = LIBDIR / "libatehip.so"
+    lib = LIBDIR / hip_lib_name(debug)
     if jobs or not lib.exists():
         _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-Wl,-z,defs", "-o", str(lib), *map(str, objs)])
     if verbose:
@@ -89,7 +113,12 @@ def build_cpu(verbose: bool = False) -> Path:
 
 
 def build_all(verbose: bool = False):
-    return build_hip(verbose), build_cpu(verbose)
+    """The production kernel library and the host library; with ATE_DEBUG=1 also the
+    device-assertion kernel library."""
+    out = (build_hip(verbose, debug=False), build_cpu(verbose))
+    if debug_enabled():
+        build_hip(verbose, debug=True)
+    return out
 
 
 if __name__ == "__main__":

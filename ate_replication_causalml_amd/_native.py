@@ -114,9 +114,11 @@ def hip():
     if _hip is None:
         import torch  # noqa: F401  (ensure torch's HIP runtime is loaded first)
         # ATE_HIP_LIB: an alternative build of the same library (e.g. the cycle-profiling
-        # variant made by tools/enet_profile.py)
+        # variant made by tools/enet_profile.py); ATE_DEBUG=1: the device-assertion build
+        # (_build.py, csrc/common.hpp ATE_DASSERT)
+        debug = os.environ.get("ATE_DEBUG", "0") not in ("", "0")
         p = Path(os.environ["ATE_HIP_LIB"]) if os.environ.get("ATE_HIP_LIB") else \
-            _LIBDIR / "libatehip.so"
+            _LIBDIR / ("libatehip_debug.so" if debug else "libatehip.so")
         if not p.exists():
             raise NativeMissing(
                 f"{p} not found: build it with `python -m ate_replication_causalml_amd._build` "

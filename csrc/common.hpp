@@ -111,4 +111,20 @@ inline int grid_for(int64_t n, int block, int cap = 2048) {
 
 }  // namespace ate
 
+// Device bounds checks: compiled in by a debug build (-DATE_DEVICE_ASSERT;
+// ATE_DEBUG=1, ate_replication_causalml_amd/_build.py -> _lib/libatehip_debug.so) and out
+// of the production library (the condition is not even evaluated). A failed check prints
+// its source site and traps, so an index bug is named instead of found by bisection.
+#ifdef ATE_DEVICE_ASSERT
+#define ATE_DASSERT(cond)                                                          \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      printf("ATE_DASSERT failed %s:%d: %s\n", __FILE__, __LINE__, #cond);         \
+      __builtin_trap();                                                            \
+    }                                                                              \
+  } while (0)
+#else
+#define ATE_DASSERT(cond) do { } while (0)
+#endif
+
 #define ATE_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)

@@ -355,6 +355,7 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         }
         int before;
         const int tot = block_flag_scan(big, scnt, before);
+        ATE_DASSERT(!big || nb + before < XBIG);
         if (big) sbig[nb + before] = j;
         nb += tot;
       }
@@ -741,6 +742,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
             tfeat[nd.id] = -1; tthr[nd.id] = -1; tleft[nd.id] = -1; tval[nd.id] = d.val;
           } else {
             const int k = ns + before, nid = nid0 + 2 * k;
+            ATE_DASSERT(nd.id < 2 * n + 1 && nid + 1 < 2 * n + 1 && d.nl >= 0 &&
+                        d.nl <= nd.hi - nd.lo && 2 * k + 1 <= n);
             tfeat[nd.id] = d.feat; tthr[nd.id] = d.thr; tleft[nd.id] = nid; tval[nd.id] = 0.0;
             S.nxt[2 * k] = XRng{nd.lo, nd.lo + d.nl, nid};
             S.nxt[2 * k + 1] = XRng{nd.lo + d.nl, nd.hi, nid + 1};
@@ -779,6 +782,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           tl += scnt[w]; tr += sreds[w];
         }
         const uint64_t below = (1ull << lane) - 1ull;
+        ATE_DASSERT(!in || (l ? ol + __popcll(bl & below) < d.nl
+                             : orr + __popcll(br & below) < cnt));
         if (in) S.keys[nd.lo + (l ? ol + __popcll(bl & below) : orr + __popcll(br & below))] = (uint32_t)i;
         lo_l += tl; lo_r += tr;
         __syncthreads();

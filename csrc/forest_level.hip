@@ -366,7 +366,11 @@ __global__ __launch_bounds__(256) void lv_classify_kernel(const LNode* __restric
     int base = 0;
     if (lane == leader) base = atomicAdd(&counts[k], __popcll(mk));
     base = __shfl(base, leader, 64);
-    if (c == k) lists[(int64_t)k * ncur + base + __popcll(mk & ((1ull << lane) - 1ull))] = j;
+    if (c == k) {
+      const int pos = base + __popcll(mk & ((1ull << lane) - 1ull));
+      ATE_DASSERT(pos < ncur);
+      lists[(int64_t)k * ncur + pos] = j;
+    }
   }
 }
 
@@ -405,6 +409,8 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   const int nk = min(LV_FG, nf - k0);
   const LNode nd = a.cur[blist[slot]];
   const int n = a.fp.n;
+  ATE_DASSERT(nd.lo <= item_q0[it] && item_q0[it] <= item_q1[it] && item_q1[it] <= nd.hi &&
+              nd.hi <= n && nk <= LV_FG && k0 + nk <= LV_MAXF);
   const int32_t* wt = a.w + (int64_t)nd.tree * n;
   for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
   int fi[LV_FG], sp[LV_FG];
@@ -758,6 +764,7 @@ __global__ __launch_bounds__(256) void lv_part_wave_kernel(LvArgs a, const int32
       const int i = a.idx[q];
       const bool gl = (bl >> lane) & 1ull;
       const int l = lb + __popcll(bl & below);
+      ATE_DASSERT(gl ? l < cl : cl + (b * 64 + lane - l) < m);
       if (gl) a.idx2[nd.lo + l] = i;
       else a.idx2[nd.lo + cl + (b * 64 + lane - l)] = i;
     }
@@ -829,6 +836,7 @@ __global__ __launch_bounds__(256) void lv_part_scatter_kernel(LvArgs a, const in
     }
     const int lb = run + off + __popcll(bl & ((1ull << lane) - 1ull));   // lefts before q
     if (q < q1) {
+      ATE_DASSERT(gl ? lb < nlt : nlt + (q - nd.lo - lb) < nd.hi - nd.lo);
       if (gl) a.idx2[nd.lo + lb] = i;
       else a.idx2[nd.lo + nlt + (q - nd.lo - lb)] = i;
     }
@@ -863,6 +871,7 @@ __global__ __launch_bounds__(256) void lv_children_kernel(LvArgs a, int ncur,
     const int lid = nid + 2 * r;
     a.left[(int64_t)t * a.cap + nd.id] = lid;
     const int nlft = a.nl[j];
+    ATE_DASSERT(nd.id < a.cap && lid + 1 < a.cap && nlft >= 0 && nlft <= nd.hi - nd.lo);
     nxt[2 * excl[j]] = {t, nd.lo, nd.lo + nlft, lid};
     nxt[2 * excl[j] + 1] = {t, nd.lo + nlft, nd.hi, lid + 1};
   }

@@ -215,6 +215,7 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
   if (wk[0] < 0) return;                                    // uniform: spare workgroup
   const int64_t s = wk[1], e = wk[2];
   const int j0 = yb * FB, nf = min(FB, p - j0);
+  ATE_DASSERT(wk[0] < nn && sseg[wk[0]] <= s && s <= e && e <= sseg[wk[0] + 1] && nf > 0);
   {
     ulonglong2* z = reinterpret_cast<ulonglong2*>(sh);
     for (int t = threadIdx.x; t < SLAB / 2; t += NTH) z[t] = make_ulonglong2(0, 0);
@@ -569,6 +570,7 @@ __global__ __launch_bounds__(NT) void gbdt_part_count_kernel(
       if (q >= q1) continue;
       int b = 2 * nn;
       if (q < sseg[nn] && sft[kk[u]] >= 0) b = 2 * kk[u] + (bv[u] > sth[kk[u]] ? 1 : 0);
+      ATE_DASSERT(b <= 2 * nn && b < MAXB && kk[u] < nn);
       bkt[q] = (uint8_t)b;
       atomicAdd(&lc[b], 1);
     }
@@ -635,7 +637,9 @@ __global__ __launch_bounds__(NT) void gbdt_part_scatter_kernel(
   const int64_t q0 = wgi * R, q1 = min(n_train, q0 + R);
   for (int64_t q = q0 + threadIdx.x; q < q1; q += NT) {
     const int b = bkt[q];
+    ATE_DASSERT(b < nb);
     const int64_t dst = off[b] + atomicAdd(&lr[b], 1);
+    ATE_DASSERT(dst >= 0 && dst < n_train);
     idx2[dst] = idx[q];
     gh2[dst] = gh[q];
   }

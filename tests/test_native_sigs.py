@@ -39,3 +39,25 @@ def test_hip_library_builds():
     from ate_replication_causalml_amd import _build
     lib = _build.build_hip()
     assert lib.exists() and lib.stat().st_size > 10000
+
+
+def test_debug_build_adds_device_assertions(monkeypatch):
+    """ATE_DEBUG=1: the kernel sources compile with -DATE_DEVICE_ASSERT
+    into a separate library (build/debug, _lib/libatehip_debug.so) that the loader picks;
+    the production compile line and library are unchanged."""
+    from pathlib import Path
+    from ate_replication_causalml_amd import _build as B
+    src = B.CSRC / "forest_level.hip"
+    prod = B.hip_compile_cmd(src, Path("x.o"))
+    dbg = B.hip_compile_cmd(src, Path("x.o"), debug=True)
+    assert "-DATE_DEVICE_ASSERT" in dbg and "-DATE_DEVICE_ASSERT" not in prod
+    assert [f for f in dbg if f != "-DATE_DEVICE_ASSERT"] == prod   # same flags otherwise
+    assert "-ffp-contract=off" in dbg                           # bit-exact forest files
+    assert B.hip_lib_name(True) == "libatehip_debug.so" and B.hip_lib_name() == "libatehip.so"
+    monkeypatch.setenv("ATE_DEBUG", "1")
+    assert B.debug_enabled()
+    monkeypatch.setenv("ATE_DEBUG", "0")
+    assert not B.debug_enabled()
+    # every kernel file with heavy index arithmetic carries checks
+    for f in ("forest_level.hip", "gbdt.hip", "enet.hip", "forest_exact.hip"):
+        assert "ATE_DASSERT(" in (B.CSRC / f).read_text(), f
