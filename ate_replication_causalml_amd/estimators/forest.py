@@ -136,23 +136,31 @@ def _double_ml_body(Xb, y, w, ev, en, num_trees, seed):
     return (halves[0] + halves[1]) / 2
 
 
-def _causal_forest_body(Xb, y, w, num_trees, nt, seed):
+def _causal_forest_body(Xb, y, w, ev, en, num_trees, nt, seed):
     """Device body of causal_forest_ate (models/forest.causal_forest + average_treatment_
-    effect with grf defaults, no host sync): [AIPW ATE, SE, mean CATE, sqrt(mean var)]."""
+    effect with grf defaults, no host sync): [AIPW ATE, SE, mean CATE, sqrt(mean var)].
+    ``ev, en``: the exact mode's device value table (grf's exact split values), None:
+    256-bin histograms. The orthogonalisation forests use ci.group.size = 1 (grf)."""
     p = Xb.shape[0]
-    grf = dict(mtry=F.grf_mtry(p), min_node=5, sampling=1, honesty=True, group=2,
-               mtry_poisson=True, alpha=0.05, sample_fraction=0.5)
+    grf = dict(mtry=F.grf_mtry(p), min_node=5, sampling=1, honesty=True, mtry_poisson=True,
+               alpha=0.05, sample_fraction=0.5)
 
     def oob(fr):
         return fr.predict_state(Xb, True, fr.new_state(Xb.shape[1]), 7, host=False)
 
-    fy = F.fit_forest_binned(Xb, (None, None), F.KIND_REG, r1=y, ntree=nt, seed=seed + 1, **grf)
-    fw = F.fit_forest_binned(Xb, (None, None), F.KIND_REG, r1=w, ntree=nt, seed=seed + 2, **grf)
+    def grow(kind, ntree, sd, group, **kw):
+        if ev is not None:
+            return F.fit_forest_exact(Xb, F.DeviceExactBins(ev, en), kind, ntree=ntree, seed=sd,
+                                      group=group, **grf, **kw)
+        return F.fit_forest_binned(Xb, (None, None), kind, ntree=ntree, seed=sd, group=group,
+                                   **grf, **kw)
+
+    fy = grow(F.KIND_REG, nt, seed + 1, 1, r1=y)
+    fw = grow(F.KIND_REG, nt, seed + 2, 1, r1=w)
     y_hat, w_hat = oob(fy), oob(fw)
     y_hat = torch.where(torch.isnan(y_hat), y.mean(), y_hat)
     w_hat = torch.where(torch.isnan(w_hat), w.mean(), w_hat)
-    fc = F.fit_forest_binned(Xb, (None, None), F.KIND_CAUSAL, r1=w - w_hat, r2=y - y_hat,
-                             ntree=num_trees, seed=seed, **grf)
+    fc = grow(F.KIND_CAUSAL, num_trees, seed, 2, r1=w - w_hat, r2=y - y_hat)
     out = oob(fc)
     tau_oob, var_oob = out[:, 0], out[:, 1]
     w_res, y_res = w - w_hat, y - y_hat
@@ -217,28 +225,30 @@ def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning"
 
 
 def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest(GRF)",
-                      device=None, nuisance_trees=None, comm=None, graph=True):
+                      device=None, nuisance_trees=None, comm=None, graph=True, splits="auto"):
     """E15 (ate_replication.Rmd:250-272): grf causal forest; published row = AIPW
     ``estimate_average_effect``; diagnostics carry the "incorrect" mean-CATE ATE and
-    sqrt(mean(var)) the reference prints (ate_replication.md:294)."""
+    sqrt(mean(var)) the reference prints (ate_replication.md:294). ``splits``: "auto" =
+    grf's exact split values up to 65,536 rows (df_mod), else 256-bin histograms."""
     dev = resolve_device(device)
+    splits = F.resolve_splits(splits, len(as_np(Y)))
     if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
         # one hipGraph launch: Y.hat / W.hat OOB regression forests, the honest causal
         # forest on the centred data, its OOB CATEs and the AIPW average effect
         from ..utils.graphs import estimator_graphs
         Xn = as_np(X)
-        edges = F.bin_edges(Xn)
-        Xb = F.bin_matrix(Xn, *edges, dev)
+        Xb, ev, en = _device_bins(Xn, splits, dev)
         y = torch.as_tensor(as_np(Y), device=dev)
         w = torch.as_tensor(as_np(W), device=dev)
         nt = nuisance_trees or max(50, num_trees // 4)
-        out, g = estimator_graphs.run("causal_forest", _causal_forest_body, (Xb, y, w),
+        out, g = estimator_graphs.run("causal_forest", _causal_forest_body, (Xb, y, w, ev, en),
                                       num_trees, nt, seed)
         v = out.cpu().numpy()
         return AteResult.make(method, v[0], v[1], ate_bad=float(v[2]), se_bad=float(v[3]),
-                              hipgraph=g)
+                              hipgraph=g, splits=splits)
     cf = F.causal_forest(as_np(X), as_np(Y), as_np(W), num_trees=num_trees, seed=seed,
-                         nuisance_trees=nuisance_trees, backend=_backend(device), comm=comm)
+                         nuisance_trees=nuisance_trees, backend=_backend(device), comm=comm,
+                         splits=splits)
     est, se = F.average_treatment_effect(cf)
     return AteResult.make(method, est, se, ate_bad=float(np.nanmean(cf.tau_oob)),
                           se_bad=float(np.sqrt(np.nanmean(cf.var_oob))))

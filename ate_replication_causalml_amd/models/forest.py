@@ -16,11 +16,14 @@ csrc/forest_common.hpp and grow bit-identical trees from the same Philox streams
 Continuous covariates are quantile-binned to <= 256 bins (exact for <= 256 distinct
 values); splits are at bin boundaries.
 
-Exact-split mode (``splits="exact"``, randomForest kinds 0/1 with bootstrap sampling):
-bins are the ranks of every feature's distinct values (uint16, <= 65536 rows), splits
-can fall between any two consecutive distinct in-node values and sit at their midpoint
-(randomForest's ``findbestsplit``). GPU: csrc/forest_exact.hip, host twin
-grow_tree_exact in csrc/cpu/forest_cpu.cpp -- the same trees bit for bit.
+Exact-split mode (``splits="exact"``): bins are the ranks of every feature's distinct
+values (uint16, <= 65536 rows), splits can fall between any two consecutive distinct
+in-node values. randomForest (bootstrap, kinds 0/1): the threshold is their midpoint
+(``findbestsplit``); grf (half-samples, honesty, little bags; kinds 1/2): the left value
+itself (x <= v goes left), so new rows are binned by #{values < x}. GPU:
+csrc/forest_exact.hip, host twin grow_tree_exact in csrc/cpu/forest_cpu.cpp -- the same
+trees bit for bit. ``splits="auto"`` picks exact splits up to 65,536 rows (the tutorial's
+scale, where randomForest and grf themselves split on exact values).
 """
 from __future__ import annotations
 
@@ -148,14 +151,18 @@ class ExactBins:
         return DeviceExactBins(torch.as_tensor(self.vals, device=dev),
                                torch.as_tensor(self.nval, device=dev))
 
-    def bin(self, X) -> np.ndarray:
-        """uint16 [p][n] column-major bins of X (host)."""
+    def bin(self, X, grf: bool = False) -> np.ndarray:
+        """uint16 [p][n] column-major bins of X (host): #{midpoints < x} (randomForest's
+        midpoint thresholds) or, ``grf``, #{values < x} (grf's x <= value rule). Both are
+        the value's rank for a value in the table."""
         Xh = np.asarray(X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else X,
                         dtype=np.float64)
         p = self.vals.shape[0]
         out = np.empty((p, Xh.shape[0]), dtype=np.uint16)
         for j in range(p):
-            out[j] = np.searchsorted(self.mids[j, :self.nval[j] - 1], Xh[:, j], side="left")
+            ref = self.vals[j, :self.nval[j]] if grf else self.mids[j, :self.nval[j] - 1]
+            out[j] = np.minimum(np.searchsorted(ref, Xh[:, j], side="left"),
+                                self.nval[j] - 1)
         return out
 
 
@@ -234,7 +241,7 @@ class Forest:
         if X is None:
             return self.Xb_train
         if self.exact is not None:
-            b = torch.from_numpy(self.exact.bin(X))
+            b = torch.from_numpy(self.exact.bin(X, grf=self.params.sampling == 1))
             return b.to(self.device) if self.backend == "gpu" else b
         dev = self.device if self.backend == "gpu" else None
         return bin_matrix(X, self.edges, self.nedges, dev)
@@ -268,11 +275,13 @@ class Forest:
                 tchunk = max(1, min(self.params.ntree, (1 << 28) // max(n2, 1)))
                 leaves = torch.empty(tchunk * n2, dtype=torch.int32, device=dev)
                 out = torch.empty(n2 * width, dtype=torch.float64, device=dev)
+                g = max(1, self.params.group) if self.params.kind == KIND_CAUSAL else 1
+                tchunk = max(g, tchunk // g * g)
                 _native.call("ate_forest_predict16", ctypes.addressof(self.params),
                              Xb.data_ptr(), n2, int(oob), self.cap, self.feat.data_ptr(),
                              self.thr.data_ptr(), self.left.data_ptr(), self.val.data_ptr(),
-                             self.inbag.data_ptr(), leaves.data_ptr(), tchunk, state.data_ptr(),
-                             out.data_ptr(), phases, s)
+                             self.inbag.data_ptr(), 0 if self.est is None else self.est.data_ptr(),
+                             leaves.data_ptr(), tchunk, state.data_ptr(), out.data_ptr(), phases, s)
                 if not phases & 4:
                     return None
                 return out if not host else out.cpu().numpy()
@@ -356,11 +365,13 @@ def fit_forest(X, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None, min
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "gpu" else None
     if splits == "exact":
         eb = edges if isinstance(edges, ExactBins) else exact_bins(X)
-        Xb = torch.from_numpy(eb.bin(X))
+        Xb = torch.from_numpy(eb.bin(X))          # training rows: ranks either way
         if dev is not None:
             Xb = Xb.to(dev)
-        return fit_forest_exact(Xb, eb, kind, y=y, r1=r1, ntree=ntree, mtry=mtry,
-                                min_node=min_node, sampling=sampling, seed=seed,
+        return fit_forest_exact(Xb, eb, kind, y=y, r1=r1, r2=r2, ntree=ntree, mtry=mtry,
+                                min_node=min_node, sampling=sampling, honesty=honesty,
+                                group=group, mtry_poisson=mtry_poisson, alpha=alpha,
+                                sample_fraction=sample_fraction, seed=seed,
                                 tree_offset=tree_offset)
     if splits != "binned":
         raise ValueError(f"splits must be 'binned' or 'exact', got {splits!r}")
@@ -477,24 +488,34 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
     return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xbn)
 
 
-def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, ntree=500, mtry=None,
-                     min_node=1, sampling=0, seed=1, tree_offset=0) -> Forest:
+def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None,
+                     min_node=1, sampling=0, honesty=False, group=1, mtry_poisson=False,
+                     alpha=0.0, sample_fraction=0.5, seed=1, tree_offset=0) -> Forest:
     """Exact-split forest on value-rank bins ``Xb`` (uint16 [p][n]; a device tensor grows on
-    the GPU, csrc/forest_exact.hip, a host one on the CPU twin). randomForest sampling,
-    kinds 0/1. ``eb``: ExactBins (or, on the GPU, its DeviceExactBins)."""
-    if sampling != 0 or kind not in (KIND_CLASS, KIND_REG):
-        raise ValueError("exact-split forests: randomForest sampling, classification or "
-                         "regression")
+    the GPU, csrc/forest_exact.hip, a host one on the CPU twin). randomForest sampling
+    (``sampling=0``): kinds 0/1, midpoint thresholds. grf sampling (``sampling=1``): kinds
+    1/2 with half-samples / little bags (``group``), ``honesty`` and the J2 estimation
+    statistics; the left value is the threshold. ``eb``: ExactBins (or, on the GPU, its
+    DeviceExactBins)."""
+    if sampling == 0 and kind not in (KIND_CLASS, KIND_REG):
+        raise ValueError("exact-split randomForest forests: classification or regression")
+    if sampling == 1 and kind not in (KIND_REG, KIND_CAUSAL):
+        raise ValueError("exact-split grf forests: regression or causal")
+    if kind == KIND_CAUSAL and r2 is None:
+        raise ValueError("causal forests need r1 = W~ and r2 = Y~")
     gpu = isinstance(Xb, torch.Tensor) and Xb.is_cuda
     p, n = Xb.shape
     if n > EXACT_MAX_ROWS:
         raise ValueError(f"exact-split forests take at most {EXACT_MAX_ROWS} rows (got {n})")
     if mtry is None:
         mtry = max(1, int(math.floor(math.sqrt(p))))
-    fp = ForestParams(kind=kind, sampling=0, ntree=ntree, mtry=min(mtry, p), min_node=min_node,
-                      honesty=0, group=1, mtry_poisson=0, alpha=0.0, sample_fraction=0.5,
-                      pois0=math.exp(-min(mtry, p)), seed=seed, p=p, n=n, t0=tree_offset)
+    fp = ForestParams(kind=kind, sampling=sampling, ntree=ntree, mtry=min(mtry, p),
+                      min_node=min_node, honesty=int(honesty), group=max(1, group),
+                      mtry_poisson=int(mtry_poisson), alpha=alpha,
+                      sample_fraction=sample_fraction, pois0=math.exp(-min(mtry, p)), seed=seed,
+                      p=p, n=n, t0=tree_offset)
     cap = 2 * n + 1
+    need_est = sampling == 1
     h = lambda a: None if a is None else (a.cpu().numpy() if isinstance(a, torch.Tensor) else
                                            np.asarray(a))
     if gpu:
@@ -504,11 +525,15 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, ntree=500, mtry=None,
             yt = y.to(dev, torch.uint8)
         else:
             yt = None if y is None else torch.as_tensor(h(y).astype(np.uint8), device=dev)
-        if isinstance(r1, torch.Tensor):
-            v = r1.to(dev, torch.float64) * FIX
-            r1t = torch.where(v >= 0, torch.floor(v + 0.5), torch.ceil(v - 0.5)).to(torch.int64)
-        else:
-            r1t = None if r1 is None else torch.as_tensor(to_fix(h(r1)), device=dev)
+
+        def fixt(r):
+            if r is None:
+                return None
+            if isinstance(r, torch.Tensor):
+                v = r.to(dev, torch.float64) * FIX
+                return torch.where(v >= 0, torch.floor(v + 0.5), torch.ceil(v - 0.5)).to(torch.int64)
+            return torch.as_tensor(to_fix(h(r)), device=dev)
+        r1t, r2t = fixt(r1), fixt(r2)
         de = eb.on(dev) if isinstance(eb, ExactBins) else eb
         vals, nval = de.vals, de.nval
         feat = torch.empty(ntree * cap, dtype=torch.int32, device=dev)
@@ -517,6 +542,7 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, ntree=500, mtry=None,
         val = torch.zeros(ntree * cap, dtype=torch.float64, device=dev)
         nnodes = torch.empty(ntree, dtype=torch.int32, device=dev)
         inbag = torch.empty(ntree * n, dtype=torch.uint8, device=dev)
+        est = torch.zeros(ntree * cap * 5, dtype=torch.int64, device=dev) if need_est else None
         per = _native.hip().ate_forest_exact_scratch_bytes(n, 1)
         chunk = max(1, min(ntree, (1 << 30) // per))       # scratch <= ~1 GiB
         scratch = torch.empty(per * chunk, dtype=torch.uint8, device=dev)
@@ -526,29 +552,32 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, ntree=500, mtry=None,
         for t0 in range(0, ntree, chunk):
             _native.call("ate_forest_fit_exact", ctypes.addressof(fp), t0, min(chunk, ntree - t0),
                          Xb.data_ptr(), vals.data_ptr(), de.ldv, nval.data_ptr(), p_(yt), p_(r1t),
-                         cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(), val.data_ptr(),
-                         nnodes.data_ptr(), inbag.data_ptr(), scratch.data_ptr(), s)
+                         p_(r2t), cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(),
+                         val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
+                         scratch.data_ptr(), s)
         del scratch
-        return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, None, None, None, Xb,
+        return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, est, None, None, Xb,
                       exact=eb)
     Xbn = np.ascontiguousarray(h(Xb), dtype=np.uint16)
     ycls = None if y is None else h(y).astype(np.uint8)
     r1f = None if r1 is None else to_fix(h(r1))
+    r2f = None if r2 is None else to_fix(h(r2))
     feat = np.empty(ntree * cap, dtype=np.int32)
     thr = np.empty_like(feat)
     left = np.empty_like(feat)
     val = np.zeros(ntree * cap)
     nnodes = np.empty(ntree, dtype=np.int32)
     inbag = np.empty(ntree * n, dtype=np.uint8)
+    est = np.zeros(ntree * cap * 5, dtype=np.int64) if need_est else None
     vals = np.ascontiguousarray(eb.vals)
     nval = np.ascontiguousarray(eb.nval, dtype=np.int32)
     rc = _native.cpu().atecpu_forest_fit_exact(
         ctypes.byref(fp), _ptr(Xbn), _ptr(vals), ctypes.c_int(eb.ldv), _ptr(nval), _ptr(ycls),
-        _ptr(r1f), ctypes.c_int(cap), _ptr(feat), _ptr(thr), _ptr(left), _ptr(val), _ptr(nnodes),
-        _ptr(inbag), ctypes.c_int(_nthreads()))
+        _ptr(r1f), _ptr(r2f), ctypes.c_int(cap), _ptr(feat), _ptr(thr), _ptr(left), _ptr(val),
+        _ptr(nnodes), _ptr(inbag), _ptr(est), ctypes.c_int(_nthreads()))
     if rc != 0:
         raise RuntimeError("atecpu_forest_fit_exact failed")
-    return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, None, None, None, Xbn,
+    return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, est, None, None, Xbn,
                   exact=eb)
 
 
@@ -574,12 +603,16 @@ def grf_mtry(p):
 
 
 def regression_forest(X, y, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
-                      sample_fraction=0.5, group=2, seed=1, backend=None) -> Forest:
-    """grf::regression_forest defaults; OOB predictions via ``oob_predict``."""
-    p = np.asarray(X).shape[1]
+                      sample_fraction=0.5, group=2, seed=1, backend=None, splits="binned",
+                      edges=None) -> Forest:
+    """grf::regression_forest defaults; OOB predictions via ``oob_predict``.
+    ``splits``: "exact" (grf's exact values), "binned" or "auto" (exact up to 65,536 rows)."""
+    X = np.asarray(X, dtype=np.float64)
+    p = X.shape[1]
     return fit_forest(X, KIND_REG, r1=y, ntree=num_trees, mtry=grf_mtry(p), min_node=min_node,
                       sampling=1, honesty=honesty, group=group, mtry_poisson=True, alpha=alpha,
-                      sample_fraction=sample_fraction, seed=seed, backend=backend)
+                      sample_fraction=sample_fraction, seed=seed, backend=backend,
+                      splits=resolve_splits(splits, X.shape[0]), edges=edges)
 
 
 @dataclass
@@ -595,43 +628,45 @@ class CausalForestFit:
 
 def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
                   sample_fraction=0.5, group=2, seed=12345, nuisance_trees=None,
-                  backend=None, comm=None) -> CausalForestFit:
+                  backend=None, comm=None, splits="auto", nuisance_group=1) -> CausalForestFit:
     """grf::causal_forest(X, Y, W, num.trees, honesty=TRUE, seed) (ate_replication.Rmd:250-255):
-    OOB regression forests for Y.hat and W.hat, then causal trees on the centred
-    (W - W.hat, Y - Y.hat)."""
+    OOB regression forests for Y.hat and W.hat (grf's orthogonalisation forests:
+    max(50, num.trees / 4) trees, ``ci.group.size = 1`` -> ``nuisance_group``), then causal
+    trees in little bags of ``group`` on the centred (W - W.hat, Y - Y.hat). ``splits``:
+    "auto" = grf's exact split values up to 65,536 rows (the tutorial), 256-bin histograms
+    above; "exact" / "binned" force one."""
     X = np.asarray(X, dtype=np.float64)
     Y = np.asarray(Y, dtype=np.float64)
     W = np.asarray(W, dtype=np.float64)
     nt = nuisance_trees or max(50, num_trees // 4)
-    edges = bin_edges(X)
+    splits = resolve_splits(splits, X.shape[0])
+    edges = exact_bins(X) if splits == "exact" else bin_edges(X)
     p = X.shape[1]
-    grf = dict(mtry=grf_mtry(p), min_node=min_node, sampling=1, honesty=honesty, group=group,
+    grf = dict(mtry=grf_mtry(p), min_node=min_node, sampling=1, honesty=honesty,
                mtry_poisson=True, alpha=alpha, sample_fraction=sample_fraction, backend=backend,
-               edges=edges)
+               edges=edges, splits=splits)
     if comm is not None and comm.world_size > 1:
         # tree-parallel: every rank grows its share of each forest (C05 all-reduces)
-        fy = fit_forest_sharded(X, KIND_REG, nt, comm, r1=Y, seed=seed + 1, **grf)
-        fw = fit_forest_sharded(X, KIND_REG, nt, comm, r1=W, seed=seed + 2, **grf)
+        fy = fit_forest_sharded(X, KIND_REG, nt, comm, r1=Y, seed=seed + 1, group=nuisance_group,
+                                **grf)
+        fw = fit_forest_sharded(X, KIND_REG, nt, comm, r1=W, seed=seed + 2, group=nuisance_group,
+                                **grf)
         y_hat = predict_tree_parallel(fy, comm, oob=True)
         w_hat = predict_tree_parallel(fw, comm, oob=True)
         y_hat = np.where(np.isnan(y_hat), Y.mean(), y_hat)
         w_hat = np.where(np.isnan(w_hat), W.mean(), w_hat)
         fc = fit_forest_sharded(X, KIND_CAUSAL, num_trees, comm, r1=W - w_hat, r2=Y - y_hat,
-                                seed=seed, **grf)
+                                seed=seed, group=group, **grf)
         out = predict_tree_parallel(fc, comm, oob=True)
         return CausalForestFit(fc, y_hat, w_hat, out[:, 0], out[:, 1], Y, W)
-    fy = regression_forest(X, Y, nt, honesty, min_node, alpha, sample_fraction, group,
-                           seed + 1, backend)
-    fw = regression_forest(X, W, nt, honesty, min_node, alpha, sample_fraction, group,
-                           seed + 2, backend)
+    fy = fit_forest(X, KIND_REG, r1=Y, ntree=nt, seed=seed + 1, group=nuisance_group, **grf)
+    fw = fit_forest(X, KIND_REG, r1=W, ntree=nt, seed=seed + 2, group=nuisance_group, **grf)
     y_hat = fy.predict_raw(None, oob=True)
     w_hat = fw.predict_raw(None, oob=True)
     y_hat = np.where(np.isnan(y_hat), Y.mean(), y_hat)
     w_hat = np.where(np.isnan(w_hat), W.mean(), w_hat)
-    fc = fit_forest(X, KIND_CAUSAL, r1=W - w_hat, r2=Y - y_hat, ntree=num_trees, mtry=grf_mtry(p),
-                    min_node=min_node, sampling=1, honesty=honesty, group=group, mtry_poisson=True,
-                    alpha=alpha, sample_fraction=sample_fraction, seed=seed, backend=backend,
-                    edges=edges)
+    fc = fit_forest(X, KIND_CAUSAL, r1=W - w_hat, r2=Y - y_hat, ntree=num_trees, seed=seed,
+                    group=group, **grf)
     out = fc.predict_raw(None, oob=True)
     return CausalForestFit(fc, y_hat, w_hat, out[:, 0], out[:, 1], Y, W)
 

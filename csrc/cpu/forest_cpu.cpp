@@ -40,6 +40,76 @@ static std::vector<int> select_rows(const ForestParams& fp, const std::vector<in
   return out;
 }
 
+// The rows of tree tg: randomForest's bootstrap counts (sampling 0) or grf's samples
+// (sampling 1): with little bags (group > 1) the group's half-sample H (its rows are the
+// in-bag rows of every tree of the group), then the tree's subsample of
+// floor(|H| * sample_fraction * group) rows of H; with group == 1 the tree's subsample of
+// floor(n * sample_fraction) rows directly (grf's ci.group.size = 1: no half-sample);
+// with honesty the subsample's random half J1 grows the tree (w = 1) and the rest, J2,
+// fills the estimation statistics. Same Algorithm S streams as csrc/forest.hip /
+// csrc/forest_exact.hip.
+static void draw_rows(const ForestParams& fp, int tg, std::vector<int32_t>& w, uint8_t* inb,
+                      std::vector<int>& est_rows) {
+  const int n = fp.n;
+  if (fp.sampling == 0) {
+    for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)]++;
+    for (int i = 0; i < n; ++i) inb[i] = w[i] > 0;
+    return;
+  }
+  std::vector<int> all(n);
+  std::iota(all.begin(), all.end(), 0);
+  std::vector<int> S;
+  std::memset(inb, 0, n);
+  if (fp.group > 1) {
+    const int g = tg / fp.group;
+    std::vector<int> H = select_rows(fp, all, n / 2, (uint32_t)g);
+    for (int i : H) inb[i] = 1;
+    double f = fp.sample_fraction * fp.group;
+    if (f > 1.0) f = 1.0;
+    S = f >= 1.0 ? H : select_rows(fp, H, (int64_t)std::floor(H.size() * f), 0x10000u + (uint32_t)tg);
+  } else {
+    S = select_rows(fp, all, (int64_t)std::floor(n * fp.sample_fraction), 0x10000u + (uint32_t)tg);
+    for (int i : S) inb[i] = 1;
+  }
+  std::vector<int> J1 = S;
+  if (fp.honesty) {
+    J1 = select_rows(fp, S, (int64_t)(S.size() / 2), 0x20000u + (uint32_t)tg);
+    std::vector<uint8_t> in1(n, 0);
+    for (int i : J1) in1[i] = 1;
+    for (int i : S)
+      if (!in1[i]) est_rows.push_back(i);
+  } else {
+    est_rows = S;
+  }
+  for (int i : J1) w[i] = 1;
+}
+
+// grf estimation statistics of every node from the J2 (honest) rows: cnt, S1 (, S2, S11,
+// S12 for causal trees), summed along each row's path. BT: uint8 (binned) / uint16 (exact).
+template <typename BT>
+static void fill_est(const ForestParams& fp, const BT* Xb, const int64_t* r1, const int64_t* r2,
+                     const std::vector<int>& est_rows, const int32_t* feat, const int32_t* thr,
+                     const int32_t* left, int nnode, int64_t* est) {
+  std::memset(est, 0, sizeof(int64_t) * 5 * nnode);
+  for (int i : est_rows) {
+    int v = 0;
+    while (true) {
+      int64_t* e = est + (int64_t)v * 5;
+      e[0] += 1;
+      if (fp.kind == 1) {
+        e[1] += r1[i];
+      } else {
+        e[1] += r1[i];
+        e[2] += r2[i];
+        e[3] += to_fix(from_fix(r1[i]) * from_fix(r1[i]));
+        e[4] += to_fix(from_fix(r1[i]) * from_fix(r2[i]));
+      }
+      if (feat[v] < 0) break;
+      v = Xb[(int64_t)feat[v] * fp.n + i] <= thr[v] ? left[v] : left[v] + 1;
+    }
+  }
+}
+
 static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const uint8_t* ycls,
                       const int64_t* r1, const int64_t* r2, const Out& o) {
   const int n = fp.n, p = fp.p;
@@ -47,32 +117,7 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
   const int tg = fp.t0 + t;          // global tree id (RNG key)
   std::vector<int> est_rows;
   uint8_t* inb = o.inbag + (int64_t)t * n;
-  if (fp.sampling == 0) {
-    for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)]++;
-    for (int i = 0; i < n; ++i) inb[i] = w[i] > 0;
-  } else {
-    const int g = tg / fp.group;
-    std::vector<int> all(n);
-    std::iota(all.begin(), all.end(), 0);
-    std::vector<int> H = select_rows(fp, all, n / 2, (uint32_t)g);
-    std::memset(inb, 0, n);
-    for (int i : H) inb[i] = 1;
-    double f = fp.sample_fraction * fp.group;
-    if (f > 1.0) f = 1.0;
-    std::vector<int> S = f >= 1.0 ? H : select_rows(fp, H, (int64_t)std::floor(H.size() * f),
-                                                   0x10000u + (uint32_t)tg);
-    std::vector<int> J1 = S;
-    if (fp.honesty) {
-      J1 = select_rows(fp, S, (int64_t)(S.size() / 2), 0x20000u + (uint32_t)tg);
-      std::vector<uint8_t> in1(n, 0);
-      for (int i : J1) in1[i] = 1;
-      for (int i : S)
-        if (!in1[i]) est_rows.push_back(i);
-    } else {
-      est_rows = S;
-    }
-    for (int i : J1) w[i] = 1;
-  }
+  draw_rows(fp, tg, w, inb, est_rows);
   std::vector<int> idx;
   for (int i = 0; i < n; ++i)
     if (w[i] > 0) idx.push_back(i);
@@ -234,43 +279,29 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
   }
   o.nnodes[t] = next_id;
   // ---- grf: estimation statistics of every node from the J2 (honest) rows
-  if (fp.sampling == 1 && o.est) {
-    int64_t* est = o.est + base * 5;
-    std::memset(est, 0, sizeof(int64_t) * 5 * next_id);
-    for (int i : est_rows) {
-      int v = 0;
-      while (true) {
-        int64_t* e = est + (int64_t)v * 5;
-        e[0] += 1;
-        if (fp.kind == 1) {
-          e[1] += r1[i];
-        } else {
-          e[1] += r1[i];
-          e[2] += r2[i];
-          e[3] += to_fix(from_fix(r1[i]) * from_fix(r1[i]));
-          e[4] += to_fix(from_fix(r1[i]) * from_fix(r2[i]));
-        }
-        if (feat[v] < 0) break;
-        v = Xb[(int64_t)feat[v] * n + i] <= thr[v] ? left[v] : left[v] + 1;
-      }
-    }
-  }
+  if (fp.sampling == 1 && o.est)
+    fill_est(fp, Xb, r1, r2, est_rows, feat, thr, left, next_id, o.est + base * 5);
 }
 
-// Exact-split mode (forest_common.hpp::exact_threshold_bin; GPU twin csrc/forest_exact.hip):
-// uint16 value-rank bins, randomForest sampling (bootstrap), kinds 0/1. A node's candidate
-// feature is scanned over its rows sorted by (bin, row); the criterion is evaluated at every
-// boundary between two consecutive DISTINCT in-node values, in ascending order, with the same
-// integer statistics, formulas and (feature slot, position) tie-break as the binned engine.
+// Exact-split mode (GPU twin csrc/forest_exact.hip): uint16 value-rank bins. A node's
+// candidate feature is scanned over its rows sorted by (bin, row); the criterion is
+// evaluated at every boundary between two consecutive DISTINCT in-node values, in
+// ascending order, with the same integer statistics, formulas and (feature slot,
+// position) tie-break as the binned engine. randomForest sampling (0): kinds 0/1, the
+// threshold is the value midpoint (forest_common.hpp::exact_threshold_bin). grf sampling
+// (1): kinds 1/2 with half-samples, honesty and J2 estimation statistics; the threshold is
+// the left value itself (x <= v goes left). Kind 2 (causal) scans the node's pseudo-
+// outcomes rho with the per-position statistic 1 + treated * 2^32 (count and treated count
+// in one int64 prefix sum) so each child keeps >= 1 treated and >= 1 control row.
 static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, const double* vals,
                             int ldv, const int32_t* nval, const uint8_t* ycls, const int64_t* r1,
-                            const Out& o) {
+                            const int64_t* r2, const Out& o) {
   const int n = fp.n, p = fp.p;
   std::vector<int32_t> w(n, 0);
   const int tg = fp.t0 + t;
   uint8_t* inb = o.inbag + (int64_t)t * n;
-  for (int j = 0; j < n; ++j) w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)]++;
-  for (int i = 0; i < n; ++i) inb[i] = w[i] > 0;
+  std::vector<int> est_rows;
+  draw_rows(fp, tg, w, inb, est_rows);
   std::vector<int> idx;
   for (int i = 0; i < n; ++i)
     if (w[i] > 0) idx.push_back(i);
@@ -285,28 +316,50 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
   std::vector<int> tmp(m);
   std::vector<uint64_t> keys(m);
   std::vector<int> perm(p);
+  std::vector<int64_t> rho(fp.kind == 2 ? n : 0);
+  const int64_t LO32 = 0xffffffffll;
   for (int depth = 0; !cur.empty(); ++depth) {
     std::vector<Rng> nxt;
     for (const Rng& nd : cur) {
       const int v = nd.id;
-      int64_t nw = 0, n1 = 0, s1 = 0;
+      int64_t nw = 0, n1 = 0, s1 = 0, sw = 0, sy = 0, sww = 0, swy = 0;
       for (int q = nd.lo; q < nd.hi; ++q) {
         const int i = idx[q];
         nw += w[i];
         if (fp.kind == 0) n1 += (int64_t)w[i] * ycls[i];
-        else s1 += (int64_t)w[i] * r1[i];
+        else if (fp.kind == 1) s1 += (int64_t)w[i] * r1[i];
+        else {
+          sw += r1[i];
+          sy += r2[i];
+          sww += to_fix(from_fix(r1[i]) * from_fix(r1[i]));
+          swy += to_fix(from_fix(r1[i]) * from_fix(r2[i]));
+        }
       }
       const double dn = (double)nw;
       bool terminal = nw <= fp.min_node || depth >= MAX_DEPTH - 1;
       if (fp.kind == 0 && (n1 == 0 || n1 == nw)) terminal = true;
+      CausalNode cn{0, 0, 0, 0};
+      if (fp.kind == 2) {
+        cn = causal_node(dn, sw, sy, sww, swy);
+        if (!(cn.varw > 0.0)) terminal = true;
+      }
       int bf = -1, blo = -1, bhi = -1;
       if (!terminal) {
+        int64_t stot = s1;
+        if (fp.kind == 2) {
+          stot = 0;
+          for (int q = nd.lo; q < nd.hi; ++q) {
+            const int i = idx[q];
+            rho[i] = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
+            stot += rho[i];
+          }
+        }
         double parent;
         if (fp.kind == 0) {
           double a = (double)(nw - n1), b = (double)n1;
           parent = (a * a + b * b) / dn;
         } else {
-          double sd = from_fix(s1);
+          double sd = from_fix(stot);
           parent = (sd * sd) / dn;
         }
         const int minc = min_child(fp, dn);
@@ -316,6 +369,9 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
           uint32_t r = rand_below(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, k), (uint32_t)(p - k));
           std::swap(perm[k], perm[k + r]);
         }
+        int64_t ntreat = 0;
+        if (fp.kind == 2)
+          for (int q = nd.lo; q < nd.hi; ++q) ntreat += from_fix(r1[idx[q]]) > cn.wbar ? 1 : 0;
         double best = -INFINITY;
         const int cnt = nd.hi - nd.lo;
         for (int k = 0; k < nf; ++k) {
@@ -330,18 +386,25 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
             if (fp.kind == 0) {
               c0 += (int64_t)w[i] * (1 - ycls[i]);
               c1 += (int64_t)w[i] * ycls[i];
-            } else {
+            } else if (fp.kind == 1) {
               c0 += w[i];
               c1 += (int64_t)w[i] * r1[i];
+            } else {
+              c0 += 1 + ((from_fix(r1[i]) > cn.wbar ? 1ll : 0ll) << 32);
+              c1 += rho[i];
             }
             const int b = (int)(keys[s] >> 32), bn = (int)(keys[s + 1] >> 32);
             if (b == bn) continue;
-            const int64_t nl = fp.kind == 0 ? c0 + c1 : c0;
+            const int64_t nl = fp.kind == 0 ? c0 + c1 : (c0 & LO32);
             const int64_t nr = nw - nl;
             if (nl < minc || nr < minc) continue;
+            if (fp.kind == 2) {
+              const int64_t ct = c0 >> 32, tr = ntreat - ct;
+              if (ct < 1 || nl - ct < 1 || tr < 1 || nr - tr < 1) continue;
+            }
             const double crit = fp.kind == 0
                 ? gini_crit((double)c0, (double)c1, (double)(nw - n1 - c0), (double)(n1 - c1))
-                : mse_crit(from_fix(c1), (double)nl, from_fix(s1 - c1), (double)nr);
+                : mse_crit(from_fix(c1), (double)nl, from_fix(stot - c1), (double)nr);
             if (crit > best) {
               best = crit;
               bf = f;
@@ -362,12 +425,15 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
           else if (2 * n1 < nw) vote = 0;
           else vote = (int)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, 4095)) & 1u);
           val[v] = vote;
-        } else {
+        } else if (fp.kind == 1) {
           val[v] = from_fix(s1) / dn;
+        } else {
+          val[v] = 0.0;
         }
         continue;
       }
-      const int tb = exact_threshold_bin(vals + (int64_t)bf * ldv, nval[bf], blo, bhi);
+      const int tb = fp.sampling == 1 ? blo
+                                      : exact_threshold_bin(vals + (int64_t)bf * ldv, nval[bf], blo, bhi);
       const uint16_t* xf = Xb + (int64_t)bf * n;
       int nl = 0;
       for (int q = nd.lo; q < nd.hi; ++q)
@@ -387,20 +453,23 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
     cur.swap(nxt);
   }
   o.nnodes[t] = next_id;
+  if (fp.sampling == 1 && o.est)
+    fill_est(fp, Xb, r1, r2, est_rows, feat, thr, left, next_id, o.est + base * 5);
 }
 
 }  // namespace
 
 ATECPU_API int atecpu_forest_fit_exact(const ForestParams* fpp, const uint16_t* Xb, const double* vals,
                                        int ldv, const int32_t* nval, const uint8_t* ycls,
-                                       const int64_t* r1, int cap, int32_t* feat, int32_t* thr,
-                                       int32_t* left, double* val, int32_t* nnodes, uint8_t* inbag,
-                                       int nthreads) {
+                                       const int64_t* r1, const int64_t* r2, int cap, int32_t* feat,
+                                       int32_t* thr, int32_t* left, double* val, int32_t* nnodes,
+                                       uint8_t* inbag, int64_t* est, int nthreads) {
   const ForestParams fp = *fpp;
-  if (fp.p >= 4094 || fp.n <= 0 || fp.sampling != 0 || fp.kind == 2) return -1;
-  Out o{cap, feat, thr, left, val, nnodes, inbag, nullptr};
+  if (fp.p >= 4094 || fp.n <= 0) return -1;
+  if (fp.sampling == 0 ? fp.kind == 2 : (fp.kind == 0 || !est)) return -1;
+  Out o{cap, feat, thr, left, val, nnodes, inbag, est};
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
-  for (int t = 0; t < fp.ntree; ++t) grow_tree_exact(fp, t, Xb, vals, ldv, nval, ycls, r1, o);
+  for (int t = 0; t < fp.ntree; ++t) grow_tree_exact(fp, t, Xb, vals, ldv, nval, ycls, r1, r2, o);
   return 0;
 }
 

@@ -139,25 +139,38 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
     for (int i = tid; i < n; i += NT) inb[i] = S.w[i] > 0;
     if (tid == 0) sestn = 0;
   } else if (tid == 0) {
-    // Algorithm S (sequential by definition): group half-sample H, tree subsample S,
-    // honesty split J1 (grow) / J2 (estimate). tmp holds H, then S; est_rows holds J2.
-    const int g = tg / fp.group;
-    int nh = 0;
-    const int64_t kh = n / 2;
-    for (int i = 0; i < n && nh < kh; ++i)
-      if (select_next(fp.seed, (uint32_t)g, (uint64_t)i, (int64_t)(n - i), kh - nh)) S.tmp[nh++] = i;
+    // Algorithm S (sequential by definition): group half-sample H (group > 1), tree
+    // subsample S, honesty split J1 (grow) / J2 (estimate). tmp holds H, then S; est_rows
+    // holds J2. group == 1 (grf ci.group.size = 1): S drawn from all rows directly.
+    // Spec: cpu/forest_cpu.cpp draw_rows.
     for (int i = 0; i < n; ++i) inb[i] = 0;
-    for (int q = 0; q < nh; ++q) inb[S.tmp[q]] = 1;
-    double f = fp.sample_fraction * fp.group;
-    if (f > 1.0) f = 1.0;
-    int ns = nh;
-    if (f < 1.0) {
-      const int64_t ks = (int64_t)floor(nh * f);
+    int ns;
+    if (fp.group > 1) {
+      const int g = tg / fp.group;
+      int nh = 0;
+      const int64_t kh = n / 2;
+      for (int i = 0; i < n && nh < kh; ++i)
+        if (select_next(fp.seed, (uint32_t)g, (uint64_t)i, (int64_t)(n - i), kh - nh)) S.tmp[nh++] = i;
+      for (int q = 0; q < nh; ++q) inb[S.tmp[q]] = 1;
+      double f = fp.sample_fraction * fp.group;
+      if (f > 1.0) f = 1.0;
+      ns = nh;
+      if (f < 1.0) {
+        const int64_t ks = (int64_t)floor(nh * f);
+        int c = 0;
+        for (int q = 0; q < nh && c < ks; ++q)
+          if (select_next(fp.seed, 0x10000u + (uint32_t)tg, (uint64_t)q, (int64_t)(nh - q), ks - c))
+            S.tmp[c++] = S.tmp[q];
+        ns = c;
+      }
+    } else {
+      const int64_t ks = (int64_t)floor(n * fp.sample_fraction);
       int c = 0;
-      for (int q = 0; q < nh && c < ks; ++q)
-        if (select_next(fp.seed, 0x10000u + (uint32_t)tg, (uint64_t)q, (int64_t)(nh - q), ks - c))
-          S.tmp[c++] = S.tmp[q];
+      for (int i = 0; i < n && c < ks; ++i)
+        if (select_next(fp.seed, 0x10000u + (uint32_t)tg, (uint64_t)i, (int64_t)(n - i), ks - c))
+          S.tmp[c++] = i;
       ns = c;
+      for (int q = 0; q < ns; ++q) inb[S.tmp[q]] = 1;
     }
     int ne = 0;
     if (fp.honesty) {
@@ -761,6 +774,7 @@ __global__ __launch_bounds__(256) void forest_leaf16_kernel(ForestParams fp,
                                                             const int32_t* __restrict__ thr,
                                                             const int32_t* __restrict__ left,
                                                             const uint8_t* __restrict__ inbag,
+                                                            const int64_t* __restrict__ est,
                                                             int32_t* __restrict__ leaves) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int t = t0 + blockIdx.y;
@@ -768,10 +782,15 @@ __global__ __launch_bounds__(256) void forest_leaf16_kernel(ForestParams fp,
   int32_t* out = leaves + (int64_t)blockIdx.y * n2 + i;
   if (oob && inbag[(int64_t)t * fp.n + i]) { *out = -1; return; }
   const int64_t b = (int64_t)t * cap;
-  int v = 0;
-  while (feat[b + v] >= 0)
+  // grf (honest) trees predict from the deepest node on the path with J2 rows
+  const bool honest = fp.sampling == 1 && est;
+  int v = 0, last_ok = 0;
+  while (true) {
+    if (honest && est[(b + v) * 5] > 0) last_ok = v;
+    if (feat[b + v] < 0) break;
     v = Xb[(int64_t)feat[b + v] * n2 + i] <= thr[b + v] ? left[b + v] : left[b + v] + 1;
-  *out = v;
+  }
+  *out = honest ? last_ok : v;
 }
 
 // kind 0/1: running (sum, count) per row over trees in ascending order; per-tree values
@@ -949,17 +968,19 @@ ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob,
 }
 
 // exact-split forests: uint16 bins and the unpacked (feat, thr, left) arrays
+// est: grf estimation statistics (sampling 1), else null
 ATE_API int ate_forest_predict16(const void* fpp, const void* Xb, int n2, int oob, int cap,
                                  const void* feat, const void* thr, const void* left,
-                                 const void* val, const void* inbag, void* leaves, int tchunk,
-                                 void* state, void* out, int phases, void* stream) {
+                                 const void* val, const void* inbag, const void* est, void* leaves,
+                                 int tchunk, void* state, void* out, int phases, void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
+  if (fp.sampling == 1 && !est) return -1;
   hipStream_t st = (hipStream_t)stream;
-  return forest_predict_impl(fp, n2, cap, val, nullptr, leaves, tchunk, state, out, phases, st,
+  return forest_predict_impl(fp, n2, cap, val, est, leaves, tchunk, state, out, phases, st,
                              [&](dim3 g, int t0) {
     hipLaunchKernelGGL(forest_leaf16_kernel, g, dim3(256), 0, st, fp, (const uint16_t*)Xb, n2, oob,
                        cap, t0, (const int32_t*)feat, (const int32_t*)thr, (const int32_t*)left,
-                       (const uint8_t*)inbag, (int32_t*)leaves);
+                       (const uint8_t*)inbag, (const int64_t*)est, (int32_t*)leaves);
   });
 }
 

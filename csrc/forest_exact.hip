@@ -20,7 +20,11 @@
 //    scan, an argmax reduction;
 //  * child ids are assigned after the level in list order (a workgroup scan of the split
 //    flags), so numbering equals the host engine's.
-// Only randomForest sampling (bootstrap) and kinds 0/1 (classification, regression).
+// randomForest sampling (bootstrap; kinds 0/1, midpoint thresholds) and grf sampling (half-
+// samples, honesty, J2 estimation statistics; kinds 1/2, the left value as threshold):
+// grf's causal_forest / regression_forest split on exact values (ate_replication.Rmd:250).
+// Kind 2 scans the node's pseudo-outcomes rho with the per-position statistic 1 + treated
+// * 2^32 (count and treated count in one int64 prefix sum).
 #include "common.hpp"
 #include "forest_common.hpp"
 
@@ -79,6 +83,7 @@ struct XScratch {
   XRng* cur;        // [n + 1]
   XRng* nxt;        // [n + 1]
   XDec* dec;        // [n + 1]
+  int32_t* est;     // [n] grf J2 (estimation) rows
 };
 
 __host__ __device__ inline int np2(int n) {
@@ -91,7 +96,8 @@ __host__ __device__ inline int64_t align16(int64_t b) { return (b + 15) & ~(int6
 
 __host__ __device__ inline int64_t tree_bytes(int n) {
   return align16(8ll * n) * 2 + align16(4ll * n) * 2 + align16(4ll * np2(n)) +
-         align16(12ll * (n + 1)) * 2 + align16((int64_t)sizeof(XDec) * (n + 1));
+         align16(12ll * (n + 1)) * 2 + align16((int64_t)sizeof(XDec) * (n + 1)) +
+         align16(4ll * n);
 }
 
 __device__ XScratch scratch_at(char* base, int n) {
@@ -104,7 +110,8 @@ __device__ XScratch scratch_at(char* base, int n) {
   s.keys = (uint32_t*)p; p += align16(4ll * np2(n));
   s.cur = (XRng*)p; p += align16(12ll * (n + 1));
   s.nxt = (XRng*)p; p += align16(12ll * (n + 1));
-  s.dec = (XDec*)p;
+  s.dec = (XDec*)p; p += align16((int64_t)sizeof(XDec) * (n + 1));
+  s.est = (int32_t*)p;
   return s;
 }
 
@@ -137,7 +144,9 @@ __device__ __forceinline__ int64_t permute_i64(int dst_lane, int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-struct NodeStats { int64_t nw, n1, s1; };
+// nw rows (weighted), n1 class-1 weight (kind 0), s1 response / pseudo-outcome sum (kinds 1/2);
+// kind 2: ntreat rows above the node's mean treatment, cn the node's causal constants
+struct NodeStats { int64_t nw, n1, s1, ntreat; CausalNode cn; };
 
 // leaf value (forest_cpu.cpp grow_tree_exact): majority vote with a Philox coin on ties /
 // the node mean of the response
@@ -147,13 +156,24 @@ __device__ double leaf_value(const ForestParams& fp, int tg, int v, const NodeSt
     if (2 * st.n1 < st.nw) return 0.0;
     return (double)(rand_u32(fp.seed, P_RF_MTRY, (uint32_t)tg, node_index(v, 4095)) & 1u);
   }
+  if (fp.kind == 2) return 0.0;
   return from_fix(st.s1) / (double)st.nw;
 }
 
 __device__ bool is_terminal(const ForestParams& fp, const NodeStats& st, int depth) {
   bool terminal = st.nw <= fp.min_node || depth >= MAX_DEPTH - 1;
   if (fp.kind == 0 && (st.n1 == 0 || st.n1 == st.nw)) terminal = true;
+  if (fp.kind == 2 && !(st.cn.varw > 0.0)) terminal = true;
   return terminal;
+}
+
+// kind-2 node sums of one row (cpu/forest_cpu.cpp grow_tree_exact): W~, Y~, W~^2, W~ Y~
+__device__ __forceinline__ void causal_row(const int64_t* r1, const int64_t* r2, int i, int64_t& a,
+                                           int64_t& b, int64_t& c, int64_t& d) {
+  a = r1[i];
+  b = r2[i];
+  c = to_fix(from_fix(r1[i]) * from_fix(r1[i]));
+  d = to_fix(from_fix(r1[i]) * from_fix(r2[i]));
 }
 
 __device__ double parent_crit(const ForestParams& fp, const NodeStats& st) {
@@ -169,19 +189,28 @@ __device__ double parent_crit(const ForestParams& fp, const NodeStats& st) {
 // criterion at a boundary with left sums (c0, c1); -inf when a child is too small
 __device__ __forceinline__ double boundary_crit(const ForestParams& fp, const NodeStats& st, int minc,
                                                 int64_t c0, int64_t c1) {
-  const int64_t nl = fp.kind == 0 ? c0 + c1 : c0;
+  const int64_t nl = fp.kind == 0 ? c0 + c1 : (fp.kind == 2 ? (c0 & 0xffffffffll) : c0);
   const int64_t nr = st.nw - nl;
   if (nl < minc || nr < minc) return -INFINITY;
+  if (fp.kind == 2) {                  // each child keeps >= 1 treated and >= 1 control row
+    const int64_t ct = c0 >> 32, tr = st.ntreat - ct;
+    if (ct < 1 || nl - ct < 1 || tr < 1 || nr - tr < 1) return -INFINITY;
+  }
   return fp.kind == 0
       ? gini_crit((double)c0, (double)c1, (double)(st.nw - st.n1 - c0), (double)(st.n1 - c1))
       : mse_crit(from_fix(c1), (double)nl, from_fix(st.s1 - c1), (double)nr);
 }
 
-// per-row statistics in scan order: kind 0 (w (1-y), w y), kind 1 (w, w r1)
+// per-row statistics in scan order: kind 0 (w (1-y), w y), kind 1 (w, w r1), kind 2
+// (1 + treated 2^32, rho)
 __device__ __forceinline__ void row_stats(const ForestParams& fp, const int32_t* w, const uint8_t* ycls,
-                                          const int64_t* r1, int i, int64_t& a0, int64_t& a1) {
+                                          const int64_t* r1, const int64_t* r2, const CausalNode& cn,
+                                          int i, int64_t& a0, int64_t& a1) {
   const int64_t wi = w[i];
-  if (fp.kind == 0) {
+  if (fp.kind == 2) {
+    a0 = 1 + ((from_fix(r1[i]) > cn.wbar ? 1ll : 0ll) << 32);
+    a1 = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
+  } else if (fp.kind == 0) {
     const int64_t y = ycls[i];
     a0 = wi * (1 - y);
     a1 = wi * y;
@@ -273,9 +302,10 @@ __device__ void wave_bitonic(uint32_t* K, int N2, int lane) {
 __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const double* __restrict__ vals,
     int ldv, const int32_t* __restrict__ nval, const uint8_t* __restrict__ ycls,
-    const int64_t* __restrict__ r1, int cap, int32_t* __restrict__ feat, int32_t* __restrict__ thr,
-    int32_t* __restrict__ left, double* __restrict__ val, int32_t* __restrict__ nnodes,
-    uint8_t* __restrict__ inbag, char* __restrict__ scratch) {
+    const int64_t* __restrict__ r1, const int64_t* __restrict__ r2, int cap,
+    int32_t* __restrict__ feat, int32_t* __restrict__ thr, int32_t* __restrict__ left,
+    double* __restrict__ val, int32_t* __restrict__ nnodes, uint8_t* __restrict__ inbag,
+    int64_t* __restrict__ est_o, char* __restrict__ scratch) {
   // one LDS key buffer: the whole of it for a workgroup-level node, a quarter (WCAP keys)
   // per wave for the wave-level nodes (the two phases never overlap)
   __shared__ __attribute__((aligned(16))) char sarena[ARENA];
@@ -283,9 +313,9 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
   __shared__ int sperm[XW][XPMAX];
   __shared__ double sredc[XW];
   __shared__ int sreds[XW];
-  __shared__ int64_t sred64[3][XW];
+  __shared__ int64_t sred64[5][XW];
   __shared__ int scnt[XW + 1];
-  __shared__ int sncur, snext_id, sm, snbig;
+  __shared__ int sncur, snext_id, sm, snbig, sestn;
   __shared__ int sbig[XBIG];                  // this level's workgroup-level nodes
   const int t = tbeg + blockIdx.x;            // tree within this forest
   const int tg = fp.t0 + t;                   // global tree id (RNG key)
@@ -303,17 +333,73 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
   int64_t* Xw0 = (int64_t*)(wsl + WCAP * 4);
   int64_t* Xw1 = Xw0 + WCAP;
 
-  // ---- bootstrap weights (integer atomics: order-free), in-bag mask, row list
+  // ---- weights: bootstrap counts (integer atomics: order-free), or grf's samples (Algorithm
+  // S, sequential by definition, thread 0; cpu/forest_cpu.cpp draw_rows): the group's
+  // half-sample (its rows are the in-bag rows), the tree's subsample, J1 (w = 1) / J2 (est)
   for (int i = tid; i < n; i += XT) S.w[i] = 0;
   __syncthreads();
-  for (int j = tid; j < n; j += XT)
-    atomicAdd(&S.w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)], 1);
+  if (fp.sampling == 0) {
+    for (int j = tid; j < n; j += XT)
+      atomicAdd(&S.w[rand_below(fp.seed, P_RF_BOOT, (uint32_t)tg, (uint64_t)j, (uint32_t)n)], 1);
+    if (tid == 0) sestn = 0;
+  } else if (tid == 0) {
+    int32_t* tmp = (int32_t*)S.keys;            // >= n entries, free until the first level
+    for (int i = 0; i < n; ++i) inb[i] = 0;
+    int ns;
+    if (fp.group > 1) {
+      const int g = tg / fp.group;
+      int nh = 0;
+      const int64_t kh = n / 2;
+      for (int i = 0; i < n && nh < kh; ++i)
+        if (select_next(fp.seed, (uint32_t)g, (uint64_t)i, (int64_t)(n - i), kh - nh)) tmp[nh++] = i;
+      for (int q = 0; q < nh; ++q) inb[tmp[q]] = 1;
+      double f = fp.sample_fraction * fp.group;
+      if (f > 1.0) f = 1.0;
+      ns = nh;
+      if (f < 1.0) {
+        const int64_t ks = (int64_t)floor(nh * f);
+        int c = 0;
+        for (int q = 0; q < nh && c < ks; ++q)
+          if (select_next(fp.seed, 0x10000u + (uint32_t)tg, (uint64_t)q, (int64_t)(nh - q), ks - c))
+            tmp[c++] = tmp[q];
+        ns = c;
+      }
+    } else {
+      const int64_t ks = (int64_t)floor(n * fp.sample_fraction);
+      int c = 0;
+      for (int i = 0; i < n && c < ks; ++i)
+        if (select_next(fp.seed, 0x10000u + (uint32_t)tg, (uint64_t)i, (int64_t)(n - i), ks - c))
+          tmp[c++] = i;
+      ns = c;
+      for (int q = 0; q < ns; ++q) inb[tmp[q]] = 1;
+    }
+    int ne = 0;
+    if (fp.honesty) {
+      const int64_t k1 = ns / 2;
+      int c = 0;
+      for (int q = 0; q < ns; ++q) {
+        const int i = tmp[q];
+        if (c < k1 && select_next(fp.seed, 0x20000u + (uint32_t)tg, (uint64_t)q, (int64_t)(ns - q), k1 - c)) {
+          S.w[i] = 1;
+          ++c;
+        } else {
+          S.est[ne++] = i;
+        }
+      }
+    } else {
+      for (int q = 0; q < ns; ++q) {
+        S.w[tmp[q]] = 1;
+        S.est[ne++] = tmp[q];
+      }
+    }
+    sestn = ne;
+  }
   __syncthreads();
   int m = 0;                                  // uniform running count
   for (int c0 = 0; c0 < n; c0 += XT) {
     const int i = c0 + tid;
     const bool in = i < n && S.w[i] > 0;
-    if (i < n) inb[i] = in;
+    if (i < n && fp.sampling == 0) inb[i] = in;
     const uint64_t b = __ballot(in);
     if (lane == 0) scnt[wid] = __popcll(b);
     __syncthreads();
@@ -371,22 +457,35 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       const int j = sbig[jb];
       const XRng nd = S.cur[j];
       const int cnt = nd.hi - nd.lo;
-      // node statistics
-      int64_t a = 0, b1 = 0, c = 0;
+      // node statistics (kind 2: n, SW, SY, SWW, SWY -> the node's causal constants)
+      int64_t a = 0, b1 = 0, c = 0, d2 = 0, e2 = 0;
       for (int q = nd.lo + tid; q < nd.hi; q += XT) {
         const int i = S.idx[q];
         a += S.w[i];
         if (fp.kind == 0) b1 += (int64_t)S.w[i] * ycls[i];
-        else c += (int64_t)S.w[i] * r1[i];
+        else if (fp.kind == 1) c += (int64_t)S.w[i] * r1[i];
+        else {
+          int64_t x, y, z, u;
+          causal_row(r1, r2, i, x, y, z, u);
+          b1 += x; c += y; d2 += z; e2 += u;
+        }
       }
       a = wave_sum64(a); b1 = wave_sum64(b1); c = wave_sum64(c);
-      if (lane == 0) { sred64[0][wid] = a; sred64[1][wid] = b1; sred64[2][wid] = c; }
-      __syncthreads();
-      NodeStats st{0, 0, 0};
-      for (int q = 0; q < XW; ++q) {
-        st.nw += sred64[0][q]; st.n1 += sred64[1][q]; st.s1 += sred64[2][q];
+      d2 = wave_sum64(d2); e2 = wave_sum64(e2);
+      if (lane == 0) {
+        sred64[0][wid] = a; sred64[1][wid] = b1; sred64[2][wid] = c;
+        sred64[3][wid] = d2; sred64[4][wid] = e2;
       }
-      __syncthreads();                        // sred64 reused by the next node
+      __syncthreads();
+      NodeStats st{0, 0, 0, 0, CausalNode{0, 0, 0, 0}};
+      int64_t tot[5] = {0, 0, 0, 0, 0};
+      for (int q = 0; q < XW; ++q)
+        for (int r = 0; r < 5; ++r) tot[r] += sred64[r][q];
+      __syncthreads();                        // sred64 reused below / by the next node
+      st.nw = tot[0];
+      if (fp.kind == 0) st.n1 = tot[1];
+      else if (fp.kind == 1) st.s1 = tot[2];
+      else st.cn = causal_node((double)tot[0], tot[1], tot[2], tot[3], tot[4]);
       if (is_terminal(fp, st, depth)) {
         if (tid == 0) S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
         continue;
@@ -406,14 +505,29 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       const int N2 = np2(cnt);
       uint32_t* K = N2 <= XLDS ? skeys : S.keys;
       // per-position statistics once per node (the feature loop reads them by sorted key)
+      int64_t srho = 0, stre = 0;
       for (int qb = tid; qb < cnt; qb += XT * 8) {
         int iv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) iv[u] = qb + u * XT < cnt ? S.idx[nd.lo + qb + u * XT] : 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-          if (qb + u * XT < cnt)
-            row_stats(fp, S.w, ycls, r1, iv[u], S.sx0[nd.lo + qb + u * XT], S.sx1[nd.lo + qb + u * XT]);
+          if (qb + u * XT < cnt) {
+            int64_t x0, x1;
+            row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
+            S.sx0[nd.lo + qb + u * XT] = x0;
+            S.sx1[nd.lo + qb + u * XT] = x1;
+            srho += x1;
+            stre += x0 >> 32;
+          }
+      }
+      if (fp.kind == 2) {                     // rho sum and treated count of the node
+        srho = wave_sum64(srho); stre = wave_sum64(stre);
+        if (lane == 0) { sred64[0][wid] = srho; sred64[1][wid] = stre; }
+        __syncthreads();
+        st.s1 = 0; st.ntreat = 0;
+        for (int q = 0; q < XW; ++q) { st.s1 += sred64[0][q]; st.ntreat += sred64[1][q]; }
+        __syncthreads();
       }
       double best = -INFINITY;                // thread 0's running best over features
       int bf = -1, blo = -1, bhi = -1, bnl = 0;
@@ -539,7 +653,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       if (tid == 0) {
         const double parent = parent_crit(fp, st);
         if (bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent)))
-          S.dec[j] = XDec{1, bf, exact_threshold_bin(vals + (int64_t)bf * ldv, nval[bf], blo, bhi),
+          S.dec[j] = XDec{1, bf, fp.sampling == 1 ? blo
+                                 : exact_threshold_bin(vals + (int64_t)bf * ldv, nval[bf], blo, bhi),
                           bnl, 0.0};
         else
           S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
@@ -564,17 +679,27 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           // ---- a row per lane: ranks by lane compares, sorted order by ds_permute
           const bool live = lane < cnt;
           const int i = live ? S.idx[nd.lo + lane] : 0;
+          NodeStats st{0, 0, 0, 0, CausalNode{0, 0, 0, 0}};
+          if (fp.kind == 2) {                 // the node's causal constants first
+            int64_t ca = 0, cb = 0, cc = 0, cd = 0;
+            if (live) causal_row(r1, r2, i, ca, cb, cc, cd);
+            st.nw = wave_sum64(live ? 1 : 0);
+            st.cn = causal_node((double)st.nw, wave_sum64(ca), wave_sum64(cb), wave_sum64(cc),
+                                wave_sum64(cd));
+          }
           int64_t x0 = 0, x1 = 0;
-          if (live) row_stats(fp, S.w, ycls, r1, i, x0, x1);
-          NodeStats st;
+          if (live) row_stats(fp, S.w, ycls, r1, r2, st.cn, i, x0, x1);
           if (fp.kind == 0) {
             st.nw = wave_sum64(x0 + x1);
             st.n1 = wave_sum64(x1);
             st.s1 = 0;
-          } else {
+          } else if (fp.kind == 1) {
             st.nw = wave_sum64(x0);
             st.n1 = 0;
             st.s1 = wave_sum64(x1);
+          } else {
+            st.s1 = wave_sum64(x1);
+            st.ntreat = wave_sum64(x0 >> 32);
           }
           if (is_terminal(fp, st, depth)) {
             if (lane == 0) S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
@@ -631,7 +756,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           }
           const double parent = parent_crit(fp, st);
           const bool split = bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent));
-          const int tb = split ? wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane) : -1;
+          const int tb = !split ? -1 : fp.sampling == 1 ? blo
+                                : wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane);
           if (lane == 0)
             S.dec[j] = split ? XDec{1, bf, tb, bnl, 0.0}
                              : XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
@@ -643,21 +769,34 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         int iv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) iv[u] = lane + 64 * u < cnt ? S.idx[nd.lo + lane + 64 * u] : 0;
+        NodeStats st{0, 0, 0, 0, CausalNode{0, 0, 0, 0}};
+        if (fp.kind == 2) {                   // the node's causal constants first
+          int64_t ca = 0, cb = 0, cc = 0, cd = 0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (lane + 64 * u < cnt) {
+              int64_t x, y, z, v2;
+              causal_row(r1, r2, iv[u], x, y, z, v2);
+              ca += x; cb += y; cc += z; cd += v2;
+            }
+          st.cn = causal_node((double)cnt, wave_sum64(ca), wave_sum64(cb), wave_sum64(cc),
+                              wave_sum64(cd));
+        }
         int64_t a = 0, b1 = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int q = lane + 64 * u;
           if (q < cnt) {
             int64_t x0, x1;
-            row_stats(fp, S.w, ycls, r1, iv[u], x0, x1);
+            row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
             Xw0[q] = x0; Xw1[q] = x1;
             a += x0; b1 += x1;
           }
         }
         a = wave_sum64(a); b1 = wave_sum64(b1);
-        NodeStats st;
         if (fp.kind == 0) { st.nw = a + b1; st.n1 = b1; st.s1 = 0; }
-        else { st.nw = a; st.n1 = 0; st.s1 = b1; }
+        else if (fp.kind == 1) { st.nw = a; st.n1 = 0; st.s1 = b1; }
+        else { st.nw = a & 0xffffffffll; st.ntreat = a >> 32; st.s1 = b1; }
         if (is_terminal(fp, st, depth)) {
           if (lane == 0) S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
           continue;
@@ -714,7 +853,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         }
         const double parent = parent_crit(fp, st);
         const bool split = bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent));
-        const int tb = split ? wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane) : -1;
+        const int tb = !split ? -1 : fp.sampling == 1 ? blo
+                              : wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane);
         if (lane == 0)
           S.dec[j] = split ? XDec{1, bf, tb, bnl, 0.0}
                            : XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
@@ -828,6 +968,37 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     __syncthreads();
   }
   if (tid == 0) nnodes[t] = snext_id;
+  // ---- grf: estimation statistics of every node from the J2 (honest) rows (order-free
+  // int64 atomics; cpu/forest_cpu.cpp fill_est)
+  if (fp.sampling == 1 && est_o) {
+    __syncthreads();
+    const int nn = snext_id;
+    int64_t* est = est_o + base * 5;
+    for (int e = tid; e < nn * 5; e += XT) est[e] = 0;
+    __syncthreads();
+    const int ne = sestn;
+    for (int q = tid; q < ne; q += XT) {
+      const int i = S.est[q];
+      int v = 0;
+      while (true) {
+        ATE_DASSERT(v >= 0 && v < nn);
+        int64_t* e = est + (int64_t)v * 5;
+        atomicAdd((unsigned long long*)&e[0], 1ull);
+        if (fp.kind == 1) {
+          atomicAdd((unsigned long long*)&e[1], (unsigned long long)r1[i]);
+        } else {
+          int64_t x, y, z, u;
+          causal_row(r1, r2, i, x, y, z, u);
+          atomicAdd((unsigned long long*)&e[1], (unsigned long long)x);
+          atomicAdd((unsigned long long*)&e[2], (unsigned long long)y);
+          atomicAdd((unsigned long long*)&e[3], (unsigned long long)z);
+          atomicAdd((unsigned long long*)&e[4], (unsigned long long)u);
+        }
+        if (tfeat[v] < 0) break;
+        v = Xb[(int64_t)tfeat[v] * n + i] <= tthr[v] ? tleft[v] : tleft[v] + 1;
+      }
+    }
+  }
 }
 
 }  // namespace
@@ -837,18 +1008,21 @@ ATE_API int64_t ate_forest_exact_scratch_bytes(int n, int ntree) {
 }
 
 // Grow trees [tbeg, tbeg + ntree_chunk) of the forest (scratch: ntree_chunk trees).
+// grf sampling (fp.sampling == 1, kinds 1/2) needs est ([ntree * cap][5] int64).
 ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, const void* Xb,
                                  const void* vals, int ldv, const void* nval, const void* ycls,
-                                 const void* r1, int cap, void* feat, void* thr, void* left,
-                                 void* val, void* nnodes, void* inbag, void* scratch, void* stream) {
+                                 const void* r1, const void* r2, int cap, void* feat, void* thr,
+                                 void* left, void* val, void* nnodes, void* inbag, void* est,
+                                 void* scratch, void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
-  if (fp.p > XPMAX || fp.n <= 0 || fp.n > 65536 || fp.sampling != 0 || fp.kind == 2) return -1;
+  if (fp.p > XPMAX || fp.n <= 0 || fp.n > 65536) return -1;
+  if (fp.sampling == 0 ? fp.kind == 2 : (fp.kind == 0 || !est || (fp.kind == 2 && !r2))) return -1;
   if (tbeg < 0 || nchunk < 1 || tbeg + nchunk > fp.ntree) return -1;
   hipLaunchKernelGGL(forest_exact_kernel, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
                      (const uint16_t*)Xb, (const double*)vals, ldv, (const int32_t*)nval,
-                     (const uint8_t*)ycls, (const int64_t*)r1, cap, (int32_t*)feat, (int32_t*)thr,
-                     (int32_t*)left, (double*)val, (int32_t*)nnodes, (uint8_t*)inbag,
-                     (char*)scratch);
+                     (const uint8_t*)ycls, (const int64_t*)r1, (const int64_t*)r2, cap,
+                     (int32_t*)feat, (int32_t*)thr, (int32_t*)left, (double*)val, (int32_t*)nnodes,
+                     (uint8_t*)inbag, (int64_t*)est, (char*)scratch);
   ATE_CHECK_LAUNCH();
   return 0;
 }

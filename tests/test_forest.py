@@ -262,3 +262,61 @@ def test_exact_splits_new_data_prediction_uses_midpoints():
     assert (nn == 3).all() and (thr[::fr.cap] == 1).all()     # bins 0,1 | 2,3: at 2.5
     np.testing.assert_array_equal(fr.predict_proba(np.array([[0.0], [1.0], [4.0], [5.0]])),
                                   [0, 0, 1, 1])
+
+
+def test_grf_exact_splits_use_the_left_value_as_threshold():
+    """grf splits x <= v (the value itself), randomForest at the midpoint: a regression
+    step between the table values 1 and 4 goes to bin 1 in both, but a NEW row x = 2.2
+    (below the midpoint 2.5, above the value 1) goes left under randomForest and right
+    under grf (ate_replication.Rmd:250: grf::causal_forest's orthogonalisation forests)."""
+    x = np.array([0.0, 1.0, 4.0, 5.0] * 200)[:, None]
+    y = np.where(x[:, 0] > 2, 1.0, 0.0)
+    g = F.regression_forest(x, y, num_trees=8, seed=3, backend="cpu", splits="exact",
+                            min_node=1, alpha=0.0)
+    feat, thr, _, _, nn = g.tree_arrays()
+    assert (thr[::g.cap][feat[::g.cap] >= 0] == 1).all()         # root split after value 1
+    assert g.predict_proba(np.array([[2.2]]))[0] == pytest.approx(1.0)
+    assert g.predict_proba(np.array([[0.5]]))[0] == pytest.approx(0.0)
+    r = F.fit_forest(x, F.KIND_REG, r1=y, ntree=8, seed=3, backend="cpu", splits="exact")
+    assert r.predict_proba(np.array([[2.2]]))[0] == pytest.approx(0.0)
+
+
+def test_grf_sampling_little_bags_and_group_one():
+    """grf's samples: with little bags (ci.group.size = 2) both trees of a group share the
+    group's half-sample as in-bag rows; with ci.group.size = 1 (grf's Y.hat / W.hat
+    forests) each tree's in-bag rows are its own floor(n * sample.fraction) subsample;
+    with honesty the J2 half fills the estimation counts (root count = |J2|)."""
+    r = np.random.default_rng(1)
+    n = 2001
+    X = r.normal(size=(n, 4))
+    y = X[:, 0] + r.normal(size=n)
+    g2 = F.fit_forest(X, F.KIND_REG, r1=y, ntree=4, sampling=1, honesty=True, group=2,
+                      min_node=5, seed=7, backend="cpu", splits="exact")
+    ib = np.asarray(g2.inbag).reshape(4, n)
+    assert (ib.sum(1) == n // 2).all()
+    np.testing.assert_array_equal(ib[0], ib[1])
+    np.testing.assert_array_equal(ib[2], ib[3])
+    assert (ib[0] != ib[2]).any()
+    est = np.asarray(g2.est).reshape(4, g2.cap, 5)
+    assert (est[:, 0, 0] == (n // 2) - (n // 2) // 2).all()      # J2 = |S| - |J1|
+    g1 = F.fit_forest(X, F.KIND_REG, r1=y, ntree=4, sampling=1, honesty=True, group=1,
+                      min_node=5, seed=7, backend="cpu", splits="exact")
+    ib1 = np.asarray(g1.inbag).reshape(4, n)
+    assert (ib1.sum(1) == n // 2).all() and (ib1[0] != ib1[1]).any()
+
+
+def test_causal_forest_auto_uses_exact_splits_at_tutorial_scale():
+    """causal_forest(splits="auto") grows grf's exact-split honest forests up to 65,536 rows
+    (the exact engine's uint16 value ranks) and recovers a heterogeneous effect."""
+    r = np.random.default_rng(5)
+    n = 3000
+    X = r.normal(size=(n, 5))
+    W = (r.uniform(size=n) < 0.5).astype(float)
+    tau = 1.0 + (X[:, 0] > 0)
+    Y = X[:, 1] + tau * W + 0.3 * r.normal(size=n)
+    cf = F.causal_forest(X, Y, W, num_trees=200, seed=3, backend="cpu")
+    assert cf.forest.exact is not None and cf.forest.params.sampling == 1
+    ate, se = F.average_treatment_effect(cf)
+    assert abs(ate - tau.mean()) < 4 * se + 0.05
+    hi, lo = cf.tau_oob[X[:, 0] > 0.5], cf.tau_oob[X[:, 0] < -0.5]
+    assert np.nanmean(hi) - np.nanmean(lo) > 0.5

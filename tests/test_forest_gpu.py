@@ -178,3 +178,32 @@ def test_exact_split_engine_bit_identical_to_host(gpu, case, n):
     assert_same_forest(g, c)
     np.testing.assert_array_equal(g.oob_proba(), c.oob_proba())
     np.testing.assert_array_equal(g.predict_proba(X[:700]), c.predict_proba(X[:700]))
+
+
+@pytest.mark.parametrize("n", [3000, 20000])
+@pytest.mark.parametrize("case", ["grf_reg_g1", "grf_reg_g2", "grf_causal"])
+def test_exact_grf_engine_bit_identical_to_host(gpu, case, n):
+    """grf semantics on the exact-split engine: half-samples / little bags
+    (group 2) or direct subsamples (group 1, grf's orthogonalisation forests), honesty with
+    the J2 estimation statistics, kind-2 causal splits on pseudo-outcomes with the
+    treated / control constraint, the left value as threshold -- csrc/forest_exact.hip grows
+    the host twin's trees and estimation statistics bit for bit; OOB predictions (honest
+    leaves, little-bag variance) match."""
+    r = np.random.default_rng(12)
+    X = r.normal(size=(n, 6))
+    X[:, 2] = np.round(X[:, 2] * 2)             # ties
+    W = (r.uniform(size=n) < 1 / (1 + np.exp(-X[:, 0]))).astype(float)
+    Y = X[:, 1] + W * (1 + (X[:, 0] > 0)) + 0.5 * r.normal(size=n)
+    grf = dict(ntree=8, seed=21, splits="exact", sampling=1, honesty=True, mtry_poisson=True,
+               min_node=5, alpha=0.05, sample_fraction=0.5, mtry=F.grf_mtry(6))
+    if case == "grf_reg_g1":
+        grf.update(kind=F.KIND_REG, r1=Y, group=1)
+    elif case == "grf_reg_g2":
+        grf.update(kind=F.KIND_REG, r1=W, group=2)
+    else:
+        grf.update(kind=F.KIND_CAUSAL, r1=W - W.mean(), r2=Y - Y.mean(), group=2)
+    g = F.fit_forest(X, backend="gpu", **grf)
+    c = F.fit_forest(X, backend="cpu", **grf)
+    assert_same_forest(g, c)
+    np.testing.assert_array_equal(g.est.cpu().numpy(), np.asarray(c.est))
+    np.testing.assert_array_equal(g.predict_raw(None, oob=True), c.predict_raw(None, oob=True))
