@@ -1,0 +1,80 @@
+#!/bin/bash
+# One parameterised GPU-box session (replaces the per-session tools/gpu_r0*.sh scripts).
+#
+#   bash tools/gpu_session.sh OUT step [step ...]        (run by gpurun from the repo root)
+#
+# Every step runs under its own time limit; the session stops at the first failure
+# (a GPU fault / abort / time limit ends it: nothing more runs on the GPU). Outputs go to
+# gpurun_out/OUT/. Steps:
+#   tests          the whole GPU suite (pytest -m gpu)
+#   tests:EXPR     GPU tests selected by -k EXPR
+#   debugtests     the GPU suite on the device-assertion build (ATE_DEBUG=1, _build.py)
+#   smoke          __graft_entry__.smoke()
+#   bench          bench.py (driver defaults), one JSON line
+#   prof           rocprofv3 kernel trace + stats of a short bench, and the overlap timeline
+#   enet_ab:A,B,.. CV-LASSO stage alone for libatehip_<A>.so, ... ("new" = in-tree), x2
+#   enet_prof      cycle accounting of the path kernel (tools/enet_profile.py build)
+#   cfg3           config-3 per-GPU shard (N=1e7, p=500, 100 trees, rank 0 of 8)
+#   cfg5           config-5 per-GPU shard (N=1.25e7, p=2000, 100 trees)
+#   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
+#   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
+set -o pipefail
+OUT=gpurun_out/$1; shift
+mkdir -p "$OUT"
+ROOT=$(pwd)
+export TMPDIR=/tmp
+
+run() {   # run NAME LIMIT CMD...: time-limited step, log to $OUT/NAME.log, stop on failure
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "[$name] failed rc=$rc"; tail -25 "$OUT/$name.log"; exit $rc
+  fi
+  echo "[$name] ok: $(tail -1 "$OUT/$name.log" | cut -c1-400)"
+}
+
+for step in "$@"; do
+  case $step in
+    tests)
+      run tests 1500 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
+    tests:*)
+      run "tests_${step#tests:}" 900 python -u -m pytest tests -m gpu -x -v --timeout 240 \
+          --timeout-method thread -k "${step#tests:}" ;;
+    debugtests)
+      ATE_DEBUG=1 run debugtests 1500 python -u -m pytest tests -m gpu -x -q --timeout 240 \
+          --timeout-method thread ;;
+    smoke)
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)
+      run bench 300 python bench.py ;;
+    prof)
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 \
+          > "$ROOT/$OUT/prof.log" 2>&1 ) || { echo "[prof] failed"; tail -20 "$OUT/prof.log"; exit 1; }
+      python3 -c "import sys; sys.path.insert(0, 'tools'); import timeline; timeline.overlapped(sys.argv[1], 24)" \
+          $(find "$OUT/prof" -name "*kernel_trace.csv") > "$OUT/prof_timeline.txt" 2>&1 || true
+      echo "[prof] ok" ;;
+    enet_ab:*)
+      IFS=, read -ra libs <<< "${step#enet_ab:}"
+      for rep in 1 2; do
+        for nm in "${libs[@]}"; do
+          lib=ate_replication_causalml_amd/_lib/libatehip_$nm.so
+          [ "$nm" = new ] && lib=ate_replication_causalml_amd/_lib/libatehip.so
+          ATE_HIP_LIB=$ROOT/$lib run "enet_${nm}_$rep" 120 python tools/enet_only.py 15
+        done
+      done ;;
+    enet_prof)
+      run enet_prof 300 python tools/enet_profile.py ;;
+    cfg3)
+      run cfg3 300 python -u tools/cfg3.py --rows 10000000 --cols 500 --trees 100 --shard 0/8 ;;
+    cfg5)
+      run cfg5 400 python -u tools/cfg5.py --rows 100000000 --cols 2000 --trees 100 --shard 0/8 ;;
+    configs)
+      run configs 900 python -u tools/bench_configs.py ;;
+    replicate)
+      run replicate 600 python -u tools/replicate_timing.py ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
