@@ -553,6 +553,7 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
         for (int g0 = 0; g0 < fp.ntree; g0 += fp.group) {
           double ps = 0, pss = 0;
           int nb = 0;
+          const int gsz = g0 + fp.group <= fp.ntree ? fp.group : fp.ntree - g0;
           for (int t = g0; t < g0 + fp.group && t < fp.ntree; ++t) {
             const int64_t nd = leaf_of(t);
             if (nd < 0) continue;
@@ -562,7 +563,7 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
             const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
             ps += psi; pss += psi * psi; ++nb;
           }
-          if (nb == 0) continue;
+          if (nb == 0 || nb < gsz) continue;   // grf: complete groups only
           const double pg = ps / nb;
           gs += to_fix(pg); gss += to_fix(pg * pg); ng += 1;
           if (nb >= 2) { within += to_fix(pss / nb - pg * pg); nwithin += 1; }
@@ -589,7 +590,7 @@ static int predict_impl(const ForestParams* fpp, const BT* Xb, int n2, int oob, 
             const double between = from_fix(st[6 * n2 + i]) / ng - mean * mean;
             const double nw = (double)st[8 * n2 + i];
             const double wc = nw > 0 ? from_fix(st[7 * n2 + i]) / nw / (double)(fp.group > 1 ? fp.group - 1 : 1) : 0.0;
-            var = std::fmax(between - wc, 0.0) / (H * H);
+            var = grf_debias(between, wc, ng) / (H * H);
           }
         }
       }
@@ -619,4 +620,10 @@ ATECPU_API int atecpu_forest_predict16(const ForestParams* fpp, const uint16_t* 
                                        int phases, double* out, int nthreads) {
   return predict_impl(fpp, Xb, n2, oob, cap, feat, thr, left, val, inbag, est, state, phases, out,
                       nthreads);
+}
+
+// the little-bag variance debiaser alone (forest_common.hpp grf_debias; tests check it
+// against scipy's normal density / CDF)
+ATECPU_API double atecpu_grf_debias(double between, double noise, double groups) {
+  return grf_debias(between, noise, groups);
 }

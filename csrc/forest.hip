@@ -854,6 +854,7 @@ __global__ __launch_bounds__(256) void forest_cate2_kernel(ForestParams fp, int 
   for (int g0 = 0; g0 < nt; g0 += fp.group) {
     double ps = 0, pss = 0;
     int nb = 0;
+    const int gsz = g0 + fp.group <= nt ? fp.group : nt - g0;
     for (int tt = g0; tt < g0 + fp.group && tt < nt; ++tt) {
       const int lf = leaves[(int64_t)tt * n2 + i];
       if (lf < 0) continue;
@@ -863,7 +864,7 @@ __global__ __launch_bounds__(256) void forest_cate2_kernel(ForestParams fp, int 
       const double psi = wy - wb * y_ - yb * w_ + wb * yb - tau * (ww - 2.0 * wb * w_ + wb * wb);
       ps += psi; pss += psi * psi; ++nb;
     }
-    if (nb == 0) continue;
+    if (nb == 0 || nb < gsz) continue;   // grf: complete groups only
     const double pg = ps / nb;
     gs += to_fix(pg); gss += to_fix(pg * pg); ng += 1;
     if (nb >= 2) { within += to_fix(pss / nb - pg * pg); nwithin += 1; }
@@ -895,7 +896,7 @@ __global__ __launch_bounds__(256) void forest_final_kernel(ForestParams fp, int 
         const double nw = (double)st[8 * n2 + i];
         const double wc = nw > 0 ? from_fix(st[7 * n2 + i]) / nw / (double)(fp.group > 1 ? fp.group - 1 : 1)
                                  : 0.0;
-        var = fmax(between - wc, 0.0) / (H * H);
+        var = grf_debias(between, wc, ng) / (H * H);
       }
     }
   }

@@ -187,4 +187,69 @@ ATE_HD double causal_rho(const CausalNode& c, double w, double y) {
   return c.varw > 0.0 ? r / c.varw : 0.0;
 }
 
+// ---- little-bag variance debiasing (grf's objective Bayes debiaser)
+// The between-group variance of the little-bag scores overstates the forest's variance by
+// the within-group noise / (group - 1); grf does not subtract and clamp at zero (which gives
+// zero-width intervals whenever the noise estimate wins) but takes the posterior mean of
+// the true variance S under V ~ N(S + noise, se^2), S >= 0, a flat prior:
+//   est = V - noise, se = max(V, noise) sqrt(2 / groups), r = est / se,
+//   S_hat = est + se * phi(r) / Phi(r).
+// Host and device must give the same bits, so exp / erfc / sqrt are built here from
+// correctly rounded +, -, *, / and exact scalings (no libm: the device and host libms may
+// differ by an ulp); both sides compile without FMA contraction.
+ATE_HD double det_exp_neg(double y) {          // e^y for y <= 0 (Cody-Waite + Taylor-13)
+  if (y < -745.0) return 0.0;
+  const double k = floor(y * 1.4426950408889634 + 0.5);
+  const double f = (y - k * 6.93147180369123816490e-01) - k * 1.90821492927058770002e-10;
+  double s = 1.0 / 6227020800.0;                // 1/13!
+  const double inv[13] = {1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0, 1.0 / 362880.0,
+                          1.0 / 40320.0, 1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0,
+                          1.0 / 6.0, 0.5, 1.0, 1.0};
+  for (int i = 0; i < 13; ++i) s = s * f + inv[i];
+  return ldexp(s, (int)k);
+}
+ATE_HD double det_sqrt(double v) {             // v > 0: Newton from an exact power-of-2 guess
+  int e;
+  frexp(v, &e);                                 // v = m 2^e, m in [0.5, 1)
+  double s = ldexp(1.0, e / 2);                 // within a factor 2 of sqrt(v)
+  for (int i = 0; i < 8; ++i) s = 0.5 * (s + v / s);
+  return s;
+}
+// phi(r) / Phi(r) for the standard normal (x = -r / sqrt 2, Phi(r) = erfc(x) / 2)
+ATE_HD double det_mills(double r) {
+  const double x = -r * 0.7071067811865476;
+  if (x > 2.5) {
+    // erfc(x) = e^{-x^2} / (sqrt(pi) D), D = x + (1/2) / (x + 1 / (x + (3/2) / (x + ...)))
+    double k = x;
+    for (int j = 60; j >= 1; --j) k = x + (0.5 * j) / k;
+    return 1.4142135623730951 * k;             // Phi = e^{-x^2} / (2 sqrt(pi) D), D = k
+  }
+  const double ax = x < 0 ? -x : x;
+  const double ex = det_exp_neg(-ax * ax);
+  double erf_ax;                                // erf(|x|)
+  if (ax > 2.5) {
+    double k = ax;
+    for (int j = 60; j >= 1; --j) k = ax + (0.5 * j) / k;
+    erf_ax = 1.0 - ex * 0.5641895835477563 / k;
+  } else {                                      // positive series: e^{-x^2} sum 2^n x^{2n+1} / (2n+1)!!
+    double t = ax, s = ax;
+    const double x2 = 2.0 * ax * ax;
+    for (int n = 1; n < 90; ++n) {
+      t = t * x2 / (double)(2 * n + 1);
+      s += t;
+      if (t < s * 1e-18) break;
+    }
+    erf_ax = 1.1283791670955126 * ex * s;
+  }
+  const double erfc_x = x < 0 ? 1.0 + erf_ax : 1.0 - erf_ax;
+  return (ex * 0.3989422804014327) / (0.5 * erfc_x);
+}
+ATE_HD double grf_debias(double between, double noise, double groups) {
+  const double est = between - noise;
+  const double big = between > noise ? between : noise;
+  if (!(big > 0.0) || !(groups > 0.0)) return est > 0.0 ? est : 0.0;
+  const double se = big * det_sqrt(2.0 / groups);
+  return est + se * det_mills(est / se);
+}
+
 }  // namespace atef
