@@ -1,4 +1,5 @@
-"""Race/memory-safety checks of the host C++ code: the forest engine
+"""Race/memory-safety checks of the host C++ code: the forest engine (binned
+and exact-split trees, every sampling mode, both predictors, the variance debiaser)
 built with AddressSanitizer + UndefinedBehaviorSanitizer (GPU sanitizers are not
 available on this pool; the GPU kernels are instead checked bit-for-bit against this
 engine in tests/test_forest_gpu.py)."""
@@ -26,4 +27,4 @@ def test_forest_engine_asan_ubsan(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
-    assert r.stdout.count(" ok:") == 3
+    assert r.stdout.count(" ok:") == 9
