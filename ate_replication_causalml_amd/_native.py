@@ -47,6 +47,7 @@ _SIGS = {
     "ate_dml_finalize": "pipp",
     "ate_boot_multinomial": "ppluiipp",
     "ate_boot_poisson": "ppluiilipp",
+    "ate_enet_isa_selftest": "pp",
     "ate_enet_prepare": "piipipiipipipppppppp",
     "ate_enet_path": "pipiippppidddipppppipp",
     "ate_enet_coef": "ppiiiipppppppp",

@@ -56,12 +56,50 @@ def _all_ranks_have(ck, stage, dkey, dist, dev):
     return bool(ok.item())
 
 
-def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey):
-    """Held-out predictions of E[Y|X], E[W|X] for every fold (device tensors)."""
+def _pair_dist(dist):
+    """The context of the second of two concurrently running fits: its own communicator
+    (``dup``), or None when collectives cannot be duplicated (then the fits run serially)."""
+    if dist is None or dist.world == 1:
+        return dist
+    dup = getattr(dist.comm, "dup", None)
+    if dup is None:
+        return None
+    from ..parallel.dist import DistContext
+    return DistContext(dup(), dist.row_offset, dist.n_total)
+
+
+def _fit_pair(fit, jobs, dev, dists):
+    """Run ``fit(target, loss, train, dist)`` for the two jobs of a fold side by side, each on
+    its own HIP stream (the models are independent: E[Y|X] and E[W|X] on the same rows; a
+    level's histogram of one overlaps the other's small deep levels and host stepping).
+    Same trees as serially. ``dists``: one context per job (own communicators)."""
+    from concurrent.futures import ThreadPoolExecutor
+    main = torch.cuda.current_stream(dev)
+
+    def run(i):
+        st = torch.cuda.Stream(device=dev)
+        st.wait_stream(main)
+        with torch.cuda.device(dev), torch.cuda.stream(st):
+            out = fit(*jobs[i], dists[i])
+        main.wait_stream(st)
+        st.synchronize()
+        return out
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        return list(ex.map(run, range(2)))
+
+
+def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent=False):
+    """Held-out predictions of E[Y|X], E[W|X] for every fold (device tensors). ``fit(target,
+    loss, train, dist)``. ``concurrent`` (GPU): a fold's two fits run side by side on two
+    streams, the second with a duplicated communicator -- the same bits, but slower on the
+    config-5 shard (1.31 vs 1.18 s for 20 trees: the histogram kernels fill the GPU alone and
+    two of them contend for L2; profiles/r04_cfg5), so off by default."""
     ey = torch.zeros_like(y)
     ew = torch.zeros_like(w)
     ly, lw = _loss(y, dist), _loss(w, dist)
     tag = "" if dist is None else f".r{dist.rank}of{dist.world}"
+    d2 = _pair_dist(dist) if (concurrent and dev.type == "cuda") else None
+    pair = concurrent and dev.type == "cuda" and (dist is None or d2 is not None)
     for k in range(K):
         ho = fid == k
         stage = f"dml_gbdt_fold{k}{tag}"
@@ -71,8 +109,12 @@ def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey):
             pw = torch.as_tensor(z["ew"], device=dev)
         else:
             # held-out predictions = the trainer's running scores of the rows it skipped
-            py = torch.where(ho, _response(fit(y, ly, ~ho), dev), torch.zeros_like(y))
-            pw = torch.where(ho, _response(fit(w, lw, ~ho), dev), torch.zeros_like(w))
+            if pair:
+                my, mw = _fit_pair(fit, [(y, ly, ~ho), (w, lw, ~ho)], dev, [dist, d2])
+            else:
+                my, mw = fit(y, ly, ~ho, dist), fit(w, lw, ~ho, dist)
+            py = torch.where(ho, _response(my, dev), torch.zeros_like(y))
+            pw = torch.where(ho, _response(mw, dev), torch.zeros_like(w))
             if checkpoint is not None:
                 checkpoint.save(stage, dkey, ey=py.cpu().numpy(), ew=pw.cpu().numpy())
         ey = torch.where(ho, py, ey)
@@ -93,15 +135,15 @@ def dml_plr_gbdt(Y, W, X, folds=5, n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
     edges = G.global_bin_edges(Xn, dist, device=dev)
     Xb = G.binned(Xn, edges, dev)          # binned once, shared by all 2K fits
     kw = dict(n_trees=n_trees, depth=depth, lr=lr, lam=lam, min_child=min_child,
-              backend=backend, edges=edges, dist=dist, Xb=Xb)
+              backend=backend, edges=edges, Xb=Xb)
     y = torch.as_tensor(Yn, dtype=torch.float64, device=dev)
     w = torch.as_tensor(Wn, dtype=torch.float64, device=dev)
     fid_t = torch.as_tensor(fid, device=dev)
 
-    def fit(target, loss, train):
+    def fit(target, loss, train, d):
         tr = train if backend == "gpu" else train.cpu().numpy()
         tg = target if backend == "gpu" else target.cpu().numpy()
-        return G.fit_gbdt(None, tg, loss=loss, train=tr, **kw)
+        return G.fit_gbdt(None, tg, loss=loss, train=tr, dist=d, **kw)
 
     dkey = _data_key(checkpoint, Yn, Wn, Xn, np.array([folds, n_trees, depth, lr, lam,
                                                        min_child, seed, fold_stream], float))
@@ -184,7 +226,7 @@ def bin_panel(pan, edges=None, edge_rows=G.EDGE_SAMPLE, dist=None):
 
 def dml_plr_gbdt_panel(pan, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0,
                        method="DML cross-fit (GBDT)", dist=None, checkpoint=None,
-                       data_key="", edge_rows=G.EDGE_SAMPLE):
+                       data_key="", edge_rows=G.EDGE_SAMPLE, concurrent=False):
     """Config 5 on an HBM-resident panel (data/device_dgp.synthetic_panel, segment k =
     fold k; with ``dist`` this rank's slice of every fold): device binning from the global
     edge sample, then the K-fold cross-fit on the resident row-major bins with Y, W,
@@ -201,17 +243,17 @@ def dml_plr_gbdt_panel(pan, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0
     w = pan.col("W").index_select(0, rows).double()
     fid = torch.repeat_interleave(torch.arange(K, device=dev), nr)
     kw = dict(n_trees=n_trees, depth=depth, lr=lr, lam=lam, min_child=min_child,
-              backend="gpu", edges=edges, Xb=(Xr, ldr), dist=dist)
+              backend="gpu", edges=edges, Xb=(Xr, ldr))
 
-    def fit(target, loss, train):
-        return G.fit_gbdt(None, target, loss=loss, train=train, **kw)
+    def fit(target, loss, train, d):
+        return G.fit_gbdt(None, target, loss=loss, train=train, dist=d, **kw)
 
     dkey = ""
     if checkpoint is not None:
         from .crossfit import _panel_key
         dkey = _panel_key(pan, data_key, pan.n, len(pan.xcols), n_trees, depth, lr, lam,
                           min_child, edge_rows)
-    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey)
+    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent)
     mom = S.dml_moments_exact(y - ey, w - ew, dist)
     n_all = dist.n_total if dist is not None else pan.n
     return read_result(S.dml_finalize(mom, "plr"), method, n=n_all, trees=n_trees, depth=depth)

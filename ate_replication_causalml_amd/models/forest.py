@@ -284,7 +284,10 @@ class Forest:
                              leaves.data_ptr(), tchunk, state.data_ptr(), out.data_ptr(), phases, s)
                 if not phases & 4:
                     return None
-                return out if not host else out.cpu().numpy()
+                if not host:
+                    return out.view(n2, width) if width > 1 else out
+                res = out.cpu().numpy()
+                return res.reshape(n2, width) if width > 1 else res
             if self.packed is None:
                 self.packed = torch.zeros(self.params.ntree * self.cap * 2, dtype=torch.int32,
                                           device=dev)

@@ -44,6 +44,9 @@ class LocalComm:
     def barrier(self):
         pass
 
+    def dup(self):
+        return self
+
 
 class TorchComm:
     def __init__(self, group=None):
@@ -73,6 +76,14 @@ class TorchComm:
         out = [torch.empty_like(t) for _ in range(self.world_size)]
         self.dist.all_gather(out, t.contiguous(), group=self.group)
         return out
+
+    def dup(self):
+        """A second communicator over the same ranks (a new process group; a collective
+        call: every rank creates it in the same order). Concurrently running fits each need
+        their own, so their collectives cannot interleave differently on different ranks."""
+        ranks = self.dist.get_process_group_ranks(self.group) if self.group is not None \
+            else list(range(self.dist.get_world_size()))
+        return TorchComm(self.dist.new_group(ranks))
 
     def broadcast_(self, t, src=0):
         self.dist.broadcast(t, src=src, group=self.group)

@@ -18,6 +18,8 @@
 //  select:   cvm, cvsd, lambda.min, lambda.1se with glmnet's rules.
 #include <cstdlib>
 
+#include <utility>
+
 #include "common.hpp"
 
 #include <type_traits>
@@ -210,6 +212,84 @@ __device__ __forceinline__ void select_lane1(int i, int lane, double& a, double 
   a = __hiloint2double(a1, a0);
 }
 
+// ---- row-blocked broadcast (the lasso dense walk, ENET_ROWWALK)
+// u += bcast(d) * nc, bcast = lane C of each 16-lane row (DPP64 row_newbcast: v_fmac_f64
+// takes the broadcast as an operand, no readlane -> SGPR -> VALU hop on the chain). The
+// s_nop covers the VALU-write -> DPP-read hazard on d.
+template <int C>
+__device__ __forceinline__ void fmac_bcast(double& u, double d, double nc) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(u)
+               : "v"(d), "v"(nc), "i"(C));
+}
+// every 16-lane row <- row R of x (gfx950 v_permlane32_swap: rows (0,1) <-> (2,3) of the
+// two operands, then v_permlane16_swap: odd <-> even rows)
+template <int R>
+__device__ __forceinline__ double row_replicate(double x) {
+  unsigned w[2] = {(unsigned)__double2loint(x), (unsigned)__double2hiint(x)};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto p = __builtin_amdgcn_permlane32_swap(w[h], w[h], false, false);
+    const unsigned a = R < 2 ? p[0] : p[1];            // (Ra, Rb, Ra, Rb), a = R & ~1
+    const auto q = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    w[h] = (R & 1) ? q[1] : q[0];
+  }
+  return __hiloint2double((int)w[1], (int)w[0]);
+}
+
+// min(max(u, lo), hi) as the two hardware ops fmin(fmax(...)) compiles to, without the
+// canonicalising max(u, u) the compiler puts in front of a value produced by inline asm
+// (u is never NaN here, so the result is the same bits)
+__device__ __forceinline__ double clamp_hw(double u, double lo, double hi) {
+  double r;
+  asm("v_max_f64 %0, %1, %2\n\tv_min_f64 %0, %0, %3" : "=&v"(r) : "v"(u), "v"(lo), "v"(hi));
+  return r;
+}
+
+// (u - a) - min(max(u, lo), hi): the lasso step of the dense walk, with u - a issued first
+// (it only waits for u) so the clamp chain is max -> min -> sub
+__device__ __forceinline__ double lasso_step_hw(double u, double a, double lo, double hi) {
+  double t, c;
+  asm("v_add_f64 %0, %2, -%3\n\t"
+      "v_max_f64 %1, %2, %4\n\t"
+      "v_min_f64 %1, %1, %5\n\t"
+      "v_add_f64 %1, %0, -%1"
+      : "=&v"(t), "=&v"(c)
+      : "v"(u), "v"(a), "v"(lo), "v"(hi));
+  return c;
+}
+
+template <class F, int... C>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, C...>) {
+  (f(std::integral_constant<int, C>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {   // f(integral_constant<int, 0..N-1>)
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Self-test of the two cross-lane primitives above (tests/test_gpu.py): out[r * 64 + l] =
+// row_replicate<r>(x)[l] for x = lane id, out[256 + l] = u after fmac_bcast<5> with
+// u = 1, d = lane, nc = 2 (= 1 + 2 * (16 * (l >> 4) + 5)).
+__global__ void enet_isa_selftest_kernel(double* out) {
+  const int l = threadIdx.x;
+  const double x = (double)l;
+  out[l] = row_replicate<0>(x);
+  out[64 + l] = row_replicate<1>(x);
+  out[128 + l] = row_replicate<2>(x);
+  out[192 + l] = row_replicate<3>(x);
+  double u = 1.0;
+  fmac_bcast<5>(u, x, 2.0);
+  out[256 + l] = u;
+}
+
+ATE_API int ate_enet_isa_selftest(void* out, void* stream) {
+  hipLaunchKernelGGL(enet_isa_selftest_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (double*)out);
+  ATE_CHECK_LAUNCH();
+  return 0;
+}
+
 // Blocked covariance-mode coordinate descent, ONE WAVE per problem.
 //
 // glmnet's pass visits coordinates j = 0..p-1 in order and processes j iff it is nonzero
@@ -251,6 +331,10 @@ static_assert(NW >= PMAX / 64, "one pull wave per 64-column block: NW >= PMAX / 
 #define ENET_PULL_DENSE 12   //   its coordinates are pending, else a compacted row list
 #endif                       //   (sweep 4..48: 12 best, CV stage 3.12 -> 2.98 ms, same bits;
                              //   profiles/r03_enet/pull_dense_sweep.txt)
+#ifndef ENET_ROWWALK          // 1: lasso dense walk in 16-lane rows (DPP64 broadcasts inside
+#define ENET_ROWWALK 0       //   a row, permlane replicate + 16 DPP64 fmas to catch the other
+#endif                       //   rows up). Same bits, but the CV stage took 3.37-3.46 ms vs
+                             //   2.84 for the readlane walk (profiles/r04_enet/rowwalk_ab.txt)
 #ifndef ENET_DENSE_MIN       // dense (all 64 lanes, static) walk of a block when at least
 #define ENET_DENSE_MIN 28    //   this many lanes move: nonzero lanes (full pass) /
 #endif                       //   eligible lanes (active pass)
@@ -355,6 +439,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // group g = lane/16, 4 columns per lane). Returns the sum for row r = lane (the 4 lane
   // groups combined through the wave's `sred` area).
   auto pull_block = [&](int jb, int tb) __attribute__((always_inline)) -> float {
+    ATE_DASSERT(jb >= 0 && jb < T && tb >= 0 && tb < T && jb != tb);
     const int grp = lane >> 4, c4 = (lane & 15) * 4;
     const int j = jb * 64 + lane;
     const double ddj = sdc[j] - sds[tb][j];
@@ -497,6 +582,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // block in LDS. After the barrier wave 0 publishes block t, completes block tn's
   // gradient and snapshot, and moves tn's diagonal block into registers.
   auto pull_rest = [&](int t, int tn, int vpar) __attribute__((always_inline)) {     // waves 1..NW-1
+    ATE_DASSERT(t >= 0 && t < T && tn >= 0 && tn < T);
     const int my = wid - 1;
     CT acc = 0;
     if constexpr (sizeof(CT) == 4) {
@@ -538,6 +624,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       }
       const int share = (tot + NP - 1) / NP;
       const int lo = my * share, hi = min(tot, lo + share);
+      ATE_DASSERT(hi - lo <= PER);                       // the wave's slist2 region
       const uint64_t ltmask = (1ull << lane) - 1ull;
 #pragma unroll
       for (int c = 0; c < TMAX; ++c) {
@@ -758,6 +845,43 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
             // same value: 11 instructions per step instead of 15 (profiles/r03_enet).
             const double a0v = at;
             double usnap = u;
+#if ENET_ROWWALK
+            // Row-blocked order of the SAME fmas: lane k still applies d_0, d_1, ..., d_63
+            // in coordinate order (fma(nc, d, u) == fma(-c, d, u) bit for bit). Row r's 16
+            // coordinates are walked with exec = row r only, each step broadcasting d_i
+            // inside the row by DPP64 (chain max -> min -> sub -> fmac: no readlane hop);
+            // then every other row catches up on d_16r..d_16r+15 (row r replicated to all
+            // rows by two permlane swaps, 16 DPP64 fmas). d_i is re-derived from lane i's
+            // snapshot by the same operations as in the walk, so it is the same value.
+            const int row = lane >> 4;
+            auto row_pass = [&](auto r_tag) __attribute__((always_inline)) {
+              constexpr int R = decltype(r_tag)::value;
+              if (row == R) {
+                asm volatile("s_nop 4");                 // exec write -> DPP
+                static_for<16>([&](auto c_tag) __attribute__((always_inline)) {
+                  constexpr int C = decltype(c_tag)::value, I = R * 16 + C;
+                  const double dd = lasso_step_hw(u, a0v, -thr_e, thr_e);
+                  const float ci = I < 32 ? dg_lo[I] : dg_hi[I - 32];
+                  select_lane1(I, lane, usnap, u);
+                  fmac_bcast<C>(u, dd, -(double)ci);
+                });
+              }
+              const double cls = fmin(fmax(usnap, -thr_e), thr_e);
+              const double rep = row_replicate<R>((usnap - a0v) - cls);
+              if (row != R) {
+                asm volatile("s_nop 4");
+                static_for<16>([&](auto c_tag) __attribute__((always_inline)) {
+                  constexpr int C = decltype(c_tag)::value, I = R * 16 + C;
+                  const float ci = I < 32 ? dg_lo[I] : dg_hi[I - 32];
+                  fmac_bcast<C>(u, rep, -(double)ci);
+                });
+              }
+            };
+            row_pass(std::integral_constant<int, 0>{});
+            row_pass(std::integral_constant<int, 1>{});
+            row_pass(std::integral_constant<int, 2>{});
+            row_pass(std::integral_constant<int, 3>{});
+#else
 #pragma unroll
             for (int i = 0; i < 64; ++i) {
               const double cl = fmin(fmax(u, -thr_e), thr_e);
@@ -769,6 +893,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
               select_lane1(i, lane, usnap, u);
               u = __builtin_fma(-(double)ci, d, u);
             }
+#endif
             {
               const double cl = fmin(fmax(usnap, -thr_e), thr_e);
               gbef = usnap - a0v;

@@ -123,6 +123,20 @@ def test_dml_gbdt_panel_dist_world1_equals_plain(gpu):
     assert a.ate == b.ate and a.se == b.se
 
 
+def test_dml_gbdt_panel_concurrent_pair_equals_serial(gpu):
+    """A fold's E[Y|X] and E[W|X] fits on two streams (boosting._fit_pair) give the same
+    bits as one after the other, with and without a (one-rank) row-sharded context."""
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt_panel
+    from ate_replication_causalml_amd.parallel.comm import LocalComm
+    from ate_replication_causalml_amd.parallel.dist import DistContext
+    pan = synthetic_panel(60000, p=37, folds=5, seed=9, dtype="bf16", device=gpu)
+    for dist in (None, DistContext(LocalComm(), 0, pan.n)):
+        a = dml_plr_gbdt_panel(pan, n_trees=6, depth=5, dist=dist, concurrent=True)
+        b = dml_plr_gbdt_panel(pan, n_trees=6, depth=5, dist=dist, concurrent=False)
+        assert a.ate == b.ate and a.se == b.se
+
+
 def test_dml_gbdt_panel_matches_host_arrays(gpu):
     """Panel path (device binning from the global sample, device Y/W/scores) == the
     host-array path on the same stored values (same edges: the full-data strided sample)."""

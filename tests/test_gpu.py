@@ -175,6 +175,18 @@ def test_enet_cv_kernels_vs_cpu(gpu):
     assert np.allclose(rg.cvm[0, :nl].cpu().numpy(), rc.cvm[0, :nl].numpy(), rtol=1e-6)
 
 
+def test_enet_cross_lane_primitives(gpu):
+    """csrc/enet.hip row_replicate (permlane32/16 swaps) and fmac_bcast (DPP64
+    row_newbcast), the broadcasts of the row-blocked lasso walk, on gfx950."""
+    out = torch.zeros(320, dtype=torch.float64, device=gpu)
+    _native.call("ate_enet_isa_selftest", out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    o = out.cpu().numpy()
+    lane = np.arange(64)
+    for r in range(4):
+        np.testing.assert_array_equal(o[r * 64:(r + 1) * 64], 16 * r + (lane & 15))
+    np.testing.assert_array_equal(o[256:], 1 + 2 * (16 * (lane >> 4) + 5))
+
+
 def test_enet_fold_wait_timeout_poisons_and_raises(gpu, monkeypatch):
     """The CV fold problems spin (bounded) on their full-data problem's lambda progress
     (csrc/enet.hip). Forcing the bound to zero polls makes fold waits time out: the launch

@@ -41,6 +41,9 @@ class _ShardComm:
     def barrier(self):
         pass
 
+    def dup(self):
+        return self
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -52,6 +55,9 @@ def main():
     ap.add_argument("--seed", type=int, default=13)
     ap.add_argument("--shard", default=None)
     ap.add_argument("--checkpoint", default=None, help="directory: per-fold held-out predictions")
+    ap.add_argument("--concurrent", action="store_true",
+                    help="fit a fold's E[Y|X] and E[W|X] side by side on two streams "
+                         "(default: one after the other)")
     a = ap.parse_args()
     import torch
     from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
@@ -81,7 +87,8 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     r = dml_plr_gbdt_panel(pan, n_trees=a.trees, depth=a.depth, dist=dist, checkpoint=ck,
-                           data_key=f"synthetic.{n}.{a.cols}.{a.seed}")
+                           data_key=f"synthetic.{n}.{a.cols}.{a.seed}",
+                           concurrent=a.concurrent)
     torch.cuda.synchronize()
     comm.barrier()
     secs = time.perf_counter() - t1
@@ -91,7 +98,7 @@ def main():
         print(json.dumps({
             "config": 5, "estimator": "DML-PLR 5-fold, GBDT nuisances (E[Y|X], E[W|X]), HBM panel",
             "rows_total": n, "rows_this_rank": pan.n, "p": a.cols, "trees": a.trees,
-            "depth": a.depth, "world": world, "shard": a.shard, "seconds": float(el.item()),
+            "depth": a.depth, "world": world, "shard": a.shard, "concurrent": a.concurrent, "seconds": float(el.item()),
             "generate_s": t_gen, "rows_per_s": n / float(el.item()), "ate": r.ate, "se": r.se,
             "ate_hex": float(r.ate).hex(), "se_hex": float(r.se).hex()}), flush=True)
     if world > 1 and not a.shard:

@@ -14,8 +14,10 @@
 #   prof           rocprofv3 kernel trace + stats of a short bench, and the overlap timeline
 #   enet_ab:A,B,.. CV-LASSO stage alone for libatehip_<A>.so, ... ("new" = in-tree), x2
 #   enet_prof      cycle accounting of the path kernel (tools/enet_profile.py build)
+#   gram_ab:A,B,.. the bf16 Gram tile kernel alone (tools/gram_only.py) per library, x2
 #   cfg3           config-3 per-GPU shard (N=1e7, p=500, 100 trees, rank 0 of 8)
-#   cfg5           config-5 per-GPU shard (N=1.25e7, p=2000, 100 trees)
+#   cfg5           config-5 per-GPU shard (N=1.25e7, p=2000, 100 trees); cfg5c: concurrent Y/W fits
+#   cfg5small      a small config-5 shard, concurrent then serial Y/W fits
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
 set -o pipefail
@@ -64,12 +66,26 @@ for step in "$@"; do
           ATE_HIP_LIB=$ROOT/$lib run "enet_${nm}_$rep" 120 python tools/enet_only.py 15
         done
       done ;;
+    gram_ab:*)
+      IFS=, read -ra libs <<< "${step#gram_ab:}"
+      for rep in 1 2; do
+        for nm in "${libs[@]}"; do
+          lib=ate_replication_causalml_amd/_lib/libatehip_$nm.so
+          [ "$nm" = new ] && lib=ate_replication_causalml_amd/_lib/libatehip.so
+          ATE_HIP_LIB=$ROOT/$lib ATE_GRAM_STAGE=tiles run "gram_${nm}_$rep" 120 python tools/gram_only.py
+        done
+      done ;;
     enet_prof)
       run enet_prof 300 python tools/enet_profile.py ;;
     cfg3)
       run cfg3 300 python -u tools/cfg3.py --rows 10000000 --cols 500 --trees 100 --shard 0/8 ;;
     cfg5)
       run cfg5 400 python -u tools/cfg5.py --rows 100000000 --cols 2000 --trees 100 --shard 0/8 ;;
+    cfg5c)
+      run cfg5c 400 python -u tools/cfg5.py --rows 100000000 --cols 2000 --trees 100 --shard 0/8 --concurrent ;;
+    cfg5small)   # 1/8 of a shard: both orders, same bits
+      run cfg5small_c 200 python -u tools/cfg5.py --rows 12500000 --cols 2000 --trees 20 --shard 0/8 --concurrent && \
+      run cfg5small_s 200 python -u tools/cfg5.py --rows 12500000 --cols 2000 --trees 20 --shard 0/8 ;;
     configs)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
