@@ -726,6 +726,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       // LDS latency hides under the recurrence
       double dc0 = 0.0, ds0 = 0.0;
       if (wid == 0) {
+#ifdef ENET_PROF
+        const long long tv0_ = clock64();
+#endif
         // this block's diagonal row into registers (deposited by the last visit's DMA or
         // by pull()): dg_lo[i] / dg_hi[i-32] = C[t*64+lane][t*64+i]
 #pragma unroll
@@ -771,6 +774,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): dg_* landed; no waits in the loop
 #ifdef ENET_PROF
         const long long tloop0_ = clock64();
+        if (lane == 0) sprof[wid][17] += (unsigned long long)(tloop0_ - tv0_);   // prologue cycles
 #endif
         auto step = [&]() __attribute__((always_inline)) -> bool {
 #pragma clang fp contract(off)
@@ -1084,6 +1088,10 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // stored), the fold problem polls that counter (relaxed, bounded spin) and acquires
   // before reading. All problems of a launch are co-resident (one workgroup per problem,
   // grid <= #CUs); a timed-out spin ends the fold path (npass_out = -1 flags it).
+#ifdef ENET_PROF
+  const long long kc0_ = clock64();
+  const unsigned long long kw0_ = wall_clock64();
+#endif
   const bool is_fold = pr.ulam_src >= 0;
   bool timed_out = false;
   for (int m = 0; m < nlam; ++m) {
@@ -1169,6 +1177,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   if (tid < 24) {
     unsigned long long acc = 0;
     for (int w = 0; w < NW; ++w) acc += sprof[w][tid];
+    // [10] / [11]: shader clock cycles and 100 MHz wall ticks of the whole path (clock rate)
+    if (tid == 10) acc = (unsigned long long)(clock64() - kc0_);
+    if (tid == 11) acc = wall_clock64() - kw0_;
     atomicAdd(&enet_prof[q][tid], acc);
   }
 #endif

@@ -20,6 +20,7 @@
 #   cfg5small      a small config-5 shard, concurrent then serial Y/W fits
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
+#   gramdump       the bench panel's fold Gram stack -> OUT/gram_dump (tools/dump_bench_gram.py)
 set -o pipefail
 OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"
@@ -90,6 +91,8 @@ for step in "$@"; do
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
       run replicate 600 python -u tools/replicate_timing.py ;;
+    gramdump)    # the bench panel's fold Gram stack for tools/enet_sim.py
+      run gramdump 200 python -u tools/dump_bench_gram.py "$OUT/gram_dump" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
