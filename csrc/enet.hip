@@ -335,11 +335,174 @@ static_assert(NW >= PMAX / 64, "one pull wave per 64-column block: NW >= PMAX / 
 #define ENET_ROWWALK 0       //   a row, permlane replicate + 16 DPP64 fmas to catch the other
 #endif                       //   rows up). Same bits, but the CV stage took 3.37-3.46 ms vs
                              //   2.84 for the readlane walk (profiles/r04_enet/rowwalk_ab.txt)
+#ifndef ENET_MODE_S          // small-active-set mode (fp32 C): while at most ENET_S_ENTER
+#define ENET_MODE_S 1        //   coordinates have ever moved, passes run in wave 0 over all p
+#endif                       //   coordinates with the movers' Gram columns cached in LDS
+#ifndef ENET_S_ENTER
+#define ENET_S_ENTER 40
+#endif
+#ifndef ENET_S_FETCH         // ... and while a lambda fetched at most this many new columns:
+#define ENET_S_FETCH 8       //   a fetch is an L2/HBM round trip on the mode-S chain, so a
+#endif                       //   problem whose active set grows fast (dense W fits) leaves early
+constexpr int S_UNION = 112 * 1024;          // LDS shared by mode L's blocks and mode S's cache
+constexpr int S_CAP = S_UNION / (PMAX * 4);  // cached columns (56)
 #ifndef ENET_DENSE_MIN       // dense (all 64 lanes, static) walk of a block when at least
 #define ENET_DENSE_MIN 28    //   this many lanes move: nonzero lanes (full pass) /
 #endif                       //   eligible lanes (active pass)
 
-template <typename CT>
+#define LDS_AS __attribute__((address_space(3)))
+struct PassS {
+  double dlx, rsq;
+};
+// ---- mode S: small active set (glmnet covariance mode's own design: the Gram columns
+// of the coordinates that have moved are kept on chip). While few coordinates have ever
+// moved, a pass runs in wave 0 alone over ALL p coordinates, lane l holding g, a, vp of
+// coordinates k = s * 64 + l (s = 0..7) in registers: the next coordinate that can move
+// (eligible, and nonzero or |g| > vp * lambda; in index order past the last one) comes
+// from eight ballots, and a move updates all p gradients from the mover's cached column
+// (fetched from C's row j -- C is symmetric -- on its first move). Exactly glmnet's
+// sequential pass (full: every coordinate; active: the ever-moved ones), with every
+// gradient exact at all times: nothing is pending when the problem switches to mode L.
+// fp32 C only; the gradients accumulate in fp64. Returns max d^2 (wave-uniform).
+// A separate (not inlined) function: its SGPR-heavy walk would otherwise push the path
+// kernel's own SGPRs into spills (8 -> 91) inside the mode-L walks. LDS operands arrive as
+// address-space-3 pointers, so they stay ds_* accesses.
+__device__ __noinline__ PassS enet_pass_s(bool full, int T, int ldc, double ab, double dem,
+                                          const float* __restrict__ Cf, LDS_AS double* sg,
+                                          LDS_AS double* sa, const LDS_AS double* svp,
+                                          LDS_AS int* sflag, LDS_AS int* sslot,
+                                          LDS_AS float* sccache, LDS_AS int* sever_n,
+                                          LDS_AS int* sncache,
+                                          LDS_AS unsigned long long* sprof_row) {
+  const int lane = threadIdx.x & 63;
+#ifdef ENET_PROF
+  const long long tps0_ = clock64();
+  unsigned long long nit_ = 0, nfetch_ = 0;
+#endif
+  double gS[8], aS[8], tS[8];
+  int slS[8];
+  // per-lane flag bits (VGPR, not 24 SGPR masks): bit s = coordinate s*64+lane is visited
+  // by this pass (eligible; in an active pass also ever moved), bit 8+s = ever moved
+  int flb = 0;
+#pragma unroll
+  for (int s8 = 0; s8 < 8; ++s8) {   // sets past the padded width ldc: never eligible
+    const int k = s8 * 64 + lane;
+    const bool in = s8 < T;          // (their LDS entries are not initialised)
+    gS[s8] = in ? sg[k] : 0.0;
+    aS[s8] = in ? sa[k] : 0.0;
+    tS[s8] = in ? svp[k] * ab : 0.0;
+    slS[s8] = in ? sslot[k] : -1;
+    const int f = in ? sflag[k] : 0;
+    if ((f & 1) && (full || (f & 2))) flb |= 1 << s8;
+    if (f & 2) flb |= 1 << (8 + s8);
+  }
+  int ncache = __builtin_amdgcn_readfirstlane(*sncache);   // uniform (SGPR) counters
+  int ever_n = __builtin_amdgcn_readfirstlane(*sever_n);
+  double dlx = 0.0, rsq_add = 0.0;
+#ifdef ENET_PROF
+  const long long tpl0_ = clock64();
+#endif
+  // The pass walks the sets in order (static: every register array is indexed with a
+  // compile-time set, no 8-way selects); inside set s the candidates are re-evaluated after
+  // every move, for the lanes past the mover only (the sets after s are evaluated when the
+  // walk reaches them, with their gradients as they are then: glmnet's order exactly).
+  static_for<8>([&](auto s_tag) __attribute__((always_inline)) {
+    constexpr int SJ = decltype(s_tag)::value;
+    if (SJ >= T) return;
+    uint64_t live = ~0ull;   // lanes of this set not yet passed
+    for (;;) {
+      const bool c = ((flb >> SJ) & 1) & ((aS[SJ] != 0.0) | (fabs(gS[SJ] + aS[SJ]) > tS[SJ]));
+      const uint64_t cm = __builtin_amdgcn_ballot_w64(c) & live;
+      if (!cm) break;
+      const int lj = __ffsll((unsigned long long)cm) - 1;
+      live = lj == 63 ? 0ull : (~0ull << (lj + 1));
+#ifdef ENET_PROF
+      ++nit_;
+#endif
+      const int j = SJ * 64 + lj;
+      const double gj = readlane_d(gS[SJ], lj);
+      const double aj = readlane_d(aS[SJ], lj);
+      const double tj = readlane_d(tS[SJ], lj);
+      int slj = __builtin_amdgcn_readlane(slS[SJ], lj);
+      const double uj = gj + aj;
+      double an = copysign(fmax(fabs(uj) - tj, 0.0), uj);
+      if (dem != 0.0) an = an / (1.0 + svp[j] * dem);
+      const double d = an - aj;
+      if (__builtin_amdgcn_readfirstlane((int)(d == 0.0))) continue;
+      // the mover's column: cached, newly cached, or (cache full) read from C directly
+      float cv[8];
+      if (slj < 0 && ncache < S_CAP) {
+#ifdef ENET_PROF
+        ++nfetch_;
+#endif
+        slj = ncache++;
+        const float* Cj = Cf + (int64_t)j * ldc;
+        LDS_AS float* dst = sccache + slj * PMAX;
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) {
+          const int k = s8 * 64 + lane;
+          const float v = k < ldc ? Cj[k] : 0.f;
+          cv[s8] = v;
+          dst[(s8 >> 2) * 256 + lane * 4 + (s8 & 3)] = v;
+        }
+        if (lane == 0) sslot[j] = slj;
+        if (lane == lj) slS[SJ] = slj;
+      } else if (slj >= 0) {
+        const LDS_AS float* src = sccache + slj * PMAX + lane * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {   // two 16-byte LDS reads
+          cv[e] = src[e];
+          cv[4 + e] = src[256 + e];
+        }
+      } else {
+        const float* Cj = Cf + (int64_t)j * ldc;
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) cv[s8] = s8 * 64 + lane < ldc ? Cj[s8 * 64 + lane] : 0.f;
+      }
+#pragma unroll
+      for (int s8 = 0; s8 < 8; ++s8) gS[s8] = __builtin_fma(-(double)cv[s8], d, gS[s8]);
+      // bookkeeping of j (glmnet: the gradient BEFORE the move enters rsq)
+      const int evj = __builtin_amdgcn_readlane(flb, lj);
+      if (!((evj >> (8 + SJ)) & 1)) ++ever_n;
+      if (lane == lj) {
+        flb |= 1 << (8 + SJ);
+        aS[SJ] = an;
+      }
+      rsq_add += d * (2.0 * gj - d);
+      dlx = fmax(dlx, d * d);
+    }
+  });
+#ifdef ENET_PROF
+  if (lane == 0) sprof_row[23] += (unsigned long long)(clock64() - tpl0_);   // [23] loop only
+#endif
+#pragma unroll
+  for (int s8 = 0; s8 < 8; ++s8) {
+    if (s8 < T) {
+      const int k = s8 * 64 + lane;
+      sg[k] = gS[s8];
+      sa[k] = aS[s8];
+      if ((flb >> (8 + s8)) & 1) sflag[k] |= 2;
+    }
+  }
+  if (lane == 0) {
+    *sever_n = ever_n;
+    *sncache = ncache;
+  }
+#ifdef ENET_PROF
+  if (lane == 0) {   // mode S: [19] passes, [20] candidates visited, [21] cycles, [22] fetches
+    sprof_row[19] += 1ull;
+    sprof_row[20] += nit_;
+    sprof_row[21] += (unsigned long long)(clock64() - tps0_);
+    sprof_row[22] += nfetch_;
+  }
+#endif
+  return PassS{dlx, rsq_add};
+}
+
+// LASSO: alpha == 1 (dem == 0 at every lambda): the elastic-net walk and scaling are not
+// compiled into that instantiation (the kernel's code is ~60 KB against a 64 KB instruction
+// cache shared by two CUs; every unused walk variant is cache pressure on the hot one).
+template <typename CT, bool LASSO>
 __global__ __launch_bounds__(NTH) void enet_path_kernel(
     const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
     const unsigned char* __restrict__ ju_s, const double* __restrict__ ys_s,
@@ -350,7 +513,24 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     long spin_max) {
   constexpr int TMAX = PMAX / 64;
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
-  __shared__ double sds[TMAX][PMAX];      // per-block snapshots of Dcum (32 KB)
+  // Mode L's snapshots and staged blocks share one LDS region with mode S's column cache
+  // (mode S only runs before the first mode-L pass and never again; the switch re-zeroes the
+  // snapshots). sds: per-block snapshots of Dcum (32 KB); sCn2 / sCorr: see below.
+  __shared__ __attribute__((aligned(16))) unsigned char s_union[S_UNION];
+  double(&sds)[TMAX][PMAX] = *reinterpret_cast<double(*)[TMAX][PMAX]>(s_union);
+  float(&sCn2)[2][64 * 64] = *reinterpret_cast<float(*)[2][64 * 64]>(s_union + 32768);
+  float(&sCorr)[64 * 64] = *reinterpret_cast<float(*)[64 * 64]>(s_union + 65536);
+  // mode S: column slot c holds C[k][j] for every k at (c * PMAX + (k >> 8) * 256 + (k & 63) * 4
+  // + ((k >> 6) & 3)) floats: lane l's 8 coordinates k = s * 64 + l are two 16-byte reads
+  float* const sccache = reinterpret_cast<float*>(s_union);
+  __shared__ int sslot[PMAX];             // mode S: cache slot of coordinate k (-1: none)
+  __shared__ int sever_n;                 // mode S: coordinates that have ever moved
+  __shared__ int sncache;                 // mode S: cached columns
+  // phase-B hand-offs without a second barrier: wave 0's publication count (visits whose
+  // block t it has published) and the pull waves' phase-B arrival count (NP per visit
+  // with a prefetch block)
+  __shared__ int spub, sarr;
+  __shared__ int sfetch0;                 // mode S: cached columns at the lambda's start
   __shared__ int sflag[PMAX];             // bit0 ju, bit1 active
   __shared__ double spart2[2][NW][64];    // pull partials (and fp64 own-delta corr, slot 0),
                                           // double-buffered by visit parity
@@ -377,8 +557,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // (wave 0 loads it into registers at the start of its recurrence), the pull waves DMA the
   // next visited block's into sCn2[cpar ^ 1]. Keeping the recurrence's registers out of the
   // loop-carried state leaves the pull waves' code the whole register budget (no spills).
-  __shared__ __attribute__((aligned(16))) float sCn2[2][64 * 64];
-  __shared__ __attribute__((aligned(16))) float sCorr[64 * 64];   // C[t rows][tn cols] (fp32 C)
+  // sCn2[2][64 * 64], sCorr[64 * 64] (C[t rows][tn cols], fp32 C): in s_union above
   __shared__ __attribute__((aligned(16))) float sdall[64];         // wave 0: block t's deltas
   __shared__ int svis[8], snv, sblk_any[8];
   __shared__ double sdl;
@@ -414,6 +593,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     sflag[k] = (in && ju_s[(int64_t)pr.train * p + k]) ? 1 : 0;
   }
   for (int e = tid; e < TMAX * PMAX; e += NTH) (&sds[0][0])[e] = 0.0;
+  for (int k = tid; k < PMAX; k += NTH) sslot[k] = -1;
+  if (tid == 0) { sever_n = 0; sncache = 0; spub = 0; sarr = 0; sfetch0 = 0; }
   __syncthreads();
   const int nlam = pr.ulam_src >= 0 ? L : pr.nlam_req;
   const double alf = pr.ulam_src >= 0 ? 1.0 : pow(flmin, 1.0 / (double)(nlam - 1));
@@ -544,7 +725,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       for (; e < cnt; ++e) acc += colt[(int64_t)slist[c0 + e] * ldc] * sdelta[c0 + e];
     }
 #ifdef ENET_PROF
-    if (lane == 0) sprof[wid][5] += (unsigned long long)cnt;
+    if (sizeof(CT) != 4 && lane == 0) sprof[wid][5] += (unsigned long long)cnt;
 #endif
     // block t's 64x64 diagonal block -> sCn2[cpar] (wave 0 moves it into registers at the
     // start of the visit): sCn2[i * 64 + c] = C[t*64 + i][t*64 + c]. Rows >= p are clamped
@@ -665,6 +846,14 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   };
 
   int ready = -1;   // block whose gradient and diagonal registers a pass end left current
+  int nvis = 0;     // visits so far (all waves, uniform)
+  int narr = 0;     // ... of them with a prefetch block (phase-B arrivals expected: NP each)
+  // LDS hand-off waits (workgroup scope): spin with s_sleep until *c >= target, then acquire
+  auto wait_ge = [&](int* c, int target) __attribute__((always_inline)) {
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
   // Block tn's gradient is completed lazily: the visit that pulls for tn leaves the pull
   // partials (spart2[par]) and the own-delta correction partials (scorr2[par], or slot 0
   // of spart2 with fp64 C) in LDS, and the next visit's recurrence wave folds them into
@@ -685,7 +874,31 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     for (int w = 1; w < NW; ++w) sp += spart2[par][w][lane];
     return sp;
   };
+  bool modeS = sizeof(CT) == 4 && ENET_MODE_S != 0;
   auto pass = [&](bool full) __attribute__((always_inline)) -> double {
+    if (modeS) {
+      if (wid == 0) {
+        const PassS r = enet_pass_s(
+            full, T, ldc, ab, dem, reinterpret_cast<const float*>(Cq), (LDS_AS double*)sg,
+            (LDS_AS double*)sa, (const LDS_AS double*)svp, (LDS_AS int*)sflag,
+            (LDS_AS int*)sslot, (LDS_AS float*)sccache, (LDS_AS int*)&sever_n,
+            (LDS_AS int*)&sncache,
+#ifdef ENET_PROF
+            (LDS_AS unsigned long long*)&sprof[0][0]
+#else
+            nullptr
+#endif
+        );
+        if (lane == 0) {
+          sdl = r.dlx;
+          rsq_l += r.rsq;
+        }
+      }
+      __syncthreads();
+      const double r = sdl;
+      __syncthreads();
+      return r;
+    }
     double dlx_l = 0.0;
     for (int t = wid; t < T; t += NW) {     // blocks holding an active coordinate
       const bool a = full || ((sflag[t * 64 + lane] & 3) == 3);
@@ -737,15 +950,18 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           dg_hi[i] = sCn2[cpar][(i + 32) * 64 + lane];
         }
         dc0 = sdc[k];
-        ds0 = sds[t][k];
         gt = sg[k];
-        if (v > 0) gt = gt - pending_sum(vpar ^ 1);   // block t was the last visit's tn
+        // block t was the last visit's tn: its phase-B own-delta partials and snapshot come
+        // from the pull waves' arrivals (no second barrier per visit)
+        if (v > 0) wait_ge(&sarr, NP * narr);
+        ds0 = sds[t][k];
+        if (v > 0) gt = gt - pending_sum(vpar ^ 1);
         at = sa[k];
         const double vpt = svp[k];
         fl = sflag[k];
         const bool elig = (fl & 1) && (full || (fl & 2));
         const double thr_l = vpt * ab;
-        const double rden = dem == 0.0 ? 1.0 : 1.0 / (1.0 + vpt * dem);
+        const double rden = (LASSO || dem == 0.0) ? 1.0 : 1.0 / (1.0 + vpt * dem);
         // Each lane changes at most once per visit (lane > last): its bookkeeping is
         // deferred (delta + the gradient it was computed from), so the loop body is the
         // bare coordinate recurrence.
@@ -837,9 +1053,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         const uint64_t nzm = __builtin_amdgcn_ballot_w64(elig && at != 0.0);
         const int ncand = full ? __popcll(nzm) : __popcll(em);
         auto dense_walk = [&](auto lasso_tag) __attribute__((always_inline)) {
-          constexpr bool LASSO = decltype(lasso_tag)::value;
+          constexpr bool LW = decltype(lasso_tag)::value;   // lasso walk
           const double thr_e = elig ? thr_l : __builtin_inf();
-          if constexpr (LASSO) {
+          if constexpr (LW) {
             // lasso: an = u - clamp(u, -thr, thr) and d = (u - a) - clamp(u), so the serial
             // chain is max -> min -> sub -> sub -> readlane -> fma (u), and the gradient is
             // not carried per step (g = u - a_visit_start after the walk). Lane i's own
@@ -893,7 +1109,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
               const float ci = i < 32 ? dg_lo[i] : dg_hi[i - 32];
               const double d = readlane_d(dd, i);
               // in asm: left to itself the compiler materialises 64 constant lane masks in
-              // SGPRs and spills them
+              // SGPRs and spills them (an exec-masked v_mov_b64 instead measured 2 % slower:
+              // profiles/r04_enet/snap_exec_ab.txt)
               select_lane1(i, lane, usnap, u);
               u = __builtin_fma(-(double)ci, d, u);
             }
@@ -926,8 +1143,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         };
         if (!ENET_BALLOT_ONLY && ncand >= ENET_DENSE_MIN) {
           moved = ~0ull;
-          if (dem == 0.0) dense_walk(std::true_type{});
-          else dense_walk(std::false_type{});
+          if (LASSO || dem == 0.0) dense_walk(std::true_type{});
+          else if constexpr (!LASSO) dense_walk(std::false_type{});
         } else if (full || ENET_BALLOT_ONLY) {
           while (step() && step()) {
           }
@@ -1002,6 +1219,10 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         if (lane == 0) sprof[wid][2] += (unsigned long long)(wall_clock64() - ta_);
 #endif
       } else if (tn >= 0) {
+        // wave 0's publication of every earlier visit (Dcum of its blocks) and every pull
+        // wave's last phase B (sCorr is re-filled below) must be complete
+        wait_ge(&spub, nvis);
+        wait_ge(&sarr, NP * narr);
         pull_rest(t, tn, vpar);
 #ifdef ENET_PROF
         if (wid == 1 && lane == 0)
@@ -1031,6 +1252,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
             if (lane == 0) scorr_ok[vpar] = schg;
           }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&spub, nvis + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef ENET_PROF
         if (lane == 0) sprof[wid][9] += (unsigned long long)(wall_clock64() - tb_);
 #endif
@@ -1053,22 +1276,28 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         // snapshot of block tn for every column block except t (unchanged this phase)
         for (int j = my * 64 + lane; j < ldc; j += NP * 64)
           if ((j >> 6) != t) sds[tn][j] = sdc[j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&sarr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef ENET_PROF
         if (wid == 1 && lane == 0) sprof[wid][16] += (unsigned long long)(wall_clock64() - tb_);
 #endif
       }
-      __syncthreads();
-      if (tn >= 0) cpar ^= 1;              // tn's diagonal block is in the other buffer
+      if (tn >= 0) {
+        cpar ^= 1;                         // tn's diagonal block is in the other buffer
+        ++narr;
+      }
+      ++nvis;
       PROF_T(tc_);
       PROF_ADD(0, tc_ - tb_);
     }
     if (ready >= 0) {   // the prefetched block's gradient: fold its pending partials now
       if (wid == 0) {
+        wait_ge(&sarr, NP * narr);
         const int kr = ready * 64 + lane;
         sg[kr] = sg[kr] - pending_sum((nv - 1) & 1);
       }
-      __syncthreads();
     }
+    __syncthreads();   // every phase B of the pass is complete past here
     const double dlx = wave_max(dlx_l);
     if (tid == 0) sdl = dlx;
     __syncthreads();
@@ -1129,9 +1358,12 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     } else if (m == 0) {
       alm = BIGL;
     } else if (m == 1) {
-      // lambda_max needs the exact current gradient of every coordinate
-      for (int t = 0; t < T; ++t) pull(t);
-      ready = -1;
+      // lambda_max needs the exact current gradient of every coordinate (mode S keeps
+      // every gradient exact)
+      if (!modeS) {
+        for (int t = 0; t < T; ++t) pull(t);
+        ready = -1;
+      }
       double mx = 0.0;
       for (int k = lane; k < p; k += 64)
         if ((sflag[k] & 1) && svp[k] > 0.0) mx = fmax(mx, fabs(sg[k]) / svp[k]);
@@ -1141,7 +1373,23 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       alm *= alf;
     }
     ab = alm * alpha;
-    dem = alm * (1.0 - alpha);
+    dem = LASSO ? 0.0 : alm * (1.0 - alpha);
+    // leave mode S for good once many coordinates have moved or the last lambda fetched
+    // many new columns (cheap in mode L, where a new mover's row is pulled by the helpers)
+    const int fetched = sncache - sfetch0;
+    __syncthreads();
+    if (tid == 0) sfetch0 = sncache;
+    if (modeS && (sever_n > ENET_S_ENTER || fetched > ENET_S_FETCH)) {
+      // to mode L for the rest of the path: every gradient is exact (Dcum = 0), so the
+      // snapshots the column cache overwrote restart at zero and every block is pulled anew
+      modeS = false;
+      for (int e = tid; e < TMAX * PMAX; e += NTH) (&sds[0][0])[e] = 0.0;
+      ready = -1;
+      __syncthreads();
+    }
+#ifdef ENET_PROF
+    const unsigned long long tpass0_ = wall_clock64();
+#endif
     while (npass < maxit) {
       ++npass;
       double dl = pass(true);
@@ -1152,6 +1400,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         if (dl < thr) break;
       }
     }
+#ifdef ENET_PROF
+    if (tid == 0) sprof[0][5] += wall_clock64() - tpass0_;   // [5]: wall ticks inside passes
+#endif
     double* ap = apath + ((int64_t)q * L + m) * p;
     for (int k = tid; k < p; k += NTH) ap[k] = sa[k];
     rsq = wave_sum(rsq_l);
@@ -1214,14 +1465,17 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
   // ATE_ENET_SPIN_MAX overrides it (tests force the timeout path with 0)
   const char* sm = getenv("ATE_ENET_SPIN_MAX");
   const long spin_max = sm ? atol(sm) : (1l << 26);
-#define LAUNCH_C(CTT)                                                                          \
-  hipLaunchKernelGGL((enet_path_kernel<CTT>), dim3(nwg), dim3(NTH), 0, s, (const CTT*)C,       \
+#define LAUNCH_C(CTT, LS)                                                                      \
+  hipLaunchKernelGGL((enet_path_kernel<CTT, LS>), dim3(nwg), dim3(NTH), 0, s, (const CTT*)C,   \
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
                      (int*)npass_out, L, (int*)progress, spin_max)
-  if (c_f32) LAUNCH_C(float);
-  else LAUNCH_C(double);
+  const bool lasso = alpha == 1.0;
+  if (c_f32 && lasso) LAUNCH_C(float, true);
+  else if (c_f32) LAUNCH_C(float, false);
+  else if (lasso) LAUNCH_C(double, true);
+  else LAUNCH_C(double, false);
 #undef LAUNCH_C
   ATE_CHECK_LAUNCH();
   return 0;
