@@ -5,8 +5,9 @@ SURVEY.md K11-K14 + C04).
 GPU (csrc/gbdt.hip) or the numpy reference (reference/gbdt.py) — same spec, same
 integer histogram sums, so the same trees. With ``dist`` (row shards), each level's
 compact node histograms are all-reduced (C04, exact int64) on the fit's stream between
-steps of the native level loop (``ate_gbdt_run``), and every rank takes the same split
-decisions; the base score is an exact fixed-point mean and the bin edges come from a
+steps of the native level loop (``ate_gbdt_run``) -- at world W > 1 reduce-scattered by
+feature slice, each rank searching its slice and the per-block split candidates
+all-gathered (``c04_slices``) -- and every rank takes the same split decisions; the base score is an exact fixed-point mean and the bin edges come from a
 GLOBAL row sample (``global_bin_edges``), so a row-sharded fit grows the same trees bit
 for bit at every world size.
 """
@@ -174,13 +175,16 @@ def fit_gbdt(X, y, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
             Xbh = Xb[0][:, :p].t().cpu().numpy()          # device row-major panel
         else:
             Xbh = np.asarray(Xb[0].cpu() if isinstance(Xb[0], torch.Tensor) else Xb[0])
-        red = None
+        red = c04 = None
         if dist is not None and dist.world > 1:
             def red(a):
                 t = torch.from_numpy(np.ascontiguousarray(a))
                 return dist.sum_(t).numpy()
+            nr, pw = c04_slices(p, dist)
+            if nr > 1:
+                c04 = SlicedC04(dist, p, nr, pw)
         tr = ref.fit(Xbh, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
-                     hist_reduce=red)
+                     hist_reduce=red, c04=c04)
         return GbdtModel(tr.feat, tr.thr, tr.value, tr.base, loss, depth, edges, "cpu",
                          tr.predict_binned(Xbh))
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -219,7 +223,8 @@ class FitArgs(ctypes.Structure):
                 ("y", P), ("f", P), ("idx", P * 2), ("gh", P * 2), ("bkt", P), ("cnt", P),
                 ("base", P), ("btot", P), ("seg", P * 2), ("tot", P), ("feat", P), ("thr", P),
                 ("value", P), ("H", P * 2), ("Hs", P), ("slab", P), ("slab_cap", ctypes.c_int64),
-                ("cand", P)]
+                ("cand", P), ("nr", ctypes.c_int), ("rk", ctypes.c_int), ("pw", ctypes.c_int),
+                ("pl", ctypes.c_int), ("Hl", P), ("candg", P)]
 
 
 class RunState(ctypes.Structure):
@@ -229,6 +234,65 @@ class RunState(ctypes.Structure):
 
 
 MAXB = 2 ** (MAX_DEPTH - 1) + 1    # csrc/gbdt.hip MAXB: partition buckets + retired
+
+
+def c04_slices(p, dist):
+    """Feature-sliced C04 geometry (nr, pw): nr rank blocks of pw = ceil(p / nr) features
+    (rank r owns [r * pw, min(p, r * pw + pw))), or (1, p) for a single device, when
+    ATE_GBDT_C04=allreduce, or when some rank's slice would be empty (p small next to
+    the world size)."""
+    import os
+    if dist is None or dist.world == 1 or os.environ.get("ATE_GBDT_C04", "") == "allreduce":
+        return 1, p
+    w = dist.world
+    pw = -(-p // w)
+    if p - (w - 1) * pw < 1:
+        return 1, p
+    return w, pw
+
+
+class SlicedC04:
+    """Feature-sliced C04 for the numpy reference fit (reference/gbdt.fit ``c04``): the
+    scheme of the device stepper (csrc/gbdt.hip header) with host collectives."""
+
+    def __init__(self, dist, p, nr, pw):
+        self.dist, self.p, self.nr, self.pw = dist, p, nr, pw
+        self.joff = dist.rank * pw
+        self.pl = min(pw, p - self.joff)
+
+    def scatter(self, hist):
+        nn = hist.shape[0]
+        img = np.zeros((nn, self.nr * self.pw, 256, 2), dtype=np.int64)
+        img[:, :self.p] = hist
+        # rank-block-major [nr][nn][pw][256][2]: rank r's reduce-scatter chunk is its slice
+        t = torch.from_numpy(np.ascontiguousarray(
+            img.reshape(nn, self.nr, self.pw, 256, 2).transpose(1, 0, 2, 3, 4))).reshape(-1)
+        out = torch.empty(t.numel() // self.nr, dtype=torch.int64)
+        self.dist.comm.reduce_scatter_(out, t)
+        return out.numpy().reshape(nn, self.pw, 256, 2)[:, :self.pl]
+
+    def pick(self, sps):
+        nn = len(sps)
+        c = np.zeros((nn, 5), dtype=np.int64)
+        c[:, 0] = np.float64(-np.inf).view(np.int64)
+        for k, sp in enumerate(sps):
+            if sp is not None:
+                c[k] = [np.float64(sp[0]).view(np.int64), *sp[1:]]
+        g = torch.empty(self.nr * c.size, dtype=torch.int64)
+        self.dist.comm.all_gather_into_(g, torch.from_numpy(c.reshape(-1)))
+        g = g.numpy().reshape(self.nr, nn, 5)
+        out = []
+        for k in range(nn):
+            best = None
+            for r in range(self.nr):
+                gain = float(g[r, k, 0].view(np.float64))
+                if gain == -np.inf:
+                    continue
+                key = (-gain, int(g[r, k, 1]), int(g[r, k, 2]))
+                if best is None or key < best[0]:
+                    best = (key, (gain, *(int(v) for v in g[r, k, 1:])))
+            out.append(None if best is None else best[1])
+        return out
 
 
 def exact_base(y_train, n_train, loss, dist=None):
@@ -278,15 +342,22 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
     btot = torch.empty(MAXB, **i32)
     seg = [torch.zeros(MAXB + 1, **i32), torch.zeros(MAXB + 1, **i32)]
     tot = torch.zeros(2 * M, **i64)
-    per = 512 * p
-    H = [torch.empty(2 ** (depth - 1) * per, **i64) for _ in range(2)]
-    Hs = torch.empty(max(1, 2 ** (depth - 2)) * per, **i64)
     # rule 1 (hessian child rule + a pause per level for the histogram all-reduce) for
     # every row-sharded fit, world 1 included (the same code path as world W)
     rule = 0 if dist is None else 1
+    # world W > 1: feature-sliced C04 (reduce-scatter of the level histograms, split search
+    # on this rank's pw features, all-gather of the candidates; csrc/gbdt.hip header)
+    nr, pw = c04_slices(p, dist) if rule == 1 else (1, p)
+    rk = dist.rank if nr > 1 else 0
+    slots = max(1, 2 ** (depth - 2))
+    H = [torch.empty(2 ** (depth - 1) * 512 * pw, **i64) for _ in range(2)]
+    Hs = torch.empty(slots * 512 * nr * pw, **i64)
+    Hl = torch.empty(slots * 512 * pw, **i64) if nr > 1 else None
     cap = int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule))
     slab = torch.empty(cap, **i64)
-    cand = torch.empty((1 << max(depth - 1, 0)) * (-(-p // 8)) * 4, **i64)   # 32-B Cand
+    ncand = (1 << max(depth - 1, 0)) * (-(-pw // 8)) * 4                     # 32-B Cand
+    cand = torch.empty(ncand, **i64)
+    candg = torch.empty(nr * ncand, **i64) if nr > 1 else None
     P = ctypes.c_void_p
     a = FitArgs(Xr=Xr.data_ptr(), ldr=ldr, n=n, n_train=n_train, p=p, depth=depth,
                 n_trees=n_trees, loss=LOSS[loss], rule=rule, W=W, lam=lam,
@@ -294,7 +365,10 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
                 y=yt.data_ptr(), f=f.data_ptr(), bkt=bkt.data_ptr(), cnt=cntb.data_ptr(),
                 base=baseb.data_ptr(), btot=btot.data_ptr(), tot=tot.data_ptr(),
                 feat=feat.data_ptr(), thr=thr.data_ptr(), value=value.data_ptr(),
-                Hs=Hs.data_ptr(), slab=slab.data_ptr(), slab_cap=cap, cand=cand.data_ptr())
+                Hs=Hs.data_ptr(), slab=slab.data_ptr(), slab_cap=cap, cand=cand.data_ptr(),
+                nr=nr, rk=rk, pw=pw, pl=min(pw, p - rk * pw),
+                Hl=Hl.data_ptr() if Hl is not None else None,
+                candg=candg.data_ptr() if candg is not None else None)
     a.idx = (P * 2)(idx[0].data_ptr(), idx[1].data_ptr())
     a.gh = (P * 2)(gh[0].data_ptr(), gh[1].data_ptr())
     a.seg = (P * 2)(seg[0].data_ptr(), seg[1].data_ptr())
@@ -303,13 +377,20 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
     run = _native.hip().ate_gbdt_run
     while True:
         # the stepper enqueues a level's kernels on the current stream; a row-sharded fit
-        # pauses after each level's compact histograms, which are all-reduced (C04) on the
-        # same stream -- no host callback, no host sync
+        # pauses after each level's compact histograms, which are all-reduced (C04) -- or,
+        # feature-sliced, reduce-scattered, and after the slice's split search its
+        # candidates all-gathered -- on the same stream: no host callback, no host sync
         rc = run(ctypes.addressof(a), ctypes.addressof(st),
                  ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         if rc == 0:
             break
-        if rc != 1 or dist is None:
+        if rc not in (1, 2) or dist is None or (rc == 2 and nr == 1):
             raise RuntimeError(f"ate_gbdt_run failed with status {rc}")
-        dist.sum_(Hs[:st.red_count])
+        m = st.red_count
+        if rc == 1 and nr == 1:
+            dist.sum_(Hs[:m])
+        elif rc == 1:
+            dist.comm.reduce_scatter_(Hl[:m // nr], Hs[:m])
+        else:
+            dist.comm.all_gather_into_(candg[:nr * m], cand[:m])
     return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu", f)

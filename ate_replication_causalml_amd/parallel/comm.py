@@ -38,6 +38,14 @@ class LocalComm:
     def all_gather(self, t):
         return [t]
 
+    def all_gather_into_(self, out, t):
+        out.copy_(t.reshape(out.shape))
+        return out
+
+    def reduce_scatter_(self, out, t):
+        out.copy_(t.reshape(out.shape))
+        return out
+
     def broadcast_(self, t, src=0):
         return t
 
@@ -75,6 +83,32 @@ class TorchComm:
     def all_gather(self, t):
         out = [torch.empty_like(t) for _ in range(self.world_size)]
         self.dist.all_gather(out, t.contiguous(), group=self.group)
+        return out
+
+    def _host_staged(self, *ts):
+        # gloo's tensor-form reduce-scatter / all-gather are host-side: device tensors are
+        # staged through host copies (gloo rehearsals only; RCCL runs them on the device)
+        return not self.capturable and any(x.is_cuda for x in ts)
+
+    def all_gather_into_(self, out, t):
+        """out (contiguous, world * t.numel() elements) = rank-ordered concatenation."""
+        if self._host_staged(out, t):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            self.dist.all_gather_into_tensor(h, t.cpu().contiguous(), group=self.group)
+            return out.copy_(h)
+        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def reduce_scatter_(self, out, t):
+        """out = this rank's chunk (rank-ordered, out.numel() elements each) of the SUM of
+        every rank's t: (W-1)/W of t's bytes on each ring link, half an all-reduce."""
+        if self._host_staged(out, t):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            self.dist.reduce_scatter_tensor(h, t.cpu().contiguous(), op=self.dist.ReduceOp.SUM,
+                                            group=self.group)
+            return out.copy_(h)
+        self.dist.reduce_scatter_tensor(out, t.contiguous(), op=self.dist.ReduceOp.SUM,
+                                        group=self.group)
         return out
 
     def dup(self):
@@ -142,6 +176,17 @@ class ThreadSimComm:
         self.w.barrier.wait()
         out = [s.clone() for s in self.w.slots]
         self.w.barrier.wait()
+        return out
+
+    def all_gather_into_(self, out, t):
+        parts = self.all_gather(t)
+        out.copy_(torch.cat([q.reshape(-1) for q in parts]).reshape(out.shape))
+        return out
+
+    def reduce_scatter_(self, out, t):
+        acc = self._reduce(t.detach().clone(), lambda a, b: a + b).reshape(-1)
+        n = out.numel()
+        out.copy_(acc[self.rank * n:(self.rank + 1) * n].reshape(out.shape))
         return out
 
     def broadcast_(self, t, src=0):

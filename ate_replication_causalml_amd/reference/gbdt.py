@@ -92,9 +92,13 @@ def best_split(hist, G, H, lam, min_child, min_gain):
 
 
 def fit(Xb, y, train, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0,
-        min_gain=0.0, hist_reduce=None):
+        min_gain=0.0, hist_reduce=None, c04=None):
     """Xb [p, n] uint8, y [n], train [n] bool. ``hist_reduce`` (optional) sums a node
-    histogram stack across row shards (the C04 all-reduce in the distributed path)."""
+    histogram stack across row shards (the C04 all-reduce in the distributed path).
+    ``c04`` (optional, with ``hist_reduce`` for the scalar sums): feature-sliced C04 --
+    ``c04.scatter(hist)`` returns this rank's summed feature slice [nn, pl, 256, 2] (global
+    features ``c04.joff ...``), ``c04.pick(cands)`` the best of every rank's per-node
+    candidates (gain desc, feature asc, bin asc: the single-device argmax)."""
     p, n = Xb.shape
     M = 2 ** (depth + 1) - 1
     ytr = y[train]
@@ -127,14 +131,26 @@ def fit(Xb, y, train, loss="squared", n_trees=100, depth=6, lr=0.1, lam=1.0, min
                         acc = np.zeros(nn * 256, dtype=np.int64)
                         np.add.at(acc, idx, w)
                         hist[:, j, :, c] = acc.reshape(nn, 256)
-                if hist_reduce is not None:
+                if c04 is not None:
+                    hist = c04.scatter(hist)
+                elif hist_reduce is not None:
                     hist = hist_reduce(hist)
+            sps = [None] * nn
+            for k in range(nn):
+                hk = 2 ** d - 1 + k
+                if d < depth and not (d > 0 and feat[t, (hk - 1) // 2] < 0):
+                    sps[k] = best_split(hist[k], *tot[hk], lam, min_child, min_gain)
+                    if c04 is not None and sps[k] is not None:
+                        g_, j_, b_, gl_, hl_ = sps[k]
+                        sps[k] = (g_, j_ + c04.joff, b_, gl_, hl_)
+            if c04 is not None and d < depth:
+                sps = c04.pick(sps)
             for k in range(nn):
                 hk = 2 ** d - 1 + k
                 if d > 0 and feat[t, (hk - 1) // 2] < 0:
                     continue                       # parent is a leaf / absent: no node
                 G, H = tot[hk]
-                sp = best_split(hist[k], G, H, lam, min_child, min_gain) if d < depth else None
+                sp = sps[k]
                 if sp is None:
                     feat[t, hk] = -1
                     value[t, hk] = -lr * (G / FIX) / (H / FIX + lam)

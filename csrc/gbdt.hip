@@ -34,7 +34,15 @@
 //   compact histogram with the element count to all-reduce; the caller enqueues the
 //   collective on the same stream (torch.distributed / RCCL, no host sync) and calls
 //   again. A single-device fit runs to completion in one call. Root totals come from
-//   the (reduced) level-0 histogram.
+//   the (reduced) level-0 histogram;
+// * feature-sliced C04 (world W > 1): the compact histograms are written rank-block-major
+//   ([W][slot][c][bin][pw], pw = ceil(p / W) features per rank), the caller REDUCE-
+//   SCATTERS them (each rank receives the sums of its own feature slice: half the ring
+//   bytes of an all-reduce), expand + split search run on the slice only, and the stepper
+//   pauses once more for an all-gather of the per-(node, block) candidates (32 B each);
+//   the final reduction over all ranks' candidates picks the same (gain, feature, bin) as
+//   a single device, so the trees stay bit-identical at every world size (the
+//   data-parallel scheme of LightGBM's voting-free mode).
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
@@ -320,9 +328,13 @@ __global__ __launch_bounds__(NTH) void gbdt_hist_kernel(
 // Hs[slot][c][b][j] (feature-minor) = sum of the slabs of histogrammed node k, slot 0 at
 // the root, slot k >> 1 below (the histogrammed child of parent k >> 1; gbdt_expand_kernel
 // puts the level in node order). Nodes without a histogram of their own write nothing.
+// Feature-sliced layout (nr > 1 rank blocks of pw features, nr * pw >= p): entry (slot, c,
+// bin, j) goes to block r = j / pw at ((r * nsl + slot) * 512 + cb) * pw + j - r * pw
+// (nsl = slots of this level), the padding features past p are written as zeros; nr = 1,
+// pw = p is the plain [slot][c][b][j] image.
 __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
     const u64* __restrict__ slab, const int32_t* __restrict__ seg, const int64_t* tot, int rule,
-    int nn, int p, int d, int64_t CH, int ydim, int64_t* __restrict__ Hs) {
+    int nn, int p, int d, int64_t CH, int ydim, int64_t* __restrict__ Hs, int nr, int pw) {
   __shared__ int sseg[MAXN + 1], sacc[MAXN + 1], snch[MAXN];
   const int k = blockIdx.y;
   if (threadIdx.x <= nn) sseg[threadIdx.x] = seg[threadIdx.x];
@@ -331,10 +343,17 @@ __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
   if (threadIdx.x == 0) gbdt_plan(sseg, tot, rule, nn, d, CH, sacc, snch);
   __syncthreads();
   const int a = sacc[k], c = snch[k];
-  const int64_t per = 512LL * p;
-  int64_t* Hk = Hs + (d == 0 ? 0 : (k >> 1)) * per;
+  const int P = nr * pw;                                    // padded feature count
+  const int64_t per = 512LL * P;
+  const int slot = d == 0 ? 0 : (k >> 1), nsl = d == 0 ? 1 : nn >> 1;
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
-    const int cb = (int)(t / p), j = (int)(t - (int64_t)cb * p);
+    const int cb = (int)(t / P), j = (int)(t - (int64_t)cb * P);
+    const int r = j / pw;
+    int64_t* dst = Hs + ((int64_t)(r * nsl + slot) * 512 + cb) * pw + (j - r * pw);
+    if (j >= p) {
+      *dst = 0;
+      continue;
+    }
     const int yb = j / FB, fl = j - yb * FB;
     // slab image [bin][channel][slot] (gbdt_hist_kernel); Hs is [channel][bin][feature]
     const int bc = ((cb & 255) << 1) | (cb >> 8);
@@ -349,7 +368,7 @@ __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
       v3 += sp[(i + 3) * stride];
     }
     for (; i < c; ++i) v0 += sp[i * stride];
-    Hk[t] = (int64_t)(v0 + v1 + v2 + v3);
+    *dst = (int64_t)(v0 + v1 + v2 + v3);
   }
 }
 
@@ -402,25 +421,29 @@ struct Cand {               // best split of one (node, feature block)
   int j, b;
   int64_t gl, hl;
 };
+static_assert(sizeof(Cand) == 32, "Cand: 32 B (models/gbdt.py sizes cand as 4 int64 each)");
 
 // grid (node, 8-feature block): the block's histograms are staged feature-major in LDS
 // ([c][f][bin], so a lane's 4 consecutive bins are two 16-B reads); wave = feature,
 // lane = 4 bins: lane totals, in-wave exclusive scan, running prefix and the gains of
 // the 4 split points (ascending bins, strict > keeps the lowest on ties), wave argmax
 // (gain desc, feature asc, bin asc); the workgroup's best goes to cand[node][block].
+// H has row stride p and holds features [joff, joff + pc) (a rank's slice; pc <= p, the
+// slice's blocks past pc yield -inf candidates); candidates carry GLOBAL feature indices.
 __global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
-    const int64_t* __restrict__ H, int p, int d, int depth, double lam, int64_t min_child,
-    const int64_t* __restrict__ tot, const int32_t* __restrict__ feat, Cand* __restrict__ cand) {
+    const int64_t* __restrict__ H, int p, int pc, int joff, int d, int depth, double lam,
+    int64_t min_child, const int64_t* __restrict__ tot, const int32_t* __restrict__ feat,
+    Cand* __restrict__ cand) {
   __shared__ __attribute__((aligned(16))) int64_t sh[2 * SFB * 256];
   __shared__ Cand wb[NTS / 64];
   const int k = blockIdx.x, yb = blockIdx.y, ydim = gridDim.y;
   const int hk = (1 << d) - 1 + k;
   if (d >= depth || (d > 0 && feat[(hk - 1) / 2] < 0)) return;
-  const int j0 = yb * SFB, nf = min(SFB, p - j0);
+  const int j0 = yb * SFB, nf = min(SFB, pc - j0);
   const int64_t* Hk = H + (int64_t)k * 512 * p + j0;
   {
     constexpr int PER = 2 * SFB * 256 / NTS;                // entries per thread
-    const int fl = threadIdx.x & (SFB - 1), fc = min(fl, nf - 1);
+    const int fl = threadIdx.x & (SFB - 1), fc = max(0, min(fl, nf - 1));
     int64_t v[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -438,7 +461,7 @@ __global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
   const int64_t G = tot[2 * hk], Hh = tot[2 * hk + 1];
   const double gf = (double)G / GFIX, hf = (double)Hh / GFIX;
   const double parent = gf * gf / (hf + lam);
-  Cand lb{-INFINITY, j0 + f, 0x7fffffff, 0, 0};
+  Cand lb{-INFINITY, joff + j0 + f, 0x7fffffff, 0, 0};
   if (f < nf) {                                             // uniform per wave
     const longlong2* pg = reinterpret_cast<const longlong2*>(sh + f * 256 + 4 * lane);
     const longlong2* ph = reinterpret_cast<const longlong2*>(sh + (SFB + f) * 256 + 4 * lane);
@@ -460,7 +483,7 @@ __global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
         const double glf = (double)GL / GFIX, hlf = (double)HL / GFIX;
         const double grf = gf - glf, hrf = hf - hlf;
         const double gain = glf * glf / (hlf + lam) + grf * grf / (hrf + lam) - parent;
-        if (gain > lb.gain) lb = {gain, j0 + f, 4 * lane + i, GL, HL};
+        if (gain > lb.gain) lb = {gain, joff + j0 + f, 4 * lane + i, GL, HL};
       }
     }
   }
@@ -485,11 +508,13 @@ __global__ __launch_bounds__(NTS) void gbdt_split_search_kernel(
 }
 
 // one wave per node of level d: best candidate over the feature blocks -> split (and the
-// children's totals) or leaf value; children of leaves / absent nodes are marked -2
+// children's totals) or leaf value; children of leaves / absent nodes are marked -2.
+// Candidates of node k: cand[r * rstride + k * ydim + y] for nr rank blocks (all-gathered
+// feature slices; nr = 1 on a single device)
 __global__ __launch_bounds__(64) void gbdt_split_final_kernel(
-    const Cand* __restrict__ cand, int ydim, int d, int depth, double min_gain, double lam,
-    double lr, int64_t* __restrict__ tot, int32_t* __restrict__ feat, int32_t* __restrict__ thr,
-    double* __restrict__ value) {
+    const Cand* __restrict__ cand, int ydim, int nr, int64_t rstride, int d, int depth,
+    double min_gain, double lam, double lr, int64_t* __restrict__ tot, int32_t* __restrict__ feat,
+    int32_t* __restrict__ thr, double* __restrict__ value) {
   const int k = blockIdx.x, lane = threadIdx.x;
   const int hk = (1 << d) - 1 + k;
   if (d > 0 && feat[(hk - 1) / 2] < 0) {
@@ -498,8 +523,9 @@ __global__ __launch_bounds__(64) void gbdt_split_final_kernel(
   }
   Cand lb{-INFINITY, 0x7fffffff, 0x7fffffff, 0, 0};
   if (d < depth)
-    for (int y = lane; y < ydim; y += 64) {
-      const Cand c = cand[(int64_t)k * ydim + y];
+    for (int y = lane; y < nr * ydim; y += 64) {
+      const int r = y / ydim;
+      const Cand c = cand[r * rstride + (int64_t)k * ydim + (y - r * ydim)];
       if (better(c.gain, c.j, c.b, Best{lb.gain, lb.j, lb.b})) lb = c;
     }
 #pragma unroll
@@ -770,11 +796,20 @@ struct GbdtFitArgs {
   u64* slab;              // [slab_cap] partial histograms
   int64_t slab_cap;
   Cand* cand;             // [2^(depth-1) * ceil(p / 8)] split candidates (32 B each)
+  // feature-sliced C04 (nr > 1; rule 1): rank `rk` of nr owns features [rk * pw, rk * pw +
+  // pl); Hs is then [nr][slots][2][256][pw], Hl [slots][2][256][pw] receives the reduce-
+  // scatter, candg [nr][2^(depth-1) * ceil(pw / 8)] Cands the candidate all-gather.
+  // nr = 1: Hl, candg unused.
+  int nr, rk, pw, pl;
+  int64_t* Hl;
+  Cand* candg;
 };
 
 // Resumable position of a fit (models/gbdt.py::RunState): tree t, level d, ping-pong
-// index cur, resume = 1 when re-entering after the caller all-reduced level d's compact
-// histograms (red_count int64 entries at the start of Hs).
+// index cur, resume = 1 when re-entering after the caller all-reduced (nr = 1) or reduce-
+// scattered (nr > 1) level d's compact histograms (red_count int64 entries at the start
+// of Hs), 2 after the caller all-gathered the level's candidates (red_count int64 entries
+// of a.cand per rank, into a.candg).
 struct GbdtRunState {
   int t, d, cur, resume;
   int64_t red_count;
@@ -825,8 +860,10 @@ ATE_API int64_t ate_gbdt_slab_entries(int64_t n_train, int p, int depth, int rul
 }
 
 // Runs the fit from the position in *state to completion (returns 0), or until a
-// row-sharded fit (rule 1) needs level d's compact histograms all-reduced across ranks
-// (returns 1; state->red_count int64 entries at a.Hs; call again to continue).
+// row-sharded fit (rule 1) needs level d's compact histograms all-reduced (nr = 1) or
+// reduce-scattered into a.Hl (nr > 1) across ranks (returns 1; state->red_count int64
+// entries at a.Hs), or, feature-sliced, the level's split candidates all-gathered into
+// a.candg (returns 2; state->red_count int64 entries at a.cand). Call again to continue.
 ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
   const GbdtFitArgs& a = *static_cast<const GbdtFitArgs*>(args);
   GbdtRunState& s = *static_cast<GbdtRunState*>(state);
@@ -835,9 +872,18 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
     return -1;
   if ((a.n_train + a.R - 1) / a.R > a.W) return -2;
   if (a.slab_cap < ate_gbdt_slab_entries(a.n_train, a.p, a.depth, a.rule)) return -5;
+  const bool sliced = a.nr > 1;
+  if (sliced && (a.rule != 1 || a.rk < 0 || a.rk >= a.nr || a.pw < 1 || (int64_t)a.nr * a.pw < a.p ||
+                 a.pl < 1 || a.pl > a.pw || a.rk * a.pw + a.pl > a.p || !a.Hl || !a.candg))
+    return -6;
   const int M = (1 << (a.depth + 1)) - 1;
-  const int ydim = (a.p + FB - 1) / FB, ydim_s = (a.p + SFB - 1) / SFB;
-  const int64_t per = 512LL * a.p;
+  const int ydim = (a.p + FB - 1) / FB;
+  // histogram image / split search geometry of this rank: all p features, or its slice
+  const int hp = sliced ? a.pw : a.p, hc = sliced ? a.pl : a.p, joff = sliced ? a.rk * a.pw : 0;
+  const int nr = sliced ? a.nr : 1;
+  const int ydim_s = (hp + SFB - 1) / SFB;
+  const int64_t per = 512LL * hp;
+  int64_t* Hsrc = sliced ? a.Hl : a.Hs;
   // ablation switch (profiling only): 1 no LDS atomics, 2 no bin gather, 4 no slab store,
   // 8 G atomics only, 16 H atomics as u32
   const char* hm = getenv("ATE_GBDT_HIST_MODE");
@@ -857,35 +903,45 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
       const int nn = 1 << d;
       int64_t* Hc = a.H[d & 1];
       const int64_t* Hp = a.H[(d + 1) & 1];
+      const int nsl = d == 0 ? 1 : nn / 2;                 // compact histogram slots
       if (d < a.depth) {
-        if (!s.resume) {
+        if (s.resume == 0) {
           int64_t CH, nwg;
           gbdt_hist_geom(a.n_train, a.p, d, a.rule, &CH, &nwg);
           hipLaunchKernelGGL(hmode ? gbdt_hist_kernel<true> : gbdt_hist_kernel<false>,
                              dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr,
                              a.ldr, a.idx[cur], a.gh[cur], a.seg[cur], a.tot, a.rule, nn, a.p, d,
                              CH, ydim, a.slab, hmode, a.loss);
+          const int64_t perP = 512LL * nr * hp;
           hipLaunchKernelGGL(gbdt_hist_reduce_kernel,
-                             dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 256), nn),
+                             dim3((unsigned)std::min<int64_t>((perP + NT - 1) / NT, 256), nn),
                              dim3(NT), 0, st, a.slab, a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
-                             ydim, a.Hs);
+                             ydim, a.Hs, nr, hp);
           if (a.rule == 1) {
             ATE_CHECK_LAUNCH();
             s.resume = 1;
-            s.red_count = (d == 0 ? 1 : nn / 2) * per;
-            return 1;                                     // caller all-reduces Hs
+            s.red_count = nsl * perP;
+            return 1;                       // caller all-reduces / reduce-scatters Hs
+          }
+        }
+        if (s.resume <= 1) {
+          if (d == 0) hipLaunchKernelGGL(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, Hsrc, hp, a.tot);
+          hipLaunchKernelGGL(gbdt_expand_kernel,
+                             dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 128), nsl),
+                             dim3(NT), 0, st, Hsrc, Hp, Hc, a.seg[cur], a.tot, ft, a.rule, hp, d);
+          hipLaunchKernelGGL(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc,
+                             hp, hc, joff, d, a.depth, a.lam, a.min_child, a.tot, ft, a.cand);
+          if (sliced) {
+            ATE_CHECK_LAUNCH();
+            s.resume = 2;
+            s.red_count = (int64_t)nn * ydim_s * (sizeof(Cand) / sizeof(int64_t));
+            return 2;                                     // caller all-gathers cand
           }
         }
         s.resume = 0;
-        if (d == 0) hipLaunchKernelGGL(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, a.Hs, a.p, a.tot);
-        hipLaunchKernelGGL(gbdt_expand_kernel,
-                           dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 128),
-                                d == 0 ? 1 : nn / 2),
-                           dim3(NT), 0, st, a.Hs, Hp, Hc, a.seg[cur], a.tot, ft, a.rule, a.p, d);
-        hipLaunchKernelGGL(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc, a.p,
-                           d, a.depth, a.lam, a.min_child, a.tot, ft, a.cand);
       }
-      hipLaunchKernelGGL(gbdt_split_final_kernel, dim3(nn), dim3(64), 0, st, a.cand, ydim_s, d,
+      hipLaunchKernelGGL(gbdt_split_final_kernel, dim3(nn), dim3(64), 0, st,
+                         sliced ? a.candg : a.cand, ydim_s, nr, (int64_t)nn * ydim_s, d,
                          a.depth, a.min_gain, a.lam, a.lr, a.tot, ft, th, vt);
       if (d + 1 < a.depth) {
         const int nb = 2 * nn + 1;

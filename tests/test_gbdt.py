@@ -58,6 +58,55 @@ def test_gbdt_row_sharded_equals_single(world):
         assert m.base == m1.base
 
 
+def test_c04_slice_geometry():
+    class D:
+        def __init__(self, w):
+            self.world, self.rank = w, 0
+    assert G.c04_slices(5, None) == (1, 5)
+    assert G.c04_slices(5, D(1)) == (1, 5)
+    assert G.c04_slices(5, D(2)) == (2, 3)
+    assert G.c04_slices(5, D(3)) == (3, 2)
+    assert G.c04_slices(5, D(4)) == (1, 5)          # rank 3's slice would be empty
+    assert G.c04_slices(2000, D(8)) == (8, 250)
+
+
+@pytest.mark.parametrize("world,mode", [(2, "sliced"), (3, "sliced"), (3, "allreduce")])
+def test_gbdt_feature_sliced_c04_equals_single(world, mode, monkeypatch):
+    """Feature-sliced C04 (reduce-scatter of each level's histograms, split search on the
+    rank's slice, all-gather of the per-node candidates): the signal sits in features owned
+    by different ranks (first and last), so the winning split comes from any rank; the
+    trees equal the single-device ones bit for bit, and so do those of the all-reduce
+    scheme (ATE_GBDT_C04=allreduce)."""
+    if mode == "allreduce":
+        monkeypatch.setenv("ATE_GBDT_C04", "allreduce")
+    r = np.random.default_rng(7)
+    X = r.normal(size=(1500, 7))
+    y = np.sin(X[:, 6]) + 0.7 * (X[:, 0] > 0.3) - 0.4 * X[:, 3] + 0.1 * r.normal(size=1500)
+    m1 = G.fit_gbdt(X, y, n_trees=6, depth=4, backend="cpu")
+    calls = []
+    orig = G.SlicedC04.scatter
+
+    def spy(self, hist):
+        calls.append(self.pl)
+        return orig(self, hist)
+    monkeypatch.setattr(G.SlicedC04, "scatter", spy)
+
+    def fn(comm):
+        d = DistContext.for_rank(comm, len(y))
+        return G.fit_gbdt(d.local(X), d.local(y), n_trees=6, depth=4, backend="cpu", dist=d)
+
+    for m in run_simulated(world, fn):
+        np.testing.assert_array_equal(m.feat, m1.feat)
+        np.testing.assert_array_equal(m.thr, m1.thr)
+        np.testing.assert_array_equal(m.value, m1.value)
+    assert set(m1.feat[m1.feat >= 0].tolist()) >= {0, 6}
+    if mode == "sliced":
+        pw = -(-7 // world)
+        assert sorted(set(calls)) == sorted({pw, 7 - (world - 1) * pw})
+    else:
+        assert not calls
+
+
 def test_global_edges_equal_single_device_edges_large_n():
     """n > the edge sample: each rank's rows of the global strided sample, gathered, give
     exactly sample_bin_edges of the whole matrix."""

@@ -18,6 +18,7 @@
 #   cfg3           config-3 per-GPU shard (N=1e7, p=500, 100 trees, rank 0 of 8)
 #   cfg5           config-5 per-GPU shard (N=1.25e7, p=2000, 100 trees); cfg5c: concurrent Y/W fits
 #   cfg5small      a small config-5 shard, concurrent then serial Y/W fits
+#   c04_ab         a small config-5 shard: feature-sliced C04 vs ATE_GBDT_C04=allreduce, x2
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
 #   gramdump       the bench panel's fold Gram stack -> OUT/gram_dump (tools/dump_bench_gram.py)
@@ -87,6 +88,12 @@ for step in "$@"; do
     cfg5small)   # 1/8 of a shard: both orders, same bits
       run cfg5small_c 200 python -u tools/cfg5.py --rows 12500000 --cols 2000 --trees 20 --shard 0/8 --concurrent && \
       run cfg5small_s 200 python -u tools/cfg5.py --rows 12500000 --cols 2000 --trees 20 --shard 0/8 ;;
+    c04_ab)      # 1/8 of a shard, feature-sliced C04 (default at --shard 0/8) vs all-reduce, x2
+      for rep in 1 2; do
+        run c04_sliced_$rep 200 python -u tools/cfg5.py --rows 12500000 --cols 2000 --trees 20 --shard 0/8 && \
+        ATE_GBDT_C04=allreduce run c04_allreduce_$rep 200 python -u tools/cfg5.py --rows 12500000 \
+          --cols 2000 --trees 20 --shard 0/8 || exit 1
+      done ;;
     configs)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
