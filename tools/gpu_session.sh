@@ -19,6 +19,7 @@
 #   cfg5           config-5 per-GPU shard (N=1.25e7, p=2000, 100 trees); cfg5c: concurrent Y/W fits
 #   cfg5small      a small config-5 shard, concurrent then serial Y/W fits
 #   c04_ab         a small config-5 shard: feature-sliced C04 vs ATE_GBDT_C04=allreduce, x2
+#   micro          tools/micro/mfma_peak (matrix / vector peaks) and the fp64 Gram alone
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
 #   gramdump       the bench panel's fold Gram stack -> OUT/gram_dump (tools/dump_bench_gram.py)
@@ -94,6 +95,9 @@ for step in "$@"; do
         ATE_GBDT_C04=allreduce run c04_allreduce_$rep 200 python -u tools/cfg5.py --rows 12500000 \
           --cols 2000 --trees 20 --shard 0/8 || exit 1
       done ;;
+    micro)       # MFMA / vector FMA peaks and the fp64 Gram alone
+      run mfma_peak 60 ./tools/micro/mfma_peak && \
+      run gram_f64 200 python -u tools/gram_f64_time.py ;;
     configs)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
