@@ -20,6 +20,7 @@
 #   cfg5small      a small config-5 shard, concurrent then serial Y/W fits
 #   c04_ab         a small config-5 shard: feature-sliced C04 vs ATE_GBDT_C04=allreduce, x2
 #   micro          tools/micro/mfma_peak (matrix / vector peaks) and the fp64 Gram alone
+#   lvgaps         idle gaps of the host-driven forest level engine (kernel trace)
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
 #   gramdump       the bench panel's fold Gram stack -> OUT/gram_dump (tools/dump_bench_gram.py)
@@ -98,6 +99,14 @@ for step in "$@"; do
     micro)       # MFMA / vector FMA peaks and the fp64 Gram alone
       run mfma_peak 60 ./tools/micro/mfma_peak && \
       run gram_f64 200 python -u tools/gram_f64_time.py ;;
+    lvgaps)      # one config-3 forest on the level engine under a kernel trace: idle gaps
+      ( cd /tmp && ENGINES=level timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+          -d "$ROOT/$OUT/lvprof" -o lv -- python3 "$ROOT/tools/forest_level_probe.py" \
+          > "$ROOT/$OUT/lvgaps_run.log" 2>&1 ) || { echo "[lvgaps] failed"; tail -20 "$OUT/lvgaps_run.log"; exit 1; }
+      python3 tools/gap_summary.py $(find "$OUT/lvprof" -name "*kernel_trace.csv") lv_ \
+          > "$OUT/lvgaps.txt" 2>&1
+      echo "[lvgaps] ok: $(cat "$OUT/lvgaps.txt")"
+      ENGINES=level run lvplain 200 python -u tools/forest_level_probe.py ;;
     configs)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
