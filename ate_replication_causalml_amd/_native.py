@@ -71,7 +71,7 @@ _SIGS = {
     "ate_select_compact": "plppddpppp" + "p",
     "ate_gbdt_run": "ppp",
     "ate_lv_boot": "ppp",
-    "ate_lv_classify": "piiippp",
+    "ate_lv_classify": "pipiippp",
     "ate_lv_decide": "ppipipipippppp" + "iipip",
     "ate_lv_partition": "ppipippppipp",
     "ate_lv_scatter": "pppppippp",

@@ -6,9 +6,10 @@ so an 8e6-row bootstrap tree no longer lives on one CU (BASELINE config 3). Tree
 same bits as the one-workgroup-per-tree kernel and the host twin (forest_common.hpp spec):
 randomForest semantics, kinds 0 (classification) / 1 (regression), bootstrap sampling.
 
-Per level the host reads three small things to size the next launches: the node-class
-counts, the position ranges of the big nodes (their work items), and the next level's
-length. Everything else stays on the device.
+Per level the host reads, in one transfer, the node-class counts and the level's length
+(the previous level's split count, left on the device by the children step), plus, on
+levels with big nodes, their position ranges (their work items), to size the launches.
+Everything else stays on the device.
 """
 from __future__ import annotations
 
@@ -116,7 +117,8 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
     dec = torch.zeros((lcap, 4), **i32)
     nl = torch.zeros(lcap, **i32)
     brank = torch.zeros(T, **i32)
-    counts = torch.zeros(4, **i32)
+    counts = torch.zeros(5, **i32)
+    nsplit = None            # device [1]: split count of the previous level (None: root level)
     nf_max = min(fp.mtry, p)
     ngroups = -(-nf_max // LV_FG)
     hist = None
@@ -156,18 +158,22 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
             tp[name] += t1 - t0
         return t1
     depth = 0
-    while ncur > 0:
+    ncur_ub = ncur           # upper bound of the level length (exact at the root)
+    while ncur_ub > 0:
         t0 = tick(None, None)
         h.idx, h.idx2 = idx.data_ptr(), idx2.data_ptr()
         h.cur, h.dec, h.nl = cur.data_ptr(), dec.data_ptr(), nl.data_ptr()
         h.depth = depth
-        lists = torch.empty(4 * ncur, **i32)
+        lists = torch.empty(4 * ncur_ub, **i32)
         counts.zero_()
-        _native.call("ate_lv_classify", cur.data_ptr(), ncur, t2, t3, lists.data_ptr(),
-                     counts.data_ptr(), s)
-        nsmall, nmid, nmid2, nbig = (int(v) for v in counts.cpu())
+        _native.call("ate_lv_classify", cur.data_ptr(), ncur_ub,
+                     nsplit.data_ptr() if nsplit is not None else None, t2, t3,
+                     lists.data_ptr(), counts.data_ptr(), s)
+        nsmall, nmid, nmid2, nbig, ncur = (int(v) for v in counts.cpu())   # the level's sync
+        if ncur == 0:
+            break
         t0 = tick("classify", t0) if prof else None
-        L = [lists[k * ncur:k * ncur + c] for k, c in enumerate((nsmall, nmid, nmid2, nbig))]
+        L = [lists[k * ncur_ub:k * ncur_ub + c] for k, c in enumerate((nsmall, nmid, nmid2, nbig))]
         P = lambda t: t.data_ptr() if t is not None else None
         items, nitems, drawn, nfo = (None, None, None), 0, None, None
         if nbig:
@@ -205,15 +211,14 @@ def grow(Xb: torch.Tensor, fp: F.ForestParams, yt=None, r1t=None, big=None, chun
                          P(pitems[1]), P(pitems[2]), npit, ipre.data_ptr(), nlb32.data_ptr(), s)
         t0 = tick("partition", t0) if prof else None
         flags = dec[:ncur, 0]
-        excl, tot = exclusive_cumsum(flags.contiguous(), total=True)
-        total = int(tot.item())
+        excl, nsplit = exclusive_cumsum(flags.contiguous(), total=True)   # stays on device
         _native.call("ate_lv_children", ctypes.addressof(h), ncur, excl.data_ptr(),
                      brank.data_ptr(), next_id.data_ptr(), nxt.data_ptr(), s)
         if prof:
             tick("children", t0)
         cur, nxt = nxt, cur
         idx, idx2 = idx2, idx
-        ncur = 2 * total
+        ncur_ub = 2 * ncur   # each node has at most two children
         depth += 1
     if prof:
         import sys

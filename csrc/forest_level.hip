@@ -348,11 +348,19 @@ __global__ __launch_bounds__(256) void lv_boot_kernel(ForestParams fp, int32_t* 
 // classes: 0 small (<= 64 rows: wave decide, wave partition), 1 mid (<= t2 rows: workgroup
 // decide, wave partition), 2 mid-large (<= t3: workgroup decide, chunked partition), 3 big
 // (> t3: multi-workgroup decide, chunked partition). One atomic per wave and class.
-__global__ __launch_bounds__(256) void lv_classify_kernel(const LNode* __restrict__ cur, int ncur,
+// The level length is 2 * nsplit[0] (the previous level's split count, still on the device:
+// the host learns it with the class counts, counts[4], in ONE read per level) or, with no
+// nsplit, ncur_ub; the grid and the class lists' stride are sized for ncur_ub.
+__global__ __launch_bounds__(256) void lv_classify_kernel(const LNode* __restrict__ cur,
+                                                          int ncur_ub,
+                                                          const int32_t* __restrict__ nsplit,
                                                           int t2, int t3, int32_t* __restrict__ lists,
                                                           int32_t* __restrict__ counts) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
+  const int ncur = nsplit ? 2 * nsplit[0] : ncur_ub;
+  ATE_DASSERT(ncur <= ncur_ub);
+  if (j == 0) counts[4] = ncur;
   int c = -1;
   if (j < ncur) {
     const int m = cur[j].hi - cur[j].lo;
@@ -369,7 +377,7 @@ __global__ __launch_bounds__(256) void lv_classify_kernel(const LNode* __restric
     if (c == k) {
       const int pos = base + __popcll(mk & ((1ull << lane) - 1ull));
       ATE_DASSERT(pos < ncur);
-      lists[(int64_t)k * ncur + pos] = j;
+      lists[(int64_t)k * ncur_ub + pos] = j;
     }
   }
 }
@@ -987,12 +995,13 @@ ATE_API int ate_lv_boot(const void* fpp, void* w, void* stream) {
   return 0;
 }
 
-ATE_API int ate_lv_classify(const void* cur, int ncur, int t2, int t3, void* lists, void* counts,
-                            void* stream) {
-  if (ncur <= 0) return 0;
-  hipLaunchKernelGGL(lv_classify_kernel, dim3((ncur + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, (const LNode*)cur, ncur, t2, t3, (int32_t*)lists,
-                     (int32_t*)counts);
+// counts[0..3]: class sizes (zeroed by the caller), counts[4]: the level length
+ATE_API int ate_lv_classify(const void* cur, int ncur_ub, const void* nsplit, int t2, int t3,
+                            void* lists, void* counts, void* stream) {
+  if (ncur_ub <= 0) return 0;
+  hipLaunchKernelGGL(lv_classify_kernel, dim3((ncur_ub + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, (const LNode*)cur, ncur_ub, (const int32_t*)nsplit, t2,
+                     t3, (int32_t*)lists, (int32_t*)counts);
   ATE_CHECK_LAUNCH();
   return 0;
 }
