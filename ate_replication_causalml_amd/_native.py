@@ -52,8 +52,8 @@ _SIGS = {
     "ate_enet_path": "pipiippppidddipppppipp",
     "ate_enet_coef": "ppiiiipppppppp",
     "ate_enet_cvloss_gauss": "pippiipppiiipp",
-    "ate_cv_select": "pppiipipppp",
-    "ate_enet_pick": "ppiiiipp",
+    "ate_cv_select": "pppiipippppip",
+    "ate_enet_pick": "ppiiipppip",
     "ate_dml_resid_moments": "ipllpipipiiiiiippp",
     "ate_dml_resid_exact": "pllpipipiiiiiiippp",
     "ate_lognet_path": "iplpiipipipdddippippppppppp",

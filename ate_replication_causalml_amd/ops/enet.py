@@ -62,6 +62,16 @@ def poison_if_truncated(fold_npass: torch.Tensor, *ts):
     return [torch.where(bad, nan, t) for t in ts]
 
 
+def _zeroed(dev, *specs):
+    """Zero-filled tensors (shape, dtype) carved from ONE buffer: one fill launch instead of
+    one per tensor (they sit on the single call's critical path; 256-B aligned views)."""
+    sizes = [int(np.prod(sh)) * torch.empty((), dtype=dt).element_size() for sh, dt in specs]
+    offs = np.concatenate([[0], np.cumsum([(b + 255) // 256 * 256 for b in sizes])])
+    buf = torch.zeros(int(offs[-1]), dtype=torch.uint8, device=dev)
+    return [buf[int(o):int(o) + b].view(dt).view(sh)
+            for (sh, dt), o, b in zip(specs, offs[:-1], sizes)]
+
+
 def _rescale_vp(vp, p):
     vp = np.ones(p) if vp is None else np.maximum(np.asarray(vp, float), 0)
     return vp * p / vp.sum()
@@ -164,7 +174,13 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     yc = const(ycols, torch.int32, dev)
     c_f32 = int(panel_dtype != torch.float64)
     ldc = (p + 63) // 64 * 64   # zero-padded row stride (16-B aligned row segments)
-    C = torch.zeros((nt, p, ldc), dtype=torch.float32 if c_f32 else torch.float64, device=dev)
+    nf = len(full_probs)
+    probs_all = list(full_probs) + list(fold_probs)
+    nq = len(probs_all)
+    i32 = torch.int32
+    C, apath, rsq, nlam, npass, progress = _zeroed(
+        dev, ((nt, p, ldc), torch.float32 if c_f32 else torch.float64), ((nq, L, p), torch.float64),
+        ((nq, L), torch.float64), ((nq,), i32), ((nq,), i32), ((nq,), i32))
     g = torch.empty((nt, ny, p), **f64)
     xm = torch.empty((nt, p), **f64)
     xs = torch.empty((nt, p), **f64)
@@ -178,16 +194,8 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     vp_t = const(np.asarray(vp, dtype=np.float64), torch.float64, dev)
     # ONE launch: full problems [0, nf) + fold problems [nf, nq); fold problems consume
     # their source's lambda sequence as it is published (device-side progress flags)
-    nf = len(full_probs)
-    probs_all = list(full_probs) + list(fold_probs)
-    nq = len(probs_all)
     pr = _probs_tensor(probs_all, dev)
-    apath = torch.zeros((nq, L, p), **f64)
     lams = torch.full((nq, L), float("nan"), **f64)
-    rsq = torch.zeros((nq, L), **f64)
-    nlam = torch.zeros(nq, dtype=torch.int32, device=dev)
-    npass = torch.zeros(nq, dtype=torch.int32, device=dev)
-    progress = torch.zeros(nq, dtype=torch.int32, device=dev)
     _native.call("ate_enet_path", C.data_ptr(), c_f32, g.data_ptr(), p, ny, ju.data_ptr(),
                  ys.data_ptr(), vp_t.data_ptr(), pr.data_ptr(), nq, alpha, flmin, thresh,
                  maxit, apath.data_ptr(), lams.data_ptr(), rsq.data_ptr(), nlam.data_ptr(),
@@ -208,18 +216,17 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     cvsd = torch.empty((nf, L), **f64)
     sel = torch.empty((nf, 2), dtype=torch.int32, device=dev)
     K = fold_index.shape[1]
+    # a fold whose spin on its source's progress flag timed out (npass = -1; csrc/enet.hip)
+    # has a truncated path: cvm, and so lambda.min / lambda.1se, would silently change --
+    # the select and pick kernels NaN-poison cvm / cvsd / the picked coefficients then
+    fold_npass = npass[nf:]
     _native.call("ate_cv_select", cvraw.data_ptr(), fidx.data_ptr(), nfold_t.data_ptr(), K, nf,
-                 nlam.data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), s)
+                 nlam.data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(),
+                 fold_npass.data_ptr(), nq - nf, s)
     cmin = torch.empty((nf, p + 1), **f64)
     c1se = torch.empty((nf, p + 1), **f64)
-    _native.call("ate_enet_pick", coef.data_ptr(), sel.data_ptr(), 0, p, L, nf,
-                 cmin.data_ptr(), s)
-    _native.call("ate_enet_pick", coef.data_ptr(), sel.data_ptr(), 1, p, L, nf,
-                 c1se.data_ptr(), s)
-    # a fold whose spin on its source's progress flag timed out (npass = -1; csrc/enet.hip)
-    # has a truncated path: cvm, and so lambda.min / lambda.1se, would silently change
-    fold_npass = npass[nf:]
-    cvm, cvsd, cmin, c1se = poison_if_truncated(fold_npass, cvm, cvsd, cmin, c1se)
+    _native.call("ate_enet_pick", coef.data_ptr(), sel.data_ptr(), p, L, nf, cmin.data_ptr(),
+                 c1se.data_ptr(), fold_npass.data_ptr(), nq - nf, s)
     return EnetCvResult(lams[:nf], nlam[:nf], cvm, cvsd, sel, coef[:nf], cmin, c1se, full_keys,
                         npass[:nf], fold_npass)
 

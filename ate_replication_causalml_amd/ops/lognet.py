@@ -119,7 +119,8 @@ def cv_lognet(panel, xcols, ycol, penalty_factor=None, alpha=1.0, nlambda=100,
     cvsd = torch.empty((1, L), **f64)
     sel = torch.empty((1, 2), dtype=torch.int32, device=dev)
     _native.call("ate_cv_select", cvraw.data_ptr(), fidx.data_ptr(), nfold.data_ptr(), K, 1,
-                 nlam.data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), s)
+                 nlam.data_ptr(), L, cvm.data_ptr(), cvsd.data_ptr(), sel.data_ptr(), None, 0,
+                 s)
     coef = torch.cat([a0[0][:, None], beta[0]], 1)
     sl = sel[0].long()
     from .enet import poison_if_truncated

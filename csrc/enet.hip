@@ -1652,13 +1652,32 @@ ATE_API int ate_enet_cvloss_gauss(const void* G, int P, const void* hold, const 
 // attaining min cvm; idx_1se = first with cvm <= cvm[min] + cvsd[min].
 // One wave per full problem; lanes own lambdas m = lane + 64 c (c < 4, L <= 256) with the
 // per-lambda arithmetic of a serial scan, then wave reductions pick the first indices.
+// fnp[0 .. nfp): the launch's fold-problem pass counts; any < 0 (a fold path that timed out
+// waiting for its source's lambdas, enet_path_kernel) NaN-poisons cvm / cvsd (and, in
+// enet_pick_kernel, the picked coefficients): device-side, capturable, no extra launches.
+__device__ __forceinline__ bool any_truncated(const int* fnp, int nfp) {
+  bool bad = false;
+  if (fnp)
+    for (int i = threadIdx.x; i < nfp; i += blockDim.x) bad |= fnp[i] < 0;
+  return __syncthreads_or(bad) != 0;
+}
+
 __global__ __launch_bounds__(64) void cv_select_kernel(
     const double* __restrict__ cvraw, const int* __restrict__ fold_probs,
     const double* __restrict__ nfold, int K, int nfull, const int* __restrict__ nlam_full, int L,
-    double* __restrict__ cvm, double* __restrict__ cvsd, int* __restrict__ sel) {
+    double* __restrict__ cvm, double* __restrict__ cvsd, int* __restrict__ sel,
+    const int* __restrict__ fnp, int nfp) {
   const int f = blockIdx.x;
   const int lane = threadIdx.x;
   if (f >= nfull) return;
+  if (any_truncated(fnp, nfp)) {
+    for (int m = lane; m < L; m += 64) {
+      cvm[(int64_t)f * L + m] = NAN;
+      cvsd[(int64_t)f * L + m] = NAN;
+    }
+    if (lane == 0) { sel[2 * f] = 0; sel[2 * f + 1] = 0; }
+    return;
+  }
   const int nl = nlam_full[f];
   double wsum = 0.0;
   for (int k = 0; k < K; ++k) wsum += nfold[f * K + k];
@@ -1715,28 +1734,37 @@ __global__ __launch_bounds__(64) void cv_select_kernel(
 
 ATE_API int ate_cv_select(const void* cvraw, const void* fold_probs, const void* nfold, int K,
                           int nfull, const void* nlam_full, int L, void* cvm, void* cvsd, void* sel,
-                          void* stream) {
+                          const void* fold_npass, int nfp, void* stream) {
   if (L > 256) return -1;
   hipLaunchKernelGGL(cv_select_kernel, dim3(nfull), dim3(64), 0, (hipStream_t)stream,
                      (const double*)cvraw, (const int*)fold_probs, (const double*)nfold, K, nfull,
-                     (const int*)nlam_full, L, (double*)cvm, (double*)cvsd, (int*)sel);
+                     (const int*)nlam_full, L, (double*)cvm, (double*)cvsd, (int*)sel,
+                     (const int*)fold_npass, nfp);
   ATE_CHECK_LAUNCH();
   return 0;
 }
 
-// gather the selected coefficient vector for each full problem: out[f][p+1]
+// gather the selected coefficient vectors of each full problem: out_min[f][p+1] (lambda.min,
+// blockIdx.y 0) and out_1se[f][p+1] (lambda.1se, blockIdx.y 1); NaN when a fold path of the
+// launch was truncated (any_truncated)
 __global__ void enet_pick_kernel(const double* __restrict__ coef, const int* __restrict__ sel,
-                                 int which, int p, int L, int nfull, double* __restrict__ out) {
-  const int f = blockIdx.x;
+                                 int p, int L, int nfull, double* __restrict__ out_min,
+                                 double* __restrict__ out_1se, const int* __restrict__ fnp,
+                                 int nfp) {
+  const int f = blockIdx.x, which = blockIdx.y;
+  double* out = which ? out_1se : out_min;
+  const bool bad = any_truncated(fnp, nfp);
   const int m = sel[2 * f + which];
   for (int j = threadIdx.x; j <= p; j += blockDim.x)
-    out[(int64_t)f * (p + 1) + j] = coef[((int64_t)f * L + m) * (p + 1) + j];
+    out[(int64_t)f * (p + 1) + j] = bad ? NAN : coef[((int64_t)f * L + m) * (p + 1) + j];
 }
 
-ATE_API int ate_enet_pick(const void* coef, const void* sel, int which, int p, int L, int nfull,
-                          void* out, void* stream) {
-  hipLaunchKernelGGL(enet_pick_kernel, dim3(nfull), dim3(128), 0, (hipStream_t)stream,
-                     (const double*)coef, (const int*)sel, which, p, L, nfull, (double*)out);
+ATE_API int ate_enet_pick(const void* coef, const void* sel, int p, int L, int nfull,
+                          void* out_min, void* out_1se, const void* fold_npass, int nfp,
+                          void* stream) {
+  hipLaunchKernelGGL(enet_pick_kernel, dim3(nfull, 2), dim3(128), 0, (hipStream_t)stream,
+                     (const double*)coef, (const int*)sel, p, L, nfull, (double*)out_min,
+                     (double*)out_1se, (const int*)fold_npass, nfp);
   ATE_CHECK_LAUNCH();
   return 0;
 }

@@ -21,6 +21,7 @@
 #   c04_ab         a small config-5 shard: feature-sliced C04 vs ATE_GBDT_C04=allreduce, x2
 #   micro          tools/micro/mfma_peak (matrix / vector peaks) and the fp64 Gram alone
 #   lvgaps         idle gaps of the host-driven forest level engine (kernel trace)
+#   single         kernel trace of bench.py: the last single-fit replay's critical path
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
 #   gramdump       the bench panel's fold Gram stack -> OUT/gram_dump (tools/dump_bench_gram.py)
@@ -107,6 +108,13 @@ for step in "$@"; do
           > "$OUT/lvgaps.txt" 2>&1
       echo "[lvgaps] ok: $(cat "$OUT/lvgaps.txt")"
       ENGINES=level run lvplain 200 python -u tools/forest_level_probe.py ;;
+    single)      # kernel trace of bench.py: the last single-fit replay's critical path
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+          -d "$ROOT/$OUT/single" -o single -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 \
+          --parity 0 > "$ROOT/$OUT/single_run.log" 2>&1 ) || { echo "[single] failed"; tail -20 "$OUT/single_run.log"; exit 1; }
+      python3 tools/single_fit_timeline.py $(find "$OUT/single" -name "*kernel_trace.csv") \
+          > "$OUT/single_timeline.txt" 2>&1
+      echo "[single] ok: $(tail -14 "$OUT/single_timeline.txt")" ;;
     configs)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
