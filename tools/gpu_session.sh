@@ -22,6 +22,7 @@
 #   micro          tools/micro/mfma_peak (matrix / vector peaks) and the fp64 Gram alone
 #   lvgaps         idle gaps of the host-driven forest level engine (kernel trace)
 #   single         kernel trace of bench.py: the last single-fit replay's critical path
+#   ktrace_ab:A,B[:RX] kernel trace of bench.py per library (ATE_HIP_LIB), mean time of RX kernels
 #   configs        all BASELINE configs on one GPU (tools/bench_configs.py)
 #   replicate      the 14-row tutorial driver, warm timing (tools/replicate_timing.py)
 #   gramdump       the bench panel's fold Gram stack -> OUT/gram_dump (tools/dump_bench_gram.py)
@@ -115,6 +116,22 @@ for step in "$@"; do
       python3 tools/single_fit_timeline.py $(find "$OUT/single" -name "*kernel_trace.csv") \
           > "$OUT/single_timeline.txt" 2>&1
       echo "[single] ok: $(tail -14 "$OUT/single_timeline.txt")" ;;
+    ktrace_ab:*) # ktrace_ab:A,B,..[:REGEX] kernel-trace bench.py per library, mean time of REGEX kernels
+      spec=${step#ktrace_ab:}; IFS=: read -r libs_csv rx <<< "$spec"; rx=${rx:-enet_cvloss}
+      IFS=, read -ra libs <<< "$libs_csv"
+      for nm in "${libs[@]}"; do
+        lib=ate_replication_causalml_amd/_lib/libatehip_$nm.so
+        [ "$nm" = new ] && lib=ate_replication_causalml_amd/_lib/libatehip.so
+        ( cd /tmp && ATE_HIP_LIB=$ROOT/$lib timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+            -d "$ROOT/$OUT/kt_$nm" -o kt -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --parity 0 \
+            > "$ROOT/$OUT/kt_$nm.log" 2>&1 ) || { echo "[kt_$nm] failed"; tail -20 "$OUT/kt_$nm.log"; exit 1; }
+        python3 -c "
+import csv, re, sys, statistics as st
+r = [x for x in csv.DictReader(open(sys.argv[1])) if re.search(sys.argv[2], x['Kernel_Name'])]
+d = [(int(x['End_Timestamp']) - int(x['Start_Timestamp'])) / 1e3 for x in r]
+print(sys.argv[3], len(d), 'kernels, mean %.1f us, median %.1f us' % (st.mean(d), st.median(d)))
+" $(find "$OUT/kt_$nm" -name "*kernel_trace.csv") "$rx" "$nm" | tee -a "$OUT/ktrace_ab.txt"
+      done ;;
     configs)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
