@@ -547,7 +547,15 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         inbag = torch.empty(ntree * n, dtype=torch.uint8, device=dev)
         est = torch.zeros(ntree * cap * 5, dtype=torch.int64, device=dev) if need_est else None
         per = _native.hip().ate_forest_exact_scratch_bytes(n, 1)
-        chunk = max(1, min(ntree, (1 << 30) // per))       # scratch <= ~1 GiB
+        # trees per launch: two resident per CU, so a launch wants >= 512 of them and as
+        # few tails as possible. A 1-GiB scratch cap held 264 trees of 5e4 rows (half the CUs
+        # idle, a tail per launch; config 4 2.53 s); when 1 GiB holds < 1024 trees the cap is
+        # 2048 trees' worth up to 8 GiB (config 4 1.43 s, same trees; profiles/r04_cfg4).
+        # ATE_EXACT_SCRATCH_MB overrides.
+        env_mb = int(os.environ.get("ATE_EXACT_SCRATCH_MB", "0"))
+        cap_b = env_mb << 20 if env_mb else \
+            (1 << 30 if (1 << 30) // per >= 1024 else min(8 << 30, 2048 * per))
+        chunk = max(1, min(ntree, cap_b // per))
         scratch = torch.empty(per * chunk, dtype=torch.uint8, device=dev)
         Xb = Xb.contiguous()
         p_ = lambda a: 0 if a is None else a.data_ptr()

@@ -28,7 +28,8 @@ def main():
     def sync():
         torch.cuda.synchronize()
 
-    for splits in ("exact", "binned", "exact", "binned"):
+    modes = os.environ.get("MODES", "exact,binned,exact,binned").split(",")
+    for splits in modes:
         t = {}
         sync()
         t0 = time.perf_counter()
