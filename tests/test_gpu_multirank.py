@@ -36,28 +36,31 @@ def test_two_ranks_on_one_gpu_match_one_process(gpu):
     assert two["se"] == pytest.approx(ref["se"], rel=1e-9)
 
 
-@pytest.mark.parametrize("cols,c04", [(40, "sliced"), (37, "sliced"), (40, "allreduce")])
-def test_cfg5_gbdt_two_ranks_on_one_gpu_bitwise(gpu, cols, c04):
+@pytest.mark.parametrize("cols,c04,ranks", [(40, "sliced", 2), (37, "sliced", 2),
+                                             (40, "allreduce", 2), (40, "sliced", 3)])
+def test_cfg5_gbdt_two_ranks_on_one_gpu_bitwise(gpu, cols, c04, ranks):
     """Config 5's row-sharded DML-GBDT (tools/cfg5.py) with two ranks sharing the GPU
     (gloo collectives): device edge sample, per-level int64 histograms reduce-scattered by
     feature slice with the split candidates all-gathered (37 columns: rank 1's slice is one
     feature short) or all-reduced whole (ATE_GBDT_C04=allreduce), exact moments -> the
-    SAME BITS as one process holding all rows."""
+    SAME BITS as one process holding all rows. Three ranks: slices of 14, 14 and 12
+    features."""
     cfg5 = os.path.join(ROOT, "tools", "cfg5.py")
     args = ["--rows", "200000", "--cols", str(cols), "--trees", "6", "--depth", "4"]
     env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     if c04 == "allreduce":
         env["ATE_GBDT_C04"] = "allreduce"
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29657",
-                        cfg5, *args], capture_output=True, text=True, env=env, timeout=240)
+                        f"--nproc-per-node={ranks}", "--master-addr=127.0.0.1",
+                        "--master-port=29657", cfg5, *args], capture_output=True, text=True,
+                       env=env, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     two = _json(r.stdout)
     one = subprocess.run([sys.executable, cfg5, *args], capture_output=True, text=True,
                          timeout=240)
     assert one.returncode == 0, one.stderr[-3000:]
     ref = _json(one.stdout)
-    assert two["world"] == 2 and ref["world"] == 1
+    assert two["world"] == ranks and ref["world"] == 1
     assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)
 
 
