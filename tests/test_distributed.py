@@ -110,3 +110,25 @@ def test_tree_parallel_forests_equal_single(world):
         np.testing.assert_array_equal(cf.w_hat, cf1.w_hat)
         np.testing.assert_array_equal(cf.tau_oob, cf1.tau_oob)
         np.testing.assert_array_equal(cf.var_oob, cf1.var_oob)
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_reduce_scatter_and_all_gather_into(world):
+    """Communicator primitives of the feature-sliced C04: reduce_scatter_ returns this rank's
+    chunk of the rank-ordered sum, all_gather_into_ the rank-ordered concatenation."""
+    from ate_replication_causalml_amd.parallel.comm import LocalComm
+
+    def fn(comm):
+        r = comm.rank
+        t = torch.arange(4 * comm.world_size, dtype=torch.int64) * (r + 1)
+        out = torch.empty(4, dtype=torch.int64)
+        comm.reduce_scatter_(out, t)
+        g = torch.empty(3 * comm.world_size, dtype=torch.int64)
+        comm.all_gather_into_(g, torch.full((3,), r, dtype=torch.int64))
+        return out, g
+
+    res = [fn(LocalComm())] if world == 1 else run_simulated(world, fn)
+    scale = sum(r + 1 for r in range(world))
+    for r, (out, g) in enumerate(res):
+        assert out.tolist() == [scale * v for v in range(4 * r, 4 * r + 4)]
+        assert g.tolist() == [q for q in range(world) for _ in range(3)]
