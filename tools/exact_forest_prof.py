@@ -2,6 +2,7 @@
 
   python tools/exact_forest_prof.py --build   # here: cross-compile the profiling library
   python tools/exact_forest_prof.py           # on the GPU box: one tree of df_mod, ticks
+  python tools/exact_forest_prof.py --causal  # ... tree 0 of a config-4 grf causal forest
 """
 import ctypes
 import os
@@ -40,15 +41,29 @@ def run():
     from ate_replication_causalml_amd.models import forest as F
     lib = _native.hip()
     lib.ate_exact_prof_read.argtypes = [ctypes.c_void_p]
-    m, _ = apply_selection_bias(make_tutorial_data(50000, 1991), 0.85, 0.85, "reference")
     dev = torch.device("cuda", 0)
-    eb = F.exact_bins(m.X)
-    Xb = torch.from_numpy(eb.bin(m.X)).to(dev)
-    w = torch.as_tensor(m.W, device=dev)
-    F.fit_forest_exact(Xb, eb, F.KIND_CLASS, y=w, ntree=1, seed=3)
+    if "--causal" in sys.argv:
+        # one grf causal tree of config 4 (n=5e4, p=21: little bags, honesty, Poisson mtry 21)
+        d = make_tutorial_data(50000, seed=12)
+        X = np.asarray(d.X, dtype=np.float64)
+        eb = F.exact_bins(X)
+        Xb = torch.from_numpy(eb.bin(X, grf=True)).to(dev)
+        Wc = np.asarray(d.W, dtype=np.float64)
+        Yc = np.asarray(d.Y, dtype=np.float64)
+        kw = dict(r1=Wc - Wc.mean(), r2=Yc - Yc.mean(), ntree=2, mtry=F.grf_mtry(X.shape[1]),
+                  min_node=5, sampling=1, honesty=True, group=2, mtry_poisson=True, alpha=0.05,
+                  sample_fraction=0.5, seed=12345)
+        fit = lambda: F.fit_forest_exact(Xb, eb, F.KIND_CAUSAL, **kw)
+    else:
+        m, _ = apply_selection_bias(make_tutorial_data(50000, 1991), 0.85, 0.85, "reference")
+        eb = F.exact_bins(m.X)
+        Xb = torch.from_numpy(eb.bin(m.X)).to(dev)
+        w = torch.as_tensor(m.W, device=dev)
+        fit = lambda: F.fit_forest_exact(Xb, eb, F.KIND_CLASS, y=w, ntree=1, seed=3)
+    fit()
     torch.cuda.synchronize()
     lib.ate_exact_prof_reset()
-    F.fit_forest_exact(Xb, eb, F.KIND_CLASS, y=w, ntree=1, seed=3)
+    fit()
     torch.cuda.synchronize()
     buf = np.zeros(24, dtype=np.uint64)
     lib.ate_exact_prof_read(buf.ctypes.data_as(ctypes.c_void_p))
