@@ -549,12 +549,12 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         per = _native.hip().ate_forest_exact_scratch_bytes(n, 1)
         # trees per launch: two resident per CU, so a launch wants >= 512 of them and as
         # few tails as possible. A 1-GiB scratch cap held 264 trees of 5e4 rows (half the CUs
-        # idle, a tail per launch; config 4 2.53 s); when 1 GiB holds < 1024 trees the cap is
-        # 2048 trees' worth up to 8 GiB (config 4 1.43 s, same trees; profiles/r04_cfg4).
-        # ATE_EXACT_SCRATCH_MB overrides.
+        # idle, a tail per launch; config 4 2.53 s); when 1 GiB cannot hold the whole forest
+        # the cap is 2048 trees' worth up to 8 GiB (config 4 1.43 s, same trees;
+        # profiles/r04_cfg4). ATE_EXACT_SCRATCH_MB overrides.
         env_mb = int(os.environ.get("ATE_EXACT_SCRATCH_MB", "0"))
         cap_b = env_mb << 20 if env_mb else \
-            (1 << 30 if (1 << 30) // per >= 1024 else min(8 << 30, 2048 * per))
+            (1 << 30 if (1 << 30) // per >= ntree else min(8 << 30, 2048 * per))
         chunk = max(1, min(ntree, cap_b // per))
         scratch = torch.empty(per * chunk, dtype=torch.uint8, device=dev)
         Xb = Xb.contiguous()
