@@ -103,3 +103,23 @@ def test_segmented_step_matches_eager_on_simulated_ranks():
     for sharded, unsharded in got:
         torch.testing.assert_close(sharded, unsharded, rtol=0, atol=0)
         torch.testing.assert_close(sharded, want, rtol=1e-9, atol=1e-12)
+
+
+def test_zeroed_views_share_one_buffer():
+    """ops/enet._zeroed: the path kernel's zero-initialised outputs carved from one buffer
+    (one fill launch), typed, shaped, zero, 256-B aligned and non-overlapping."""
+    from ate_replication_causalml_amd.ops.enet import _zeroed
+    specs = [((3, 5, 64), torch.float32), ((12, 100, 7), torch.float64), ((12, 100), torch.float64),
+             ((12,), torch.int32), ((12,), torch.int32), ((12,), torch.int32)]
+    ts = _zeroed(torch.device("cpu"), *specs)
+    base = ts[0].untyped_storage().data_ptr()
+    spans = []
+    for t, (sh, dt) in zip(ts, specs):
+        assert tuple(t.shape) == sh and t.dtype == dt and t.is_contiguous()
+        assert bool((t == 0).all())
+        assert t.untyped_storage().data_ptr() == base          # one allocation
+        off = t.data_ptr() - base
+        assert off % 256 == 0
+        spans.append((off, off + t.numel() * t.element_size()))
+    spans.sort()
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
