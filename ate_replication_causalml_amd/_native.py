@@ -58,7 +58,11 @@ _SIGS = {
     "ate_dml_resid_exact": "pllpipipiiiiiiippp",
     "ate_lognet_path": "iplpiipipipdddippippppppppp",
     "ate_lognet_cvloss": "iplpiippipppipp",
-    "ate_dgp_fill": "iplllllu" + "iip",
+    "ate_dgp_fill": "iplllllp" + "uiipp",
+    "ate_sel_block_rows": "",
+    "ate_sel_gen_count": "upilllpp",
+    "ate_sel_gen_flags": "upillpp",
+    "ate_sel_gen_mark": "upiplllpiplp",
     "ate_forest_fit": "pppppi" + "pppppppp" + "ip",
     "ate_forest_predict": "ppiiipppppippip",
     "ate_forest_pack": "pippppppp",

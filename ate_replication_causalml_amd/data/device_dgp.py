@@ -4,6 +4,21 @@ row-sharded across ranks) for the scaled configs (N = 1e6 .. 1e8, p = 21 .. 2000
 Global row g belongs to fold ``g * K // N``; rank r of R holds the r-th contiguous
 slice of every fold. Rows are a pure function of (seed, g) (``csrc/dgp.hip``), so
 the union of all shards is the same data set for every world size.
+
+Two data-generating processes (``dgp=``):
+
+* ``"tutorial"`` -- the tutorial's ``df_mod`` at scale: the calibrated
+  latent-voter model (dgp.TUTORIAL) drawn as an RCT, then the selection-bias transform of
+  ``ate_replication.Rmd:97-121`` over the generated rows (data/panel_selection.py): the
+  first round(0.85 k) treated likely voters and control unlikely voters in generated-row
+  order are dropped, and exactly N rows are kept (``n_generated`` records how many were
+  drawn). W is confounded with the vote history, yob and city; "row g" above is then the
+  g-th KEPT row.
+* ``"tutorial-rct"`` -- the same calibrated model WITHOUT the transform: the tutorial's
+  unbiased ``df`` at scale (its naive difference in means is the "oracle" row).
+* ``"rct"`` -- the survey's scratch panel constants (dgp.PANEL) without selection: W is
+  independent of X (a pure RCT), the path solver's worst case (every coordinate of the W
+  nuisance is noise).
 """
 from __future__ import annotations
 
@@ -15,6 +30,7 @@ from ..ops.panel import DevicePanel, empty_panel, dtype_code
 from . import dgp as host_dgp
 
 N_TUTORIAL_COLS = 21
+DGPS = ("tutorial", "tutorial-rct", "rct")
 
 
 def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1, align: int = 0):
@@ -38,12 +54,24 @@ def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1, align: 
 
 def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991,
                     dtype: str = "bf16", device="cpu", rank: int = 0, world: int = 1,
-                    blocked: bool = False, align: int = 0) -> DevicePanel:
+                    blocked: bool = False, align: int = 0, dgp: str = "rct", comm=None,
+                    selection=None, compat: str = "reference") -> DevicePanel:
     """``align`` > 0: block-aligned rank slices (fold_slices); the panel then records
-    ``exact_block`` = align, the row block of the exact (world-size-invariant) Gram."""
+    ``exact_block`` = align, the row block of the exact (world-size-invariant) Gram.
+
+    ``dgp="tutorial"``: ``n_total`` rows are KEPT by the selection transform; ``comm``
+    shards its candidate counting over the ranks (one all-reduce of per-block counts);
+    ``selection``: a PanelSelection already planned for these (n_total, seed) (e.g. by the
+    bf16 panel, reused for its float64 parity twin). The panel records ``dgp``,
+    ``n_generated`` and ``selection``."""
     if p < N_TUTORIAL_COLS:
         raise ValueError("p must be >= 21 (tutorial columns)")
+    if dgp not in DGPS:
+        raise ValueError(f"dgp must be one of {DGPS}, got {dgp!r}")
+    if comm is not None:
+        rank, world = comm.rank, comm.world_size
     p_extra = p - N_TUTORIAL_COLS
+    params = host_dgp.PANEL if dgp == "rct" else host_dgp.TUTORIAL
     slices = fold_slices(n_total, folds, rank, world, align)
     hi_lo = dtype == "bf16"
     names = ["one"] + [f"x{j}" for j in range(p)] + ["W", "Y"]
@@ -54,21 +82,36 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
     pan = empty_panel([c for _, c in slices], P, dtype=dtype, device=device, blocked=blocked)
     pan.cols = {nm: i for i, nm in enumerate(names)}
     pan.xcols = [pan.cols[f"x{j}"] for j in range(p)]
-    # global row ids of this shard (panel order)
+    # global (kept) row ids of this shard (panel order)
     rid = torch.full((pan.ld,), -1, dtype=torch.int64, device=device)
     for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
         rid[r0:r0 + cnt] = torch.arange(g0, g0 + cnt, device=device)
     pan.row_index = rid
     pan.identity = len(slices) == 1 and slices[0][0] == 0
+    gids = None
+    sel = None
+    if dgp == "tutorial":
+        from .panel_selection import kept_gids, plan_selection
+        sel = selection if selection is not None else plan_selection(
+            n_total, seed, params, comm=comm, device=pan.data.device, compat=compat)
+        if sel.n_keep != n_total or sel.seed != seed:
+            raise ValueError("selection plan does not match (n_total, seed)")
+        gids = kept_gids(sel, slices, device=pan.data.device)
+    offs = np.concatenate([[0], np.cumsum([c for _, c in slices])])
     if pan.data.is_cuda:
         s = torch.cuda.current_stream().cuda_stream
-        for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
+        pblk = np.ascontiguousarray(params.device_block())
+        for k, ((g0, cnt), (r0, _)) in enumerate(zip(slices, pan.seg_bounds)):
+            gp = 0 if gids is None or cnt == 0 else gids[int(offs[k]):].data_ptr()
             _native.call("ate_dgp_fill", dtype_code(pan.data), pan.data.data_ptr(),
-                         *pan.strides(), int(r0), cnt, g0, seed, p_extra, int(hi_lo), s)
+                         *pan.strides(), int(r0), cnt, g0, gp, seed, p_extra, int(hi_lo),
+                         pblk.ctypes.data, s)
     else:
         cm = torch.zeros((pan.P, pan.ld), dtype=pan.data.dtype) if blocked else pan.data
-        for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
-            cts, binc, extra, W, Y, _ = host_dgp.raw_columns(cnt, seed, p_extra, row_offset=g0)
+        for k, ((g0, cnt), (r0, _)) in enumerate(zip(slices, pan.seg_bounds)):
+            idx = None if gids is None else gids[int(offs[k]):int(offs[k]) + cnt].numpy()
+            cts, binc, extra, W, Y, _ = host_dgp.raw_columns(cnt, seed, p_extra, row_offset=g0,
+                                                              params=params, idx=idx)
             cols = [np.ones(cnt), *cts.T, *binc.T, *extra.T, W, Y]
             if hi_lo:
                 cols += [W, np.zeros(cnt), Y, np.zeros(cnt)]
@@ -78,4 +121,8 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
             pan.data.copy_(cm.reshape(pan.P, -1, 64).permute(1, 0, 2))
     pan.n = sum(c for _, c in slices)
     pan.exact_block = int(align)
+    pan.dgp = dgp
+    pan.selection = sel
+    pan.n_generated = sel.n_gen if sel is not None else n_total
+    pan.gen_ids = gids
     return pan

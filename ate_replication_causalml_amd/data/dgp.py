@@ -57,6 +57,13 @@ class DgpParams:
     yob_latent: float = 0.3
     factor_load: float = 0.6
 
+    def device_block(self) -> np.ndarray:
+        """The float32[18] parameter block of csrc/dgp.hip (load_params)."""
+        fl = self.factor_load
+        return np.array([self.intercept, *self.b_hist, self.b_latent, self.tau_logit,
+                         self.p_treat, *self.hist_thresh, self.hist_latent, self.yob_latent,
+                         fl, np.sqrt(1 - fl ** 2)], dtype=np.float32)
+
 
 # The scaled-config panels (data/device_dgp.synthetic_panel, the bench) and the HIP
 # generator csrc/dgp.hip: the survey's scratch constants (one history threshold).
@@ -113,11 +120,14 @@ class TutorialData:
 
 
 def raw_columns(n: int, seed: int, p_extra: int = 0, row_offset: int = 0,
-                params: DgpParams = PANEL):
-    """Unscaled draws for rows [row_offset, row_offset+n) (``params``: PANEL = the model of
-    the HIP generator csrc/dgp.hip, row for row)."""
+                params: DgpParams = PANEL, idx=None):
+    """Unscaled draws for rows [row_offset, row_offset+n), or for the generated-row ids
+    ``idx`` (the model of the HIP generator csrc/dgp.hip, row for row; float64 here, float32
+    on the device)."""
     P = params
-    idx = np.arange(row_offset, row_offset + n, dtype=np.uint64)
+    idx = np.arange(row_offset, row_offset + n, dtype=np.uint64) if idx is None else \
+        np.asarray(idx, dtype=np.uint64)
+    n = len(idx)
     f = _normal(seed, S_FACTOR, idx)
     fl = P.factor_load
     cts = np.empty((n, 15))
@@ -142,6 +152,25 @@ def raw_columns(n: int, seed: int, p_extra: int = 0, row_offset: int = 0,
         else:
             extra[:, j] = fl * f + np.sqrt(1 - fl ** 2) * z
     return cts, np.column_stack([sex, hist]), extra, W, Y, tau_i
+
+
+def selection_flags(seed: int, idx, params: DgpParams, compat: str = "reference") -> np.ndarray:
+    """Host twin of csrc/dgp.hip sel_flag for generated rows ``idx``: 1 treated candidate,
+    2 control candidate, 0 neither (ate_replication.Rmd:103-110 on the population-
+    standardised yob / city, i.e. +-2 on the raw N(0,1) draws; quirk Q17 under
+    compat="reference")."""
+    P = params
+    idx = np.asarray(idx, dtype=np.uint64)
+    yob = _normal(seed, S_CTS + 0, idx)
+    city = _normal(seed, S_CTS + 1, idx)
+    latent = _normal(seed, S_LATENT, idx) + P.yob_latent * yob
+    h = [(_normal(seed, S_HIST + k, idx) + P.hist_latent * latent > P.hist_thresh[k])
+         for k in range(5)]
+    W = _uniform(seed, S_W, idx) < P.p_treat
+    last = h[3] if compat == "reference" else h[4]
+    dt = h[0] | h[1] | h[2] | h[3] | last | (city > 2) | (yob > 2)
+    dc = ~h[0] | ~h[1] | ~h[2] | ~h[3] | ~h[4] | (city < -2) | (yob < -2)
+    return np.where(W, np.where(dt, 1, 0), np.where(dc, 2, 0)).astype(np.uint8)
 
 
 def r_scale(a: np.ndarray) -> np.ndarray:

@@ -64,8 +64,17 @@ def _pair_dist(dist):
     dup = getattr(dist.comm, "dup", None)
     if dup is None:
         return None
+    # created once per communicator and cached on it: dup() is a new process group (a
+    # collective every rank runs in the same order), never re-made per cross-fit call
+    second = getattr(dist.comm, "_pair_dup", None)
+    if second is None:
+        second = dup()
+        try:
+            dist.comm._pair_dup = second
+        except AttributeError:      # a communicator type without instance attributes
+            pass
     from ..parallel.dist import DistContext
-    return DistContext(dup(), dist.row_offset, dist.n_total)
+    return DistContext(second, dist.row_offset, dist.n_total)
 
 
 def _fit_pair(fit, jobs, dev, dists):

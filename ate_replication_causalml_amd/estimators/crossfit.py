@@ -32,6 +32,9 @@ from ..parallel import rng
 from ..result import AteResult
 from .common import as_np, resolve_device
 
+# format tag of the config-4 forest checkpoint key (bump when the forest outputs change)
+CF_CKPT_VERSION = 2
+
 
 def _backend(dev):
     return "gpu" if dev.type == "cuda" else "cpu"
@@ -413,7 +416,13 @@ def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_se
     key, tag = "", ""
     if checkpoint is not None:
         from ..utils.checkpoint import fingerprint
-        key = fingerprint(Yn, Wn, Xn, np.array([num_trees, seed, nuisance_trees or 0]))
+        # everything that changes the forest outputs: the resolved split engine, the
+        # orthogonalisation forests' little-bag size, the causal split rule and a format tag
+        # (an older checkpoint of binned / group-2 / unbalanced-split forests must not load)
+        sp = F.resolve_splits("auto", len(Yn))
+        key = fingerprint(Yn, Wn, Xn, np.array([num_trees, seed, nuisance_trees or 0]),
+                          np.frombuffer(f"v{CF_CKPT_VERSION}|{sp}|ng1|{F.CAUSAL_SPLIT_RULE}"
+                                        .encode(), dtype=np.uint8))
         tag = "" if comm is None or comm.world_size == 1 else f".r{comm.rank}of{comm.world_size}"
     stage = f"cf_fit{tag}"
     ranges = [(b0, min(boot_chunk, B - b0)) for b0 in range(0, B, boot_chunk)]

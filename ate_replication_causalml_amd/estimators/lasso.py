@@ -331,10 +331,16 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
     p1 = len(pan.xcols) + 1
 
     n_rows = int(np.asarray(seg_counts if seg_counts is not None else pan.seg_nreal).sum())
+    if exact:
+        # limb range guard, once per layout and agreed over ranks (a rank raising alone
+        # would leave its peers blocked in the limb all-reduce): here, eagerly on every
+        # rank, not inside the (captured) Gram phase
+        from ..ops.gram import check_exact_range
+        check_exact_range(pan, n_rows, comm=comm if dist else None)
 
     def phase_gram(_):
         if exact:
-            return {"GX": gram(pan, stage="tiles", exact=True, n_total=n_rows)}
+            return {"GX": gram(pan, stage="tiles", exact=True, n_total=n_rows, checked=True)}
         return {"G": gram(pan, stage="tiles") if G is None else G}
 
     def phase_gram_reduce(st):

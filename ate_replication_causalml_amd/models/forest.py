@@ -51,6 +51,8 @@ class ForestParams(ctypes.Structure):
 
 KIND_CLASS, KIND_REG, KIND_CAUSAL = 0, 1, 2
 FIX = float(2 ** 32)
+# causal-split admissibility rule the engines implement (part of checkpoint keys)
+CAUSAL_SPLIT_RULE = "arm1"
 
 
 def to_fix(v) -> np.ndarray:
@@ -272,11 +274,12 @@ class Forest:
             dev = self.device
             s = torch.cuda.current_stream().cuda_stream
             if self.exact is not None:
-                tchunk = max(1, min(self.params.ntree, (1 << 28) // max(n2, 1)))
+                # trees per chunk rounded to the little-bag group BEFORE sizing the leaf
+                # buffer (a 1-tree chunk of a group-2 forest becomes 2 trees)
+                g = max(1, self.params.group) if self.params.kind == KIND_CAUSAL else 1
+                tchunk = max(g, min(self.params.ntree, (1 << 28) // max(n2, 1)) // g * g)
                 leaves = torch.empty(tchunk * n2, dtype=torch.int32, device=dev)
                 out = torch.empty(n2 * width, dtype=torch.float64, device=dev)
-                g = max(1, self.params.group) if self.params.kind == KIND_CAUSAL else 1
-                tchunk = max(g, tchunk // g * g)
                 _native.call("ate_forest_predict16", ctypes.addressof(self.params),
                              Xb.data_ptr(), n2, int(oob), self.cap, self.feat.data_ptr(),
                              self.thr.data_ptr(), self.left.data_ptr(), self.val.data_ptr(),
@@ -552,9 +555,12 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         # idle, a tail per launch; config 4 2.53 s); when 1 GiB cannot hold the whole forest
         # the cap is 2048 trees' worth up to 8 GiB (config 4 1.43 s, same trees;
         # profiles/r04_cfg4). ATE_EXACT_SCRATCH_MB overrides.
+        # Inside a stream capture (estimator graphs) the scratch would live as long as the
+        # graph's private pool: capped at 1 GiB there, so cached graphs do not each pin GBs.
         env_mb = int(os.environ.get("ATE_EXACT_SCRATCH_MB", "0"))
+        capturing = torch.cuda.is_current_stream_capturing()
         cap_b = env_mb << 20 if env_mb else \
-            (1 << 30 if (1 << 30) // per >= ntree else min(8 << 30, 2048 * per))
+            (1 << 30 if capturing or (1 << 30) // per >= ntree else min(8 << 30, 2048 * per))
         chunk = max(1, min(ntree, cap_b // per))
         scratch = torch.empty(per * chunk, dtype=torch.uint8, device=dev)
         Xb = Xb.contiguous()

@@ -248,20 +248,30 @@ _STAGES = {"all": 3, "tiles": 1, "reduce": 2}
 EXACT_LIMB_BOUND = 2.0 ** 38   # |Gram entry| bound of the fixed 2^24-scale int64 limbs
 
 
-def check_exact_range(panel: DevicePanel, n_total: int | None = None, w=None):
+def check_exact_range(panel: DevicePanel, n_total: int | None = None, w=None, comm=None):
     """Raise if the exact mode's fixed-scale limbs could wrap: the hi limb of an entry is
     floor(v 2^24) summed over chunks in int64, exact only while every |G_jk| < 2^38, and
     |G_jk| <= max_i |x_ij| max_i |x_ik| * n_total (weighted: times max |w|). ``n_total``:
     rows over ALL ranks (weak scaling grows it). One reduction over the panel; skipped
-    inside a graph capture (the guard runs on the eager first call of a layout)."""
+    inside a graph capture (the guard runs on the eager first call of a layout).
+
+    ``comm`` (world > 1): the max |x| (and max |w|) are all-reduced first, so every rank
+    takes the same decision -- a rank that raised alone would leave its peers blocked in
+    the limb all-reduce. Call it where every rank runs it eagerly (estimators/lasso.py
+    dml_phases does, once per layout)."""
     X = panel.data
     if X.is_cuda and torch.cuda.is_current_stream_capturing():
         return
     dims = (0, 2) if panel.blocked else 1                 # no |X| temporary of the panel
     amax = torch.maximum(X.amax(dim=dims), -X.amin(dim=dims)).double()
-    bound = float(amax.max()) ** 2 * float(n_total or panel.n)
+    m = torch.stack([amax.max(), w.abs().max().double() if w is not None
+                     else torch.ones((), dtype=torch.float64, device=amax.device)])
+    if comm is not None and comm.world_size > 1:
+        comm.all_reduce_max_(m)
+    xm, wm = (float(v) for v in m.cpu())
+    bound = xm ** 2 * float(n_total or panel.n)
     if w is not None:
-        bound *= float(w.abs().max())
+        bound *= wm
     if not bound < EXACT_LIMB_BOUND:
         raise ValueError(f"exact Gram: entries up to {bound:.3g} exceed the int64 limb range "
                          f"(2^38 = {EXACT_LIMB_BOUND:.3g}); rescale the columns or use the "
@@ -270,7 +280,7 @@ def check_exact_range(panel: DevicePanel, n_total: int | None = None, w=None):
 
 def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor | None = None,
          out: torch.Tensor | None = None, stage: str = "all", exact: bool = False,
-         n_total: int | None = None) -> torch.Tensor:
+         n_total: int | None = None, checked: bool = False) -> torch.Tensor:
     """Per-segment Gram stack [nseg, P, P] (fp64). ``w``: optional row weights (panel order).
 
     stage (paired-tile bf16 Gram): "tiles" launches only the tile kernel (slab partials),
@@ -282,9 +292,10 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     row block per chunk and the chunk partials summed as int64 limbs (ops/exact.py);
     returns the limb stack [2, nseg, P, P] (int64): all-reduce it over row shards, then
     ops.exact.from_limbs gives the same fp64 Gram at every world size (``n_total``: rows
-    over all ranks, for the limb range check ``check_exact_range``)."""
+    over all ranks, for the limb range check ``check_exact_range``; ``checked``: the
+    caller already ran that check with every rank agreeing, skip it here)."""
     X = panel.data
-    if exact and stage != "reduce":
+    if exact and stage != "reduce" and not checked:
         check_exact_range(panel, n_total, w)
     if not X.is_cuda:
         if exact:

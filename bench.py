@@ -11,29 +11,35 @@ fused held-out residual pass + orthogonal-score moments (csrc/dml.hip) ->
 all-reduce of the moments (C06) -> theta / SE on device.
 Nothing is cached across steps; every nuisance is refit each step.
 
+Data (``--dgp``, default ``tutorial``): the tutorial's selection-biased ``df_mod`` at
+scale (data/device_dgp.py, data/panel_selection.py): the calibrated
+latent-voter model drawn as an RCT, then ``ate_replication.Rmd:97-121``'s transform over
+the generated rows (the first round(0.85 k) treated likely voters and control unlikely
+voters dropped), N = 1e7 rows KEPT per GPU (``n_generated`` in the JSON: ~5.5e7 drawn),
+21 tutorial covariates + 479 extra nuisance covariates, generated directly in HBM
+(random-init equivalent: there is no dataset download). W is confounded with the vote
+history there. ``--also-rct 1`` (default) then measures the same step on the RCT panel
+(``--dgp rct``: W independent of X, every coordinate of the W path moves -- the path
+solver's worst case) and reports it under ``"rct"``.
+
 Three cross-fits are in flight at every world size (``--inflight 3``): ``ms_per_step`` is
 the wall time per completed cross-fit (throughput); ``single_fit_ms`` in the JSON is the
-latency of one cross-fit alone. The Grams of all fits run back to back on one
-low-priority stream; each fit's path solve / residual pass / score runs on its own
-high-priority stream beside the next fit's Gram (``--stagger 2``). The panel uses the
-64-row blocked layout (``--blocked 1``: one contiguous HBM run per Gram K-step). With
-RCCL the all-reduces (C01 Gram stack, C08 coefficients, C06 moments) are captured inside
-the fit's graph (utils/graphs.SegmentedStep), so a fit is the same two graph launches
-(Gram tiles on the Gram stream; everything else on the fit's stream) at every world
-size; if capture of the collectives fails they run eagerly between graph segments and
-the JSON says so (``collectives_captured``). Each in-flight fit owns an RCCL communicator
-(``communicators`` in the JSON): the fits' graphs replay concurrently on their own
-streams, and no two of them may run collectives of one communicator at the same time.
+latency of one cross-fit alone (SURVEY.md §7.5 protocol: median of >= 5 single-call
+replays, each bracketed by device syncs; ``single_fit_rows_per_s`` = N / that). The Grams
+of all fits run back to back on one low-priority stream; each fit's path solve / residual
+pass / score runs on its own high-priority stream beside the next fit's Gram
+(``--stagger 2``). The panel uses the 64-row blocked layout (``--blocked 1``). With RCCL
+the all-reduces (C01 Gram stack, C08 coefficients, C06 moments) are captured inside the
+fit's graph (utils/graphs.SegmentedStep), so a fit is the same two graph launches at every
+world size; if capture of the collectives fails they run eagerly between graph segments
+and the JSON says so (``collectives_captured``). Each in-flight fit owns an RCCL
+communicator (``communicators``).
 
-Latency (SURVEY.md §7.5 protocol): ``single_fit_ms`` is the MEDIAN of >= 5 single-call
-replays, each bracketed by device syncs (``single_fit_ms_all`` lists them).
+Parity (``--parity 1``, untimed): the same kept rows as a float64 panel, fp64 Gram and
+fp64 path solves; the JSON reports |dATE| / SE_f64 and the relative SE difference.
 
 Scaling: weak by default (N=1e7 rows per GPU; at N=1 GPU this is exactly the
 BASELINE config); ``--scaling strong`` keeps N=1e7 in total.
-
-Data: synthetic rows of the tutorial DGP shape (21 tutorial covariates + 479
-extra nuisance covariates), generated directly in HBM (random-init equivalent:
-there is no dataset download). Usage:
 
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -41,6 +47,7 @@ there is no dataset download). Usage:
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -54,16 +61,23 @@ import time
 CPU_BASELINE_ROWS_PER_S = 1.154e6
 
 
-def main():
+def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=float, default=1e7,
-                    help="rows per GPU (weak scaling) or in total (strong scaling)")
+                    help="rows per GPU (weak scaling) or in total (strong scaling); with "
+                         "--dgp tutorial these are rows KEPT by the selection transform")
     ap.add_argument("--p", type=int, default=500)
     ap.add_argument("--folds", type=int, default=5)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "f64"])
+    ap.add_argument("--dgp", default="tutorial", choices=["tutorial", "rct", "tutorial-rct"],
+                    help="tutorial: the selection-biased df_mod at scale (default); rct: W "
+                         "independent of X (the path solver's worst case)")
+    ap.add_argument("--also-rct", type=int, default=1,
+                    help="after the --dgp tutorial measurement, time the same step on the RCT "
+                         "panel too (JSON key 'rct')")
     # weak (default): every GPU holds N=1e7 rows of the named config, so N=1 is exactly
     # the BASELINE config and rows/s measures the data-parallel design. The CV-LASSO
     # path solve is O(p^2 * lambdas) and independent of N, so at a fixed total N it is
@@ -81,10 +95,8 @@ def main():
                          "K-step, ops/panel.py); 0: column-major")
     ap.add_argument("--stagger", type=int, default=2,
                     help="1: a fit's Gram waits for the previous fit's Gram (event between "
-                         "the streams), so one fit's Gram overlaps the other's path solve "
-                         "instead of both Grams, then both paths, running together; 2: the "
-                         "Grams of all fits run on one low-priority stream and the rest of "
-                         "each fit on its own high-priority stream")
+                         "the streams); 2: the Grams of all fits run on one low-priority "
+                         "stream and the rest of each fit on its own high-priority stream")
     ap.add_argument("--exact", type=int, default=0,
                     help="1: world-size-invariant exact reduction mode (block-aligned row "
                          "shards, int64-limb Gram all-reduce, exact score moments: the same "
@@ -92,46 +104,35 @@ def main():
     ap.add_argument("--inflight", type=int, default=-1,
                     help="independent cross-fits in flight (one hipGraph + stream + Gram "
                          "workspace each); every timed step is still one complete DML-ATE")
-    args = ap.parse_args()
+    return ap.parse_args()
 
+
+def measure(args, comm, device, dgp, n_total, slot_comms_cache):
+    """Build the ``dgp`` panel, capture the in-flight fits, time ``args.steps`` steps and
+    the single-call latency. Returns a dict (and the panel, for the parity refit)."""
     import torch
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from ate_replication_causalml_amd.parallel import comm as C
     from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
-    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel, global_seg_counts
-
-    comm = C.from_env()
-    emulate = int(os.environ.get("ATE_BENCH_EMULATE_WORLD", "0"))
-    if emulate > 1 and comm.world_size == 1:
-        # diagnostic only (tools/emulate_ranks.sh): rank 0's share of a world-W step on one
-        # GPU -- its row shard, its path solves -- with no-op collectives (values are not
-        # the world-W result; the JSON says "emulated_world")
-        comm = C.LocalComm()
-        comm.world_size = emulate
-    else:
-        emulate = 0
+    from ate_replication_causalml_amd.estimators.lasso import (EXACT_BLOCK, dml_phases,
+                                                               global_seg_counts)
+    from ate_replication_causalml_amd.ops.gram import plan_slot
+    from ate_replication_causalml_amd.parallel import comm as C
+    from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
     world, rank = comm.world_size, comm.rank
-    if torch.cuda.is_available():
-        torch.cuda.set_device(C.local_device())
-        device = torch.device("cuda", torch.cuda.current_device())
-    else:
-        device = torch.device("cpu")
-    n_total = int(args.rows) * (world if args.scaling == "weak" else 1)
-    from ate_replication_causalml_amd.estimators.lasso import EXACT_BLOCK
-    pan = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed, dtype=args.dtype,
-                          blocked=bool(args.blocked) and args.dtype == "bf16",
-                          device=device, rank=rank, world=world,
-                          align=EXACT_BLOCK if args.exact else 0)
 
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize()
 
+    sync()
+    t_gen = time.perf_counter()
+    pan = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed, dtype=args.dtype,
+                          blocked=bool(args.blocked) and args.dtype == "bf16",
+                          device=device, rank=rank, world=world,
+                          align=EXACT_BLOCK if args.exact else 0, dgp=dgp,
+                          comm=comm if world > 1 else None)
+    sync()
+    t_gen = time.perf_counter() - t_gen
     seg_counts = global_seg_counts(pan, comm)   # fold sizes: data layout, fixed across steps
-
-    from ate_replication_causalml_amd.estimators.lasso import dml_phases
-    from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
-    from ate_replication_causalml_amd.ops.gram import plan_slot
     use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
     # Independent cross-fits in flight at EVERY world size (same setting for the whole
     # 1/2/4/8 curve): the CV path solve is a latency-bound serial recurrence that fills few
@@ -142,14 +143,18 @@ def main():
     # kernels share the communicator's channel buffers, and captured graphs replayed on
     # different streams carry no order between them), while each fit's own collectives
     # stay in stream order on its private communicator. gloo (CPU) ops are synchronous
-    # calls: one communicator serves every slot.
-    slot_comms = [comm] * inflight
-    if world > 1 and inflight > 1 and isinstance(comm, C.TorchComm) and comm.capturable:
-        import torch.distributed as tdist
-        slot_comms = [comm] + [C.TorchComm(tdist.new_group(list(range(world))))
-                               for _ in range(inflight - 1)]
-        for c in slot_comms[1:]:
-            c.barrier()             # create each communicator now, outside any capture
+    # calls: one communicator serves every slot. Made once per process (reused by the
+    # second measurement).
+    if "slots" not in slot_comms_cache:
+        slot_comms = [comm] * inflight
+        if world > 1 and inflight > 1 and isinstance(comm, C.TorchComm) and comm.capturable:
+            import torch.distributed as tdist
+            slot_comms = [comm] + [C.TorchComm(tdist.new_group(list(range(world))))
+                                   for _ in range(inflight - 1)]
+            for c in slot_comms[1:]:
+                c.barrier()             # create each communicator now, outside any capture
+        slot_comms_cache["slots"] = slot_comms
+    slot_comms = slot_comms_cache["slots"]
     if inflight > 1:
         # Gram workgroup count beside another fit's path solve: 1024 for two fits in
         # lockstep (profiles/r01_bench/wg_inflight.log); staggered, 824-4096 are within 3 %
@@ -188,12 +193,12 @@ def main():
 
     gram_stream = None
     fit_streams = []
+    fit_done = [None] * inflight
     if args.stagger == 2 and inflight > 1 and device.type == "cuda":
         lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
             else (0, -1)
         gram_stream = torch.cuda.Stream(device, priority=lo)
         fit_streams = [torch.cuda.Stream(device, priority=hi) for _ in range(inflight)]
-        fit_done = [None] * inflight
 
     def split_streams(i):
         # Gram of fit i on the shared low-priority stream (after fit i's previous solve
@@ -234,6 +239,7 @@ def main():
             phases = [in_slot(ph, i) for ph in staggered(
                 dml_phases(pan, args.folds, "min", comm=slot_comms[i], seg_counts=seg_counts,
                            exact=bool(args.exact)), i)]
+
             def agree(ok):
                 t = torch.tensor([float(ok)], device=device)
                 comm.all_reduce_min_(t)
@@ -279,12 +285,6 @@ def main():
         with torch.cuda.stream(streams[i]):
             return runs[i]()["res"]
 
-    import contextlib
-    from ate_replication_causalml_amd.utils.guards import collective_timeout
-    # a dead peer must end the job with a message, not hang the other ranks in RCCL
-    guard = collective_timeout(float(os.environ.get("ATE_COLLECTIVE_TIMEOUT", "900")),
-                               "bench step") if world > 1 else contextlib.nullcontext()
-    guard.__enter__()
     for k in range(args.warmup):
         res = run_step(k)
     sync()
@@ -334,30 +334,97 @@ def main():
     lats = sorted(float(v) for v in lat_t.cpu())
     lat = lats[len(lats) // 2]
     ate, se = [float(v) for v in res.detach().cpu()]
-    n_inflight = len(runs)
-    parity = None
-    if args.parity and args.dtype != "f64":
-        # ATE/SE parity (the metric's second half), untimed: the same rows generated as a
-        # float64 panel, fp64 Gram and fp64 path solves (the path tests/test_gpu.py pins
-        # against the float64 reference estimator at small N)
-        del runs
-        from ate_replication_causalml_amd.ops.gram import clear_plans
-        clear_plans()
-        t2 = time.perf_counter()
-        pan64 = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed,
-                                dtype="f64", device=device, rank=rank, world=world)
-        r64 = dml_crossfit_panel(pan64, args.folds, "min", comm=comm, seg_counts=seg_counts)[0]
-        a64, s64 = [float(v) for v in r64.detach().cpu()]
-        parity = {"reference": "same rows as a float64 panel: fp64 Gram + fp64 CV-LASSO paths",
-                  "ate_f64": a64, "se_f64": s64, "abs_diff_ate": abs(ate - a64),
-                  "rel_diff_se": abs(se - s64) / abs(s64), "seconds": time.perf_counter() - t2}
-        del pan64
-        clear_plans()
-    guard.__exit__(None, None, None)
-    ms = elapsed / args.steps * 1e3
     if not (math.isfinite(ate) and math.isfinite(se)):
         from ate_replication_causalml_amd.utils.guards import NumericalError
         raise NumericalError(f"bench step returned ate={ate} se={se} (truncated CV fold path?)")
+    ms = elapsed / args.steps * 1e3
+    out = {
+        "dgp": dgp, "ms_per_step": ms, "rows_per_s": n_total / (ms / 1e3),
+        "single_fit_ms": lat * 1e3, "single_fit_ms_all": [round(v * 1e3, 4) for v in lats],
+        "single_fit_step": lat_kind, "single_fit_rows_per_s": n_total / lat,
+        "ate": ate, "se": se, "ate_hex": ate.hex(), "se_hex": se.hex(),
+        "n_kept": n_total, "n_generated": int(pan.n_generated) * 1,
+        "panel_gen_s": t_gen, "hipgraph": graphed, "inflight": len(runs),
+        "graphs_per_fit": graphs_per_fit, "collectives_captured": collectives_captured,
+        "communicators": len({id(c) for c in slot_comms}),
+        "layout": "blocked64" if pan.blocked else "colmajor",
+        "stagger": bool(args.stagger and len(runs) > 1 and device.type == "cuda"),
+    }
+    if world > 1 and pan.selection is not None:
+        out["n_generated"] = int(pan.selection.n_gen)
+    del runs, lat_step
+    return out, pan, seg_counts
+
+
+def main():
+    args = parse()
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ate_replication_causalml_amd.parallel import comm as C
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    from ate_replication_causalml_amd.ops.gram import clear_plans
+
+    comm = C.from_env()
+    emulate = int(os.environ.get("ATE_BENCH_EMULATE_WORLD", "0"))
+    if emulate > 1 and comm.world_size == 1:
+        # diagnostic only (tools/emulate_ranks.sh): rank 0's share of a world-W step on one
+        # GPU -- its row shard, its path solves -- with no-op collectives (values are not
+        # the world-W result; the JSON says "emulated_world")
+        comm = C.LocalComm()
+        comm.world_size = emulate
+    else:
+        emulate = 0
+    world, rank = comm.world_size, comm.rank
+    if torch.cuda.is_available():
+        torch.cuda.set_device(C.local_device())
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    n_total = int(args.rows) * (world if args.scaling == "weak" else 1)
+
+    from ate_replication_causalml_amd.utils.guards import collective_timeout
+    # a dead peer must end the job with a message, not hang the other ranks in RCCL
+    guard = collective_timeout(float(os.environ.get("ATE_COLLECTIVE_TIMEOUT", "900")),
+                               "bench step") if world > 1 else contextlib.nullcontext()
+    guard.__enter__()
+    cache = {}
+    main_m, pan, seg_counts = measure(args, comm, device, args.dgp, n_total, cache)
+    parity = None
+    if args.parity and args.dtype != "f64":
+        # ATE/SE parity (the metric's second half), untimed: the same kept rows generated as
+        # a float64 panel (the selection plan is reused: same rows), fp64 Gram and fp64 path
+        # solves (the path tests/test_gpu.py pins against the float64 reference estimator)
+        clear_plans()
+        t2 = time.perf_counter()
+        pan64 = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed,
+                                dtype="f64", device=device, rank=rank, world=world,
+                                dgp=args.dgp, selection=pan.selection)
+        r64 = dml_crossfit_panel(pan64, args.folds, "min", comm=comm, seg_counts=seg_counts)[0]
+        a64, s64 = [float(v) for v in r64.detach().cpu()]
+        ate, se = main_m["ate"], main_m["se"]
+        parity = {"reference": "same kept rows as a float64 panel: fp64 Gram + fp64 CV-LASSO "
+                               "paths", "dgp": args.dgp,
+                  "ate_f64": a64, "se_f64": s64, "abs_diff_ate": abs(ate - a64),
+                  "abs_diff_ate_in_se": abs(ate - a64) / abs(s64),
+                  "rel_diff_se": abs(se - s64) / abs(s64),
+                  "within_tolerance": bool(abs(ate - a64) <= 0.01 * abs(s64)
+                                           and abs(se - s64) <= 1e-3 * abs(s64)),
+                  "tolerance": "|dATE| <= 0.01 SE_f64 and |dSE| <= 1e-3 SE_f64",
+                  "seconds": time.perf_counter() - t2}
+        del pan64
+        clear_plans()
+    del pan
+    rct = None
+    if args.also_rct and args.dgp != "rct":
+        clear_plans()
+        if device.type == "cuda":
+            torch.cuda.empty_cache()
+        rct, rpan, _ = measure(args, comm, device, "rct", n_total, cache)
+        del rpan
+        clear_plans()
+    guard.__exit__(None, None, None)
+    ms = main_m["ms_per_step"]
     rows_per_s = n_total / (ms / 1e3)
     if rank == 0:
         out = {
@@ -373,7 +440,10 @@ def main():
             "vs_baseline": rows_per_s / CPU_BASELINE_ROWS_PER_S,
             "baseline": "CPU bound: fp32 fold Grams alone, 8-core host (BASELINE.md)",
             "dtype": args.dtype,
-            "data": "synthetic (tutorial DGP shape, generated on device)",
+            "data": ("synthetic: the tutorial's selection-biased df_mod at scale (calibrated "
+                     "latent-voter DGP + ate_replication.Rmd:97-121 transform over generated "
+                     "rows), generated on device" if args.dgp == "tutorial" else
+                     f"synthetic ({args.dgp} panel, tutorial DGP shape, generated on device)"),
             "config": {
                 "model": "DML-PLR 5-fold cross-fit, CV-LASSO nuisances (100 lambdas, inner 4-fold CV)",
                 "global_batch": n_total,
@@ -382,25 +452,33 @@ def main():
                 "p": args.p,
                 "folds": args.folds,
                 "parallelism": f"dp{world}",
-                "inflight": n_inflight,
-                "layout": "blocked64" if pan.blocked else "colmajor",
-                "stagger": bool(args.stagger and n_inflight > 1 and device.type == "cuda"),
+                "dgp": args.dgp,
+                "n_kept": n_total,
+                "n_generated": main_m["n_generated"],
+                "inflight": main_m["inflight"],
+                "layout": main_m["layout"],
+                "stagger": main_m["stagger"],
             },
-            "ate": ate,
-            "se": se,
-            "ate_hex": ate.hex(),
-            "se_hex": se.hex(),
-            "hipgraph": graphed,
-            "inflight": n_inflight,
-            "single_fit_ms": lat * 1e3,
-            "single_fit_ms_all": [round(v * 1e3, 4) for v in lats],
-            "single_fit_step": lat_kind,
-            "single_fit_rows_per_s": n_total / lat,
-            "graphs_per_fit": graphs_per_fit,
+            "ate": main_m["ate"],
+            "se": main_m["se"],
+            "ate_hex": main_m["ate_hex"],
+            "se_hex": main_m["se_hex"],
+            "hipgraph": main_m["hipgraph"],
+            "inflight": main_m["inflight"],
+            "single_fit_ms": main_m["single_fit_ms"],
+            "single_fit_ms_all": main_m["single_fit_ms_all"],
+            "single_fit_step": main_m["single_fit_step"],
+            "single_fit_rows_per_s": main_m["single_fit_rows_per_s"],
+            "graphs_per_fit": main_m["graphs_per_fit"],
             "exact": bool(args.exact),
-            "collectives_captured": collectives_captured,
-            "communicators": len({id(c) for c in slot_comms}),
+            "collectives_captured": main_m["collectives_captured"],
+            "communicators": main_m["communicators"],
+            "panel_gen_s": main_m["panel_gen_s"],
             "parity": parity,
+            "rct": None if rct is None else {k: rct[k] for k in (
+                "ms_per_step", "rows_per_s", "single_fit_ms", "single_fit_ms_all",
+                "single_fit_rows_per_s", "ate", "se", "ate_hex", "se_hex", "hipgraph",
+                "inflight")},
         }
         if emulate > 1:
             out["emulated_world"] = emulate
