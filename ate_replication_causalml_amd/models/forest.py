@@ -51,8 +51,10 @@ class ForestParams(ctypes.Structure):
 
 KIND_CLASS, KIND_REG, KIND_CAUSAL = 0, 1, 2
 FIX = float(2 ** 32)
-# causal-split admissibility rule the engines implement (part of checkpoint keys)
-CAUSAL_SPLIT_RULE = "arm1"
+# causal-split admissibility rule the engines implement (part of checkpoint keys):
+# grf stabilize.splits=TRUE -- each child holds >= max(ceil(alpha n), 1) rows on both sides
+# of the node's mean centred treatment (csrc/forest_common.hpp)
+CAUSAL_SPLIT_RULE = "grf-stabilize"
 
 
 def to_fix(v) -> np.ndarray:

@@ -26,8 +26,9 @@ Spec, per tree ``tg`` (global tree index, the RNG stream):
             strict improvement: the first maximum wins (exact-split mode: bins are value
             ranks; randomForest places the threshold at the values' midpoint, grf at the
             lower value); each child needs
-            max(ceil(alpha * n_node), 1) rows (causal: >= 1 treated and >= 1 control row,
-            treated = W~ above the node mean); split only if best > parent + 1e-12 max(1,
+            minc = max(ceil(alpha * n_node), 1) rows (causal: grf's stabilize.splits rule,
+            minc rows with W~ below the node mean AND minc rows with W~ >= it in each
+            child); split only if best > parent + 1e-12 max(1,
             |parent|) and the node has more than ``min_node`` rows (not pure, kind 0;
             Var(W~) > 0, kind 2); at most 64 levels;
   leaves    kind 0: majority vote of the weighted class counts, ties by a Philox coin at
@@ -210,7 +211,7 @@ def grow_tree(Xb, P: Params, tg: int, y=None, r1=None, r2=None, exact=None):
                     sd = from_fix(stot)
                     parent = sd * sd / dn
                 minc = 1 if P.alpha <= 0.0 else max(1, int(math.ceil(P.alpha * dn)))
-                treated = {i: P.kind == 2 and from_fix(r1[i]) > wbar for i in rows}
+                treated = {i: P.kind == 2 and from_fix(r1[i]) >= wbar for i in rows}
                 ntreat = sum(treated.values())
                 best = -math.inf
                 for f in _tried_features(P, p, tg, v, _num_features(P, p, tg, v)):
@@ -240,7 +241,7 @@ def grow_tree(Xb, P: Params, tg: int, y=None, r1=None, r2=None, exact=None):
                         else:
                             if P.kind == 2:
                                 tr = ntreat - ct
-                                if ct < 1 or nl - ct < 1 or tr < 1 or nr - tr < 1:
+                                if ct < minc or nl - ct < minc or tr < minc or nr - tr < minc:
                                     continue
                             sl, sr = from_fix(cs), from_fix(stot - cs)
                             crit = (sl * sl) / float(nl) + (sr * sr) / float(nr)

@@ -206,7 +206,7 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
             } else {
               h0[b] += 1;
               hs[b] += rho[i];
-              ht[b] += from_fix(r1[i]) > cn.wbar ? 1 : 0;
+              ht[b] += from_fix(r1[i]) >= cn.wbar ? 1 : 0;
             }
           }
           int64_t c0 = 0, c1 = 0, cs = 0, ct = 0;
@@ -227,7 +227,7 @@ static void grow_tree(const ForestParams& fp, int t, const uint8_t* Xb, const ui
             } else {
               if (fp.kind == 2) {
                 int64_t tr = ntreat - ct;
-                if (ct < 1 || nl - ct < 1 || tr < 1 || nr - tr < 1) continue;
+                if (ct < minc || nl - ct < minc || tr < minc || nr - tr < minc) continue;
               }
               crit = mse_crit(from_fix(cs), (double)nl, from_fix(stot - cs), (double)nr);
             }
@@ -371,7 +371,7 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
         }
         int64_t ntreat = 0;
         if (fp.kind == 2)
-          for (int q = nd.lo; q < nd.hi; ++q) ntreat += from_fix(r1[idx[q]]) > cn.wbar ? 1 : 0;
+          for (int q = nd.lo; q < nd.hi; ++q) ntreat += from_fix(r1[idx[q]]) >= cn.wbar ? 1 : 0;
         double best = -INFINITY;
         const int cnt = nd.hi - nd.lo;
         for (int k = 0; k < nf; ++k) {
@@ -390,7 +390,7 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
               c0 += w[i];
               c1 += (int64_t)w[i] * r1[i];
             } else {
-              c0 += 1 + ((from_fix(r1[i]) > cn.wbar ? 1ll : 0ll) << 32);
+              c0 += 1 + ((from_fix(r1[i]) >= cn.wbar ? 1ll : 0ll) << 32);
               c1 += rho[i];
             }
             const int b = (int)(keys[s] >> 32), bn = (int)(keys[s + 1] >> 32);
@@ -400,7 +400,7 @@ static void grow_tree_exact(const ForestParams& fp, int t, const uint16_t* Xb, c
             if (nl < minc || nr < minc) continue;
             if (fp.kind == 2) {
               const int64_t ct = c0 >> 32, tr = ntreat - ct;
-              if (ct < 1 || nl - ct < 1 || tr < 1 || nr - tr < 1) continue;
+              if (ct < minc || nl - ct < minc || tr < minc || nr - tr < minc) continue;
             }
             const double crit = fp.kind == 0
                 ? gini_crit((double)c0, (double)c1, (double)(nw - n1 - c0), (double)(n1 - c1))

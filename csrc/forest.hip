@@ -350,7 +350,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
           } else {
             atomicAdd((unsigned long long*)&hist[wid][0][b], 1ull);
             atomicAdd((unsigned long long*)&hist[wid][2][b], (unsigned long long)rho);
-            if (from_fix(a1) > cn.wbar) atomicAdd((unsigned long long*)&hist[wid][3][b], 1ull);
+            if (from_fix(a1) >= cn.wbar) atomicAdd((unsigned long long*)&hist[wid][3][b], 1ull);
           }
         };
         // per feature: clear, accumulate (by the caller), scan, evaluate, argmax
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
             return gini_crit((double)L0, (double)L1, (double)(nw - n1 - L0), (double)(n1 - L1));
           if (fp.kind == 2) {
             const int64_t tr = ntreat - LT;
-            if (LT < 1 || nl - LT < 1 || tr < 1 || nr - tr < 1) return -INFINITY;
+            if (LT < minc || nl - LT < minc || tr < minc || nr - tr < minc) return -INFINITY;
           }
           return mse_crit(from_fix(LS), (double)nl, from_fix(stot - LS), (double)nr);
         };
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
             for (int j = 0; j < mrows; ++j) {
               const int64_t r1j = ((int64_t)__builtin_amdgcn_readlane((int)(cr1 >> 32), j) << 32) |
                                   (uint32_t)__builtin_amdgcn_readlane((int)cr1, j);
-              t += from_fix(r1j) > cn.wbar ? 1 : 0;
+              t += from_fix(r1j) >= cn.wbar ? 1 : 0;
             }
             ntreat = t;
           }
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
                     if (in) {
                       L0 += 1;
                       LS += rhoj;
-                      LT += from_fix(r1j) > cn.wbar ? 1 : 0;
+                      LT += from_fix(r1j) >= cn.wbar ? 1 : 0;
                     }
                   }
                 }

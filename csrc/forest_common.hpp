@@ -17,8 +17,12 @@
 //  kind 1 REGRESSION      maximise SL^2/nL + SR^2/nR (variance reduction); leaf = mean.
 //  kind 2 CAUSAL          grf gradient tree: per node W~, Y~ means, tau_P, pseudo-outcome
 //                          rho_i = (W~i - Wbar)((Y~i - Ybar) - tau_P (W~i - Wbar)) / Var(W~),
-//                          then a regression split on rho; each child needs >= 1 treated
-//                          and >= 1 control row (W~ above / below the node mean).
+//                          then a regression split on rho. Split balance is grf's
+//                          stabilize.splits = TRUE rule (its instrumental splitting rule
+//                          with the treatment as instrument): each child must hold at least
+//                          minc = max(ceil(alpha * n_node), 1) rows with W~ BELOW the node's
+//                          mean W~ and minc rows with W~ >= that mean ("treated" / "control"
+//                          sides; alpha = 0.05 -> tens of rows per side in a 1,000-row node).
 //  Sampling 0 (randomForest): bootstrap, n draws with replacement -> integer weights.
 //  Sampling 1 (grf): trees come in little bags of `group` trees sharing a half-sample
 //    (floor(n*sample_fraction*group) rows without replacement); with honesty each tree

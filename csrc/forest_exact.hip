@@ -194,7 +194,7 @@ __device__ __forceinline__ double boundary_crit(const ForestParams& fp, const No
   if (nl < minc || nr < minc) return -INFINITY;
   if (fp.kind == 2) {                  // each child keeps >= 1 treated and >= 1 control row
     const int64_t ct = c0 >> 32, tr = st.ntreat - ct;
-    if (ct < 1 || nl - ct < 1 || tr < 1 || nr - tr < 1) return -INFINITY;
+    if (ct < minc || nl - ct < minc || tr < minc || nr - tr < minc) return -INFINITY;
   }
   return fp.kind == 0
       ? gini_crit((double)c0, (double)c1, (double)(st.nw - st.n1 - c0), (double)(st.n1 - c1))
@@ -208,7 +208,7 @@ __device__ __forceinline__ void row_stats(const ForestParams& fp, const int32_t*
                                           int i, int64_t& a0, int64_t& a1) {
   const int64_t wi = w[i];
   if (fp.kind == 2) {
-    a0 = 1 + ((from_fix(r1[i]) > cn.wbar ? 1ll : 0ll) << 32);
+    a0 = 1 + ((from_fix(r1[i]) >= cn.wbar ? 1ll : 0ll) << 32);
     a1 = to_fix(causal_rho(cn, from_fix(r1[i]), from_fix(r2[i])));
   } else if (fp.kind == 0) {
     const int64_t y = ycls[i];

@@ -119,3 +119,81 @@ def test_variance_is_calibrated_under_a_null_effect():
     assert abs(ths.mean()) < 3 * np.sqrt(vs.mean() / (R * 10))
     cover = np.mean(np.abs(ths) <= 1.96 * np.sqrt(vs))
     assert cover >= 0.88, cover
+
+
+def _stabilize_data():
+    """One feature x = 0..399 (distinct values); below x = 30 a strong effect but only 2 of
+    the 30 rows on the treated side of the node's mean W~, so the unconstrained best root
+    split (x <= 29) leaves the left child 2 treated-side rows."""
+    n = 400
+    x = np.arange(n, dtype=float)
+    r = np.random.default_rng(1)
+    wt = np.where(np.arange(n) % 2 == 0, 0.5, -0.5)
+    wt[:30] = -0.5
+    wt[[3, 17]] = 0.5
+    yt = np.where(x < 30, 3.0 * wt, 0.0) + 0.01 * r.normal(size=n)
+    return x[:, None], wt - wt.mean(), yt - yt.mean()
+
+
+def _root_best(x, wt, yt, minc, rule):
+    """Brute-force root split on the pseudo-outcomes: 'arm1' = >= 1 row on each side of the
+    mean W~ per child (the previous rule), 'stabilize' = >= minc (grf stabilize.splits)."""
+    wbar, ybar = wt.mean(), yt.mean()
+    cww = (wt * wt).mean() - wbar * wbar
+    tau = ((wt * yt).mean() - wbar * ybar) / cww
+    rho = (wt - wbar) * ((yt - ybar) - tau * (wt - wbar)) / cww
+    o = np.argsort(x[:, 0], kind="stable")
+    big = (wt >= wbar)[o]
+    n = len(o)
+    best, arg = -np.inf, None
+    for k in range(1, n):
+        nl, nr = k, n - k
+        lt, rt = int(big[:k].sum()), int(big[k:].sum())
+        need = 1 if rule == "arm1" else minc
+        if nl < minc or nr < minc or lt < need or nl - lt < need or rt < need or nr - rt < need:
+            continue
+        sl, sr = rho[o][:k].sum(), rho[o][k:].sum()
+        c = sl * sl / nl + sr * sr / nr
+        if c > best:
+            best, arg = c, k - 1          # threshold rank: x <= arg goes left
+    return arg
+
+
+@pytest.mark.parametrize("splits", ["exact", "binned"])
+def test_stabilize_splits_rule_pins_the_root(splits):
+    """grf's stabilize.splits = TRUE (forest_common.hpp kind 2): with alpha = 0.05 at a
+    400-row root each child needs >= 20 rows on both sides of the mean W~. The old ">= 1
+    row per side" rule would split at x <= 29 (two treated-side rows on the left); the
+    engine splits where the new rule's best is, and the oracle grows the same tree."""
+    from ate_replication_causalml_amd.reference import forest as R
+    X, wt, yt = _stabilize_data()
+    old = _root_best(X, wt, yt, 20, "arm1")
+    new = _root_best(X, wt, yt, 20, "stabilize")
+    assert old == 29 and new != old
+    kw = dict(ntree=1, mtry=1, min_node=5, sampling=1, honesty=False, group=1,
+              mtry_poisson=False, alpha=0.05, sample_fraction=1.0, seed=3)
+    eng = F.fit_forest(X, F.KIND_CAUSAL, r1=wt, r2=yt, backend="cpu", splits=splits, **kw)
+    feat, thr, left, val, nn = eng.tree_arrays()
+    assert feat[0] == 0
+    if splits == "exact":
+        assert thr[0] == new                       # value rank = x for distinct integers
+    else:
+        edges, ne = eng.edges, eng.nedges
+        # the binned engine's root threshold bin covers x <= new (400 distinct values in
+        # 256 quantile bins: the admissible boundary nearest the exact one)
+        cut = edges[0, thr[0]]
+        assert abs(cut - (new + 0.5)) <= 2.0
+        assert cut > 29.5 + 1
+    # the oracle (reference/forest.py) grows the same tree from the written spec
+    if splits == "exact":
+        eb = F.exact_bins(X)
+        Xb = eb.bin(X)
+    else:
+        Xb = F.bin_matrix(X, eng.edges, eng.nedges, None).numpy()
+    P = R.Params(kind=2, sampling=1, mtry=1, min_node=5, honesty=False, group=1,
+                 mtry_poisson=False, alpha=0.05, sample_fraction=1.0, seed=3)
+    ref = R.grow_forest(Xb, P, 1, r1=F.to_fix(wt), r2=F.to_fix(yt),
+                        exact=eb if splits == "exact" else None)
+    assert int(nn[0]) == ref[0]["nnodes"]
+    np.testing.assert_array_equal(thr[:ref[0]["nnodes"]][ref[0]["feat"] >= 0],
+                                  ref[0]["thr"][ref[0]["feat"] >= 0])
