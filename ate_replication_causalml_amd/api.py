@@ -247,7 +247,7 @@ def ate_causal_forest(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest
             return R.causal_forest_ate(Y, W, X, num_trees=num_trees, seed=seed, method=method)
         from .estimators import forest as DF
         return DF.causal_forest_ate(Y, W, X, num_trees=num_trees, seed=seed, method=method,
-                                    device=run.device())
+                                    device=run.device(), compat=run.compat)
 
 
 def ate_aipw_crossfit(Y, W, X, folds=5, learner="rf", num_trees=500, run=None, comm=None,
@@ -271,7 +271,7 @@ def ate_causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, run
         return causal_forest_bootstrap(Y, W, X, num_trees=num_trees, B=B, seed=seed,
                                        boot_seed=run.seed,
                                        device=run.device() if not _ref(run) else "cpu",
-                                       comm=comm)
+                                       comm=comm, compat=run.compat)
 
 
 # ------------------------------------------------------------------ driver

@@ -127,12 +127,11 @@ class _Flags:
 
 
 def plan_selection(n_keep: int, seed: int, params: DgpParams, comm=None, device="cpu",
-                   pt: float = 0.85, pc: float = 0.85, compat: str = "reference",
-                   rank: int | None = None, world: int | None = None) -> PanelSelection:
+                   pt: float = 0.85, pc: float = 0.85, compat: str = "reference") -> PanelSelection:
     """Find n_gen (the generated rows whose transform keeps exactly ``n_keep``) and the
-    per-block counts. Blocks are counted sharded over ``comm`` (else, with ``rank``/``world``
-    given but no communicator, every rank counts all blocks itself: same integers)."""
-    if pt != pc and not (0 < pt <= 1 and 0 < pc <= 1):
+    per-block counts. Blocks are counted sharded over ``comm`` (without one, a rank counts
+    every block itself: the same integers)."""
+    if not (0 < pt <= 1 and 0 < pc <= 1):
         raise ValueError("pt, pc must be in (0, 1]")
     fl = _Flags(seed, params, compat, device)
     r, w = (comm.rank, comm.world_size) if comm is not None else (0, 1)
@@ -252,3 +251,20 @@ def kept_gids(sel: PanelSelection, slices, device="cpu") -> torch.Tensor:
     if total and (out < 0).any():
         raise AssertionError("selection left a kept-row slot unfilled")
     return torch.from_numpy(out)
+
+
+def selected_rows(n_keep: int, seed: int, p_extra: int = 0, compat: str = "reference",
+                  device="cpu"):
+    """The tutorial's df_mod at any size as host arrays (dgp.TutorialData): the calibrated
+    model's generated rows, selected by the transform over generated-row order (flags on
+    ``device``: the GPU's float32 draws or the host's float64 twin), then the kept rows'
+    columns drawn on the host (population-standardised continuous covariates, as the
+    panels; configs 3 / 4 on host-resident data: tools/cfg4.py)."""
+    from . import dgp as D
+    sel = plan_selection(n_keep, seed, D.TUTORIAL, device=device, compat=compat)
+    g = kept_gids(sel, [(0, n_keep)], device=device).cpu().numpy()
+    cts, binc, extra, W, Y, tau_i = D.raw_columns(n_keep, seed, p_extra, params=D.TUTORIAL,
+                                                  idx=g)
+    names = list(D.COVARIATES) + [f"x_extra{j}" for j in range(p_extra)]
+    X = np.column_stack([cts, binc, extra]) if p_extra else np.column_stack([cts, binc])
+    return D.TutorialData(X=X, W=W, Y=Y, names=names, tau_true=float(tau_i.mean())), sel

@@ -403,7 +403,8 @@ def aipw_rf_crossfit_panel(pan, num_trees=100, seed=1991, clip=0.01, comm=None,
 
 def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_seed=1991,
                             method="Causal Forest(GRF) + bootstrap SE", device=None, comm=None,
-                            nuisance_trees=None, checkpoint=None, boot_chunk=250) -> AteResult:
+                            nuisance_trees=None, checkpoint=None, boot_chunk=250,
+                            compat="reference") -> AteResult:
     """Config 4: grf-style causal forest (trees sharded over ``comm``), AIPW scores
     Gamma_i from the OOB CATEs, and B multinomial bootstrap replicates of mean(Gamma)
     sharded over the ranks (C07); SE = sd of the replicates. The scores are formed and
@@ -448,7 +449,11 @@ def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_se
     Yd, Wd, yh, wh, to = t(Yn), t(Wn), t(y_hat), t(w_hat), t(tau_oob)
     w_res = Wd - wh
     tau = torch.where(torch.isnan(to), torch.nanmean(to), to)
-    what = wh.clamp(1e-6, 1 - 1e-6)
+    # grf's AIPW does not clip W.hat (compat="reference"; a poor-overlap warning as grf);
+    # compat="textbook" clips it to [1e-6, 1 - 1e-6]
+    F.overlap_warning(float(wh.min()), float(wh.max()))
+    what = wh if compat == "reference" else wh.clamp(F.AIPW_TEXTBOOK_CLIP,
+                                                     1 - F.AIPW_TEXTBOOK_CLIP)
     g = tau + w_res / (what * (1 - what)) * (Yd - yh - tau * w_res)
     n = g.numel()
     est, se_aipw = g.mean(), g.std() / math.sqrt(n)      # models/forest.average_treatment_effect

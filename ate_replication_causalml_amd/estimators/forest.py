@@ -136,9 +136,11 @@ def _double_ml_body(Xb, y, w, ev, en, num_trees, seed):
     return (halves[0] + halves[1]) / 2
 
 
-def _causal_forest_body(Xb, y, w, ev, en, num_trees, nt, seed):
+def _causal_forest_body(Xb, y, w, ev, en, num_trees, nt, seed, clip=None):
     """Device body of causal_forest_ate (models/forest.causal_forest + average_treatment_
-    effect with grf defaults, no host sync): [AIPW ATE, SE, mean CATE, sqrt(mean var)].
+    effect with grf defaults, no host sync): [AIPW ATE, SE, mean CATE, sqrt(mean var),
+    min W.hat, max W.hat]. ``clip``: None = grf (no clipping), else W.hat clipped to
+    [clip, 1 - clip] (compat="textbook").
     ``ev, en``: the exact mode's device value table (grf's exact split values), None:
     256-bin histograms. The orthogonalisation forests use ci.group.size = 1 (grf)."""
     p = Xb.shape[0]
@@ -165,11 +167,12 @@ def _causal_forest_body(Xb, y, w, ev, en, num_trees, nt, seed):
     tau_oob, var_oob = out[:, 0], out[:, 1]
     w_res, y_res = w - w_hat, y - y_hat
     tau = torch.where(torch.isnan(tau_oob), torch.nanmean(tau_oob), tau_oob)
-    what = w_hat.clamp(1e-6, 1 - 1e-6)
+    what = w_hat if clip is None else w_hat.clamp(clip, 1 - clip)
     gamma = tau + w_res / (what * (1 - what)) * (y_res - tau * w_res)
     n = gamma.numel()
     return torch.stack([gamma.mean(), gamma.std(unbiased=True) / n ** 0.5,
-                        torch.nanmean(tau_oob), torch.sqrt(torch.nanmean(var_oob))])
+                        torch.nanmean(tau_oob), torch.sqrt(torch.nanmean(var_oob)),
+                        w_hat.min(), w_hat.max()])
 
 
 def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, device=None, comm=None,
@@ -225,12 +228,16 @@ def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning"
 
 
 def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest(GRF)",
-                      device=None, nuisance_trees=None, comm=None, graph=True, splits="auto"):
+                      device=None, nuisance_trees=None, comm=None, graph=True, splits="auto",
+                      compat="reference"):
     """E15 (ate_replication.Rmd:250-272): grf causal forest; published row = AIPW
     ``estimate_average_effect``; diagnostics carry the "incorrect" mean-CATE ATE and
     sqrt(mean(var)) the reference prints (ate_replication.md:294). ``splits``: "auto" =
-    grf's exact split values up to 65,536 rows (df_mod), else 256-bin histograms."""
+    grf's exact split values up to 65,536 rows (df_mod), else 256-bin histograms.
+    ``compat="reference"``: grf's AIPW without clipping W.hat (a poor-overlap warning, as
+    grf); "textbook": W.hat clipped to [1e-6, 1 - 1e-6]."""
     dev = resolve_device(device)
+    clip = None if compat == "reference" else F.AIPW_TEXTBOOK_CLIP
     splits = F.resolve_splits(splits, len(as_np(Y)))
     if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
         # one hipGraph launch: Y.hat / W.hat OOB regression forests, the honest causal
@@ -242,13 +249,16 @@ def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest
         w = torch.as_tensor(as_np(W), device=dev)
         nt = nuisance_trees or max(50, num_trees // 4)
         out, g = estimator_graphs.run("causal_forest", _causal_forest_body, (Xb, y, w, ev, en),
-                                      num_trees, nt, seed)
+                                      num_trees, nt, seed, clip)
         v = out.cpu().numpy()
+        F.overlap_warning(float(v[4]), float(v[5]))
         return AteResult.make(method, v[0], v[1], ate_bad=float(v[2]), se_bad=float(v[3]),
-                              hipgraph=g, splits=splits)
+                              hipgraph=g, splits=splits, w_hat_min=float(v[4]),
+                              w_hat_max=float(v[5]))
     cf = F.causal_forest(as_np(X), as_np(Y), as_np(W), num_trees=num_trees, seed=seed,
                          nuisance_trees=nuisance_trees, backend=_backend(device), comm=comm,
                          splits=splits)
-    est, se = F.average_treatment_effect(cf)
+    est, se = F.average_treatment_effect(cf, clip)
     return AteResult.make(method, est, se, ate_bad=float(np.nanmean(cf.tau_oob)),
-                          se_bad=float(np.sqrt(np.nanmean(cf.var_oob))))
+                          se_bad=float(np.sqrt(np.nanmean(cf.var_oob))),
+                          w_hat_min=float(np.min(cf.w_hat)), w_hat_max=float(np.max(cf.w_hat)))

@@ -690,14 +690,31 @@ def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
     return CausalForestFit(fc, y_hat, w_hat, out[:, 0], out[:, 1], Y, W)
 
 
-def average_treatment_effect(cf: CausalForestFit):
+AIPW_TEXTBOOK_CLIP = 1e-6    # compat="textbook": W.hat clipped to [clip, 1 - clip]
+
+
+def overlap_warning(w_min: float, w_max: float, what="W.hat"):
+    """grf does not clip the propensity in its AIPW average effect; it warns when the
+    estimated propensities come close to 0 or 1 (poor overlap). Same here: a warning, and
+    with W.hat exactly 0 or 1 the scores are infinite (as in grf)."""
+    if not (w_min > 0.05 and w_max < 0.95):
+        import warnings
+        warnings.warn(f"estimated propensities {what} span [{w_min:.3g}, {w_max:.3g}]: poor "
+                      "overlap, the AIPW average effect may be unstable (grf's warning; "
+                      "compat='textbook' clips W.hat)", RuntimeWarning, stacklevel=3)
+
+
+def average_treatment_effect(cf: CausalForestFit, clip: float | None = None):
     """grf ``estimate_average_effect`` / ``average_treatment_effect`` (AIPW):
     Gamma_i = tau_i + (W_i - W.hat_i)/(W.hat_i (1 - W.hat_i)) * (Y~_i - tau_i W~_i);
-    estimate = mean(Gamma), std.err = sd(Gamma)/sqrt(n)."""
+    estimate = mean(Gamma), std.err = sd(Gamma)/sqrt(n). grf does not clip W.hat (it warns
+    on poor overlap): ``clip`` = None reproduces that; a float clips W.hat to
+    [clip, 1 - clip] (the compat="textbook" option of the estimators)."""
     w_res = cf.W - cf.w_hat
     y_res = cf.Y - cf.y_hat
     tau = np.where(np.isnan(cf.tau_oob), np.nanmean(cf.tau_oob), cf.tau_oob)
-    what = np.clip(cf.w_hat, 1e-6, 1 - 1e-6)
+    overlap_warning(float(np.min(cf.w_hat)), float(np.max(cf.w_hat)))
+    what = cf.w_hat if clip is None else np.clip(cf.w_hat, clip, 1 - clip)
     gamma = tau + w_res / (what * (1 - what)) * (y_res - tau * w_res)
     n = len(gamma)
     return float(gamma.mean()), float(gamma.std(ddof=1) / math.sqrt(n))

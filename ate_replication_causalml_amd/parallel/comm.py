@@ -56,6 +56,31 @@ class LocalComm:
         return self
 
 
+class EmulatedComm(LocalComm):
+    """Rank ``rank`` of a ``world``-rank job run ALONE (tools/cfg3.py / cfg4.py --shard r/W):
+    every algorithm takes rank r's share of the work (its row / tree / replicate shard),
+    and the collectives return shape-correct local data instead of communicating. The
+    values are those of the shard, not of the world-W result: a timing of one GPU's share
+    of the job, not a way to compute it."""
+
+    def __init__(self, rank: int, world: int):
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside a world of {world}")
+        self.rank, self.world_size = int(rank), int(world)
+
+    def all_gather(self, t):
+        return [t.clone() for _ in range(self.world_size)]
+
+    def all_gather_into_(self, out, t):
+        out.copy_(t.reshape(-1).repeat(self.world_size).reshape(out.shape))
+        return out
+
+    def reduce_scatter_(self, out, t):
+        n = out.numel()
+        out.copy_(t.reshape(-1)[self.rank * n:(self.rank + 1) * n].reshape(out.shape))
+        return out
+
+
 class TorchComm:
     def __init__(self, group=None):
         import torch.distributed as dist

@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void dml_resid_kernel(
   for (int j = threadIdx.x; j < p; j += blockDim.x) xc[j] = xcols[j];
   // grid: blockIdx.y = segment; blocks stride over that segment's rows
   const int k = blockIdx.y;
+  ATE_DASSERT(k < nseg && y0 >= 0 && w0 >= 0 && vcol >= 0);
   for (int j = threadIdx.x; j <= p; j += blockDim.x) {
     cy[j] = coef[((int64_t)k * 2 + 0) * (p + 1) + j];
     cw[j] = coef[((int64_t)k * 2 + 1) * (p + 1) + j];
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(256) void dml_resid_kernel(
   __syncthreads();
   p = compact_support(cy, cw, xc, p, wcnt);
   const Seg sg = segs[k];
+  ATE_DASSERT(sg.r0 >= 0 && sg.r0 <= sg.r1 && sg.r1 <= ld);
   for (int64_t base = sg.r0 + (int64_t)blockIdx.x * 256 * RPT; base < sg.r1;
        base += (int64_t)gridDim.x * 256 * RPT) {
     double py[RPT], pw[RPT];
@@ -178,7 +180,10 @@ __global__ __launch_bounds__(256) void dml_resid_bf16_kernel(
 #pragma unroll
   for (int q = 0; q < 7; ++q) scale[q] = mode == 2 ? ldexp(1.0, (int)sh[q]) : 1.0;
   const Seg sg = segs[k];
+  ATE_DASSERT(k < nseg && sg.r0 >= 0 && sg.r0 <= sg.r1 && (sg.r0 & 7) == 0 && mode >= 0 &&
+              mode <= 2 && y0 >= 0 && w0 >= 0 && vcol >= 0);
   auto ld8 = [&](int c, int64_t i, float (&o)[8]) {
+    ATE_DASSERT((i & 7) == 0 && c >= 0);
     // (c, i) at c*cs + (i/64)*bs + i%64: column-major (cs = ld, bs = 64) or 64-row blocked
     // (cs = 64, bs = 64*P); the 8 rows never straddle a block (i % 8 == 0)
     const uint4 u = *reinterpret_cast<const uint4*>(X + (int64_t)c * cs + (i >> 6) * bs + (i & 63));

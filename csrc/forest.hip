@@ -201,6 +201,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
     const int f = (i < n && S.w[i] > 0) ? 1 : 0;
     int tot;
     const int pos = block_scan_excl<NW>(f, shi, &tot);
+    ATE_DASSERT(!f || m + pos < n);
     if (f) S.idx[m + pos] = i;
     m += tot;
   }
@@ -341,6 +342,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
         double best = -INFINITY;
         int64_t ntreat = 0;
         auto hist_row = [&](int b, int64_t wi, int yi, int64_t a1, int64_t rho) {
+          ATE_DASSERT(b >= 0 && b < NBINS);          // LDS histogram slot
           if (fp.kind == 0) {
             if (yi) atomicAdd((unsigned long long*)&hist[wid][1][b], (unsigned long long)wi);
             else atomicAdd((unsigned long long*)&hist[wid][0][b], (unsigned long long)wi);
@@ -550,6 +552,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
       // ---- record the decision (lane 0; wave 0 for a cooperative node)
       if (lane == 0 && (!coop || wid == 0)) {
         int nl_rows = 0;
+        ATE_DASSERT(v >= 0 && v < cap && (bf < 0 || (bf < p && bb >= 0 && bb < NBINS - 1)));
         if (bf >= 0) {
           feat[v] = bf;
           thr[v] = bb;
@@ -603,6 +606,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
       const int pos = block_scan_excl<NW>(f, shi, &tot);
       if (f) {
         const int v = S.cur[j].id;
+        ATE_DASSERT(v >= 0 && v < cap && id_base + 2 * (nsplit_total + pos) + 1 < cap);
         left[v] = id_base + 2 * (nsplit_total + pos);
         S.dec[j].w = nsplit_total + pos;   // split rank
       }
@@ -637,6 +641,7 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
       if (lane == 0) {
         const int r = d.w;
         const int lid = id_base + 2 * r;
+        ATE_DASSERT(nd.lo <= nd.lo + cnt_l && nd.lo + cnt_l <= nd.hi && nd.hi <= n);
         S.nxt[2 * r] = {nd.lo, nd.lo + cnt_l, lid};
         S.nxt[2 * r + 1] = {nd.lo + cnt_l, nd.hi, lid + 1};
       }
@@ -757,6 +762,7 @@ __global__ __launch_bounds__(256) void forest_leaf_kernel(ForestParams fp,
   const bool honest = fp.sampling == 1;
   int v = 0, last_ok = 0;
   while (true) {
+    ATE_DASSERT(v >= 0 && v < cap);
     const int2 nd = tree[v];
     if (honest && ((nd.y >> 8) & 1)) last_ok = v;
     const int f1 = nd.y >> 9;
@@ -786,8 +792,10 @@ __global__ __launch_bounds__(256) void forest_leaf16_kernel(ForestParams fp,
   const bool honest = fp.sampling == 1 && est;
   int v = 0, last_ok = 0;
   while (true) {
+    ATE_DASSERT(v >= 0 && v < cap);
     if (honest && est[(b + v) * 5] > 0) last_ok = v;
     if (feat[b + v] < 0) break;
+    ATE_DASSERT(feat[b + v] < fp.p);
     v = Xb[(int64_t)feat[b + v] * n2 + i] <= thr[b + v] ? left[b + v] : left[b + v] + 1;
   }
   *out = honest ? last_ok : v;
@@ -808,6 +816,7 @@ __global__ __launch_bounds__(256) void forest_vote_kernel(ForestParams fp, int n
   for (int tt = 0; tt < nt; ++tt) {
     const int lf = leaves[(int64_t)tt * n2 + i];
     if (lf < 0) continue;
+    ATE_DASSERT(lf < cap);
     const int64_t nd = (int64_t)(t0 + tt) * cap + lf;
     used += 1;
     acc += leafmean ? to_fix(val[nd]) : mean_fix(est[nd * 5 + 1], est[nd * 5]);
@@ -828,6 +837,7 @@ __global__ __launch_bounds__(256) void forest_cate1_kernel(int n2, int cap, int 
   for (int tt = 0; tt < nt; ++tt) {
     const int lf = leaves[(int64_t)tt * n2 + i];
     if (lf < 0) continue;
+    ATE_DASSERT(lf < cap);
     const int64_t* e = est + ((int64_t)(t0 + tt) * cap + lf) * 5;
     a1 += 1; aw += mean_fix(e[1], e[0]); ay += mean_fix(e[2], e[0]);
     aww += mean_fix(e[3], e[0]); awy += mean_fix(e[4], e[0]);
@@ -851,6 +861,7 @@ __global__ __launch_bounds__(256) void forest_cate2_kernel(ForestParams fp, int 
   const double tau = (from_fix(st[4 * n2 + i]) / a1 - wb * yb) / H;
   int64_t gs = st[5 * n2 + i], gss = st[6 * n2 + i], within = st[7 * n2 + i];
   int64_t nwithin = st[8 * n2 + i], ng = st[9 * n2 + i];
+  ATE_DASSERT(fp.group >= 1 && t0 % fp.group == 0);   // chunks hold whole little bags
   for (int g0 = 0; g0 < nt; g0 += fp.group) {
     double ps = 0, pss = 0;
     int nb = 0;

@@ -339,9 +339,13 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][GT * GK];   // 128 KB
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int c = L / ntiles, t = L % ntiles;
+  ATE_DASSERT(c < nchunks && t < ntiles);
   const Chunk ch = chunks[c];
   const int4 tl = tiles[t];
   const int type = tl.z;
+  // row chunks are whole K-steps of one segment; tiles name 256-column blocks a <= b
+  ATE_DASSERT(ch.row0 >= 0 && ch.row0 <= ch.row1 && ch.row0 % GK == 0 && ch.row1 % GK == 0);
+  ATE_DASSERT(tl.x >= 0 && tl.y >= tl.x && type >= 0 && type <= 2);
 #if GRAM_DIAG >= 3
   if (type != 0) return;
 #endif
@@ -399,6 +403,7 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
     const int c0 = seg_chunk0[s], c1 = seg_chunk0[s + 1];
     const float* src = slab + rem;
     const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
+    ATE_DASSERT(s < nseg && c0 >= 0 && c0 <= c1 && a >= 0 && a < P && b >= 0 && b < P);
     if (Gx) {                                       // exact mode: int64 limbs
       long long hs = 0, ls = 0;
       int ci = c0;

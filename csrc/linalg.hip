@@ -34,8 +34,10 @@ __global__ __launch_bounds__(1024) void chol_solve_kernel(
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int e = tid; e < k * k; e += nt) {
     int i = e / k, j = e % k;
+    ATE_DASSERT(cols[i] >= 0 && cols[i] < P && cols[j] >= 0 && cols[j] < P);
     L[e] = G[(int64_t)cols[i] * P + cols[j]];
   }
+  ATE_DASSERT(rhs_vec != nullptr || (rcol >= 0 && rcol < P));
   for (int i = tid; i < k; i += nt) {
     b[i] = rhs_vec ? rhs_vec[i] : G[(int64_t)cols[i] * P + rcol];
     al[i] = 0.0;
@@ -166,6 +168,7 @@ __global__ __launch_bounds__(1024) void spd_solve_kernel(const double* __restric
   extern __shared__ double sy[];          // [k]
   __shared__ int bad;
   const int a = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+  ATE_DASSERT(k > 0 && k <= 4096);       // dynamic LDS sy[k]
   const double* Ka = K + (int64_t)a * k * k;
   double* L = work + (int64_t)a * k * k;
   for (int e = tid; e < k * k; e += nt) L[e] = Ka[e];
@@ -247,6 +250,7 @@ template <typename T>
 __global__ void predict_kernel(const T* __restrict__ X, int64_t ld, int64_t n, const int* cols,
                                const double* beta, int k, int ov_idx, double ov_val, int link,
                                double* __restrict__ out) {
+  ATE_DASSERT(k >= 0 && ov_idx < k && ld >= n);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     double eta = linpred(X, ld, cols, beta, k, i, ov_idx, ov_val);
@@ -290,6 +294,7 @@ __global__ void irls_update_kernel(T* __restrict__ X, int64_t ld, int64_t n, con
                                    T* __restrict__ wout, double* __restrict__ dev_partial,
                                    const int* __restrict__ done) {
   if (done && *done) return;
+  ATE_DASSERT(ycol >= 0 && vcol >= 0 && zcol >= 0 && zcol != ycol && zcol != vcol && ld >= n);
   __shared__ double smem[16];
   double dev[1] = {0.0};
   const double eps10 = 10.0 * 2.220446049250313e-16;
@@ -322,6 +327,7 @@ __global__ void irls_check_kernel(const double* __restrict__ dev_partial, int nb
                                   double eps, int maxit, double* __restrict__ state,
                                   int* __restrict__ done) {
   if (*done) return;
+  ATE_DASSERT(nb > 0);
   double dev = 0.0;
   for (int b = 0; b < nb; ++b) dev += dev_partial[b];
   if (first) {

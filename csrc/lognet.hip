@@ -96,11 +96,13 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   const int prob = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint8_t* mk = masks + (int64_t)prob * nseg;
+  ATE_DASSERT(p > 0 && p <= PM && nseg > 0 && nseg <= MAXSEG && ycol >= 0 && L > 0);
 
   if (tid == 0) {
     int acc = 0, k = 0;
     for (int s = 0; s < nseg; ++s)
       if (mk[s]) {
+        ATE_DASSERT(segs[2 * s] >= 0 && segs[2 * s] <= segs[2 * s + 1] && segs[2 * s + 1] <= ld);
         sr0[k] = segs[2 * s];
         spre[k] = acc;
         acc += (int)(segs[2 * s + 1] - segs[2 * s]);
@@ -115,6 +117,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   const int ntr = spre[nts];
   const double w = 1.0 / (double)ntr;
   auto vrow = [&](int v) -> int64_t {
+    ATE_DASSERT(v >= 0 && v < ntr);
     int k = 0;
     while (k + 1 < nts && spre[k + 1] <= v) ++k;
     return sr0[k] + (v - spre[k]);
@@ -521,6 +524,7 @@ __global__ __launch_bounds__(NT) void lognet_cvloss_kernel(
   }
   const int s = hold[k];
   const int64_t r0 = segs[2 * s], r1 = segs[2 * s + 1];
+  ATE_DASSERT(s >= 0 && r0 >= 0 && r0 < r1 && r1 <= ld && m < L);
   const double* b = beta + ((int64_t)k * L + m) * p;
   const double b0 = a0[(int64_t)k * L + m];
   double acc[1] = {0.0};

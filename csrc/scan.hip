@@ -55,6 +55,7 @@ __global__ __launch_bounds__(SNT) void scan_tile_sum_kernel(const T* __restrict_
                                                             T* __restrict__ part) {
   __shared__ T red[SNT / 64];
   const int64_t b0 = (int64_t)blockIdx.x * STILE;
+  ATE_DASSERT(b0 < n || n == 0);
   T s = 0;
 #pragma unroll
   for (int k = 0; k < SPT; ++k) {
@@ -101,6 +102,7 @@ __global__ __launch_bounds__(SNT) void scan_apply_kernel(const T* __restrict__ i
     s += v[k];
   }
   T tot;
+  ATE_DASSERT((int64_t)blockIdx.x * STILE < n || n == 0);
   T run = part[blockIdx.x] + block_excl_scan(s, red, tot);
 #pragma unroll
   for (int k = 0; k < SPT; ++k) {

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(NT) void sel_drop_kernel(const uint8_t* flags, int6
   const int f = i < n ? flags[i] : 0;
   const int r1 = block_scan(f == 1, ws[0]) + cnt[2 * blockIdx.x];
   const int r2 = block_scan(f == 2, ws[1]) + cnt[2 * blockIdx.x + 1];
+  ATE_DASSERT(r1 >= 0 && r2 >= 0 && thr[0] >= 0 && thr[1] >= 0);
   const bool drop = (f == 1 && r1 < thr[0]) || (f == 2 && r2 < thr[1]);
   const int k = i < n && !drop;
   if (i < n) keep[i] = (uint8_t)k;
@@ -122,6 +123,7 @@ __global__ __launch_bounds__(NT) void sel_compact_kernel(const uint8_t* keep, in
   const int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x;
   const int k = i < n ? keep[i] : 0;
   const int pos = block_scan(k, ws) + koff[blockIdx.x];
+  ATE_DASSERT(!k || (pos >= 0 && pos <= i));     // a compaction never moves a row forward
   if (k) out[pos] = i;
 }
 

@@ -320,3 +320,26 @@ def test_causal_forest_auto_uses_exact_splits_at_tutorial_scale():
     assert abs(ate - tau.mean()) < 4 * se + 0.05
     hi, lo = cf.tau_oob[X[:, 0] > 0.5], cf.tau_oob[X[:, 0] < -0.5]
     assert np.nanmean(hi) - np.nanmean(lo) > 0.5
+
+
+def test_aipw_average_effect_clipping_is_a_textbook_option():
+    """grf's estimate_average_effect does not clip W.hat (it warns on poor overlap): the
+    default reproduces that; clip= (compat="textbook" in the estimators) clips W.hat."""
+    import warnings
+    r = np.random.default_rng(2)
+    n = 200
+    W = (r.uniform(size=n) < 0.5).astype(float)
+    Y = r.normal(size=n)
+    w_hat = np.clip(r.uniform(0.2, 0.8, size=n), 0, 1)
+    w_hat[0], W[0] = 1e-9, 1.0                       # one row with (almost) no overlap
+    cf = F.CausalForestFit(None, np.zeros(n), w_hat, np.zeros(n), np.ones(n), Y, W)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        grf_est, _ = F.average_treatment_effect(cf)
+    assert any("overlap" in str(x.message) for x in rec)
+    tb_est, _ = F.average_treatment_effect(cf, clip=1e-6)
+    # the unclipped score of row 0 is (1 - 1e-9) / 1e-9 * Y0 / n: ~1e6 / n
+    assert abs(grf_est - tb_est) > 100 * abs(tb_est)
+    w_c = np.clip(w_hat, 1e-6, 1 - 1e-6)
+    g = (W - w_hat) / (w_c * (1 - w_c)) * Y
+    assert np.isclose(tb_est, g.mean(), rtol=1e-12)

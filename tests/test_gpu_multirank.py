@@ -19,7 +19,7 @@ def _json(out):
 
 def test_two_ranks_on_one_gpu_match_one_process(gpu):
     bench = os.path.join(ROOT, "bench.py")
-    args = ["--steps", "3", "--warmup", "1", "--parity", "0"]
+    args = ["--steps", "3", "--warmup", "1", "--parity", "0", "--also-rct", "0"]
     env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29655",
@@ -69,7 +69,7 @@ def test_exact_mode_two_ranks_on_one_gpu_bitwise(gpu):
     two ranks sharing the GPU gives the SAME BITS as one process holding all rows; the
     default mode agrees with exact mode to rounding."""
     bench = os.path.join(ROOT, "bench.py")
-    args = ["--steps", "2", "--warmup", "1", "--parity", "0", "--exact", "1"]
+    args = ["--steps", "2", "--warmup", "1", "--parity", "0", "--exact", "1", "--also-rct", "0"]
     env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29659",
@@ -102,4 +102,25 @@ def test_cfg3_rf_two_ranks_on_one_gpu_bitwise(gpu):
     assert one.returncode == 0, one.stderr[-3000:]
     ref = _json(one.stdout)
     assert two["world"] == 2 and ref["world"] == 1 and two["trees_this_rank"] == 4
+    assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)
+
+
+def test_cfg4_causal_forest_two_ranks_on_one_gpu_bitwise(gpu):
+    """Config 4 (tools/cfg4.py) with two ranks sharing the GPU (gloo collectives): each rank
+    grows its little bags of the three forests (C05 int64 sums) and evaluates its half of
+    the bootstrap replicates (C07) -> the ATE and the bootstrap SE are the SAME BITS as one
+    process growing every tree and evaluating every replicate."""
+    cfg4 = os.path.join(ROOT, "tools", "cfg4.py")
+    args = ["--rows", "6000", "--trees", "64", "--boot", "100", "--warm", "0"]
+    env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29663",
+                        cfg4, *args], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    two = _json(r.stdout)
+    one = subprocess.run([sys.executable, cfg4, *args], capture_output=True, text=True,
+                         timeout=240)
+    assert one.returncode == 0, one.stderr[-3000:]
+    ref = _json(one.stdout)
+    assert two["world"] == 2 and ref["world"] == 1 and two["causal_trees_this_rank"] == 32
     assert two["ate_hex"] == ref["ate_hex"] and two["se_hex"] == ref["se_hex"], (two, ref)

@@ -59,5 +59,7 @@ def test_debug_build_adds_device_assertions(monkeypatch):
     monkeypatch.setenv("ATE_DEBUG", "0")
     assert not B.debug_enabled()
     # every kernel file with heavy index arithmetic carries checks
-    for f in ("forest_level.hip", "gbdt.hip", "enet.hip", "forest_exact.hip"):
+    for f in ("forest_level.hip", "gbdt.hip", "enet.hip", "forest_exact.hip", "forest.hip",
+              "gram.hip", "linalg.hip", "lognet.hip", "scan.hip", "select.hip", "dml.hip",
+              "dgp.hip"):
         assert "ATE_DASSERT(" in (B.CSRC / f).read_text(), f
