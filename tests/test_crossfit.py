@@ -50,11 +50,11 @@ def test_aipw_crossfit_glm_matches_manual():
 def test_crossfit_and_cf_bootstrap_tree_parallel():
     X, W, Y, _ = _toy(1200, 2)
     a1 = CF.aipw_crossfit(Y, W, X, learner="rf", num_trees=16, device="cpu")
-    b1 = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=50, device="cpu")
+    b1 = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=50, compat="textbook", device="cpu")
 
     def fn(comm):
         return (CF.aipw_crossfit(Y, W, X, learner="rf", num_trees=16, device="cpu", comm=comm),
-                CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=50,
+                CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=50, compat="textbook",
                                            device="cpu", comm=comm))
 
     for a, b in run_simulated(2, fn):          # fixed-point forest sums: the same bits
@@ -100,7 +100,7 @@ def test_cf_bootstrap_checkpoint_resume(tmp_path, monkeypatch):
     from ate_replication_causalml_amd.estimators import linear as L
     from ate_replication_causalml_amd.utils.checkpoint import Checkpoint
     X, W, Y, _ = _toy(800, 5)
-    kw = dict(num_trees=16, nuisance_trees=8, B=60, device="cpu", boot_chunk=20)
+    kw = dict(num_trees=16, nuisance_trees=8, B=60, device="cpu", boot_chunk=20, compat="textbook")
     want = CF.causal_forest_bootstrap(Y, W, X, **kw)
     real = L.bootstrap_replicates
     calls = {"n": 0, "die": 1}
@@ -130,7 +130,7 @@ def test_cf_bootstrap_resume_ranks_agree(tmp_path):
     across ranks), so the run completes and equals the uninterrupted one bit for bit."""
     from ate_replication_causalml_amd.utils.checkpoint import Checkpoint
     X, W, Y, _ = _toy(600, 6)
-    kw = dict(num_trees=16, nuisance_trees=8, B=40, device="cpu", boot_chunk=20)
+    kw = dict(num_trees=16, nuisance_trees=8, B=40, device="cpu", boot_chunk=20, compat="textbook")
 
     def fn(comm):
         ck = Checkpoint(tmp_path, {"cfg": 4})

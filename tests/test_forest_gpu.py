@@ -71,7 +71,7 @@ def test_device_forest_estimators_match_host(gpu, tutorial):
     Y, W, X = m.Y, m.W, m.X
     for f in (lambda d: DF.aipw_rf(Y, W, X, num_trees=60, device=d),
               lambda d: DF.double_ml(Y, W, X, num_trees=40, device=d),
-              lambda d: DF.causal_forest_ate(Y, W, X, num_trees=80, device=d)):
+              lambda d: DF.causal_forest_ate(Y, W, X, num_trees=80, device=d, compat="textbook")):
         a, b = f(gpu), f("cpu")
         assert a.ate == pytest.approx(b.ate, rel=1e-9, abs=1e-12)
         assert a.se == pytest.approx(b.se, rel=1e-9, abs=1e-12)
@@ -89,8 +89,8 @@ def test_crossfit_and_cf_bootstrap_gpu_match_host(gpu):
         g = CF.aipw_crossfit(Yb, W, X, learner=learner, device=gpu, gbdt_kw={"n_trees": 8})
         h = CF.aipw_crossfit(Yb, W, X, learner=learner, device="cpu", gbdt_kw={"n_trees": 8})
         assert g.ate == pytest.approx(h.ate, abs=5e-3) and g.se == pytest.approx(h.se, rel=0.05)
-    c = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64, device=gpu)
-    d = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64, device="cpu")
+    c = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64, compat="textbook", device=gpu)
+    d = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64, compat="textbook", device="cpu")
     assert c.ate == pytest.approx(d.ate, rel=1e-9) and c.se == pytest.approx(d.se, rel=1e-8)
 
 

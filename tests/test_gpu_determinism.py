@@ -28,7 +28,7 @@ def _cases(dev):
         "dml": lambda: lasso.dml_plr_lasso(Yc, W, X, device=dev, graph=False),
         "aipw_rf": lambda: forest.aipw_rf(Yb, W, X, num_trees=40, device=dev, graph=False),
         "causal_forest": lambda: forest.causal_forest_ate(Yc, W, X, num_trees=100, device=dev,
-                                                          graph=False),
+                                                          graph=False, compat="textbook"),
         "residual_balance": lambda: balance.residual_balance(Yc, W, X, device=dev),
     }
 

@@ -33,7 +33,7 @@ CASES = {
     "double_ml": lambda L, X, W, Yc, Yb, dev, g: _forest().double_ml(
         Yb, W, X, num_trees=40, device=dev, graph=g),
     "causal_forest": lambda L, X, W, Yc, Yb, dev, g: _forest().causal_forest_ate(
-        Yc, W, X, num_trees=200, device=dev, graph=g),
+        Yc, W, X, num_trees=200, device=dev, graph=g, compat="textbook"),
     "lasso_single": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_single(
         Yc, W, X, device=dev, graph=g),
     "lasso_usual": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_usual(

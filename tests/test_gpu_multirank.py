@@ -111,7 +111,7 @@ def test_cfg4_causal_forest_two_ranks_on_one_gpu_bitwise(gpu):
     the bootstrap replicates (C07) -> the ATE and the bootstrap SE are the SAME BITS as one
     process growing every tree and evaluating every replicate."""
     cfg4 = os.path.join(ROOT, "tools", "cfg4.py")
-    args = ["--rows", "6000", "--trees", "64", "--boot", "100", "--warm", "0"]
+    args = ["--rows", "6000", "--trees", "64", "--boot", "100", "--warm", "0", "--compat", "textbook"]
     env = dict(os.environ, ATE_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29663",

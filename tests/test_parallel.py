@@ -305,7 +305,7 @@ r = np.random.default_rng(4)
 n = 1200
 X = r.normal(size=(n, 6)); W = (r.uniform(size=n) < 0.4).astype(float)
 Y = X[:, 0] + (1 + (X[:, 1] > 0)) * W + 0.3 * r.normal(size=n)
-b = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=60, device="cpu",
+b = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=60, compat="textbook", device="cpu",
                                comm=c, boot_chunk=25)
 cf = F.causal_forest(X, Y, W, num_trees=24, nuisance_trees=12, seed=12345, backend="cpu", comm=c)
 h = lambda a: __import__("hashlib").sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
@@ -326,7 +326,7 @@ dist.destroy_process_group()
     X = r.normal(size=(n, 6))
     W = (r.uniform(size=n) < 0.4).astype(float)
     Y = X[:, 0] + (1 + (X[:, 1] > 0)) * W + 0.3 * r.normal(size=n)
-    b = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=60,
+    b = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=60, compat="textbook",
                                    device="cpu", boot_chunk=25)
     cf = F.causal_forest(X, Y, W, num_trees=24, nuisance_trees=12, seed=12345, backend="cpu")
     h = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
