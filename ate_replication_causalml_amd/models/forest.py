@@ -496,6 +496,12 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
     return Forest(fp, "cpu", cap, feat, thr, left, val, nnodes, inbag, est, edges, ne, Xbn)
 
 
+def exact_row_order(Xb: torch.Tensor) -> torch.Tensor:
+    """int32 [p][n]: for each feature, the row ids in ascending value-rank order (a stable
+    sort, so ties keep row order; the engines' splits do not depend on the order of ties)."""
+    return torch.argsort(Xb.to(torch.int32), dim=1, stable=True).to(torch.int32).contiguous()
+
+
 def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None,
                      min_node=1, sampling=0, honesty=False, group=1, mtry_poisson=False,
                      alpha=0.0, sample_fraction=0.5, seed=1, tree_offset=0) -> Forest:
@@ -551,7 +557,7 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         nnodes = torch.empty(ntree, dtype=torch.int32, device=dev)
         inbag = torch.empty(ntree * n, dtype=torch.uint8, device=dev)
         est = torch.zeros(ntree * cap * 5, dtype=torch.int64, device=dev) if need_est else None
-        per = _native.hip().ate_forest_exact_scratch_bytes(n, 1)
+        per = _native.hip().ate_forest_exact_scratch_bytes(n, p, 1)
         # trees per launch: two resident per CU, so a launch wants >= 512 of them and as
         # few tails as possible. A 1-GiB scratch cap held 264 trees of 5e4 rows (half the CUs
         # idle, a tail per launch; config 4 2.53 s); when 1 GiB cannot hold the whole forest
@@ -566,11 +572,15 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         chunk = max(1, min(ntree, cap_b // per))
         scratch = torch.empty(per * chunk, dtype=torch.uint8, device=dev)
         Xb = Xb.contiguous()
+        # the forest's rows in value order per feature (a stable sort of the ranks, once per
+        # forest): every tree's large nodes read these lists filtered to their rows instead
+        # of sorting per node (csrc/forest_exact.hip)
+        order = exact_row_order(Xb)
         p_ = lambda a: 0 if a is None else a.data_ptr()
         s = torch.cuda.current_stream().cuda_stream
         for t0 in range(0, ntree, chunk):
             _native.call("ate_forest_fit_exact", ctypes.addressof(fp), t0, min(chunk, ntree - t0),
-                         Xb.data_ptr(), vals.data_ptr(), de.ldv, nval.data_ptr(), p_(yt), p_(r1t),
+                         Xb.data_ptr(), order.data_ptr(), vals.data_ptr(), de.ldv, nval.data_ptr(), p_(yt), p_(r1t),
                          p_(r2t), cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(),
                          val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
                          scratch.data_ptr(), s)

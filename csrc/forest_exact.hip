@@ -10,6 +10,16 @@
 // distinct values, ties broken by (feature slot, position) as on the host.
 //
 // Decomposition: ONE workgroup (8 waves) per tree, level by level.
+//  * nodes of > WCAP rows (the top levels) read presorted per-feature row lists instead of
+//    sorting: the forest's rows are sorted once per feature (host: a stable argsort of the
+//    value ranks, `order` [p][n]); a tree's root list of feature f is that order filtered to
+//    its in-bag rows (one wave per feature, no workgroup barrier), and every split of a
+//    large node stable-partitions each feature's list segment into its children's segments
+//    (double-buffered, one wave per feature), so a large node's rows are in value order for
+//    every feature at all times. The split scan then gathers each row's statistics in list
+//    order: no per-node sort. Ties between equal values never matter (the criterion is only
+//    evaluated between distinct values, at the same positions for any order of ties), so the
+//    trees are the same bits as the sort-based engine and the host twin;
 //  * nodes of <= 512 rows are decided and partitioned by ONE WAVE each, without workgroup
 //    barriers (node j goes to wave j mod 8). <= 64 rows: a row per lane, ranks by 64
 //    lane compares, the sorted order built with ds_permute, prefix sums by lane shuffles;
@@ -53,29 +63,25 @@ constexpr int XW = XT / 64;        // waves per tree
 // 99 KB / 228 VGPRs. On the tutorial's forests (df_mod, 2500 / 4 x 2000 trees) the many
 // trees in flight outweigh the spills and the smaller per-wave node cap: aipw_rf 188 -> 125
 // ms, double_ml 294 -> 177 ms, the same trees (profiles/r03_forest_exact/occupancy_ab.txt).
-#ifndef EXACT_XLDS
-#define EXACT_XLDS 8192        // workgroup-level nodes above this many rows sort in global scratch
-#endif
 #ifndef EXACT_WCAP
 #define EXACT_WCAP 256
 #endif
 #ifndef EXACT_MINWG
 #define EXACT_MINWG 4          // __launch_bounds__ minimum waves per SIMD
 #endif
-constexpr int XLDS = EXACT_XLDS;   // workgroup-level node keys sorted in LDS up to this many rows
 constexpr int WCAP = EXACT_WCAP;   // nodes up to this many rows: one wave each
-// one LDS arena: the workgroup-level key buffer (XLDS keys) or, per wave, WCAP keys and the
-// WCAP per-position statistics (2 x int64) of the wave's node
+// one LDS arena: per wave, WCAP keys and the WCAP per-position statistics (2 x int64) of the
+// wave's node; or (large-node phases) a bit per row: in-bag rows / rows going left
 constexpr int WSLICE = WCAP * 4 + WCAP * 16;
 constexpr int XBIG = 65536 / WCAP + 1;     // > WCAP-row nodes of one level (n <= 65536)
-constexpr int ARENA = (XLDS * 4 > XW * WSLICE) ? XLDS * 4 : XW * WSLICE;
+constexpr int ARENA = (65536 / 8 > XW * WSLICE) ? 65536 / 8 : XW * WSLICE;
 constexpr int XPMAX = 512;         // max features
 
 struct XRng { int lo, hi, id; };
 struct XDec { int split, feat, thr, nl; double val; };
 
 struct XScratch {
-  int64_t* sx0;     // [n] per-position statistics of the workgroup-level node being decided
+  int64_t* sx0;     // [n] per-row statistics of the workgroup-level node being decided
   int64_t* sx1;     // [n]
   int32_t* w;       // [n] bootstrap weights
   int32_t* idx;     // [n] rows of the growing nodes (node = contiguous range)
@@ -84,6 +90,8 @@ struct XScratch {
   XRng* nxt;        // [n + 1]
   XDec* dec;        // [n + 1]
   int32_t* est;     // [n] grf J2 (estimation) rows
+  uint16_t* La;     // [p][n] per-feature row lists of the large nodes (value order), current
+  uint16_t* Lb;     // [p][n] ... and the next level's
 };
 
 __host__ __device__ inline int np2(int n) {
@@ -94,13 +102,13 @@ __host__ __device__ inline int np2(int n) {
 
 __host__ __device__ inline int64_t align16(int64_t b) { return (b + 15) & ~(int64_t)15; }
 
-__host__ __device__ inline int64_t tree_bytes(int n) {
+__host__ __device__ inline int64_t tree_bytes(int n, int p) {
   return align16(8ll * n) * 2 + align16(4ll * n) * 2 + align16(4ll * np2(n)) +
          align16(12ll * (n + 1)) * 2 + align16((int64_t)sizeof(XDec) * (n + 1)) +
-         align16(4ll * n);
+         align16(4ll * n) + align16(2ll * p * n) * 2;
 }
 
-__device__ XScratch scratch_at(char* base, int n) {
+__device__ XScratch scratch_at(char* base, int n, int np_) {
   XScratch s;
   char* p = base;
   s.sx0 = (int64_t*)p; p += align16(8ll * n);
@@ -111,7 +119,9 @@ __device__ XScratch scratch_at(char* base, int n) {
   s.cur = (XRng*)p; p += align16(12ll * (n + 1));
   s.nxt = (XRng*)p; p += align16(12ll * (n + 1));
   s.dec = (XDec*)p; p += align16((int64_t)sizeof(XDec) * (n + 1));
-  s.est = (int32_t*)p;
+  s.est = (int32_t*)p; p += align16(4ll * n);
+  s.La = (uint16_t*)p; p += align16(2ll * np_ * n);
+  s.Lb = (uint16_t*)p;
   return s;
 }
 
@@ -300,14 +310,15 @@ __device__ void wave_bitonic(uint32_t* K, int N2, int lane) {
 }
 
 __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
-    ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const double* __restrict__ vals,
+    ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const int32_t* __restrict__ order,
+    const double* __restrict__ vals,
     int ldv, const int32_t* __restrict__ nval, const uint8_t* __restrict__ ycls,
     const int64_t* __restrict__ r1, const int64_t* __restrict__ r2, int cap,
     int32_t* __restrict__ feat, int32_t* __restrict__ thr, int32_t* __restrict__ left,
     double* __restrict__ val, int32_t* __restrict__ nnodes, uint8_t* __restrict__ inbag,
     int64_t* __restrict__ est_o, char* __restrict__ scratch) {
-  // one LDS key buffer: the whole of it for a workgroup-level node, a quarter (WCAP keys)
-  // per wave for the wave-level nodes (the two phases never overlap)
+  // one LDS arena: a slice (WCAP keys + statistics) per wave for the wave-level nodes, or a
+  // bit per row in the large-node phases (the phases never overlap)
   __shared__ __attribute__((aligned(16))) char sarena[ARENA];
   __shared__ int64_t sw0[XW], sw1[XW];
   __shared__ int sperm[XW][XPMAX];
@@ -320,14 +331,16 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
   const int t = tbeg + blockIdx.x;            // tree within this forest
   const int tg = fp.t0 + t;                   // global tree id (RNG key)
   const int n = fp.n, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  XScratch S = scratch_at(scratch + (int64_t)blockIdx.x * tree_bytes(n), n);
+  XScratch S = scratch_at(scratch + (int64_t)blockIdx.x * tree_bytes(n, fp.p), n, fp.p);
   const int64_t base = (int64_t)t * cap;
   int32_t* tfeat = feat + base;
   int32_t* tthr = thr + base;
   int32_t* tleft = left + base;
   double* tval = val + base;
   uint8_t* inb = inbag + (int64_t)t * n;
-  uint32_t* skeys = (uint32_t*)sarena;
+  uint32_t* sbits = (uint32_t*)sarena;        // large-node phases: one bit per row
+  const uint64_t below = (1ull << lane) - 1ull;
+  auto bit = [&](int i) -> bool { return (sbits[i >> 5] >> (i & 31)) & 1u; };
   char* wsl = sarena + wid * WSLICE;          // this wave's slice: keys, then statistics
   uint32_t* Kw = (uint32_t*)wsl;
   int64_t* Xw0 = (int64_t*)(wsl + WCAP * 4);
@@ -416,6 +429,36 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     sncur = 1;
     snext_id = 1;
   }
+  // ---- presorted root lists: feature f's rows in value order = the forest-wide order of f
+  // filtered to this tree's in-bag rows (a bit per row in LDS); one wave per feature
+  if (m > WCAP) {
+    for (int e = tid; e < (n + 31) / 32; e += XT) sbits[e] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += XT)
+      if (S.w[i] > 0) atomicOr(&sbits[i >> 5], 1u << (i & 31));
+    __syncthreads();
+    for (int f = wid; f < fp.p; f += XW) {
+      const int32_t* of = order + (int64_t)f * n;
+      uint16_t* Lf = S.La + (int64_t)f * n;
+      int c = 0;
+      for (int c0 = 0; c0 < n; c0 += 64 * 8) {
+        int rv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = c0 + u * 64 + lane;
+          rv[u] = q < n ? of[q] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool keep = c0 + u * 64 + lane < n && bit(rv[u]);
+          const uint64_t b = __ballot(keep);
+          if (keep) Lf[c + __popcll(b & below)] = (uint16_t)rv[u];
+          c += __popcll(b);
+        }
+      }
+      ATE_DASSERT(c == m);
+    }
+  }
   __syncthreads();
 #ifdef EXACT_PROF
   unsigned long long tp = wall_clock64();
@@ -502,9 +545,7 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
 #endif
       const int nf = scnt[XW];
       const int minc = min_child(fp, (double)st.nw);
-      const int N2 = np2(cnt);
-      uint32_t* K = N2 <= XLDS ? skeys : S.keys;
-      // per-position statistics once per node (the feature loop reads them by sorted key)
+      // per-row statistics once per node (the feature loop gathers them in list order)
       int64_t srho = 0, stre = 0;
       for (int qb = tid; qb < cnt; qb += XT * 8) {
         int iv[8];
@@ -515,8 +556,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           if (qb + u * XT < cnt) {
             int64_t x0, x1;
             row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
-            S.sx0[nd.lo + qb + u * XT] = x0;
-            S.sx1[nd.lo + qb + u * XT] = x1;
+            S.sx0[iv[u]] = x0;
+            S.sx1[iv[u]] = x1;
             srho += x1;
             stre += x0 >> 32;
           }
@@ -527,78 +568,28 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         __syncthreads();
         st.s1 = 0; st.ntreat = 0;
         for (int q = 0; q < XW; ++q) { st.s1 += sred64[0][q]; st.ntreat += sred64[1][q]; }
-        __syncthreads();
       }
+      __syncthreads();                        // the statistics are read by other threads
+      XSUB(17);
       double best = -INFINITY;                // thread 0's running best over features
       int bf = -1, blo = -1, bhi = -1, bnl = 0;
+      // thread tid owns list positions [s0, s1) of the node's segment
+      const int ch = (cnt + XT - 1) / XT;
+      const int s0 = min(cnt, tid * ch), s1 = min(cnt, s0 + ch);
       for (int k = 0; k < nf; ++k) {
         const int f = sperm[0][k];
         const uint16_t* xf = Xb + (int64_t)f * n;
-        // 8 positions per batch: their row ids, then the bins, then the key stores (the
-        // loads of a batch are in flight together)
-        for (int sb = tid; sb < N2; sb += XT * 8) {
-          int iv[8];
-          uint32_t bv[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) iv[u] = sb + u * XT < cnt ? S.idx[nd.lo + sb + u * XT] : 0;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) bv[u] = sb + u * XT < cnt ? (uint32_t)xf[iv[u]] : 0u;
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int s = sb + u * XT;
-            if (s < N2) K[s] = s < cnt ? ((bv[u] << 16) | (uint32_t)s) : 0xFFFFFFFFu;
-          }
-        }
-        __syncthreads();
-        XSUB(17);
-        // bitonic sort, ascending. In LDS, wave w owns the contiguous chunk [w C, (w+1) C):
-        // stages with partner distance jj < C stay inside a chunk and need only the wave's
-        // own ordering (no workgroup barrier); the few with jj >= C run workgroup-wide.
-        const int C = N2 / XW;
-        const bool local = K == skeys && C >= 64;
-        for (int kk = 2; kk <= N2; kk <<= 1) {
-          int jj = kk >> 1;
-          for (; jj > 0 && (!local || jj >= C); jj >>= 1) {
-            for (int s = tid; s < N2; s += XT) {
-              const int o = s ^ jj;
-              if (o > s) {
-                const uint32_t x = K[s], y = K[o];
-                const bool up = (s & kk) == 0;
-                if ((x > y) == up) { K[s] = y; K[o] = x; }
-              }
-            }
-            __syncthreads();
-          }
-          for (; jj > 0; jj >>= 1) {            // local stages (only when `local`)
-            for (int s = wid * C + lane; s < (wid + 1) * C; s += 64) {
-              const int o = s ^ jj;
-              if (o > s) {
-                const uint32_t x = K[s], y = K[o];
-                const bool up = (s & kk) == 0;
-                if ((x > y) == up) { K[s] = y; K[o] = x; }
-              }
-            }
-            wave_sync();
-          }
-          if (local && kk >= C) __syncthreads();   // the next stage may cross chunks
-        }
-        __syncthreads();
-        XSUB(18);
-        // chunked prefix sums: thread tid owns positions [s0, s1)
-        const int ch = (cnt + XT - 1) / XT;
-        const int s0 = min(cnt, tid * ch), s1 = min(cnt, s0 + ch);
-        const int64_t* g0 = S.sx0 + nd.lo;
-        const int64_t* g1 = S.sx1 + nd.lo;
+        const uint16_t* Lf = S.La + (int64_t)f * n + nd.lo;    // the node's rows, value order
         int64_t l0 = 0, l1 = 0;
         for (int sb = s0; sb < s1; sb += 8) {
-          int qv[8];
+          int rv[8];
           int64_t a0[8], a1[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) qv[u] = sb + u < s1 ? (int)(K[sb + u] & 0xFFFFu) : 0;
+          for (int u = 0; u < 8; ++u) rv[u] = sb + u < s1 ? (int)Lf[sb + u] : 0;
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            a0[u] = sb + u < s1 ? g0[qv[u]] : 0;
-            a1[u] = sb + u < s1 ? g1[qv[u]] : 0;
+            a0[u] = sb + u < s1 ? S.sx0[rv[u]] : 0;
+            a1[u] = sb + u < s1 ? S.sx1[rv[u]] : 0;
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) { l0 += a0[u]; l1 += a1[u]; }
@@ -611,24 +602,26 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         double bc = -INFINITY;
         int bs = 0x7FFFFFFF;
         for (int sb = s0; sb < s1; sb += 8) {
-          uint32_t kv[9];
+          int rv[9];
+          uint32_t bv[9];
           int64_t a0[8], a1[8];
 #pragma unroll
-          for (int u = 0; u < 9; ++u) kv[u] = sb + u < cnt ? K[sb + u] : 0xFFFFFFFFu;
+          for (int u = 0; u < 9; ++u) rv[u] = sb + u < cnt ? (int)Lf[sb + u] : 0;
+#pragma unroll
+          for (int u = 0; u < 9; ++u) bv[u] = sb + u < cnt ? (uint32_t)xf[rv[u]] : 0xFFFFFFFFu;
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int q = (int)(kv[u] & 0xFFFFu);
-            a0[u] = sb + u < s1 ? g0[q] : 0;
-            a1[u] = sb + u < s1 ? g1[q] : 0;
+            a0[u] = sb + u < s1 ? S.sx0[rv[u]] : 0;
+            a1[u] = sb + u < s1 ? S.sx1[rv[u]] : 0;
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int s = sb + u;
-            if (s >= s1) break;
+            const int s_ = sb + u;
+            if (s_ >= s1) break;
             p0 += a0[u]; p1 += a1[u];
-            if (s + 1 < cnt && (kv[u] >> 16) != (kv[u + 1] >> 16)) {
+            if (s_ + 1 < cnt && bv[u] != bv[u + 1]) {
               const double cr = boundary_crit(fp, st, minc, p0, p1);
-              if (cr > bc) { bc = cr; bs = s; }
+              if (cr > bc) { bc = cr; bs = s_; }
             }
           }
         }
@@ -642,12 +635,13 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           if (c2 > best) {
             best = c2;
             bf = f;
-            blo = (int)(K[s2] >> 16);
-            bhi = (int)(K[s2 + 1] >> 16);
+            ATE_DASSERT(s2 >= 0 && s2 + 1 < cnt);
+            blo = (int)xf[Lf[s2]];
+            bhi = (int)xf[Lf[s2 + 1]];
             bnl = s2 + 1;
           }
         }
-        __syncthreads();                      // K, sw*, sred* reused by the next feature
+        __syncthreads();                      // sw*, sred* reused by the next feature
         XSUB(19);
       }
       if (tid == 0) {
@@ -921,15 +915,47 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           if (w < wid) { ol += scnt[w]; orr += sreds[w]; }
           tl += scnt[w]; tr += sreds[w];
         }
-        const uint64_t below = (1ull << lane) - 1ull;
         ATE_DASSERT(!in || (l ? ol + __popcll(bl & below) < d.nl
                              : orr + __popcll(br & below) < cnt));
-        if (in) S.keys[nd.lo + (l ? ol + __popcll(bl & below) : orr + __popcll(br & below))] = (uint32_t)i;
+        if (in) {
+          S.keys[nd.lo + (l ? ol + __popcll(bl & below) : orr + __popcll(br & below))] = (uint32_t)i;
+          // the row's side, for the list partitions below
+          if (l) atomicOr(&sbits[i >> 5], 1u << (i & 31));
+          else atomicAnd(&sbits[i >> 5], ~(1u << (i & 31)));
+        }
         lo_l += tl; lo_r += tr;
         __syncthreads();
       }
       for (int q = tid; q < cnt; q += XT) S.idx[nd.lo + q] = (int32_t)S.keys[nd.lo + q];
       __syncthreads();
+      // every feature's value-ordered list of the node, stable-partitioned into its children's
+      // segments of the next level's lists (one wave per feature); only large children read them
+      if (d.nl > WCAP || cnt - d.nl > WCAP) {
+        for (int f = wid; f < fp.p; f += XW) {
+          const uint16_t* src = S.La + (int64_t)f * n + nd.lo;
+          uint16_t* dst = S.Lb + (int64_t)f * n + nd.lo;
+          int ol = 0, orr = d.nl;
+          for (int c0 = 0; c0 < cnt; c0 += 64 * 8) {
+            int rv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int q = c0 + u * 64 + lane;
+              rv[u] = q < cnt ? (int)src[q] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const bool in = c0 + u * 64 + lane < cnt;
+              const bool l = in && bit(rv[u]);
+              const uint64_t bl = __ballot(l), br = __ballot(in && !l);
+              if (in) dst[l ? ol + __popcll(bl & below) : orr + __popcll(br & below)] = (uint16_t)rv[u];
+              ol += __popcll(bl);
+              orr += __popcll(br);
+            }
+          }
+          ATE_DASSERT(ol == d.nl && orr == cnt);
+        }
+        __syncthreads();
+      }
     }
     XPHASE(5);
     {                                          // wave-level nodes, staged in the wave's LDS
@@ -941,7 +967,6 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         if (!d.split) continue;
         const uint16_t* xf = Xb + (int64_t)d.feat * n;
         int lo_l = 0, lo_r = d.nl;
-        const uint64_t below = (1ull << lane) - 1ull;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
           const int q = c0 + lane;
           const bool in = q < cnt;
@@ -964,6 +989,9 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       XRng* tmp = S.cur;
       S.cur = S.nxt;
       S.nxt = tmp;
+      uint16_t* tl = S.La;                    // ... and the partitioned row lists the current
+      S.La = S.Lb;
+      S.Lb = tl;
     }
     __syncthreads();
   }
@@ -1003,14 +1031,14 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
 
 }  // namespace
 
-ATE_API int64_t ate_forest_exact_scratch_bytes(int n, int ntree) {
-  return tree_bytes(n) * (int64_t)ntree;
+ATE_API int64_t ate_forest_exact_scratch_bytes(int n, int p, int ntree) {
+  return tree_bytes(n, p) * (int64_t)ntree;
 }
 
 // Grow trees [tbeg, tbeg + ntree_chunk) of the forest (scratch: ntree_chunk trees).
 // grf sampling (fp.sampling == 1, kinds 1/2) needs est ([ntree * cap][5] int64).
 ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, const void* Xb,
-                                 const void* vals, int ldv, const void* nval, const void* ycls,
+                                 const void* order, const void* vals, int ldv, const void* nval, const void* ycls,
                                  const void* r1, const void* r2, int cap, void* feat, void* thr,
                                  void* left, void* val, void* nnodes, void* inbag, void* est,
                                  void* scratch, void* stream) {
@@ -1019,7 +1047,7 @@ ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, const vo
   if (fp.sampling == 0 ? fp.kind == 2 : (fp.kind == 0 || !est || (fp.kind == 2 && !r2))) return -1;
   if (tbeg < 0 || nchunk < 1 || tbeg + nchunk > fp.ntree) return -1;
   hipLaunchKernelGGL(forest_exact_kernel, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
-                     (const uint16_t*)Xb, (const double*)vals, ldv, (const int32_t*)nval,
+                     (const uint16_t*)Xb, (const int32_t*)order, (const double*)vals, ldv, (const int32_t*)nval,
                      (const uint8_t*)ycls, (const int64_t*)r1, (const int64_t*)r2, cap,
                      (int32_t*)feat, (int32_t*)thr, (int32_t*)left, (double*)val, (int32_t*)nnodes,
                      (uint8_t*)inbag, (int64_t*)est, (char*)scratch);

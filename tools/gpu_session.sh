@@ -15,6 +15,7 @@
 #   enet_ab:A,B,.. CV-LASSO stage alone for libatehip_<A>.so, ... ("new" = in-tree), x2
 #   enet_prof      cycle accounting of the path kernel (tools/enet_profile.py build)
 #   gram_ab:A,B,.. the bf16 Gram tile kernel alone (tools/gram_only.py) per library, x2
+#   cfg4           config 4 (tools/cfg4.py): one GPU, then rank 0 of 8 alone; cfg4phases: phase timing
 #   cfg3           config-3 per-GPU shard (N=1e7, p=500, 100 trees, rank 0 of 8)
 #   cfg5           config-5 per-GPU shard (N=1.25e7, p=2000, 100 trees); cfg5c: concurrent Y/W fits
 #   cfg5small      a small config-5 shard, concurrent then serial Y/W fits
@@ -83,6 +84,11 @@ for step in "$@"; do
       done ;;
     enet_prof)
       run enet_prof 300 python tools/enet_profile.py ;;
+    cfg4)        # config 4 on one GPU (all trees, all replicates) and rank 0's share of 8
+      run cfg4 300 python -u tools/cfg4.py --rows 50000 && \
+      run cfg4_shard 300 python -u tools/cfg4.py --rows 50000 --shard 0/8 ;;
+    cfg4phases)
+      run cfg4phases 300 python -u tools/cfg4_phases.py ;;
     cfg3)
       run cfg3 300 python -u tools/cfg3.py --rows 10000000 --cols 500 --trees 100 --shard 0/8 ;;
     cfg5)
