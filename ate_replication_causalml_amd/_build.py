@@ -113,10 +113,12 @@ def build_cpu(verbose: bool = False) -> Path:
 
 
 def build_all(verbose: bool = False):
-    """The production kernel library and the host library; with ATE_DEBUG=1 also the
-    device-assertion kernel library."""
+    """The production kernel library, the host library and the device-assertion kernel
+    library (_lib/libatehip_debug.so, loaded with ATE_DEBUG=1): both kernel libraries are
+    rebuilt from the same sources, so the debug build is never older than the production
+    one (ATE_NO_DEBUG_BUILD=1 skips it)."""
     out = (build_hip(verbose, debug=False), build_cpu(verbose))
-    if debug_enabled():
+    if os.environ.get("ATE_NO_DEBUG_BUILD", "0") in ("", "0"):
         build_hip(verbose, debug=True)
     return out
 

@@ -92,8 +92,9 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
     sel = None
     if dgp == "tutorial":
         from .panel_selection import kept_gids, plan_selection
+        pcomm = None if getattr(comm, "emulated", False) else comm   # --shard r/W: plan alone
         sel = selection if selection is not None else plan_selection(
-            n_total, seed, params, comm=comm, device=pan.data.device, compat=compat)
+            n_total, seed, params, comm=pcomm, device=pan.data.device, compat=compat)
         if sel.n_keep != n_total or sel.seed != seed:
             raise ValueError("selection plan does not match (n_total, seed)")
         gids = kept_gids(sel, slices, device=pan.data.device)

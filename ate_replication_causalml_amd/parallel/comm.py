@@ -63,6 +63,8 @@ class EmulatedComm(LocalComm):
     values are those of the shard, not of the world-W result: a timing of one GPU's share
     of the job, not a way to compute it."""
 
+    emulated = True       # its collectives do not communicate (data/panel_selection plans alone)
+
     def __init__(self, rank: int, world: int):
         if not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside a world of {world}")

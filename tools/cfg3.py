@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--forest-seed", type=int, default=1991)
     ap.add_argument("--shard", default=None)
+    ap.add_argument("--dgp", default="tutorial", choices=["tutorial", "rct", "tutorial-rct"],
+                    help="tutorial: the selection-biased df_mod at scale (N = rows kept)")
     ap.add_argument("--serial", action="store_true", help="grow the 15 forests one at a time")
     ap.add_argument("--checkpoint", default=None, help="directory: per-rank local vote sums")
     a = ap.parse_args()
@@ -48,7 +50,8 @@ def main():
     torch.cuda.set_device(C.local_device())
     dev = torch.device("cuda", torch.cuda.current_device())
     t0 = time.perf_counter()
-    pan = synthetic_panel(n, p=a.cols, folds=a.folds, seed=a.seed, dtype="bf16", device=dev)
+    pan = synthetic_panel(n, p=a.cols, folds=a.folds, seed=a.seed, dtype="bf16", device=dev,
+                          dgp=a.dgp)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     ck = None
@@ -72,7 +75,8 @@ def main():
             "config": 3, "estimator": "AIPW 5-fold cross-fit, RF nuisances (e, mu1, mu0), HBM panel",
             "rows": n, "p": a.cols, "trees_per_forest": a.trees,
             "trees_this_rank": r.diagnostics.get("trees_this_device"), "world": world,
-            "shard": a.shard, "serial": a.serial, "seconds": float(el.item()),
+            "shard": a.shard, "serial": a.serial, "dgp": a.dgp,
+            "rows_generated": int(pan.n_generated), "seconds": float(el.item()),
             "generate_s": t_gen, "rows_per_s": n / float(el.item()), "ate": r.ate, "se": r.se,
             "ate_hex": float(r.ate).hex(), "se_hex": float(r.se).hex()}), flush=True)
     if world > 1:

@@ -23,37 +23,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import ate_replication_causalml_amd  # noqa: E402,F401  (HIP queue default before torch's init)
 
 
-class _ShardComm:
-    """Rank r of W with identity collectives (--shard: one rank's work, timing only)."""
-    capturable = True
-
-    def __init__(self, rank, world):
-        self.rank, self.world_size = rank, world
-
-    def all_reduce_(self, t):
-        return t
-
-    all_reduce_max_ = all_reduce_min_ = all_reduce_
-
-    def all_gather(self, t):
-        return [t] * self.world_size
-
-    def all_gather_into_(self, out, t):
-        out.copy_(t.reshape(-1).repeat(self.world_size).reshape(out.shape))
-        return out
-
-    def reduce_scatter_(self, out, t):
-        n = out.numel()
-        out.copy_(t.reshape(-1)[self.rank * n:(self.rank + 1) * n].reshape(out.shape))
-        return out
-
-    def barrier(self):
-        pass
-
-    def dup(self):
-        return self
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=float, default=1e6)
@@ -63,6 +32,8 @@ def main():
     ap.add_argument("--folds", type=int, default=5)
     ap.add_argument("--seed", type=int, default=13)
     ap.add_argument("--shard", default=None)
+    ap.add_argument("--dgp", default="tutorial", choices=["tutorial", "rct", "tutorial-rct"],
+                    help="tutorial: the selection-biased df_mod at scale (N = rows kept)")
     ap.add_argument("--checkpoint", default=None, help="directory: per-fold held-out predictions")
     ap.add_argument("--concurrent", action="store_true",
                     help="fit a fold's E[Y|X] and E[W|X] side by side on two streams "
@@ -76,7 +47,7 @@ def main():
     n = int(a.rows)
     if a.shard:
         r, w = (int(v) for v in a.shard.split("/"))
-        comm = _ShardComm(r, w)
+        comm = C.EmulatedComm(r, w)
     else:
         comm = C.from_env()
     rank, world = comm.rank, comm.world_size
@@ -84,7 +55,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     t0 = time.perf_counter()
     pan = synthetic_panel(n, p=a.cols, folds=a.folds, seed=a.seed, dtype="bf16", device=dev,
-                          rank=rank, world=world)
+                          rank=rank, world=world, dgp=a.dgp, comm=comm if world > 1 else None)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     dist = DistContext(comm, 0, n) if world > 1 or a.shard else None
@@ -107,7 +78,8 @@ def main():
         print(json.dumps({
             "config": 5, "estimator": "DML-PLR 5-fold, GBDT nuisances (E[Y|X], E[W|X]), HBM panel",
             "rows_total": n, "rows_this_rank": pan.n, "p": a.cols, "trees": a.trees,
-            "depth": a.depth, "world": world, "shard": a.shard, "concurrent": a.concurrent, "seconds": float(el.item()),
+            "depth": a.depth, "world": world, "shard": a.shard, "dgp": a.dgp,
+            "rows_generated": int(pan.n_generated), "concurrent": a.concurrent, "seconds": float(el.item()),
             "generate_s": t_gen, "rows_per_s": n / float(el.item()), "ate": r.ate, "se": r.se,
             "ate_hex": float(r.ate).hex(), "se_hex": float(r.se).hex()}), flush=True)
     if world > 1 and not a.shard:

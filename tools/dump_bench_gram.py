@@ -19,7 +19,8 @@ from ate_replication_causalml_amd.ops.gram import gram  # noqa: E402
 out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/gram_dump"
 os.makedirs(out, exist_ok=True)
 dev = torch.device("cuda", 0)
-pan = synthetic_panel(int(1e7), p=500, folds=5, seed=1991, dtype="bf16", device=dev)
+pan = synthetic_panel(int(1e7), p=500, folds=5, seed=1991, dtype="bf16", device=dev,
+                      dgp=os.environ.get("ATE_DGP", "tutorial"))
 G = gram(pan).double().cpu().numpy()
 np.save(os.path.join(out, "G.npy"), G)
 meta = {"xcols": [int(c) for c in pan.xcols], "Y": int(pan.cols["Y"]), "W": int(pan.cols["W"]),

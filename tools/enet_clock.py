@@ -26,7 +26,7 @@ def main():
     lib = _native.hip()
     lib.ate_enet_prof_read.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
-    pan = synthetic_panel(10_000_000, p=500, folds=5, seed=1991, dtype="bf16", device=dev)
+    pan = synthetic_panel(10_000_000, p=500, folds=5, seed=1991, dtype="bf16", device=dev, dgp=os.environ.get("ATE_DGP", "tutorial"))
     Gs = G.gram(pan)
     torch.cuda.synchronize()
     from ate_replication_causalml_amd.ops.enet import cv_enet_gaussian

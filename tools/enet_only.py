@@ -13,7 +13,8 @@ from ate_replication_causalml_amd.ops.gram import gram  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 dev = torch.device("cuda", 0)
-pan = synthetic_panel(int(1e7), p=500, folds=5, seed=1991, dtype="bf16", device=dev)
+pan = synthetic_panel(int(1e7), p=500, folds=5, seed=1991, dtype="bf16", device=dev,
+                      dgp=os.environ.get("ATE_DGP", "tutorial"))
 G = gram(pan).clone()
 K = 5
 full_sets = [[s for s in range(K) if s != k] for k in range(K)]

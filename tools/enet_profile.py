@@ -41,7 +41,7 @@ def run(n, p):
     lib = _native.hip()
     lib.ate_enet_prof_read.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
-    pan = synthetic_panel(n, p=p, folds=5, seed=1991, dtype="bf16", device=dev)
+    pan = synthetic_panel(n, p=p, folds=5, seed=1991, dtype="bf16", device=dev, dgp=os.environ.get("ATE_DGP", "tutorial"))
     dml_crossfit_panel(pan, 5, "min")
     torch.cuda.synchronize()
     lib.ate_enet_prof_reset()

@@ -59,7 +59,7 @@ for step in "$@"; do
       run bench 300 python bench.py ;;
     prof)
       ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 \
+          -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --also-rct 0 \
           > "$ROOT/$OUT/prof.log" 2>&1 ) || { echo "[prof] failed"; tail -20 "$OUT/prof.log"; exit 1; }
       python3 -c "import sys; sys.path.insert(0, 'tools'); import timeline; timeline.overlapped(sys.argv[1], 24)" \
           $(find "$OUT/prof" -name "*kernel_trace.csv") > "$OUT/prof_timeline.txt" 2>&1 || true
@@ -89,6 +89,8 @@ for step in "$@"; do
       run cfg4_shard 300 python -u tools/cfg4.py --rows 50000 --shard 0/8 ;;
     cfg4phases)
       run cfg4phases 300 python -u tools/cfg4_phases.py ;;
+    xprof)       # phase ticks of one exact-split grf causal tree (tools/exact_forest_prof.py --build first)
+      run xprof 200 python -u tools/exact_forest_prof.py --causal ;;
     cfg3)
       run cfg3 300 python -u tools/cfg3.py --rows 10000000 --cols 500 --trees 100 --shard 0/8 ;;
     cfg5)
@@ -118,7 +120,7 @@ for step in "$@"; do
     single)      # kernel trace of bench.py: the last single-fit replay's critical path
       ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
           -d "$ROOT/$OUT/single" -o single -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 \
-          --parity 0 > "$ROOT/$OUT/single_run.log" 2>&1 ) || { echo "[single] failed"; tail -20 "$OUT/single_run.log"; exit 1; }
+          --parity 0 --also-rct 0 --dgp "${ATE_DGP:-tutorial}" > "$ROOT/$OUT/single_run.log" 2>&1 ) || { echo "[single] failed"; tail -20 "$OUT/single_run.log"; exit 1; }
       python3 tools/single_fit_timeline.py $(find "$OUT/single" -name "*kernel_trace.csv") \
           > "$OUT/single_timeline.txt" 2>&1
       echo "[single] ok: $(tail -14 "$OUT/single_timeline.txt")" ;;
@@ -129,7 +131,7 @@ for step in "$@"; do
         lib=ate_replication_causalml_amd/_lib/libatehip_$nm.so
         [ "$nm" = new ] && lib=ate_replication_causalml_amd/_lib/libatehip.so
         ( cd /tmp && ATE_HIP_LIB=$ROOT/$lib timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
-            -d "$ROOT/$OUT/kt_$nm" -o kt -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --parity 0 \
+            -d "$ROOT/$OUT/kt_$nm" -o kt -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --parity 0 --also-rct 0 \
             > "$ROOT/$OUT/kt_$nm.log" 2>&1 ) || { echo "[kt_$nm] failed"; tail -20 "$OUT/kt_$nm.log"; exit 1; }
         python3 -c "
 import csv, re, sys, statistics as st

@@ -12,7 +12,8 @@ from ate_replication_causalml_amd.ops import gram as gram_mod  # noqa: E402
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e7)
 variants = sys.argv[2:] or [gram_mod.GRAM_KERNEL]
 pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.device("cuda", 0),
-                      blocked=os.environ.get("ATE_BLOCKED", "1") == "1")
+                      blocked=os.environ.get("ATE_BLOCKED", "1") == "1",
+                      dgp=os.environ.get("ATE_DGP", "tutorial"))
 ref = None
 stage = os.environ.get("ATE_GRAM_STAGE", "all")   # "tiles": the tile kernel alone (no slab reduce)
 for v in variants:

@@ -25,7 +25,7 @@ def main():
     from ate_replication_causalml_amd.ops.gram import gram
     dev = torch.device("cuda:0")
     pan = synthetic_panel(int(args.n), p=args.p, folds=args.folds, seed=1991, dtype=args.dtype,
-                          device=dev)
+                          device=dev, dgp=os.environ.get("ATE_DGP", "tutorial"))
     K = args.folds
     full_sets = [[s for s in range(K) if s != k] for k in range(K)]
     ycols = [pan.cols["Y"], pan.cols["W"]]
