@@ -4,30 +4,28 @@
 //
 // Bins are uint16 ranks of each feature's distinct values, so a split can fall between ANY
 // two consecutive distinct in-node values (the binned engine, csrc/forest.hip, quantises
-// to <= 256 bins). Split search is sort-based instead of histogram-based: a node's rows
-// are sorted by (bin, position) for each candidate feature and the integer statistics are
-// prefix-summed in that order; the criterion is evaluated at every boundary between two
-// distinct values, ties broken by (feature slot, position) as on the host.
+// to <= 256 bins). Split search walks each candidate feature's rows of the node in value
+// order, prefix-summing the integer statistics; the criterion is evaluated at every
+// boundary between two distinct values, ties broken by (feature slot, position) as on the
+// host.
+//
+// No node is sorted. The forest's rows are sorted once per feature (host: a stable argsort
+// of the value ranks, `order` [p][n]); a tree's root list of feature f is that order
+// filtered to its in-bag rows (one wave per feature), and every split stable-partitions each
+// feature's list segment into its children's segments of the next level's lists (double-
+// buffered [p][n] uint16 row ids), so every node's rows are in value order for every feature
+// at all times. Ties between equal values never matter (the criterion is only evaluated
+// between distinct values, at the same positions for any order of ties): the trees are the
+// same bits as a sort per node and as the host twin.
 //
 // Decomposition: ONE workgroup (8 waves) per tree, level by level.
-//  * nodes of > WCAP rows (the top levels) read presorted per-feature row lists instead of
-//    sorting: the forest's rows are sorted once per feature (host: a stable argsort of the
-//    value ranks, `order` [p][n]); a tree's root list of feature f is that order filtered to
-//    its in-bag rows (one wave per feature, no workgroup barrier), and every split of a
-//    large node stable-partitions each feature's list segment into its children's segments
-//    (double-buffered, one wave per feature), so a large node's rows are in value order for
-//    every feature at all times. The split scan then gathers each row's statistics in list
-//    order: no per-node sort. Ties between equal values never matter (the criterion is only
-//    evaluated between distinct values, at the same positions for any order of ties), so the
-//    trees are the same bits as the sort-based engine and the host twin;
-//  * nodes of <= 512 rows are decided and partitioned by ONE WAVE each, without workgroup
-//    barriers (node j goes to wave j mod 8). <= 64 rows: a row per lane, ranks by 64
-//    lane compares, the sorted order built with ds_permute, prefix sums by lane shuffles;
-//    65..512 rows: a wave-synchronous bitonic sort of the 32-bit keys in the wave's LDS
-//    slice, the per-position statistics staged beside them, chunk sums and a wave scan;
-//  * larger nodes are decided by the whole workgroup, one at a time: a bitonic sort in LDS
-//    (<= 16384 rows) or in the tree's global scratch, chunked prefix sums with a workgroup
-//    scan, an argmax reduction;
+//  * nodes of <= WCAP (256) rows are decided and partitioned by ONE WAVE each, without
+//    workgroup barriers (node j goes to wave j mod 8): lane l owns list positions
+//    [l ch, l ch + ch), ch <= 4; the rows' statistics are gathered by row id, summed by a
+//    wave scan, and the partition moves four features' segments per batch;
+//  * larger nodes are decided by the whole workgroup, one at a time: per feature a chunk of
+//    list positions per thread, a workgroup scan of the chunk sums, an argmax reduction; their
+//    partitions run one wave per feature, the rows' sides in an LDS bit per row;
 //  * child ids are assigned after the level in list order (a workgroup scan of the split
 //    flags), so numbering equals the host engine's.
 // randomForest sampling (bootstrap; kinds 0/1, midpoint thresholds) and grf sampling (half-
@@ -70,9 +68,9 @@ constexpr int XW = XT / 64;        // waves per tree
 #define EXACT_MINWG 4          // __launch_bounds__ minimum waves per SIMD
 #endif
 constexpr int WCAP = EXACT_WCAP;   // nodes up to this many rows: one wave each
-// one LDS arena: per wave, WCAP keys and the WCAP per-position statistics (2 x int64) of the
-// wave's node; or (large-node phases) a bit per row: in-bag rows / rows going left
-constexpr int WSLICE = WCAP * 4 + WCAP * 16;
+// one LDS arena: per wave, a wave-level node's partition staging (WCAP row ids); or
+// (large-node phases) a bit per row: in-bag rows / rows going left
+constexpr int WSLICE = WCAP * 4;   // a wave-level node's partition staging (row ids)
 constexpr int XBIG = 65536 / WCAP + 1;     // > WCAP-row nodes of one level (n <= 65536)
 constexpr int ARENA = (65536 / 8 > XW * WSLICE) ? 65536 / 8 : XW * WSLICE;
 constexpr int XPMAX = 512;         // max features
@@ -90,8 +88,9 @@ struct XScratch {
   XRng* nxt;        // [n + 1]
   XDec* dec;        // [n + 1]
   int32_t* est;     // [n] grf J2 (estimation) rows
-  uint16_t* La;     // [p][n] per-feature row lists of the large nodes (value order), current
+  uint16_t* La;     // [p][n] per-feature row lists of every node (value order), current
   uint16_t* Lb;     // [p][n] ... and the next level's
+  uint8_t* side;    // [n] the side (1 = left) of every row of a splitting wave-level node
 };
 
 __host__ __device__ inline int np2(int n) {
@@ -105,7 +104,7 @@ __host__ __device__ inline int64_t align16(int64_t b) { return (b + 15) & ~(int6
 __host__ __device__ inline int64_t tree_bytes(int n, int p) {
   return align16(8ll * n) * 2 + align16(4ll * n) * 2 + align16(4ll * np2(n)) +
          align16(12ll * (n + 1)) * 2 + align16((int64_t)sizeof(XDec) * (n + 1)) +
-         align16(4ll * n) + align16(2ll * p * n) * 2;
+         align16(4ll * n) + align16(2ll * p * n) * 2 + align16(n);
 }
 
 __device__ XScratch scratch_at(char* base, int n, int np_) {
@@ -121,7 +120,8 @@ __device__ XScratch scratch_at(char* base, int n, int np_) {
   s.dec = (XDec*)p; p += align16((int64_t)sizeof(XDec) * (n + 1));
   s.est = (int32_t*)p; p += align16(4ll * n);
   s.La = (uint16_t*)p; p += align16(2ll * np_ * n);
-  s.Lb = (uint16_t*)p;
+  s.Lb = (uint16_t*)p; p += align16(2ll * np_ * n);
+  s.side = (uint8_t*)p;
   return s;
 }
 
@@ -143,15 +143,6 @@ __device__ __forceinline__ void wave_argmax(double& c, int& s) {
     const int s2 = __shfl_xor(s, o, 64);
     better(c, s, c2, s2);
   }
-}
-
-__device__ __forceinline__ uint32_t permute_u32(int dst_lane, uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_ds_permute(dst_lane << 2, (int)v);
-}
-__device__ __forceinline__ int64_t permute_i64(int dst_lane, int64_t v) {
-  const uint32_t lo = permute_u32(dst_lane, (uint32_t)(uint64_t)v);
-  const uint32_t hi = permute_u32(dst_lane, (uint32_t)((uint64_t)v >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // nw rows (weighted), n1 class-1 weight (kind 0), s1 response / pseudo-outcome sum (kinds 1/2);
@@ -294,21 +285,6 @@ __device__ int wave_threshold(const double* __restrict__ v, int blo, int bhi, in
   return lo;
 }
 
-// Ascending bitonic sort of K[0..N2) (N2 a power of two) by ONE wave (wave-synchronous LDS).
-__device__ void wave_bitonic(uint32_t* K, int N2, int lane) {
-  for (int kk = 2; kk <= N2; kk <<= 1)
-    for (int jj = kk >> 1; jj > 0; jj >>= 1) {
-      for (int s = lane; s < N2; s += 64) {
-        const int o = s ^ jj;
-        if (o > s) {
-          const uint32_t x = K[s], y = K[o];
-          if ((x > y) == ((s & kk) == 0)) { K[s] = y; K[o] = x; }
-        }
-      }
-      wave_sync();
-    }
-}
-
 __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const int32_t* __restrict__ order,
     const double* __restrict__ vals,
@@ -343,8 +319,6 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
   auto bit = [&](int i) -> bool { return (sbits[i >> 5] >> (i & 31)) & 1u; };
   char* wsl = sarena + wid * WSLICE;          // this wave's slice: keys, then statistics
   uint32_t* Kw = (uint32_t*)wsl;
-  int64_t* Xw0 = (int64_t*)(wsl + WCAP * 4);
-  int64_t* Xw1 = Xw0 + WCAP;
 
   // ---- weights: bootstrap counts (integer atomics: order-free), or grf's samples (Algorithm
   // S, sequential by definition, thread 0; cpu/forest_cpu.cpp draw_rows): the group's
@@ -431,7 +405,7 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
   }
   // ---- presorted root lists: feature f's rows in value order = the forest-wide order of f
   // filtered to this tree's in-bag rows (a bit per row in LDS); one wave per feature
-  if (m > WCAP) {
+  {
     for (int e = tid; e < (n + 31) / 32; e += XT) sbits[e] = 0u;
     __syncthreads();
     for (int i = tid; i < n; i += XT)
@@ -661,6 +635,9 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
 #endif
 
     // ================= decisions: nodes <= WCAP rows, one wave each (round-robin)
+    // Lane l owns list positions [l ch, l ch + ch) (ch = ceil(cnt / 64) <= 4) of every
+    // feature's value-ordered segment: its rows' statistics are gathered by row id, prefix-
+    // summed by a wave scan, and the boundaries between distinct values evaluated in order.
     {
       int* perm = sperm[wid];
       XRng ndn = wid < ncur ? S.cur[wid] : XRng{0, 0, 0};
@@ -669,105 +646,15 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         if (j + XW < ncur) ndn = S.cur[j + XW];   // next node's range, in flight meanwhile
         const int cnt = nd.hi - nd.lo;
         if (cnt > WCAP) continue;
-        if (cnt <= 64) {
-          // ---- a row per lane: ranks by lane compares, sorted order by ds_permute
-          const bool live = lane < cnt;
-          const int i = live ? S.idx[nd.lo + lane] : 0;
-          NodeStats st{0, 0, 0, 0, CausalNode{0, 0, 0, 0}};
-          if (fp.kind == 2) {                 // the node's causal constants first
-            int64_t ca = 0, cb = 0, cc = 0, cd = 0;
-            if (live) causal_row(r1, r2, i, ca, cb, cc, cd);
-            st.nw = wave_sum64(live ? 1 : 0);
-            st.cn = causal_node((double)st.nw, wave_sum64(ca), wave_sum64(cb), wave_sum64(cc),
-                                wave_sum64(cd));
-          }
-          int64_t x0 = 0, x1 = 0;
-          if (live) row_stats(fp, S.w, ycls, r1, r2, st.cn, i, x0, x1);
-          if (fp.kind == 0) {
-            st.nw = wave_sum64(x0 + x1);
-            st.n1 = wave_sum64(x1);
-            st.s1 = 0;
-          } else if (fp.kind == 1) {
-            st.nw = wave_sum64(x0);
-            st.n1 = 0;
-            st.s1 = wave_sum64(x1);
-          } else {
-            st.s1 = wave_sum64(x1);
-            st.ntreat = wave_sum64(x0 >> 32);
-          }
-          if (is_terminal(fp, st, depth)) {
-            if (lane == 0) S.dec[j] = XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
-            continue;
-          }
-          int nf = 0;
-          if (lane == 0) nf = draw_features(fp, tg, nd.id, perm);
-          nf = __shfl(nf, 0, 64);
-          wave_sync();
-          const int minc = min_child(fp, (double)st.nw);
-          double best = -INFINITY;
-          int bf = -1, blo = -1, bhi = -1, bnl = 0;
-          // the row's bins of up to 8 candidate features fetched together (one memory
-          // latency per 8 features instead of one per feature)
-          constexpr int PF = 8;
-          uint32_t bins[PF];
-          for (int k = 0; k < nf; ++k) {
-            const int f = perm[k];
-            if ((k % PF) == 0) {
+        static_assert(WCAP <= 64 * 4, "four rows per lane");
+        int iv[4];
 #pragma unroll
-              for (int u = 0; u < PF; ++u)
-                bins[u] = (live && k + u < nf) ? (uint32_t)Xb[(int64_t)perm[k + u] * n + i] : 0u;
-            }
-            uint32_t bk = bins[0];
-#pragma unroll
-            for (int u = 1; u < PF; ++u) bk = (k % PF) == u ? bins[u] : bk;
-            // idle lanes sort last with distinct keys (ranks cnt..63: ds_permute is a bijection)
-            const uint32_t key = live ? ((bk << 16) | (uint32_t)lane) : (0xFFFF0000u | (uint32_t)lane);
-            int rank = 0;
-            for (int q = 0; q < 64; ++q) rank += (uint32_t)__builtin_amdgcn_readlane((int)key, q) < key;
-            // lane s receives the key and statistics of the row ranked s
-            const uint32_t ks = permute_u32(rank, key);
-            int64_t c0 = permute_i64(rank, x0), c1 = permute_i64(rank, x1);
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-              const int64_t u0 = __shfl_up(c0, o, 64), u1 = __shfl_up(c1, o, 64);
-              if (lane >= o) { c0 += u0; c1 += u1; }
-            }
-            const uint32_t kn = __shfl_down(ks, 1, 64);
-            double cr = -INFINITY;
-            int s = 0x7FFFFFFF;
-            if (lane + 1 < cnt && (ks >> 16) != (kn >> 16)) {
-              cr = boundary_crit(fp, st, minc, c0, c1);
-              s = lane;
-            }
-            wave_argmax(cr, s);
-            if (cr > best) {                  // uniform
-              best = cr;
-              bf = f;
-              blo = (int)(__shfl(ks, s, 64) >> 16);
-              bhi = (int)(__shfl(kn, s, 64) >> 16);
-              bnl = s + 1;
-            }
-          }
-          const double parent = parent_crit(fp, st);
-          const bool split = bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent));
-          const int tb = !split ? -1 : fp.sampling == 1 ? blo
-                                : wave_threshold(vals + (int64_t)bf * ldv, blo, bhi, lane);
-          if (lane == 0)
-            S.dec[j] = split ? XDec{1, bf, tb, bnl, 0.0}
-                             : XDec{0, -1, -1, 0, leaf_value(fp, tg, nd.id, st)};
-          continue;
-        }
-        // ---- 64 < cnt <= WCAP: wave bitonic sort of the keys in this wave's LDS slice, the
-        // per-position statistics staged beside them
-        static_assert(WCAP <= 64 * 8, "one 8-row batch per lane");
-        int iv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) iv[u] = lane + 64 * u < cnt ? S.idx[nd.lo + lane + 64 * u] : 0;
+        for (int u = 0; u < 4; ++u) iv[u] = lane + 64 * u < cnt ? S.idx[nd.lo + lane + 64 * u] : 0;
         NodeStats st{0, 0, 0, 0, CausalNode{0, 0, 0, 0}};
         if (fp.kind == 2) {                   // the node's causal constants first
           int64_t ca = 0, cb = 0, cc = 0, cd = 0;
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
+          for (int u = 0; u < 4; ++u)
             if (lane + 64 * u < cnt) {
               int64_t x, y, z, v2;
               causal_row(r1, r2, iv[u], x, y, z, v2);
@@ -778,15 +665,13 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         }
         int64_t a = 0, b1 = 0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int q = lane + 64 * u;
-          if (q < cnt) {
+        for (int u = 0; u < 4; ++u)
+          if (lane + 64 * u < cnt) {
             int64_t x0, x1;
             row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
-            Xw0[q] = x0; Xw1[q] = x1;
+            S.sx0[iv[u]] = x0; S.sx1[iv[u]] = x1;     // by row id: the lists index rows
             a += x0; b1 += x1;
           }
-        }
         a = wave_sum64(a); b1 = wave_sum64(b1);
         if (fp.kind == 0) { st.nw = a + b1; st.n1 = b1; st.s1 = 0; }
         else if (fp.kind == 1) { st.nw = a; st.n1 = 0; st.s1 = b1; }
@@ -798,9 +683,11 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         int nf = 0;
         if (lane == 0) nf = draw_features(fp, tg, nd.id, perm);
         nf = __shfl(nf, 0, 64);
-        wave_sync();
+        // the statistics stores (global) and perm (LDS) before any lane's gathers
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int minc = min_child(fp, (double)st.nw);
-        const int N2 = np2(cnt);
         const int ch = (cnt + 63) / 64;
         const int s0 = min(cnt, lane * ch), s1 = min(cnt, s0 + ch);
         double best = -INFINITY;
@@ -808,42 +695,53 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         for (int k = 0; k < nf; ++k) {
           const int f = perm[k];
           const uint16_t* xf = Xb + (int64_t)f * n;
-          uint32_t bv[8];
+          const uint16_t* Lf = S.La + (int64_t)f * n + nd.lo;
+          int rv[4];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) bv[u] = lane + 64 * u < cnt ? (uint32_t)xf[iv[u]] : 0u;
+          for (int u = 0; u < 4; ++u) rv[u] = s0 + u < s1 ? (int)Lf[s0 + u] : 0;
+          uint32_t bv[4];
+          int64_t a0[4], a1[4];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int q = lane + 64 * u;
-            if (q < N2) Kw[q] = q < cnt ? ((bv[u] << 16) | (uint32_t)q) : 0xFFFFFFFFu;
+          for (int u = 0; u < 4; ++u) {
+            const bool in = s0 + u < s1;
+            bv[u] = in ? (uint32_t)xf[rv[u]] : 0xFFFFFFFFu;
+            a0[u] = in ? S.sx0[rv[u]] : 0;
+            a1[u] = in ? S.sx1[rv[u]] : 0;
           }
-          wave_sync();
-          wave_bitonic(Kw, N2, lane);
-          // lane owns sorted positions [s0, s1): local sums, wave exclusive scan, walk
           int64_t l0 = 0, l1 = 0;
-          for (int s = s0; s < s1; ++s) {
-            const int q = (int)(Kw[s] & 0xFFFFu);
-            l0 += Xw0[q]; l1 += Xw1[q];
-          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) { l0 += a0[u]; l1 += a1[u]; }
           int64_t p0 = wave_excl_scan64(l0, lane), p1 = wave_excl_scan64(l1, lane);
+          // the value after this lane's last position: the next lane's first (lane 63 ends
+          // at cnt, where no boundary is evaluated)
+          const uint32_t bnext = (uint32_t)__shfl_down((int)bv[0], 1, 64);
           double bc = -INFINITY;
           int bs = 0x7FFFFFFF;
-          for (int s = s0; s < s1; ++s) {
-            const int q = (int)(Kw[s] & 0xFFFFu);
-            p0 += Xw0[q]; p1 += Xw1[q];
-            if (s + 1 < cnt && (Kw[s] >> 16) != (Kw[s + 1] >> 16)) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int s_ = s0 + u;
+            if (s_ >= s1) break;
+            p0 += a0[u]; p1 += a1[u];
+            const uint32_t bn = s_ + 1 < s1 ? bv[u + 1 < 4 ? u + 1 : 3] : bnext;
+            if (s_ + 1 < cnt && bv[u] != bn) {
               const double cr = boundary_crit(fp, st, minc, p0, p1);
-              if (cr > bc) { bc = cr; bs = s; }
+              if (cr > bc) { bc = cr; bs = s_; }
             }
           }
           wave_argmax(bc, bs);
           if (bc > best) {                    // uniform
             best = bc;
             bf = f;
-            blo = (int)(Kw[bs] >> 16);
-            bhi = (int)(Kw[bs + 1] >> 16);
+            // the bins at positions bs and bs + 1, from the lanes that hold them
+            const int o0 = bs / ch, u0 = bs - o0 * ch;
+            const int o1 = (bs + 1) / ch, u1 = bs + 1 - o1 * ch;
+            uint32_t m0 = bv[0], m1 = bv[0];
+#pragma unroll
+            for (int u = 1; u < 4; ++u) { if (u == u0) m0 = bv[u]; if (u == u1) m1 = bv[u]; }
+            blo = __builtin_amdgcn_readlane((int)m0, o0);
+            bhi = __builtin_amdgcn_readlane((int)m1, o1);
             bnl = bs + 1;
           }
-          wave_sync();                        // Kw reused by the next feature
         }
         const double parent = parent_crit(fp, st);
         const bool split = bf >= 0 && best > parent + 1e-12 * fmax(1.0, fabs(parent));
@@ -929,8 +827,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       for (int q = tid; q < cnt; q += XT) S.idx[nd.lo + q] = (int32_t)S.keys[nd.lo + q];
       __syncthreads();
       // every feature's value-ordered list of the node, stable-partitioned into its children's
-      // segments of the next level's lists (one wave per feature); only large children read them
-      if (d.nl > WCAP || cnt - d.nl > WCAP) {
+      // segments of the next level's lists (one wave per feature)
+      {
         for (int f = wid; f < fp.p; f += XW) {
           const uint16_t* src = S.La + (int64_t)f * n + nd.lo;
           uint16_t* dst = S.Lb + (int64_t)f * n + nd.lo;
@@ -973,12 +871,51 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           const int i = in ? S.idx[nd.lo + q] : 0;
           const bool l = in && xf[i] <= d.thr;
           const uint64_t bl = __ballot(l), br = __ballot(in && !l);
-          if (in) Kw[l ? lo_l + __popcll(bl & below) : lo_r + __popcll(br & below)] = (uint32_t)i;
+          if (in) {
+            Kw[l ? lo_l + __popcll(bl & below) : lo_r + __popcll(br & below)] = (uint32_t)i;
+            S.side[i] = l ? 1 : 0;
+          }
           lo_l += __popcll(bl);
           lo_r += __popcll(br);
         }
-        wave_sync();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         for (int q = lane; q < cnt; q += 64) S.idx[nd.lo + q] = (int32_t)Kw[q];
+        // every feature's value-ordered segment into its children's segments of the next
+        // level's lists (four features per batch: their loads in flight together)
+        for (int f0 = 0; f0 < fp.p; f0 += 4) {
+          int rv[4][4];
+          uint8_t sv[4][4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int q = u * 64 + lane;
+              rv[e][u] = (f0 + e < fp.p && q < cnt) ? (int)S.La[(int64_t)(f0 + e) * n + nd.lo + q] : 0;
+            }
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              sv[e][u] = (f0 + e < fp.p && u * 64 + lane < cnt) ? S.side[rv[e][u]] : 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (f0 + e >= fp.p) break;
+            uint16_t* dst = S.Lb + (int64_t)(f0 + e) * n + nd.lo;
+            int ol = 0, orr = d.nl;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const bool in = u * 64 + lane < cnt;
+              const bool l = in && sv[e][u];
+              const uint64_t bl = __ballot(l), br = __ballot(in && !l);
+              if (in) dst[l ? ol + __popcll(bl & below) : orr + __popcll(br & below)] = (uint16_t)rv[e][u];
+              ol += __popcll(bl);
+              orr += __popcll(br);
+            }
+            ATE_DASSERT(ol == d.nl && orr == cnt);
+          }
+        }
         wave_sync();
       }
     }
