@@ -160,3 +160,28 @@ dist.destroy_process_group()
             got[a:a + c] = g[o:o + c]
             o += c
     assert np.array_equal(got, ref)
+
+
+def test_selected_rows_host_arrays():
+    """data/panel_selection.selected_rows: the kept rows as host arrays (configs 3 / 4)."""
+    from ate_replication_causalml_amd.data.panel_selection import selected_rows
+    d, sel = selected_rows(2000, 4)
+    assert d.X.shape == (2000, 21) and sel.n_gen > 2000
+    g = kept_gids(sel, [(0, 2000)]).numpy()
+    cts, binc, _, W, Y, _ = dgp.raw_columns(0, 4, params=dgp.TUTORIAL, idx=g)
+    assert np.array_equal(d.X, np.column_stack([cts, binc])) and np.array_equal(d.W, W)
+
+
+def test_emulated_comm_shapes():
+    """parallel/comm.EmulatedComm (tools/cfg4.py / cfg5.py --shard r/W): rank r's share of
+    every sharded algorithm, shape-correct non-communicating collectives."""
+    from ate_replication_causalml_amd.parallel.comm import EmulatedComm
+    c = EmulatedComm(2, 4)
+    t = torch.arange(3.0)
+    out = torch.empty(12)
+    assert torch.equal(c.all_gather_into_(out, t), t.repeat(4))
+    r = torch.empty(2)
+    assert torch.equal(c.reduce_scatter_(r, torch.arange(8.0)), torch.tensor([4.0, 5.0]))
+    assert len(c.all_gather(t)) == 4 and c.emulated
+    with pytest.raises(ValueError):
+        EmulatedComm(4, 4)
