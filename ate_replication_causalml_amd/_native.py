@@ -67,8 +67,8 @@ _SIGS = {
     "ate_forest_predict": "ppiiipppppippip",
     "ate_forest_pack": "pippppppp",
     "ate_forest_scratch_bytes": "ii",
-    "ate_forest_exact_scratch_bytes": "iii",
-    "ate_forest_fit_exact": "piipppippppippppppppp",
+    "ate_forest_exact_scratch_bytes": "iiii",
+    "ate_forest_fit_exact": "piiipppippppippppppppp",
     "ate_forest_predict16": "ppiiipppppppippip",
     "ate_bin_matrix": "plipppp",
     "ate_panel_xtv": "iplpipplipp",

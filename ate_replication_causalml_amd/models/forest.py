@@ -497,9 +497,30 @@ def fit_forest_binned(Xb, edges, kind: int, y=None, r1=None, r2=None, ntree=500,
 
 
 def exact_row_order(Xb: torch.Tensor) -> torch.Tensor:
-    """int32 [p][n]: for each feature, the row ids in ascending value-rank order (a stable
-    sort, so ties keep row order; the engines' splits do not depend on the order of ties)."""
-    return torch.argsort(Xb.to(torch.int32), dim=1, stable=True).to(torch.int32).contiguous()
+    """[p][n] uint32 entries (value rank << 16 | row) per feature in ascending order (held in
+    an int32 tensor): the forest-wide value order every tree filters to its in-bag rows
+    (csrc/forest_exact.hip). Ties are in row order; the splits do not depend on it."""
+    p, n = Xb.shape
+    key = (Xb.to(torch.int64) << 16) | torch.arange(n, device=Xb.device, dtype=torch.int64)
+    key = torch.sort(key, dim=1).values
+    return torch.where(key >= 2 ** 31, key - 2 ** 32, key).to(torch.int32).contiguous()
+
+
+def exact_mcap(n: int, sampling: int, group: int, sample_fraction: float, honesty: bool) -> int:
+    """A tree's in-bag (J1) row count as the exact-split kernel's sampling draws it (the bound
+    its per-position scratch is sized by): randomForest bootstrap -> n (distinct rows <= n);
+    grf: the group's half-sample floor(n / 2) (group > 1), the tree's subsample of it
+    floor(nh * min(1, sample_fraction * group)), or floor(n * sample_fraction) (group 1), then
+    honesty's half (ns // 2)."""
+    if sampling == 0:
+        return n
+    if group > 1:
+        nh = n // 2
+        f = min(1.0, sample_fraction * group)
+        ns = nh if f >= 1.0 else int(math.floor(nh * f))
+    else:
+        ns = int(math.floor(n * sample_fraction))
+    return max(1, ns // 2 if honesty else ns)
 
 
 def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtry=None,
@@ -557,7 +578,8 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         nnodes = torch.empty(ntree, dtype=torch.int32, device=dev)
         inbag = torch.empty(ntree * n, dtype=torch.uint8, device=dev)
         est = torch.zeros(ntree * cap * 5, dtype=torch.int64, device=dev) if need_est else None
-        per = _native.hip().ate_forest_exact_scratch_bytes(n, p, 1)
+        mc = exact_mcap(n, sampling, max(1, group), sample_fraction, bool(honesty))
+        per = _native.hip().ate_forest_exact_scratch_bytes(n, p, mc, 1)
         # trees per launch: two resident per CU, so a launch wants >= 512 of them and as
         # few tails as possible. A 1-GiB scratch cap held 264 trees of 5e4 rows (half the CUs
         # idle, a tail per launch; config 4 2.53 s); when 1 GiB cannot hold the whole forest
@@ -580,7 +602,7 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         s = torch.cuda.current_stream().cuda_stream
         for t0 in range(0, ntree, chunk):
             _native.call("ate_forest_fit_exact", ctypes.addressof(fp), t0, min(chunk, ntree - t0),
-                         Xb.data_ptr(), order.data_ptr(), vals.data_ptr(), de.ldv, nval.data_ptr(), p_(yt), p_(r1t),
+                         mc, Xb.data_ptr(), order.data_ptr(), vals.data_ptr(), de.ldv, nval.data_ptr(), p_(yt), p_(r1t),
                          p_(r2t), cap, feat.data_ptr(), thr.data_ptr(), left.data_ptr(),
                          val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
                          scratch.data_ptr(), s)

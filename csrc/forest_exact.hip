@@ -78,19 +78,22 @@ constexpr int XPMAX = 512;         // max features
 struct XRng { int lo, hi, id; };
 struct XDec { int split, feat, thr, nl; double val; };
 
+// Per-tree scratch. mc = the tree's in-bag (J1) row count bound (host: exact_mcap): every
+// per-position array is mc long, so a grf tree (mc = n / 4) needs a quarter of the memory.
 struct XScratch {
-  int64_t* sx0;     // [n] per-row statistics of the workgroup-level node being decided
-  int64_t* sx1;     // [n]
+  int64_t* sx0;     // [mc] per-position statistics of the nodes being decided
+  int64_t* sx1;     // [mc]
   int32_t* w;       // [n] bootstrap weights
-  int32_t* idx;     // [n] rows of the growing nodes (node = contiguous range)
-  uint32_t* keys;   // [np2] global sort keys / partition staging
-  XRng* cur;        // [n + 1]
-  XRng* nxt;        // [n + 1]
-  XDec* dec;        // [n + 1]
+  int32_t* idx;     // [mc] rows of the growing nodes by position (node = contiguous range)
+  uint32_t* keys;   // [max(n, mc)] sampling scratch / partition staging
+  XRng* cur;        // [mc + 1]
+  XRng* nxt;        // [mc + 1]
+  XDec* dec;        // [mc + 1]
   int32_t* est;     // [n] grf J2 (estimation) rows
-  uint16_t* La;     // [p][n] per-feature row lists of every node (value order), current
-  uint16_t* Lb;     // [p][n] ... and the next level's
-  uint8_t* side;    // [n] the side (1 = left) of every row of a splitting wave-level node
+  uint32_t* La;     // [p][mc] per-feature lists of every node: (value rank << 16) | position,
+  uint32_t* Lb;     // [p][mc] in value order; current level's and next level's
+  uint8_t* side;    // [mc] by position: 1 = goes left (splitting wave-level nodes)
+  uint16_t* npos;   // [mc] by position: the position after the level's partition
 };
 
 __host__ __device__ inline int np2(int n) {
@@ -101,27 +104,29 @@ __host__ __device__ inline int np2(int n) {
 
 __host__ __device__ inline int64_t align16(int64_t b) { return (b + 15) & ~(int64_t)15; }
 
-__host__ __device__ inline int64_t tree_bytes(int n, int p) {
-  return align16(8ll * n) * 2 + align16(4ll * n) * 2 + align16(4ll * np2(n)) +
-         align16(12ll * (n + 1)) * 2 + align16((int64_t)sizeof(XDec) * (n + 1)) +
-         align16(4ll * n) + align16(2ll * p * n) * 2 + align16(n);
+__host__ __device__ inline int64_t tree_bytes(int n, int p, int mc) {
+  return align16(8ll * mc) * 2 + align16(4ll * n) + align16(4ll * mc) +
+         align16(4ll * (n > mc ? n : mc)) + align16(12ll * (mc + 1)) * 2 +
+         align16((int64_t)sizeof(XDec) * (mc + 1)) + align16(4ll * n) +
+         align16(4ll * p * mc) * 2 + align16(mc) + align16(2ll * mc);
 }
 
-__device__ XScratch scratch_at(char* base, int n, int np_) {
+__device__ XScratch scratch_at(char* base, int n, int np_, int mc) {
   XScratch s;
   char* p = base;
-  s.sx0 = (int64_t*)p; p += align16(8ll * n);
-  s.sx1 = (int64_t*)p; p += align16(8ll * n);
+  s.sx0 = (int64_t*)p; p += align16(8ll * mc);
+  s.sx1 = (int64_t*)p; p += align16(8ll * mc);
   s.w = (int32_t*)p; p += align16(4ll * n);
-  s.idx = (int32_t*)p; p += align16(4ll * n);
-  s.keys = (uint32_t*)p; p += align16(4ll * np2(n));
-  s.cur = (XRng*)p; p += align16(12ll * (n + 1));
-  s.nxt = (XRng*)p; p += align16(12ll * (n + 1));
-  s.dec = (XDec*)p; p += align16((int64_t)sizeof(XDec) * (n + 1));
+  s.idx = (int32_t*)p; p += align16(4ll * mc);
+  s.keys = (uint32_t*)p; p += align16(4ll * (n > mc ? n : mc));
+  s.cur = (XRng*)p; p += align16(12ll * (mc + 1));
+  s.nxt = (XRng*)p; p += align16(12ll * (mc + 1));
+  s.dec = (XDec*)p; p += align16((int64_t)sizeof(XDec) * (mc + 1));
   s.est = (int32_t*)p; p += align16(4ll * n);
-  s.La = (uint16_t*)p; p += align16(2ll * np_ * n);
-  s.Lb = (uint16_t*)p; p += align16(2ll * np_ * n);
-  s.side = (uint8_t*)p;
+  s.La = (uint32_t*)p; p += align16(4ll * np_ * mc);
+  s.Lb = (uint32_t*)p; p += align16(4ll * np_ * mc);
+  s.side = (uint8_t*)p; p += align16(mc);
+  s.npos = (uint16_t*)p;
   return s;
 }
 
@@ -286,7 +291,8 @@ __device__ int wave_threshold(const double* __restrict__ v, int blo, int bhi, in
 }
 
 __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
-    ForestParams fp, int tbeg, const uint16_t* __restrict__ Xb, const int32_t* __restrict__ order,
+    ForestParams fp, int tbeg, int mc, const uint16_t* __restrict__ Xb,
+    const uint32_t* __restrict__ order,
     const double* __restrict__ vals,
     int ldv, const int32_t* __restrict__ nval, const uint8_t* __restrict__ ycls,
     const int64_t* __restrict__ r1, const int64_t* __restrict__ r2, int cap,
@@ -304,17 +310,18 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
   __shared__ int scnt[XW + 1];
   __shared__ int sncur, snext_id, sm, snbig, sestn;
   __shared__ int sbig[XBIG];                  // this level's workgroup-level nodes
+  __shared__ int swpre[65536 / 32];           // root lists: in-bag rows before each 32-row word
   const int t = tbeg + blockIdx.x;            // tree within this forest
   const int tg = fp.t0 + t;                   // global tree id (RNG key)
   const int n = fp.n, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  XScratch S = scratch_at(scratch + (int64_t)blockIdx.x * tree_bytes(n, fp.p), n, fp.p);
+  XScratch S = scratch_at(scratch + (int64_t)blockIdx.x * tree_bytes(n, fp.p, mc), n, fp.p, mc);
   const int64_t base = (int64_t)t * cap;
   int32_t* tfeat = feat + base;
   int32_t* tthr = thr + base;
   int32_t* tleft = left + base;
   double* tval = val + base;
   uint8_t* inb = inbag + (int64_t)t * n;
-  uint32_t* sbits = (uint32_t*)sarena;        // large-node phases: one bit per row
+  uint32_t* sbits = (uint32_t*)sarena;        // root: a bit per row; large partitions: per position
   const uint64_t below = (1ull << lane) - 1ull;
   auto bit = [&](int i) -> bool { return (sbits[i >> 5] >> (i & 31)) & 1u; };
   char* wsl = sarena + wid * WSLICE;          // this wave's slice: keys, then statistics
@@ -392,41 +399,74 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     __syncthreads();
     int off = m;
     for (int q = 0; q < wid; ++q) off += scnt[q];
-    if (in) S.idx[off + __popcll(b & ((1ull << lane) - 1ull))] = i;
+    const int at = off + __popcll(b & ((1ull << lane) - 1ull));
+    ATE_DASSERT(!in || at < mc);
+    if (in && at < mc) S.idx[at] = i;
     int tot = 0;
     for (int q = 0; q < XW; ++q) tot += scnt[q];
     m += tot;
     __syncthreads();
+  }
+  if (m > mc) {                               // the host's bound is exact; never taken
+    if (tid == 0) nnodes[t] = -1;
+    return;
   }
   if (tid == 0) {
     S.cur[0] = XRng{0, m, 0};
     sncur = 1;
     snext_id = 1;
   }
-  // ---- presorted root lists: feature f's rows in value order = the forest-wide order of f
-  // filtered to this tree's in-bag rows (a bit per row in LDS); one wave per feature
+  // ---- presorted root lists: feature f's entries (value rank, row) in value order, the
+  // forest-wide order filtered to this tree's in-bag rows (a bit per row in LDS) with the row
+  // replaced by its position: the rank of the row among the in-bag rows (S.idx is in row
+  // order at the root), from per-word prefix popcounts. One wave per feature.
   {
-    for (int e = tid; e < (n + 31) / 32; e += XT) sbits[e] = 0u;
+    const int nw32 = (n + 31) / 32;
+    for (int e = tid; e < nw32; e += XT) sbits[e] = 0u;
     __syncthreads();
     for (int i = tid; i < n; i += XT)
       if (S.w[i] > 0) atomicOr(&sbits[i >> 5], 1u << (i & 31));
     __syncthreads();
+    {                                         // swpre = exclusive prefix of the word counts
+      constexpr int WPT = (65536 / 32) / XT;  // words per thread (4)
+      int c = 0;
+#pragma unroll
+      for (int u = 0; u < WPT; ++u) {
+        const int e = tid * WPT + u;
+        c += e < nw32 ? __popc(sbits[e]) : 0;
+      }
+      int64_t ex = wave_excl_scan64(c, lane);
+      if (lane == 63) sw0[wid] = ex + c;
+      __syncthreads();
+      for (int q = 0; q < wid; ++q) ex += sw0[q];
+      int run = (int)ex;
+#pragma unroll
+      for (int u = 0; u < WPT; ++u) {
+        const int e = tid * WPT + u;
+        if (e < nw32) { swpre[e] = run; run += __popc(sbits[e]); }
+      }
+    }
+    __syncthreads();
     for (int f = wid; f < fp.p; f += XW) {
-      const int32_t* of = order + (int64_t)f * n;
-      uint16_t* Lf = S.La + (int64_t)f * n;
+      const uint32_t* of = order + (int64_t)f * n;
+      uint32_t* Lf = S.La + (int64_t)f * mc;
       int c = 0;
       for (int c0 = 0; c0 < n; c0 += 64 * 8) {
-        int rv[8];
+        uint32_t ev[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int q = c0 + u * 64 + lane;
-          rv[u] = q < n ? of[q] : 0;
+          ev[u] = q < n ? of[q] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const bool keep = c0 + u * 64 + lane < n && bit(rv[u]);
+          const int r = (int)(ev[u] & 0xFFFFu);
+          const bool keep = c0 + u * 64 + lane < n && bit(r);
           const uint64_t b = __ballot(keep);
-          if (keep) Lf[c + __popcll(b & below)] = (uint16_t)rv[u];
+          if (keep) {
+            const int pos = swpre[r >> 5] + __popc(sbits[r >> 5] & ((1u << (r & 31)) - 1u));
+            Lf[c + __popcll(b & below)] = (ev[u] & 0xFFFF0000u) | (uint32_t)pos;
+          }
           c += __popcll(b);
         }
       }
@@ -530,8 +570,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           if (qb + u * XT < cnt) {
             int64_t x0, x1;
             row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
-            S.sx0[iv[u]] = x0;
-            S.sx1[iv[u]] = x1;
+            S.sx0[nd.lo + qb + u * XT] = x0;      // by position (the list entries carry it)
+            S.sx1[nd.lo + qb + u * XT] = x1;
             srho += x1;
             stre += x0 >> 32;
           }
@@ -552,18 +592,17 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       const int s0 = min(cnt, tid * ch), s1 = min(cnt, s0 + ch);
       for (int k = 0; k < nf; ++k) {
         const int f = sperm[0][k];
-        const uint16_t* xf = Xb + (int64_t)f * n;
-        const uint16_t* Lf = S.La + (int64_t)f * n + nd.lo;    // the node's rows, value order
+        const uint32_t* Lf = S.La + (int64_t)f * mc + nd.lo;   // (rank, position), value order
         int64_t l0 = 0, l1 = 0;
         for (int sb = s0; sb < s1; sb += 8) {
-          int rv[8];
+          uint32_t ev[8];
           int64_t a0[8], a1[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) rv[u] = sb + u < s1 ? (int)Lf[sb + u] : 0;
+          for (int u = 0; u < 8; ++u) ev[u] = sb + u < s1 ? Lf[sb + u] : 0u;
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            a0[u] = sb + u < s1 ? S.sx0[rv[u]] : 0;
-            a1[u] = sb + u < s1 ? S.sx1[rv[u]] : 0;
+            a0[u] = sb + u < s1 ? S.sx0[ev[u] & 0xFFFFu] : 0;
+            a1[u] = sb + u < s1 ? S.sx1[ev[u] & 0xFFFFu] : 0;
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) { l0 += a0[u]; l1 += a1[u]; }
@@ -576,17 +615,16 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         double bc = -INFINITY;
         int bs = 0x7FFFFFFF;
         for (int sb = s0; sb < s1; sb += 8) {
-          int rv[9];
-          uint32_t bv[9];
+          uint32_t ev[9], bv[9];
           int64_t a0[8], a1[8];
 #pragma unroll
-          for (int u = 0; u < 9; ++u) rv[u] = sb + u < cnt ? (int)Lf[sb + u] : 0;
+          for (int u = 0; u < 9; ++u) ev[u] = sb + u < cnt ? Lf[sb + u] : 0u;
 #pragma unroll
-          for (int u = 0; u < 9; ++u) bv[u] = sb + u < cnt ? (uint32_t)xf[rv[u]] : 0xFFFFFFFFu;
+          for (int u = 0; u < 9; ++u) bv[u] = sb + u < cnt ? ev[u] >> 16 : 0xFFFFFFFFu;
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            a0[u] = sb + u < s1 ? S.sx0[rv[u]] : 0;
-            a1[u] = sb + u < s1 ? S.sx1[rv[u]] : 0;
+            a0[u] = sb + u < s1 ? S.sx0[ev[u] & 0xFFFFu] : 0;
+            a1[u] = sb + u < s1 ? S.sx1[ev[u] & 0xFFFFu] : 0;
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
@@ -610,8 +648,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
             best = c2;
             bf = f;
             ATE_DASSERT(s2 >= 0 && s2 + 1 < cnt);
-            blo = (int)xf[Lf[s2]];
-            bhi = (int)xf[Lf[s2 + 1]];
+            blo = (int)(Lf[s2] >> 16);
+            bhi = (int)(Lf[s2 + 1] >> 16);
             bnl = s2 + 1;
           }
         }
@@ -669,7 +707,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           if (lane + 64 * u < cnt) {
             int64_t x0, x1;
             row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
-            S.sx0[iv[u]] = x0; S.sx1[iv[u]] = x1;     // by row id: the lists index rows
+            S.sx0[nd.lo + lane + 64 * u] = x0;    // by position (the list entries carry it)
+            S.sx1[nd.lo + lane + 64 * u] = x1;
             a += x0; b1 += x1;
           }
         a = wave_sum64(a); b1 = wave_sum64(b1);
@@ -694,19 +733,18 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         int bf = -1, blo = -1, bhi = -1, bnl = 0;
         for (int k = 0; k < nf; ++k) {
           const int f = perm[k];
-          const uint16_t* xf = Xb + (int64_t)f * n;
-          const uint16_t* Lf = S.La + (int64_t)f * n + nd.lo;
-          int rv[4];
+          const uint32_t* Lf = S.La + (int64_t)f * mc + nd.lo;
+          uint32_t ev[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) rv[u] = s0 + u < s1 ? (int)Lf[s0 + u] : 0;
+          for (int u = 0; u < 4; ++u) ev[u] = s0 + u < s1 ? Lf[s0 + u] : 0u;
           uint32_t bv[4];
           int64_t a0[4], a1[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const bool in = s0 + u < s1;
-            bv[u] = in ? (uint32_t)xf[rv[u]] : 0xFFFFFFFFu;
-            a0[u] = in ? S.sx0[rv[u]] : 0;
-            a1[u] = in ? S.sx1[rv[u]] : 0;
+            bv[u] = in ? ev[u] >> 16 : 0xFFFFFFFFu;
+            a0[u] = in ? S.sx0[ev[u] & 0xFFFFu] : 0;
+            a1[u] = in ? S.sx1[ev[u] & 0xFFFFu] : 0;
           }
           int64_t l0 = 0, l1 = 0;
 #pragma unroll
@@ -792,6 +830,9 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     XPHASE(4);
 
     // ================= stable partitions by bin <= thr
+    // S.idx (rows by position) is partitioned in place per node; every position's side and
+    // new position are recorded, then each feature's entries (rank, position) move to their
+    // children's segments of the next level's lists with the position renumbered.
     for (int jb = 0; jb < nbig; ++jb) {       // large nodes: whole workgroup
       const int j = sbig[jb];
       const XRng nd = S.cur[j];
@@ -816,44 +857,50 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         ATE_DASSERT(!in || (l ? ol + __popcll(bl & below) < d.nl
                              : orr + __popcll(br & below) < cnt));
         if (in) {
-          S.keys[nd.lo + (l ? ol + __popcll(bl & below) : orr + __popcll(br & below))] = (uint32_t)i;
-          // the row's side, for the list partitions below
-          if (l) atomicOr(&sbits[i >> 5], 1u << (i & 31));
-          else atomicAnd(&sbits[i >> 5], ~(1u << (i & 31)));
+          const int dest = nd.lo + (l ? ol + __popcll(bl & below) : orr + __popcll(br & below));
+          S.keys[dest] = (uint32_t)i;
+          S.npos[nd.lo + q] = (uint16_t)dest;
+          // the position's side (a bit per position of this node in LDS)
+          const int pq = nd.lo + q;
+          if (l) atomicOr(&sbits[pq >> 5], 1u << (pq & 31));
+          else atomicAnd(&sbits[pq >> 5], ~(1u << (pq & 31)));
         }
         lo_l += tl; lo_r += tr;
         __syncthreads();
       }
       for (int q = tid; q < cnt; q += XT) S.idx[nd.lo + q] = (int32_t)S.keys[nd.lo + q];
       __syncthreads();
-      // every feature's value-ordered list of the node, stable-partitioned into its children's
-      // segments of the next level's lists (one wave per feature)
-      {
-        for (int f = wid; f < fp.p; f += XW) {
-          const uint16_t* src = S.La + (int64_t)f * n + nd.lo;
-          uint16_t* dst = S.Lb + (int64_t)f * n + nd.lo;
-          int ol = 0, orr = d.nl;
-          for (int c0 = 0; c0 < cnt; c0 += 64 * 8) {
-            int rv[8];
+      // every feature's value-ordered entries, stable-partitioned into the children's segments
+      // of the next level's lists (one wave per feature)
+      for (int f = wid; f < fp.p; f += XW) {
+        const uint32_t* src = S.La + (int64_t)f * mc + nd.lo;
+        uint32_t* dst = S.Lb + (int64_t)f * mc + nd.lo;
+        int ol = 0, orr = d.nl;
+        for (int c0 = 0; c0 < cnt; c0 += 64 * 8) {
+          uint32_t ev[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int q = c0 + u * 64 + lane;
-              rv[u] = q < cnt ? (int)src[q] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const bool in = c0 + u * 64 + lane < cnt;
-              const bool l = in && bit(rv[u]);
-              const uint64_t bl = __ballot(l), br = __ballot(in && !l);
-              if (in) dst[l ? ol + __popcll(bl & below) : orr + __popcll(br & below)] = (uint16_t)rv[u];
-              ol += __popcll(bl);
-              orr += __popcll(br);
-            }
+          for (int u = 0; u < 8; ++u) {
+            const int q = c0 + u * 64 + lane;
+            ev[u] = q < cnt ? src[q] : 0u;
           }
-          ATE_DASSERT(ol == d.nl && orr == cnt);
+          uint16_t np[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) np[u] = c0 + u * 64 + lane < cnt ? S.npos[ev[u] & 0xFFFFu] : 0;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const bool in = c0 + u * 64 + lane < cnt;
+            const bool l = in && bit((int)(ev[u] & 0xFFFFu));
+            const uint64_t bl = __ballot(l), br = __ballot(in && !l);
+            if (in)
+              dst[l ? ol + __popcll(bl & below) : orr + __popcll(br & below)] =
+                  (ev[u] & 0xFFFF0000u) | (uint32_t)np[u];
+            ol += __popcll(bl);
+            orr += __popcll(br);
+          }
         }
-        __syncthreads();
+        ATE_DASSERT(ol == d.nl && orr == cnt);
       }
+      __syncthreads();
     }
     XPHASE(5);
     {                                          // wave-level nodes, staged in the wave's LDS
@@ -872,8 +919,10 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           const bool l = in && xf[i] <= d.thr;
           const uint64_t bl = __ballot(l), br = __ballot(in && !l);
           if (in) {
-            Kw[l ? lo_l + __popcll(bl & below) : lo_r + __popcll(br & below)] = (uint32_t)i;
-            S.side[i] = l ? 1 : 0;
+            const int dl = l ? lo_l + __popcll(bl & below) : lo_r + __popcll(br & below);
+            Kw[dl] = (uint32_t)i;
+            S.side[nd.lo + q] = l ? 1 : 0;
+            S.npos[nd.lo + q] = (uint16_t)(nd.lo + dl);
           }
           lo_l += __popcll(bl);
           lo_r += __popcll(br);
@@ -885,31 +934,37 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         // every feature's value-ordered segment into its children's segments of the next
         // level's lists (four features per batch: their loads in flight together)
         for (int f0 = 0; f0 < fp.p; f0 += 4) {
-          int rv[4][4];
-          uint8_t sv[4][4];
+          uint32_t ev[4][4];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int q = u * 64 + lane;
-              rv[e][u] = (f0 + e < fp.p && q < cnt) ? (int)S.La[(int64_t)(f0 + e) * n + nd.lo + q] : 0;
+              ev[e][u] = (f0 + e < fp.p && q < cnt) ? S.La[(int64_t)(f0 + e) * mc + nd.lo + q] : 0u;
             }
+          uint8_t sv[4][4];
+          uint16_t np[4][4];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-              sv[e][u] = (f0 + e < fp.p && u * 64 + lane < cnt) ? S.side[rv[e][u]] : 0;
+            for (int u = 0; u < 4; ++u) {
+              const bool ok = f0 + e < fp.p && u * 64 + lane < cnt;
+              sv[e][u] = ok ? S.side[ev[e][u] & 0xFFFFu] : 0;
+              np[e][u] = ok ? S.npos[ev[e][u] & 0xFFFFu] : 0;
+            }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (f0 + e >= fp.p) break;
-            uint16_t* dst = S.Lb + (int64_t)(f0 + e) * n + nd.lo;
+            uint32_t* dst = S.Lb + (int64_t)(f0 + e) * mc + nd.lo;
             int ol = 0, orr = d.nl;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const bool in = u * 64 + lane < cnt;
               const bool l = in && sv[e][u];
               const uint64_t bl = __ballot(l), br = __ballot(in && !l);
-              if (in) dst[l ? ol + __popcll(bl & below) : orr + __popcll(br & below)] = (uint16_t)rv[e][u];
+              if (in)
+                dst[l ? ol + __popcll(bl & below) : orr + __popcll(br & below)] =
+                    (ev[e][u] & 0xFFFF0000u) | (uint32_t)np[e][u];
               ol += __popcll(bl);
               orr += __popcll(br);
             }
@@ -926,7 +981,7 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
       XRng* tmp = S.cur;
       S.cur = S.nxt;
       S.nxt = tmp;
-      uint16_t* tl = S.La;                    // ... and the partitioned row lists the current
+      uint32_t* tl = S.La;                    // ... and the partitioned lists the current
       S.La = S.Lb;
       S.Lb = tl;
     }
@@ -968,13 +1023,13 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
 
 }  // namespace
 
-ATE_API int64_t ate_forest_exact_scratch_bytes(int n, int p, int ntree) {
-  return tree_bytes(n, p) * (int64_t)ntree;
+ATE_API int64_t ate_forest_exact_scratch_bytes(int n, int p, int mc, int ntree) {
+  return tree_bytes(n, p, mc) * (int64_t)ntree;
 }
 
 // Grow trees [tbeg, tbeg + ntree_chunk) of the forest (scratch: ntree_chunk trees).
 // grf sampling (fp.sampling == 1, kinds 1/2) needs est ([ntree * cap][5] int64).
-ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, const void* Xb,
+ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, int mc, const void* Xb,
                                  const void* order, const void* vals, int ldv, const void* nval, const void* ycls,
                                  const void* r1, const void* r2, int cap, void* feat, void* thr,
                                  void* left, void* val, void* nnodes, void* inbag, void* est,
@@ -983,8 +1038,9 @@ ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, const vo
   if (fp.p > XPMAX || fp.n <= 0 || fp.n > 65536) return -1;
   if (fp.sampling == 0 ? fp.kind == 2 : (fp.kind == 0 || !est || (fp.kind == 2 && !r2))) return -1;
   if (tbeg < 0 || nchunk < 1 || tbeg + nchunk > fp.ntree) return -1;
+  if (mc < 1 || mc > fp.n) return -1;
   hipLaunchKernelGGL(forest_exact_kernel, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
-                     (const uint16_t*)Xb, (const int32_t*)order, (const double*)vals, ldv, (const int32_t*)nval,
+                     mc, (const uint16_t*)Xb, (const uint32_t*)order, (const double*)vals, ldv, (const int32_t*)nval,
                      (const uint8_t*)ycls, (const int64_t*)r1, (const int64_t*)r2, cap,
                      (int32_t*)feat, (int32_t*)thr, (int32_t*)left, (double*)val, (int32_t*)nnodes,
                      (uint8_t*)inbag, (int64_t*)est, (char*)scratch);

@@ -417,8 +417,10 @@ __global__ __launch_bounds__(256) void lv_big_hist_kernel(LvArgs a, const int32_
   const int nk = min(LV_FG, nf - k0);
   const LNode nd = a.cur[blist[slot]];
   const int n = a.fp.n;
+  // positions are global over the forest's trees (tree t's in-bag rows after tree t-1's),
+  // so a node's range is bounded by ntree * n, not by n
   ATE_DASSERT(nd.lo <= item_q0[it] && item_q0[it] <= item_q1[it] && item_q1[it] <= nd.hi &&
-              nd.hi <= n && nk <= LV_FG && k0 + nk <= LV_MAXF);
+              (int64_t)nd.hi <= (int64_t)a.fp.ntree * n && nk <= LV_FG && k0 + nk <= LV_MAXF);
   const int32_t* wt = a.w + (int64_t)nd.tree * n;
   for (int e = threadIdx.x; e < LV_FG * 2 * NBINS; e += 256) (&sh[0][0][0])[e] = 0;
   int fi[LV_FG], sp[LV_FG];

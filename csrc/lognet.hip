@@ -524,7 +524,7 @@ __global__ __launch_bounds__(NT) void lognet_cvloss_kernel(
   }
   const int s = hold[k];
   const int64_t r0 = segs[2 * s], r1 = segs[2 * s + 1];
-  ATE_DASSERT(s >= 0 && r0 >= 0 && r0 < r1 && r1 <= ld && m < L);
+  ATE_DASSERT(s >= 0 && r0 >= 0 && r0 <= r1 && r1 <= ld && m < L);
   const double* b = beta + ((int64_t)k * L + m) * p;
   const double b0 = a0[(int64_t)k * L + m];
   double acc[1] = {0.0};

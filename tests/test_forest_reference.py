@@ -144,3 +144,16 @@ def test_gpu_exact_split_kernel_equals_numpy_oracle(gpu, name):
     eng, ref, _ = _fit_both(name, backend="gpu", exact=True)
     assert eng.backend == "gpu"
     assert_same_trees(eng, ref)
+
+
+@pytest.mark.parametrize("n,group,sf,honesty", [(160, 2, 0.5, True), (161, 2, 0.5, False),
+                                                (500, 1, 0.5, True), (333, 1, 0.6, True),
+                                                (777, 2, 0.3, True), (50, 4, 0.5, True)])
+def test_exact_mcap_is_the_in_bag_count(n, group, sf, honesty):
+    """models/forest.exact_mcap (the per-position scratch size of csrc/forest_exact.hip) equals
+    the J1 row count the oracle's grf sampling draws for every tree."""
+    P = R.Params(kind=2, sampling=1, group=group, sample_fraction=sf, honesty=honesty, seed=7)
+    for tg in range(5):
+        w, _, _ = R._tree_rows(P, n, tg)
+        assert int((w > 0).sum()) == F.exact_mcap(n, 1, group, sf, honesty)
+    assert F.exact_mcap(n, 0, 1, 0.5, False) == n
