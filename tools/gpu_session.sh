@@ -144,6 +144,10 @@ print(sys.argv[3], len(d), 'kernels, mean %.1f us, median %.1f us' % (st.mean(d)
       run configs 900 python -u tools/bench_configs.py ;;
     replicate)
       run replicate 600 python -u tools/replicate_timing.py ;;
+    replicate:*) # replicate:NAME -- the same passes on _lib/libatehip_NAME.so
+      nm=${step#replicate:}
+      ATE_HIP_LIB=$ROOT/ate_replication_causalml_amd/_lib/libatehip_$nm.so \
+        run "replicate_$nm" 600 python -u tools/replicate_timing.py ;;
     gramdump)    # the bench panel's fold Gram stack for tools/enet_sim.py
       run gramdump 200 python -u tools/dump_bench_gram.py "$OUT/gram_dump" ;;
     *)
