@@ -13,7 +13,7 @@
 // of the value ranks, `order` [p][n]); a tree's root list of feature f is that order
 // filtered to its in-bag rows (one wave per feature), and every split stable-partitions each
 // feature's list segment into its children's segments of the next level's lists (double-
-// buffered [p][n] uint16 row ids), so every node's rows are in value order for every feature
+// buffered [p][mc] entries (value rank, position)), so every node's rows are in value order for every feature
 // at all times. Ties between equal values never matter (the criterion is only evaluated
 // between distinct values, at the same positions for any order of ties): the trees are the
 // same bits as a sort per node and as the host twin.
@@ -22,7 +22,9 @@
 //  * nodes of <= WCAP (256) rows are decided and partitioned by ONE WAVE each, without
 //    workgroup barriers (node j goes to wave j mod 8): lane l owns list positions
 //    [l ch, l ch + ch), ch <= 4; the rows' statistics are gathered by row id, summed by a
-//    wave scan, and the partition moves four features' segments per batch;
+//    wave scan, and the partition moves four features' segments per batch; in forests of
+//    mtry <= 8, nodes of <= 64 rows hold a row per lane and rank values by lane compares,
+//    and lists are not partitioned into children of <= 64 rows (no node reads them);
 //  * larger nodes are decided by the whole workgroup, one at a time: per feature a chunk of
 //    list positions per thread, a workgroup scan of the chunk sums, an argmax reduction; their
 //    partitions run one wave per feature, the rows' sides in an LDS bit per row;
@@ -68,6 +70,14 @@ constexpr int XW = XT / 64;        // waves per tree
 #define EXACT_MINWG 4          // __launch_bounds__ minimum waves per SIMD
 #endif
 constexpr int WCAP = EXACT_WCAP;   // nodes up to this many rows: one wave each
+// Nodes of <= SMALL rows hold a row per lane and rank each candidate feature's values by lane
+// compares (no list reads); their children are as small, so the lists of a split whose
+// children both have <= SMALL rows are never partitioned (most nodes of a deep tree).
+constexpr int SMALL = 64;
+// ... for forests of few candidate features per node (randomForest's mtry 4 / 7 at p = 21):
+// at grf's mtry (all 21 features) 21 lane-compare rankings per node cost more than reading
+// the node's list segments (config 4: 0.70 -> 0.76 s), so grf forests keep the lists
+constexpr int SMALL_MTRY = 8;
 // one LDS arena: per wave, a wave-level node's partition staging (WCAP row ids); or
 // (large-node phases) a bit per row: in-bag rows / rows going left
 constexpr int WSLICE = WCAP * 4;   // a wave-level node's partition staging (row ids)
@@ -245,6 +255,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// lane dst_lane receives v (ds_permute: a push, a bijection when the lanes' targets are)
+__device__ __forceinline__ uint32_t permute_u32(int dst_lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_permute(dst_lane << 2, (int)v);
+}
+__device__ __forceinline__ int64_t permute_i64(int dst_lane, int64_t v) {
+  const uint32_t lo = permute_u32(dst_lane, (uint32_t)(uint64_t)v);
+  const uint32_t hi = permute_u32(dst_lane, (uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int64_t wave_excl_scan64(int64_t v, int lane) {
   int64_t x = v;
 #pragma unroll
@@ -290,6 +310,9 @@ __device__ int wave_threshold(const double* __restrict__ v, int blo, int bhi, in
   return lo;
 }
 
+// LANES: the lane-per-row path for nodes of <= SMALL rows (forests of mtry <= SMALL_MTRY); a
+// separate instantiation, so the list-only kernel keeps its register allocation
+template <bool LANES>
 __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
     ForestParams fp, int tbeg, int mc, const uint16_t* __restrict__ Xb,
     const uint32_t* __restrict__ order,
@@ -701,14 +724,18 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           st.cn = causal_node((double)cnt, wave_sum64(ca), wave_sum64(cb), wave_sum64(cc),
                               wave_sum64(cd));
         }
-        int64_t a = 0, b1 = 0;
+        const bool small = LANES && cnt <= SMALL;
+        int64_t a = 0, b1 = 0, y0 = 0, y1 = 0;  // y*: the lane's first row (small nodes)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (lane + 64 * u < cnt) {
             int64_t x0, x1;
             row_stats(fp, S.w, ycls, r1, r2, st.cn, iv[u], x0, x1);
-            S.sx0[nd.lo + lane + 64 * u] = x0;    // by position (the list entries carry it)
-            S.sx1[nd.lo + lane + 64 * u] = x1;
+            if (!small) {
+              S.sx0[nd.lo + lane + 64 * u] = x0;  // by position (the list entries carry it)
+              S.sx1[nd.lo + lane + 64 * u] = x1;
+            }
+            if (u == 0) { y0 = x0; y1 = x1; }
             a += x0; b1 += x1;
           }
         a = wave_sum64(a); b1 = wave_sum64(b1);
@@ -731,7 +758,50 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         const int s0 = min(cnt, lane * ch), s1 = min(cnt, s0 + ch);
         double best = -INFINITY;
         int bf = -1, blo = -1, bhi = -1, bnl = 0;
-        for (int k = 0; k < nf; ++k) {
+        // a row per lane: each feature's value ranks by lane compares, the rows' statistics
+        // moved to their ranks (ds_permute) and prefix-summed; the boundaries between distinct
+        // values are the list positions' boundaries, so the decision is the same
+        const bool live = lane < cnt;
+        constexpr int PF = 4;                  // bins of up to 4 features fetched together
+        uint32_t bins[PF];
+        for (int k = 0; LANES && small && k < nf; ++k) {
+          const int f = perm[k];
+          if ((k % PF) == 0) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u)
+              bins[u] = (live && k + u < nf) ? (uint32_t)Xb[(int64_t)perm[k + u] * n + iv[0]] : 0u;
+          }
+          uint32_t bk = bins[0];
+#pragma unroll
+          for (int u = 1; u < PF; ++u) bk = (k % PF) == u ? bins[u] : bk;
+          // idle lanes rank last with distinct keys (ranks cnt..63: the permute is a bijection)
+          const uint32_t key = live ? ((bk << 16) | (uint32_t)lane) : (0xFFFF0000u | (uint32_t)lane);
+          int rank = 0;
+          for (int q = 0; q < 64; ++q) rank += (uint32_t)__builtin_amdgcn_readlane((int)key, q) < key;
+          const uint32_t ks = permute_u32(rank, key);
+          int64_t c0 = permute_i64(rank, y0), c1 = permute_i64(rank, y1);
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int64_t u0 = __shfl_up(c0, o, 64), u1 = __shfl_up(c1, o, 64);
+            if (lane >= o) { c0 += u0; c1 += u1; }
+          }
+          const uint32_t kn = __shfl_down(ks, 1, 64);
+          double cr = -INFINITY;
+          int s = 0x7FFFFFFF;
+          if (lane + 1 < cnt && (ks >> 16) != (kn >> 16)) {
+            cr = boundary_crit(fp, st, minc, c0, c1);
+            s = lane;
+          }
+          wave_argmax(cr, s);
+          if (cr > best) {                      // uniform
+            best = cr;
+            bf = f;
+            blo = (int)(__shfl(ks, s, 64) >> 16);
+            bhi = (int)(__shfl(kn, s, 64) >> 16);
+            bnl = s + 1;
+          }
+        }
+        for (int k = 0; !small && k < nf; ++k) {
           const int f = perm[k];
           const uint32_t* Lf = S.La + (int64_t)f * mc + nd.lo;
           uint32_t ev[4];
@@ -911,6 +981,8 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         const XDec d = S.dec[j];
         if (!d.split) continue;
         const uint16_t* xf = Xb + (int64_t)d.feat * n;
+        // children of <= SMALL rows never read their lists
+        const bool lists = !LANES || d.nl > SMALL || cnt - d.nl > SMALL;
         int lo_l = 0, lo_r = d.nl;
         for (int c0 = 0; c0 < cnt; c0 += 64) {
           const int q = c0 + lane;
@@ -921,8 +993,10 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
           if (in) {
             const int dl = l ? lo_l + __popcll(bl & below) : lo_r + __popcll(br & below);
             Kw[dl] = (uint32_t)i;
-            S.side[nd.lo + q] = l ? 1 : 0;
-            S.npos[nd.lo + q] = (uint16_t)(nd.lo + dl);
+            if (lists) {
+              S.side[nd.lo + q] = l ? 1 : 0;
+              S.npos[nd.lo + q] = (uint16_t)(nd.lo + dl);
+            }
           }
           lo_l += __popcll(bl);
           lo_r += __popcll(br);
@@ -931,6 +1005,10 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         for (int q = lane; q < cnt; q += 64) S.idx[nd.lo + q] = (int32_t)Kw[q];
+        if (!lists) {
+          wave_sync();
+          continue;
+        }
         // every feature's value-ordered segment into its children's segments of the next
         // level's lists (four features per batch: their loads in flight together)
         for (int f0 = 0; f0 < fp.p; f0 += 4) {
@@ -1039,7 +1117,8 @@ ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, int mc, 
   if (fp.sampling == 0 ? fp.kind == 2 : (fp.kind == 0 || !est || (fp.kind == 2 && !r2))) return -1;
   if (tbeg < 0 || nchunk < 1 || tbeg + nchunk > fp.ntree) return -1;
   if (mc < 1 || mc > fp.n) return -1;
-  hipLaunchKernelGGL(forest_exact_kernel, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
+  auto kern = fp.mtry <= SMALL_MTRY ? forest_exact_kernel<true> : forest_exact_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
                      mc, (const uint16_t*)Xb, (const uint32_t*)order, (const double*)vals, ldv, (const int32_t*)nval,
                      (const uint8_t*)ycls, (const int64_t*)r1, (const int64_t*)r2, cap,
                      (int32_t*)feat, (int32_t*)thr, (int32_t*)left, (double*)val, (int32_t*)nnodes,

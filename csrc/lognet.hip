@@ -49,15 +49,16 @@ __device__ __forceinline__ double rl_d(double v, int i) {
   return __hiloint2double(hi, lo);
 }
 
-template <int PM>
+template <int PM, int NTK>
 struct Cfg {
   static constexpr int Q = PM + 1;                        // Gram stride: 1, x_1..x_p
   static constexpr int QA = PM + 2;                       // + r/v column (gradient)
   static constexpr int NB = (QA + 3) / 4;                 // 4-wide column blocks
   static constexpr int QP = NB * 4;                       // LDS row stride (doubles)
   static constexpr int NPAIR = NB * (NB + 1) / 2;
-  static constexpr int TPT = (NPAIR + NT - 1) / NT;       // block pairs per thread
-  static constexpr int RB = PM <= 32 ? 256 : 64;          // staged rows per chunk
+  static constexpr int TPT = (NPAIR + NTK - 1) / NTK;     // block pairs per thread
+  // staged rows per chunk: one per thread up to p = 24 (LDS: 512 x 28 doubles)
+  static constexpr int RB = PM <= 24 ? NTK : PM <= 32 ? 256 : 64;
   static constexpr int NCH = (PM + 63) / 64;
 };
 
@@ -69,8 +70,8 @@ __device__ __forceinline__ double clampq(double eta) {
   return fmin(fmax(q, PMIN), 1.0 - PMIN);
 }
 
-template <typename T, int PM>
-__global__ __launch_bounds__(NT) void lognet_path_kernel(
+template <typename T, int PM, int NTK>
+__global__ __launch_bounds__(NTK) void lognet_path_kernel(
     const T* __restrict__ X, int64_t ld, const int* __restrict__ xcols, int p, int ycol,
     const int64_t* __restrict__ segs, int nseg, const uint8_t* __restrict__ masks,
     const double* __restrict__ vp_in, double alpha, double flmin, double thresh, int maxit,
@@ -78,13 +79,13 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     double* __restrict__ a0_out, double* __restrict__ beta_out, double* __restrict__ lam_out,
     double* __restrict__ dev_out, int* __restrict__ nlam_out, int* __restrict__ npass_out,
     int* __restrict__ progress, double* __restrict__ lampub) {
-  using C = Cfg<PM>;
+  using C = Cfg<PM, NTK>;
   constexpr int Q = C::Q, QP = C::QP, RB = C::RB, TPT = C::TPT, NCH = C::NCH;
   __shared__ double sC[Q * Q];
   __shared__ double sg[Q];
   __shared__ __attribute__((aligned(16))) double sZ[RB * QP];   // staged rows / reduce scratch
   __shared__ double sV[RB];
-  __shared__ double sxm[PM], sxs[PM];
+  __shared__ double sxm[PM], sxs[PM], sxr[PM];   // sxr: 1 / SD (0: constant column)
   __shared__ double sb[Q];                    // sb[0] = intercept (standardised scale)
   __shared__ int sju[PM], sxc[PM];
   __shared__ int64_t sr0[MAXSEG];
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
     spre[k] = acc;
     sictl[0] = k;
   }
-  for (int j = tid; j < p; j += NT) sxc[j] = xcols[j];
+  for (int j = tid; j < p; j += NTK) sxc[j] = xcols[j];
   __syncthreads();
   const int nts = sictl[0];
   const int ntr = spre[nts];
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   const T* Yc = X + (int64_t)ycol * ld;
 
   // ---- standardisation (population SD, weights 1/n) and the null model
-  for (int j = wid; j < p; j += NT / 64) {
+  for (int j = wid; j < p; j += NTK / 64) {
     const T* xc = X + (int64_t)sxc[j] * ld;
     double s1 = 0.0, s2 = 0.0;
     for (int v = lane; v < ntr; v += 64) {
@@ -141,15 +142,16 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
       sxm[j] = xm;
       sju[j] = xs > 0.0;
       sxs[j] = xs > 0.0 ? xs : 1.0;
+      sxr[j] = xs > 0.0 ? 1.0 / xs : 0.0;
     }
   }
   {
     double acc[1] = {0.0};
-    for (int v = tid; v < ntr; v += NT) acc[0] += ld_x(Yc, vrow(v));
+    for (int v = tid; v < ntr; v += NTK) acc[0] += ld_x(Yc, vrow(v));
     ate::block_sum<1>(acc, red);
     if (tid == 0) sctl[1] = acc[0] * w;
   }
-  for (int j = tid; j < Q; j += NT) sb[j] = 0.0;
+  for (int j = tid; j < Q; j += NTK) sb[j] = 0.0;
   __syncthreads();
   const double q0 = sctl[1];
   const double q0c = fmin(fmax(q0, PMIN), 1.0 - PMIN);
@@ -158,12 +160,12 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
 
   // ---- Gram task layout (runtime p): column blocks of 4 over [1, z_1..z_p, r/v]
   const int qa = p + 2, nb = (qa + 3) / 4, npair = nb * (nb + 1) / 2;
-  const int ngrp = npair >= NT ? 1 : NT / npair;
+  const int ngrp = npair >= NTK ? 1 : NTK / npair;
   const int grp = ngrp == 1 ? 0 : tid / npair;
   int pa[TPT], pb[TPT];
 #pragma unroll
   for (int q = 0; q < TPT; ++q) {
-    const int t = ngrp == 1 ? tid + q * NT : (q == 0 && grp < ngrp ? tid % npair : npair);
+    const int t = ngrp == 1 ? tid + q * NTK : (q == 0 && grp < ngrp ? tid % npair : npair);
     pa[q] = pb[q] = -1;
     if (t < npair) {
       int a = 0, rem = t;
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
       for (int e = 0; e < 16; ++e) acc[q][e] = 0.0;
     double devl = 0.0;
     for (int base = 0; base < ntr; base += RB) {
-      for (int t = tid; t < RB; t += NT) {
+      for (int t = tid; t < RB; t += NTK) {
         double* z = sZ + t * QP;
         if (base + t < ntr) {
           const int64_t row = vrow(base + t);
@@ -250,7 +252,9 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
             for (int u = 0; u < 16; ++u) {
               const int j = jb + u;
               if (j < p) {
-                const double zv = sju[j] ? (xr[u] - sxm[j]) / sxs[j] : 0.0;
+                // multiply by the reciprocal SD: a division per element and pass cost
+                // as much as the rest of the row's staging
+                const double zv = (xr[u] - sxm[j]) * sxr[j];
                 z[1 + j] = zv;
                 eta += zv * sb[1 + j];
               }
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
 #pragma unroll
       for (int q = 0; q < TPT; ++q)
         if (pa[q] >= 0) {
-          const int pair = tid + q * NT;
+          const int pair = tid + q * NTK;
 #pragma unroll
           for (int e = 0; e < 16; ++e) emit(pair, e, acc[q][e]);
         }
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
 #pragma unroll
         for (int e = 0; e < 16; ++e) sZ[(grp * npair + tid % npair) * 16 + e] = acc[0][e];
       __syncthreads();
-      for (int t = tid; t < npair * 16; t += NT) {
+      for (int t = tid; t < npair * 16; t += NTK) {
         double sum = 0.0;
         for (int gq = 0; gq < ngrp; ++gq) sum += sZ[(gq * npair) * 16 + t];
         emit(t >> 4, t & 15, sum);
@@ -479,7 +483,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
       a0_out[(int64_t)prob * L + m] = sb[0];
       lam_out[(int64_t)prob * L + m] = alm;
     }
-    for (int j = tid; j < p; j += NT) bo[(int64_t)m * p + j] = sb[1 + j];
+    for (int j = tid; j < p; j += NTK) bo[(int64_t)m * p + j] = sb[1 + j];
     nlam_eff = m + 1;
     __syncthreads();
   }
@@ -492,7 +496,7 @@ __global__ __launch_bounds__(NT) void lognet_path_kernel(
   // ---- back to the original scale; lambda_0 extrapolated as glmnet does
   for (int m = 0; m < nlam_eff; ++m) {
     double part[1] = {0.0};
-    for (int j = tid; j < p; j += NT) {
+    for (int j = tid; j < p; j += NTK) {
       double bj = sju[j] ? bo[(int64_t)m * p + j] / sxs[j] : 0.0;
       bo[(int64_t)m * p + j] = bj;
       part[0] += bj * sxm[j];
@@ -545,12 +549,16 @@ int launch_path(const void* X, int64_t ld, const int* xcols, int p, int ycol, co
                 double flmin, double thresh, int maxit, const double* ulam, const int* nlam_in,
                 int L, double* a0, double* beta, double* lam, double* dev, int* nlam_out,
                 int* npass, int* progress, double* lampub, hipStream_t st) {
-  if (p <= 32)
-    hipLaunchKernelGGL((lognet_path_kernel<T, 32>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
+  if (p <= 24)
+    hipLaunchKernelGGL((lognet_path_kernel<T, 24, 512>), dim3(nprob), dim3(512), 0, st, (const T*)X,
+                       ld, xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
+                       nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
+  else if (p <= 32)
+    hipLaunchKernelGGL((lognet_path_kernel<T, 32, NT>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
                        xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
                        nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   else
-    hipLaunchKernelGGL((lognet_path_kernel<T, 96>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
+    hipLaunchKernelGGL((lognet_path_kernel<T, 96, NT>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
                        xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
                        nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   return 0;

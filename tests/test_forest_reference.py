@@ -32,8 +32,8 @@ CASES = {
 }
 
 
-def _fit_both(name, backend="cpu", ntree=4, t0=0, exact=False):
-    X, w, y = _data()
+def _fit_both(name, backend="cpu", ntree=4, t0=0, exact=False, n=160):
+    X, w, y = _data(n)
     c = CASES[name]
     kind = c["kind"]
     if exact:
@@ -143,6 +143,21 @@ def test_gpu_exact_split_kernel_equals_numpy_oracle(gpu, name):
     """csrc/forest_exact.hip against the oracle."""
     eng, ref, _ = _fit_both(name, backend="gpu", exact=True)
     assert eng.backend == "gpu"
+    assert_same_trees(eng, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rf_class", "rf_reg", "grf_causal"])
+def test_gpu_exact_split_kernel_large_nodes_equals_oracle(gpu, name):
+    """n = 3000: workgroup-level nodes (> 256 rows), wave-level list nodes and lane-per-row
+    nodes (<= 64 rows, whose lists are never partitioned) in the same trees."""
+    eng, ref, _ = _fit_both(name, backend="gpu", exact=True, ntree=2, n=3000)
+    assert max(tr["nnodes"] for tr in ref) > 200
+    assert_same_trees(eng, ref)
+
+
+def test_cpu_exact_split_engine_large_nodes_equals_oracle():
+    eng, ref, _ = _fit_both("rf_reg", exact=True, ntree=1, n=3000)
     assert_same_trees(eng, ref)
 
 
