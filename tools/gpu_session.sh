@@ -84,6 +84,11 @@ for step in "$@"; do
       done ;;
     enet_prof)
       run enet_prof 300 python tools/enet_profile.py ;;
+    enet_prof_rct)
+      ATE_DGP=rct run enet_prof_rct 300 python tools/enet_profile.py ;;
+    enet_clock)  # path kernel clock alone vs beside a Gram (tools/enet_profile.py --build first)
+      run enet_clock 200 python -u tools/enet_clock.py && \
+      ATE_DGP=rct run enet_clock_rct 200 python -u tools/enet_clock.py ;;
     cfg4)        # config 4 on one GPU (all trees, all replicates) and rank 0's share of 8
       run cfg4 300 python -u tools/cfg4.py --rows 50000 && \
       run cfg4_shard 300 python -u tools/cfg4.py --rows 50000 --shard 0/8 ;;
