@@ -333,10 +333,27 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
     *reinterpret_cast<f32x4*>(out + i * 256 + lane * 4) = acc[i];
 }
 
+#ifdef GRAM_CLOCK
+// profiling build (tools/enet_profile.py --build): per-workgroup shader clock cycles [0] and
+// 100 MHz wall ticks [1] of the tile kernel, workgroups [2] (tools/enet_clock.py: the Gram's
+// clock alone and beside the CV path kernel)
+__device__ unsigned long long gram_clock[3];
+extern "C" __attribute__((visibility("default"))) int ate_gram_clock_read(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(gram_clock), sizeof(gram_clock));
+}
+extern "C" __attribute__((visibility("default"))) int ate_gram_clock_reset() {
+  static unsigned long long z[3];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(gram_clock), z, sizeof(z));
+}
+#endif
+
 __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
     const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const int4* __restrict__ tiles, int ntiles,
     const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][GT * GK];   // 128 KB
+#ifdef GRAM_CLOCK
+  const unsigned long long gc0 = clock64(), gw0 = wall_clock64();
+#endif
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int c = L / ntiles, t = L % ntiles;
   ATE_DASSERT(c < nchunks && t < ntiles);
@@ -368,6 +385,14 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
     pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
   else
     pair_wave<false>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
+#ifdef GRAM_CLOCK
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&gram_clock[0], (unsigned long long)(clock64() - gc0));
+    atomicAdd(&gram_clock[1], (unsigned long long)(wall_clock64() - gw0));
+    atomicAdd(&gram_clock[2], 1ull);
+  }
+#endif
 }
 
 // Exact (world-size-invariant) reduction: a chunk partial v is split into two int64 limbs

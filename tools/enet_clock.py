@@ -1,6 +1,8 @@
 """Shader clock of the CV path kernel alone vs beside a running Gram (DVFS under load):
 the profiling build's per-problem clock64 / wall_clock64 deltas ([10] / [11], csrc/enet.hip
-ENET_PROF) give each problem's average clock. Also the wall time of the path launch.
+ENET_PROF) give each problem's average clock. Also the wall time of the path launch. Then
+the Gram tile kernel's own clock (csrc/gram.hip GRAM_CLOCK: per-workgroup clock64 /
+wall_clock64) alone and beside path launches on another stream.
 
   python tools/enet_profile.py --build     # here: the profiling library
   python tools/enet_clock.py               # GPU box
@@ -61,6 +63,28 @@ def main():
                                          "clock_ghz_median": round(float(np.median(ghz)), 3),
                                          "clock_ghz_min": round(float(ghz.min()), 3),
                                          "clock_ghz_max": round(float(ghz.max()), 3)})
+    # the Gram tile kernel's own clock (GRAM_CLOCK build): alone, and beside path launches
+    lib.ate_gram_clock_read.argtypes = [ctypes.c_void_p]
+    for mode in ("gram_alone", "gram_beside_path", "gram_alone"):
+        torch.cuda.synchronize()
+        lib.ate_gram_clock_reset()
+        if mode == "gram_beside_path":
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(4):
+                    path()
+        e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e[0].record()
+        for _ in range(3):
+            G.gram(pan, stage="tiles")
+        e[1].record()
+        torch.cuda.synchronize()
+        gc = np.zeros(3, dtype=np.uint64)
+        lib.ate_gram_clock_read(gc.ctypes.data_as(ctypes.c_void_p))
+        out.setdefault(mode, []).append({
+            "gram_ms": round(e[0].elapsed_time(e[1]) / 3, 3),
+            "clock_ghz_mean": round(float(gc[0]) / max(float(gc[1]), 1.0) * 0.1, 3),
+            "workgroups": int(gc[2])})
     print(json.dumps(out), flush=True)
 
 

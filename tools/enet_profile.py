@@ -21,13 +21,14 @@ def build():
     from ate_replication_causalml_amd import _build as B
     B.build_hip()
     objs = sorted((ROOT / "build").glob("*.hip.o"))
-    objs = [o for o in objs if o.name != "enet.hip.o"]
-    prof_o = ROOT / "build" / "enet_prof.o"
-    subprocess.run([B.HIPCC, "-O3", "-fPIC", "-std=c++17", f"--offload-arch={B.ARCH}",
-                    "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-DENET_PROF", "-c",
-                    str(ROOT / "csrc" / "enet.hip"), "-o", str(prof_o)], check=True)
+    objs = [o for o in objs if o.name not in ("enet.hip.o", "gram.hip.o")]
+    prof = []
+    for src, flag in (("enet", "-DENET_PROF"), ("gram", "-DGRAM_CLOCK")):
+        o = ROOT / "build" / f"{src}_prof.o"
+        subprocess.run(B.hip_compile_cmd(ROOT / "csrc" / f"{src}.hip", o) + [flag], check=True)
+        prof.append(str(o))
     subprocess.run([B.HIPCC, "-shared", f"--offload-arch={B.ARCH}", "-o", str(LIB),
-                    *map(str, objs), str(prof_o)], check=True)
+                    *map(str, objs), *prof], check=True)
     print("built", LIB)
 
 
