@@ -229,6 +229,30 @@ __global__ __launch_bounds__(512) void gram_bf16_256_kernel(
 // hits L2 on what the other fetched). Every wave writes its 16x16 blocks contiguously
 // into a 272-block slab slot; a host-built table maps slab blocks to Gram blocks.
 constexpr int PAIR_SLOTS = 272;
+#ifndef GRAM_NSTAGE
+// > 2 (or GRAM_RING=1): the paired-tile K-loop runs a ring of GRAM_NSTAGE stages of 32 rows
+// (NSTAGE - 1 of them in flight while one is multiplied) instead of two 64-row stages (one
+// in flight). Measured slower (profiles/r05_gram_ring): A/B builds only.
+#define GRAM_NSTAGE 2
+#endif
+#ifndef GRAM_RING
+#define GRAM_RING (GRAM_NSTAGE > 2)
+#endif
+constexpr int PKS = GRAM_RING ? 32 : GK;                     // rows per stage
+constexpr int PNS = GRAM_NSTAGE;                             // stages in the ring
+constexpr int PAIR_LDS = PNS * 2 * GT * PKS;                 // bf16 elements
+static_assert(PAIR_LDS * 2 <= 160 * 1024, "paired-tile LDS ring exceeds 160 KB");
+
+// s_waitcnt vmcnt(n) for a runtime n <= 15 (expcnt / lgkmcnt not waited on)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define WV(k) case k: __builtin_amdgcn_s_waitcnt(0x0F70 | k); break;
+    WV(0) WV(1) WV(2) WV(3) WV(4) WV(5) WV(6) WV(7)
+    WV(8) WV(9) WV(10) WV(11) WV(12) WV(13) WV(14) WV(15)
+#undef WV
+    default: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+  }
+}
 #ifndef GRAM_CROSS
 // 1: the two workgroups of a chunk issue a stage's 64 LDS-DMA pieces in crossed orders
 // (type-1 wave w issues what type-0 wave (w+4)%8 issues), so the pair never requests the same
@@ -255,13 +279,75 @@ template <bool TRI>
 __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t cs, int64_t bs, int a0,
                                           int b0, bool haveB, bool idle, int abuf, int bbuf,
                                           int arow0, int bcol0, const Chunk& ch,
-                                          bf16_t (*lds)[2][GT * GK], float* __restrict__ out,
+                                          bf16_t* lds_raw, float* __restrict__ out,
                                           bool second) {
   constexpr int NB = TRI ? 36 : 32;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   f32x4 acc[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#if GRAM_RING
+  // ---- ring of PNS stages of PKS = 32 rows: LDS image [stage][A|B][column][32 rows], four
+  // 16-byte pieces per column, piece p stored at slot p ^ ((col >> 1) & 3) (8 consecutive
+  // lanes of a fragment read hit 8 distinct 16-byte bank groups)
+  (void)second;
+  auto buf = [&](int st, int side) { return lds_raw + (st * 2 + side) * (GT * PKS); };
+  auto stage = [&](int st, int64_t i0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int q = wid * 2 + r;                       // 16-column group
+      const int col = q * 16 + (lane >> 2);
+      const int pc = (lane & 3) ^ ((col >> 1) & 3);    // piece this lane fetches
+      const bf16_t* Xk = X + (i0 >> 6) * bs + (i0 & 63) + pc * 8;
+      glds16(Xk + (int64_t)(a0 + col) * cs, buf(st, 0) + q * 16 * PKS);
+      if (haveB) glds16(Xk + (int64_t)(b0 + col) * cs, buf(st, 1) + q * 16 * PKS);
+    }
+  };
+  auto frag = [&](const bf16_t* P_, int col, int cc) {
+    return *reinterpret_cast<const bf16x8*>(&P_[col * PKS + ((cc ^ ((col >> 1) & 3)) << 3)]);
+  };
+  const int per = haveB ? 4 : 2;                        // LDS-DMA loads per thread per stage
+  const int64_t nsteps = (ch.row1 - ch.row0) / PKS;
+  for (int j = 0; j < PNS - 1; ++j)
+    if (j < nsteps) stage(j, ch.row0 + j * PKS);
+  for (int64_t s = 0; s < nsteps; ++s) {
+    // stage s landed: at most the later stages' loads are outstanding
+    const int64_t later = nsteps - 1 - s < PNS - 2 ? nsteps - 1 - s : PNS - 2;
+    wait_vmcnt((int)later * per);
+    __syncthreads();                                    // ... in every wave; stage s-1 consumed
+    if (s + PNS - 1 < nsteps) stage((int)((s + PNS - 1) % PNS), ch.row0 + (s + PNS - 1) * PKS);
+    const int cur = (int)(s % PNS);
+    const bf16_t* As = buf(cur, abuf);
+    const bf16_t* Bs = buf(cur, bbuf);
+    if (!idle) {
+      const int cc = lane >> 4;
+      if constexpr (!TRI) {
+        bf16x8 af[8], bfr[4];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) af[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bfr[n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n],
+                                                                      acc[m * 4 + n], 0, 0, 0);
+      } else {
+        bf16x8 fr[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) fr[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+#pragma unroll
+          for (int n = m; n < 8; ++n)
+            acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fr[m], fr[n], acc[tri_index(m, n)], 0, 0, 0);
+      }
+    }
+  }
+#else
+  bf16_t (*lds)[2][GT * GK] = reinterpret_cast<bf16_t (*)[2][GT * GK]>(lds_raw);
   // which 8-column pieces this wave copies (any wave may copy any piece: the LDS image only
   // depends on q); `second` = the chunk's type-1 workgroup
   const int qw = (GRAM_CROSS == 1 && second) ? ((wid + 4) & 7) : wid;
@@ -324,6 +410,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): next stage landed
     __syncthreads();
   }
+#endif
   if (idle) return;
   // Slab block image is lane-major: float4 `lane` holds acc regs r = 0..3 = (row (l>>4)*4+r,
   // col l&15) of the 16x16 block, so each block is ONE 1-KB dwordx4 store per wave (4x fewer
@@ -350,7 +437,7 @@ extern "C" __attribute__((visibility("default"))) int ate_gram_clock_reset() {
 __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
     const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const int4* __restrict__ tiles, int ntiles,
     const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2][2][GT * GK];   // 128 KB
+  __shared__ __attribute__((aligned(16))) bf16_t lds[PAIR_LDS];   // 128 KB (ring: up to 160)
 #ifdef GRAM_CLOCK
   const unsigned long long gc0 = clock64(), gw0 = wall_clock64();
 #endif

@@ -50,6 +50,11 @@ for step in "$@"; do
     tests:*)
       run "tests_${step#tests:}" 900 python -u -m pytest tests -m gpu -x -v --timeout 240 \
           --timeout-method thread -k "${step#tests:}" ;;
+    libtests:*)  # libtests:NAME:EXPR -- GPU tests -k EXPR on _lib/libatehip_NAME.so
+      spec=${step#libtests:}; nm=${spec%%:*}; ex=${spec#*:}
+      ATE_HIP_LIB=$ROOT/ate_replication_causalml_amd/_lib/libatehip_$nm.so \
+        run "libtests_$nm" 900 python -u -m pytest tests -m gpu -x -q --timeout 240 \
+          --timeout-method thread -k "$ex" ;;
     debugtests)
       ATE_DEBUG=1 run debugtests 1500 python -u -m pytest tests -m gpu -x -q --timeout 240 \
           --timeout-method thread ;;
@@ -57,6 +62,13 @@ for step in "$@"; do
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)
       run bench 300 python bench.py ;;
+    bench_ab:*)  # bench_ab:A,B,.. -- bench.py on each _lib/libatehip_<A>.so ("new" = in-tree)
+      IFS=, read -ra libs <<< "${step#bench_ab:}"
+      for nm in "${libs[@]}"; do
+        lib=ate_replication_causalml_amd/_lib/libatehip_$nm.so
+        [ "$nm" = new ] && lib=ate_replication_causalml_amd/_lib/libatehip.so
+        ATE_HIP_LIB=$ROOT/$lib run "bench_$nm" 300 python bench.py || exit 1
+      done ;;
     prof)
       ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$ROOT/$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --also-rct 0 \
