@@ -371,8 +371,7 @@ def main():
         # diagnostic only (tools/emulate_ranks.sh): rank 0's share of a world-W step on one
         # GPU -- its row shard, its path solves -- with no-op collectives (values are not
         # the world-W result; the JSON says "emulated_world")
-        comm = C.LocalComm()
-        comm.world_size = emulate
+        comm = C.EmulatedComm(0, emulate)   # plans the tutorial selection alone
     else:
         emulate = 0
     world, rank = comm.world_size, comm.rank
