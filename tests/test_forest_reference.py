@@ -29,12 +29,16 @@ CASES = {
                        mtry_poisson=True, alpha=0.05),
     "grf_causal_g1": dict(kind=2, sampling=1, mtry=3, min_node=3, honesty=True, group=1,
                           mtry_poisson=True, alpha=0.05, sample_fraction=0.6),
+    # mtry > 8: the exact engine's list-only instantiation (csrc/forest_exact.hip SMALL_MTRY)
+    "grf_causal_m12": dict(kind=2, sampling=1, mtry=12, min_node=5, honesty=True, group=2,
+                           mtry_poisson=True, alpha=0.05, p=14),
+    "rf_reg_m10": dict(kind=1, mtry=10, min_node=5, p=14),
 }
 
 
 def _fit_both(name, backend="cpu", ntree=4, t0=0, exact=False, n=160):
-    X, w, y = _data(n)
     c = CASES[name]
+    X, w, y = _data(n, c.get("p", 6))
     kind = c["kind"]
     if exact:
         eb = F.exact_bins(X)
@@ -45,7 +49,7 @@ def _fit_both(name, backend="cpu", ntree=4, t0=0, exact=False, n=160):
     ycls = (y > np.median(y)).astype(np.uint8) if kind == 0 else None
     r1 = y if kind == 1 else (w - w.mean() if kind == 2 else None)
     r2 = (y - y.mean()) if kind == 2 else None
-    kw = {k: v for k, v in c.items() if k != "kind"}
+    kw = {k: v for k, v in c.items() if k not in ("kind", "p")}
     if exact:
         eng = F.fit_forest(X, kind, y=ycls, r1=r1, r2=r2, ntree=ntree, seed=11,
                            tree_offset=t0, backend=backend, splits="exact", edges=eb, **kw)
@@ -147,7 +151,8 @@ def test_gpu_exact_split_kernel_equals_numpy_oracle(gpu, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["rf_class", "rf_reg", "grf_causal"])
+@pytest.mark.parametrize("name", ["rf_class", "rf_reg", "grf_causal", "grf_causal_m12",
+                                  "rf_reg_m10"])
 def test_gpu_exact_split_kernel_large_nodes_equals_oracle(gpu, name):
     """n = 3000: workgroup-level nodes (> 256 rows), wave-level list nodes and lane-per-row
     nodes (<= 64 rows, whose lists are never partitioned) in the same trees."""
