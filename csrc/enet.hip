@@ -154,7 +154,7 @@ constexpr int PMAX = 512;
 #ifdef ENET_PROF
 // cycle accounting per problem (debug builds): [0] pull, [1] recurrence, [2] other,
 // [3] block visits, [4] coordinate updates, [5] pending columns pulled, [6] passes
-__device__ unsigned long long enet_prof[256][24];
+__device__ unsigned long long enet_prof[256][32];
 #define PROF_T(var) const unsigned long long var = wall_clock64()
 #define PROF_ADD(k, v) do { if (tid == 0) sprof[0][k] += (unsigned long long)(v); } while (0)
 #else
@@ -543,8 +543,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // per-wave cycle accumulators in LDS (lane 0 of a wave adds to its own row), flushed to
   // enet_prof once at kernel end: no global atomics (and their vmcnt waits at barriers)
   // inside the visit loop
-  __shared__ unsigned long long sprof[NW][24];
-  for (int e = threadIdx.x; e < NW * 24; e += blockDim.x) (&sprof[0][0])[e] = 0ull;
+  __shared__ unsigned long long sprof[NW][32];
+  for (int e = threadIdx.x; e < NW * 32; e += blockDim.x) (&sprof[0][0])[e] = 0ull;
 #endif
   __shared__ __attribute__((aligned(16))) CT sdelta[PMAX];
   __shared__ int slist[PMAX];             // compacted pending columns (per-wave quarters)
@@ -914,8 +914,12 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     }
     __syncthreads();
     const int nv = snv;
-    if (nv == 0) return 0.0;
+    if (nv == 0) {
+      PROF_ADD(13, 1ull);                  // [12]: mode-L passes with visits, [13]: empty
+      return 0.0;
+    }
     PROF_T(tp0_);
+    PROF_ADD(12, 1ull);
     if (ready != svis[0]) pull(svis[0]);   // else: brought up to date by the last visit
     ready = -1;
     PROF_T(tp1_);
@@ -953,7 +957,17 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         gt = sg[k];
         // block t was the last visit's tn: its phase-B own-delta partials and snapshot come
         // from the pull waves' arrivals (no second barrier per visit)
+#ifdef ENET_PROF
+        const long long tw0_ = clock64();
+#endif
         if (v > 0) wait_ge(&sarr, NP * narr);
+#ifdef ENET_PROF
+        const long long tw1_ = clock64();
+        if (lane == 0) {   // prologue split: [24] before the arrival wait, [25] the wait
+          sprof[wid][24] += (unsigned long long)(tw0_ - tv0_);
+          sprof[wid][25] += (unsigned long long)(tw1_ - tw0_);
+        }
+#endif
         ds0 = sds[t][k];
         if (v > 0) gt = gt - pending_sum(vpar ^ 1);
         at = sa[k];
@@ -991,6 +1005,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #ifdef ENET_PROF
         const long long tloop0_ = clock64();
         if (lane == 0) sprof[wid][17] += (unsigned long long)(tloop0_ - tv0_);   // prologue cycles
+        if (lane == 0) sprof[wid][26] += (unsigned long long)(tloop0_ - tw1_);   // [26] after the wait
 #endif
         auto step = [&]() __attribute__((always_inline)) -> bool {
 #pragma clang fp contract(off)
@@ -1163,6 +1178,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         }
 #ifdef ENET_PROF
         if (lane == 0) sprof[wid][15] += (unsigned long long)(clock64() - tloop0_);
+        const long long tpost0_ = clock64();
 #endif
         if ((moved >> lane) & 1ull) {
           const double dn = anv - at;      // == the broadcast step d of this lane
@@ -1176,10 +1192,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           const unsigned long long tl_ = wall_clock64() - ta_;
           sprof[wid][6] += tl_;
           sprof[wid][7] += nupd_;
-          if (!full) {
-            sprof[wid][12] += tl_;
-            sprof[wid][13] += nupd_;
-          }
+
           sprof[wid][14] += 1ull;    // wave-0 visits (full + active)
         }
 #endif
@@ -1217,6 +1230,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         }
 #ifdef ENET_PROF
         if (lane == 0) sprof[wid][2] += (unsigned long long)(wall_clock64() - ta_);
+        if (lane == 0) sprof[wid][28] += (unsigned long long)(clock64() - tpost0_);   // [28] post-walk
 #endif
       } else if (tn >= 0) {
         // wave 0's publication of every earlier visit (Dcum of its blocks) and every pull
@@ -1231,7 +1245,13 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
           sprof[wid][18] += (unsigned long long)(wall_clock64() - ta_);
 #endif
       }
+#ifdef ENET_PROF
+      const long long tsb_ = clock64();
+#endif
       __syncthreads();
+#ifdef ENET_PROF
+      if (wid == 0 && lane == 0) sprof[0][27] += (unsigned long long)(clock64() - tsb_);   // [27] barrier
+#endif
       PROF_T(tb_);
       PROF_ADD(1, tb_ - ta_);
       PROF_ADD(3, 1);
@@ -1425,7 +1445,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   }
 #ifdef ENET_PROF
   __syncthreads();
-  if (tid < 24) {
+  if (tid < 32) {
     unsigned long long acc = 0;
     for (int w = 0; w < NW; ++w) acc += sprof[w][tid];
     // [10] / [11]: shader clock cycles and 100 MHz wall ticks of the whole path (clock rate)
@@ -1446,7 +1466,7 @@ extern "C" __attribute__((visibility("default"))) int ate_enet_prof_read(void* h
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(enet_prof), sizeof(enet_prof));
 }
 extern "C" __attribute__((visibility("default"))) int ate_enet_prof_reset() {
-  static unsigned long long z[256][24];
+  static unsigned long long z[256][32];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(enet_prof), z, sizeof(z));
 }
 #endif

@@ -55,7 +55,7 @@ def main():
         path()
         e[1].record()
         torch.cuda.synchronize()
-        buf = np.zeros((256, 24), dtype=np.uint64)
+        buf = np.zeros((256, 32), dtype=np.uint64)
         lib.ate_enet_prof_read(buf.ctypes.data_as(ctypes.c_void_p))
         live = buf[buf[:, 11] > 0]
         ghz = live[:, 10].astype(float) / live[:, 11].astype(float) * 0.1

@@ -51,13 +51,13 @@ def run(n, p):
     _, _, cv = dml_crossfit_panel(pan, 5, "min")
     t[1].record()
     torch.cuda.synchronize()
-    buf = np.zeros((256, 24), dtype=np.uint64)
+    buf = np.zeros((256, 32), dtype=np.uint64)
     lib.ate_enet_prof_read(buf.ctypes.data_as(ctypes.c_void_p))
     rows = buf[:40]
     live = rows[rows[:, 3] > 0]
     print(json.dumps({"step_ms": t[0].elapsed_time(t[1]),
-                      "per_problem": [[int(v) for v in r[:24]] for r in live],
-                      "note": "wall_clock64 ticks (100 MHz): pull, visit-phase, wave0, visits, waves1-3 pull, cols, wave0 recurrence loop, updates, pass-start pulls, wave0 phase B, wave0 phase B up to corr, up to before the diagonal reload, active-pass recurrence, active-pass updates, wave-0 visits, loop-only shader cycles, wave-1 pull scan cycles, wave-1 phase B, wave-2 phase B, last pull wave phase A, unused, w0 B1 work, w1 B1 work, w0 after B1 barrier, w1 after B1 barrier"}))
+                      "per_problem": [[int(v) for v in r[:32]] for r in live],
+                      "note": "[0] phase B + pass-start pulls, [1] phase A, [2] wave-0 phase A, [3] visits, [4] wave-1 phase A, [5] wall ticks inside passes, [6] wave-0 loop ticks, [7] updates, [8] pass-start pulls, [9] wave-0 phase B, [10] shader cycles, [11] wall ticks (100 MHz), [12] mode-L passes with visits, [13] empty passes, [14] wave-0 visits, [15] loop-only cycles, [16] wave-1 phase B, [17] prologue cycles, [18] last pull wave phase A, [19]-[22] mode S passes / candidates / cycles / fetches, [23] mode-S loop cycles, [24] prologue before the arrival wait, [25] the wait, [26] after the wait, [27] wave-0 phase-A barrier, [28] post-walk cycles"}))
 
 
 if __name__ == "__main__":
