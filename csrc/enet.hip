@@ -955,6 +955,22 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         }
         dc0 = sdc[k];
         gt = sg[k];
+        // Everything that does not come from the pull waves' phase B is read BEFORE the
+        // arrival wait: block t's own coefficient, flag and penalty (wave 0 wrote them),
+        // and the pull partials of block t (written in phase A, before the barrier), so
+        // that only the phase-B correction partials and the snapshot remain after it.
+        // pending_sum's additions, in its order, run after the wait.
+        at = sa[k];
+        const double vpt = svp[k];
+        fl = sflag[k];
+        const int par = vpar ^ 1;
+        double pend[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pend[w] = spart2[par][w][lane];
+        const bool cok = sizeof(CT) == 4 && scorr_ok[par];
+        const bool elig = (fl & 1) && (full || (fl & 2));
+        const double thr_l = vpt * ab;
+        const double rden = (LASSO || dem == 0.0) ? 1.0 : 1.0 / (1.0 + vpt * dem);
         // block t was the last visit's tn: its phase-B own-delta partials and snapshot come
         // from the pull waves' arrivals (no second barrier per visit)
 #ifdef ENET_PROF
@@ -969,13 +985,21 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         }
 #endif
         ds0 = sds[t][k];
-        if (v > 0) gt = gt - pending_sum(vpar ^ 1);
-        at = sa[k];
-        const double vpt = svp[k];
-        fl = sflag[k];
-        const bool elig = (fl & 1) && (full || (fl & 2));
-        const double thr_l = vpt * ab;
-        const double rden = (LASSO || dem == 0.0) ? 1.0 : 1.0 / (1.0 + vpt * dem);
+        if (v > 0) {                          // == gt - pending_sum(par), same operations
+          double c0 = pend[0];
+          if constexpr (sizeof(CT) == 4) {
+            float cs = 0.f;
+            if (cok) {
+#pragma unroll
+              for (int w = 0; w < NP; ++w) cs += scorr2[par][w][lane];
+            }
+            c0 = (double)cs;
+          }
+          double sp = c0;
+#pragma unroll
+          for (int w = 1; w < NW; ++w) sp += pend[w];
+          gt = gt - sp;
+        }
         // Each lane changes at most once per visit (lane > last): its bookkeeping is
         // deferred (delta + the gradient it was computed from), so the loop body is the
         // bare coordinate recurrence.
