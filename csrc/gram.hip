@@ -262,10 +262,19 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // 2, bench step 3.81 / 3.83, profiles/r02c_gram/ab_cross.log): kept as an option, default 0.
 #define GRAM_CROSS 0
 #endif
+#ifndef GRAM_PRELOAD
+// 1: both 32-row halves' fragments of a stage are read before its MFMAs, the second half's
+// reads interleaved one per MFMA of the first (sched_group_barrier): one LDS wait per half
+// instead of one per 8 MFMAs. Tile kernel 2.59-2.62 -> 2.55-2.59 ms, same bits
+// (profiles/r05_gram_sync)
+#define GRAM_PRELOAD 1
+#endif
 #ifndef GRAM_DIAG
 #define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA,
                       // 3 = 1 with only the off-diagonal tile's workgroups (each K-step
-                      // loaded once), 4 = normal work on the off-diagonal tiles only
+                      // loaded once), 4 = normal work on the off-diagonal tiles only,
+                      // 5 = no per-stage barrier (wrong results; the cost of the stage
+                      // hand-off between the 8 waves: 2.66 -> 1.90 ms, profiles/r05_gram_sync)
 #endif
 
 __device__ __forceinline__ int tri_index(int m, int n) {   // m <= n < 8, row-major triangle
@@ -378,6 +387,63 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
 #endif
     const bf16_t* As = lds[cur][abuf];
     const bf16_t* Bs = lds[cur][bbuf];
+#if GRAM_PRELOAD
+    // every fragment of the stage (both 32-row halves) read from LDS up front, then the
+    // MFMAs: the waits on LDS leave the MFMA chains of the stage
+    if (!idle && GRAM_DIAG != 1 && GRAM_DIAG != 3) {
+      if constexpr (!TRI) {
+        bf16x8 af[2][8], bfr[2][4];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int cc = kk * 4 + (lane >> 4);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) af[kk][m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) bfr[kk][n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+              acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][m], bfr[kk][n],
+                                                                        acc[m * 4 + n], 0, 0, 0);
+        // schedule: the first half's 12 reads, then the second half's 12 reads one per
+        // MFMA of the first half, then the remaining MFMAs (mask 0x100 DS read, 0x008 MFMA)
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 52, 0);
+      } else {
+        bf16x8 fr[2][8];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int cc = kk * 4 + (lane >> 4);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) fr[kk][m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int n = m; n < 8; ++n)
+              acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  fr[kk][m], fr[kk][n], acc[tri_index(m, n)], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);
+      }
+    }
+#else
     if (!idle && GRAM_DIAG != 1 && GRAM_DIAG != 3) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -407,8 +473,11 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
         }
       }
     }
+#endif
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): next stage landed
+#if GRAM_DIAG != 5
     __syncthreads();
+#endif
   }
 #endif
   if (idle) return;
