@@ -347,3 +347,21 @@ dist.destroy_process_group()
             assert all(g == want for g in got), (world, got, want)
     finally:
         os.unlink(path)
+
+
+def test_bench_emulated_rank_share():
+    """ATE_BENCH_EMULATE_WORLD=W (tools/emulate_ranks.sh): bench.py runs rank 0's share of a
+    W-rank job in one process through parallel.comm.EmulatedComm -- the tutorial selection
+    is planned alone over W x rows kept rows, rank 0's row shard is generated -- and
+    prints one JSON line with the world-W global batch."""
+    import json
+    bench = os.path.join(ROOT, "bench.py")
+    env = dict(os.environ, ATE_BENCH_EMULATE_WORLD="3", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, bench, "--rows", "2000", "--p", "24", "--dtype", "f64",
+                        "--steps", "1", "--warmup", "1", "--also-rct", "0", "--parity", "0"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["dgp"] == "tutorial"
+    assert out["config"]["n_kept"] == 6000 and out["config"]["n_generated"] > 6000
+    assert np.isfinite(out["ate"]) and out["value"] > 0
