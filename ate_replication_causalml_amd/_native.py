@@ -49,7 +49,7 @@ _SIGS = {
     "ate_boot_poisson": "ppluiilipp",
     "ate_enet_isa_selftest": "pp",
     "ate_enet_prepare": "piipipiipipipppppppp",
-    "ate_enet_path": "pipiippppidddipppppipp",
+    "ate_enet_path": "pipiippppidddipppppippp",
     "ate_enet_coef": "ppiiiipppppppp",
     "ate_enet_cvloss_gauss": "pippiipppiiipp",
     "ate_cv_select": "pppiipippppip",

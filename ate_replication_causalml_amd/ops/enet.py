@@ -196,10 +196,12 @@ def _cv_gpu(G, P, nseg, masks, xcols, ycols, p, ny, vp, one, full_probs, fold_pr
     # their source's lambda sequence as it is published (device-side progress flags)
     pr = _probs_tensor(probs_all, dev)
     lams = torch.full((nq, L), float("nan"), **f64)
+    # each full problem's whole lambda sequence, published at its lambda 1 for the folds
+    lampub = torch.empty((nq, L), **f64)
     _native.call("ate_enet_path", C.data_ptr(), c_f32, g.data_ptr(), p, ny, ju.data_ptr(),
                  ys.data_ptr(), vp_t.data_ptr(), pr.data_ptr(), nq, alpha, flmin, thresh,
                  maxit, apath.data_ptr(), lams.data_ptr(), rsq.data_ptr(), nlam.data_ptr(),
-                 npass.data_ptr(), L, progress.data_ptr(), s)
+                 npass.data_ptr(), L, progress.data_ptr(), lampub.data_ptr(), s)
     coef = torch.empty((nq, L, p + 1), **f64)
     _native.call("ate_enet_coef", apath.data_ptr(), pr.data_ptr(), nq, p, ny, L,
                  nlam.data_ptr(), xm.data_ptr(), xs.data_ptr(), ju.data_ptr(), ym.data_ptr(),

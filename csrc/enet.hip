@@ -502,6 +502,16 @@ __device__ __noinline__ PassS enet_pass_s(bool full, int T, int ldc, double ab, 
 // LASSO: alpha == 1 (dem == 0 at every lambda): the elastic-net walk and scaling are not
 // compiled into that instantiation (the kernel's code is ~60 KB against a 64 KB instruction
 // cache shared by two CUs; every unused walk variant is cache pressure on the hot one).
+// how many lambdas a fold problem may run ahead of its source (enet_path_kernel)
+constexpr int FOLD_LEAD = 2;
+
+// glmnet's lambda_0, extrapolated from lambda_1 and lambda_2 (one definition: the source's
+// published sequence and its own lams[] must be the same bits)
+__device__ __noinline__ double lambda0_extrap(double l1, double l2) {
+#pragma clang fp contract(off)
+  return exp(2.0 * log(l1) - log(l2));
+}
+
 template <typename CT, bool LASSO>
 __global__ __launch_bounds__(NTH) void enet_path_kernel(
     const CT* __restrict__ C, const double* __restrict__ gin, int p, int ny,
@@ -510,7 +520,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     double alpha, double flmin, double thr, int maxit,
     double* __restrict__ apath, double* __restrict__ lams, double* __restrict__ rsqs,
     int* __restrict__ nlam_out, int* __restrict__ npass_out, int L, int* __restrict__ progress,
-    long spin_max) {
+    long spin_max, double* __restrict__ lampub) {
   constexpr int TMAX = PMAX / 64;
   __shared__ double sg[PMAX], sa[PMAX], svp[PMAX], sdc[PMAX];
   // Mode L's snapshots and staged blocks share one LDS region with mode S's column cache
@@ -565,6 +575,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ int schg;                    // wave 0: some coordinate of block t moved
   __shared__ double slam;
   __shared__ int savail;
+  __shared__ int snpass_ring[4];          // npass after lambda m, at m & 3 (fold truncation)
   int q;
   {
     int bid = blockIdx.x, nwg = gridDim.x;
@@ -1357,28 +1368,44 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     __hip_atomic_store(progress + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   // Fold problems run CONCURRENTLY with the full-data problem that defines their lambda
-  // sequence: it publishes lambda m (release of progress[q] = m+1 after lams[] is
-  // stored), the fold problem polls that counter (relaxed, bounded spin) and acquires
-  // before reading. All problems of a launch are co-resident (one workgroup per problem,
-  // grid <= #CUs); a timed-out spin ends the fold path (npass_out = -1 flags it).
+  // sequence: it publishes the whole sequence once lambda_max is known (lampub, release of
+  // progress[q] = 2) and progress[q] = m+1 after each lambda m >= 2; a fold polls that
+  // counter (relaxed, bounded spin) and acquires before reading, running up to FOLD_LEAD
+  // lambdas ahead of the source, and drops what it computed past the source's final count.
+  // All problems of a launch are co-resident (one workgroup per problem, grid <= #CUs); a
+  // timed-out spin ends the fold path (npass_out = -1 flags it).
 #ifdef ENET_PROF
   const long long kc0_ = clock64();
   const unsigned long long kw0_ = wall_clock64();
 #endif
   const bool is_fold = pr.ulam_src >= 0;
   bool timed_out = false;
+  int vseen = 0;                           // fold, thread 0: the source's progress last acquired
   for (int m = 0; m < nlam; ++m) {
     if (is_fold) {
       if (tid == 0) {
-        int v = 0;
-        for (long spin = 0;; ++spin) {
-          v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v > m) break;
-          if (spin > spin_max) { v = -1; break; }
-          __builtin_amdgcn_s_sleep(2);
+        // The source publishes its whole lambda sequence at its lambda 1 (progress 2,
+        // lampub) and progress m+1 after each lambda m >= 2. A fold runs lambda m once the
+        // source has finished lambda m - FOLD_LEAD (any m <= FOLD_LEAD + 1 as soon as the
+        // sequence is out): it does not trail the source by a lambda, and the lambdas it
+        // computes past the end of the source's path (at most FOLD_LEAD + 1) are
+        // discarded after the loop. Where the source has ended (FINAL) the committed
+        // lams[] values are read (the same bits as lampub).
+        const int need = m <= FOLD_LEAD + 1 ? 2 : m - FOLD_LEAD + 1;
+        // a value already acquired that satisfies this lambda needs no new load (the
+        // source only moves forward, and what it published before it is visible)
+        int v = vseen;
+        if (v < need) {
+          for (long spin = 0;; ++spin) {
+            v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v >= need) break;
+            if (spin > spin_max) { v = -1; break; }
+            __builtin_amdgcn_s_sleep(2);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (v > 0) vseen = v;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int avail = 0;
         double lv = 0.0;
         if (v < 0) {
@@ -1386,11 +1413,13 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         } else if (v >= (1 << 30)) {
           int nl = __hip_atomic_load(nlam_out + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           avail = m < nl;
+          if (avail) lv = __hip_atomic_load(lams + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
         } else {
           avail = 1;
+          lv = __hip_atomic_load(lampub + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (avail) lv = __hip_atomic_load(lams + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
         savail = avail;
         slam = lv;
       }
@@ -1413,6 +1442,20 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         if ((sflag[k] & 1) && svp[k] > 0.0) mx = fmax(mx, fabs(sg[k]) / svp[k]);
       mx = wave_max(mx);      // every wave computes the same value
       alm = alf * mx / fmax(alpha, 1e-3);
+      if (tid == 0 && L >= 3) {
+        // the whole sequence for the fold problems, by the operations the path itself
+        // uses (lams[] below): alm_m = alm_{m-1} * alf, lambda_0 extrapolated
+        double* lp = lampub + (int64_t)q * L;
+        double x = alm, x2 = alm;
+        lp[1] = x * ysq;
+        for (int mm = 2; mm < L; ++mm) {
+          x *= alf;
+          lp[mm] = x * ysq;
+          if (mm == 2) x2 = x;
+        }
+        lp[0] = lambda0_extrap(lp[1], x2 * ysq);
+        publish(2);
+      }
     } else {
       alm *= alf;
     }
@@ -1458,14 +1501,47 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       lams[(int64_t)q * L + m] = alm * ysq;
       rsqs[(int64_t)q * L + m] = rsq_all;
       if (!is_fold && m == 2)   // glmnet reports lambda_0 extrapolated from lambda_1, lambda_2
-        lams[(int64_t)q * L] = exp(2.0 * log(lams[(int64_t)q * L + 1]) - log(alm * ysq));
+        lams[(int64_t)q * L] = lambda0_extrap(lams[(int64_t)q * L + 1], alm * ysq);
       if (!is_fold && m >= 2) publish(m + 1);
     }
     m_out = m + 1;
+    if (tid == 0) snpass_ring[m & 3] = npass;
     if (pr.ulam_src < 0 && m >= 4 && m > 0) {
       if (rsq_all - rsq_prev < 1e-5 * rsq_all || rsq_all > 0.999) break;
     }
     rsq_prev = rsq_all;
+  }
+  if (is_fold) {
+    // lambdas computed past the end of the source's path: back to their launch state
+    if (tid == 0) {
+      int v = 0;
+      for (long spin = 0;; ++spin) {
+        v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= (1 << 30)) break;
+        if (spin > spin_max) { v = -1; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (v < 0) timed_out = true;
+      savail = v < 0 ? m_out
+                     : __hip_atomic_load(nlam_out + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int nl = savail;
+    if (m_out > nl) {
+      ATE_DASSERT(m_out - nl <= FOLD_LEAD + 1);
+      for (int mm = nl; mm < m_out; ++mm) {
+        double* ap = apath + ((int64_t)q * L + mm) * p;
+        for (int k = tid; k < p; k += NTH) ap[k] = 0.0;
+        if (tid == 0) {
+          lams[(int64_t)q * L + mm] = __builtin_nan("");
+          rsqs[(int64_t)q * L + mm] = 0.0;
+        }
+      }
+      npass = nl > 0 ? snpass_ring[(nl - 1) & 3] : 0;
+      m_out = nl;
+    }
   }
 #ifdef ENET_PROF
   __syncthreads();
@@ -1499,7 +1575,7 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
                           const void* ys, const void* vp, const void* probs, int nprob,
                           double alpha, double flmin, double thr, int maxit, void* apath,
                           void* lams, void* rsqs, void* nlam_out, void* npass_out, int L,
-                          void* progress, void* stream) {
+                          void* progress, void* lampub, void* stream) {
   if (p > PMAX) return -2;
   if (nprob > 256) return -3;   // co-residency of fold problems and their sources
   hipStream_t s = (hipStream_t)stream;
@@ -1514,7 +1590,7 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
-                     (int*)npass_out, L, (int*)progress, spin_max)
+                     (int*)npass_out, L, (int*)progress, spin_max, (double*)lampub)
   const bool lasso = alpha == 1.0;
   if (c_f32 && lasso) LAUNCH_C(float, true);
   else if (c_f32) LAUNCH_C(float, false);
