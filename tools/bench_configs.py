@@ -39,6 +39,10 @@ def timed(fn, reps=1, warm=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,3,4,5")
+    ap.add_argument("--dgp", default="tutorial", choices=["tutorial", "rct"],
+                    help="tutorial: the selection-biased df_mod at scale (panels: "
+                         "synthetic_panel(dgp='tutorial'); host data: the kept rows of "
+                         "data/panel_selection.selected_rows); rct: the unselected panels")
     ap.add_argument("--n3", type=int, default=200_000)
     ap.add_argument("--trees3", type=int, default=100)
     ap.add_argument("--n4", type=int, default=50_000)
@@ -65,7 +69,8 @@ def main():
     if 2 in want:
         from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
         from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
-        pan = synthetic_panel(1_000_000, p=500, folds=5, seed=7, dtype="bf16", device=dev)
+        pan = synthetic_panel(1_000_000, p=500, folds=5, seed=7, dtype="bf16", device=dev,
+                              dgp=a.dgp)
         (res, _, _), s = timed(lambda: dml_crossfit_panel(pan, 5, "min"), reps=5)
         out.append({"config": 2, "estimator": "DML-PLR (CV-LASSO)", "rows": 1_000_000, "p": 500,
                     "dtype": "bf16", "seconds": s, "rows_per_s": 1e6 / s,
@@ -73,11 +78,19 @@ def main():
         print(json.dumps(out[-1]), flush=True)
         del pan
     if 3 in want or 4 in want or 5 in want:
-        from ate_replication_causalml_amd.data.dgp import make_tutorial_data
+        from ate_replication_causalml_amd.data.dgp import make_tutorial_data as _make
+        from ate_replication_causalml_amd.data.panel_selection import selected_rows
+
+        def make_tutorial_data(n, seed, p_extra=0):
+            """host data of config 3/4/5: the tutorial's kept rows (df_mod) or the RCT"""
+            if a.dgp == "tutorial":
+                return selected_rows(n, seed, p_extra=p_extra, device=dev)[0]
+            return _make(n, seed=seed, p_extra=p_extra)
     if 3 in want and a.panel3:
         from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
         from ate_replication_causalml_amd.estimators.crossfit import aipw_rf_crossfit_panel
-        pan = synthetic_panel(a.n3, p=a.p3, folds=5, seed=11, dtype="bf16", device=dev)
+        pan = synthetic_panel(a.n3, p=a.p3, folds=5, seed=11, dtype="bf16", device=dev,
+                              dgp=a.dgp)
         shard = tuple(int(v) for v in a.shard3.split("/")) if a.shard3 else None
         r, s = timed(lambda: aipw_rf_crossfit_panel(pan, num_trees=a.trees3, tree_shard=shard,
                                                     concurrent=not a.serial3),
@@ -113,7 +126,8 @@ def main():
         # and binned in HBM (no host copy of X)
         from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
         from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt_panel
-        pan = synthetic_panel(a.n5, p=a.p5, folds=5, seed=13, dtype="bf16", device=dev)
+        pan = synthetic_panel(a.n5, p=a.p5, folds=5, seed=13, dtype="bf16", device=dev,
+                              dgp=a.dgp)
         r, s = timed(lambda: dml_plr_gbdt_panel(pan, n_trees=a.trees5, depth=6))
         out.append({"config": 5, "estimator": "DML-PLR, GBDT nuisances (depth 6), HBM panel",
                     "rows": a.n5, "p": a.p5, "trees": a.trees5, "seconds": s,
