@@ -571,6 +571,8 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   __shared__ __attribute__((aligned(16))) float sdall[64];         // wave 0: block t's deltas
   __shared__ int svis[8], snv, sblk_any[8];
   __shared__ double sdl;
+  __shared__ double srsq;                 // a lambda's R^2 (apart from sdl: fewer barriers)
+  __shared__ int snl_final;               // fold: the source's final count
   __shared__ int sany;
   __shared__ int schg;                    // wave 0: some coordinate of block t moved
   __shared__ double slam;
@@ -1356,9 +1358,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     const double dlx = wave_max(dlx_l);
     if (tid == 0) sdl = dlx;
     __syncthreads();
-    double r = sdl;
-    __syncthreads();
-    return r;
+    // sdl's next writer is a later mode-L pass, after its own barriers (mode S never
+    // follows mode L, and the lambda's R^2 goes through srsq)
+    return sdl;
   };
 
   auto publish = [&](int v) {   // thread 0 only: agent-scope release of progress[q]
@@ -1380,10 +1382,17 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
 #endif
   const bool is_fold = pr.ulam_src >= 0;
   bool timed_out = false;
-  int vseen = 0;                           // fold, thread 0: the source's progress last acquired
+  int vseen = 0;            // fold, wave 0 (uniform): the source's progress last acquired
+  // fold, wave 0: the source's published sequence in registers once it is out (lane l:
+  // lambdas l and 64 + l; L <= 128), so a lambda needs no global load
+  double lam_lo = 0.0, lam_hi = 0.0;
+  bool lam_reg = false;
   for (int m = 0; m < nlam; ++m) {
+#ifdef ENET_PROF
+    const unsigned long long tlam0_ = wall_clock64();
+#endif
     if (is_fold) {
-      if (tid == 0) {
+      if (wid == 0) {
         // The source publishes its whole lambda sequence at its lambda 1 (progress 2,
         // lampub) and progress m+1 after each lambda m >= 2. A fold runs lambda m once the
         // source has finished lambda m - FOLD_LEAD (any m <= FOLD_LEAD + 1 as soon as the
@@ -1396,37 +1405,53 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
         // source only moves forward, and what it published before it is visible)
         int v = vseen;
         if (v < need) {
-          for (long spin = 0;; ++spin) {
-            v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v >= need) break;
-            if (spin > spin_max) { v = -1; break; }
-            __builtin_amdgcn_s_sleep(2);
+          if (lane == 0) {
+            for (long spin = 0;; ++spin) {
+              v = __hip_atomic_load(progress + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (v >= need) break;
+              if (spin > spin_max) { v = -1; break; }
+              __builtin_amdgcn_s_sleep(2);
+            }
           }
+          v = __builtin_amdgcn_readfirstlane(v);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (v > 0) vseen = v;
+          if (v >= 2 && v < (1 << 30) && !lam_reg && L <= 128) {
+            const double* lp = lampub + (int64_t)pr.ulam_src * L;
+            lam_lo = lane < L ? lp[lane] : 0.0;
+            lam_hi = 64 + lane < L ? lp[64 + lane] : 0.0;
+            lam_reg = true;
+          }
         }
         int avail = 0;
         double lv = 0.0;
         if (v < 0) {
           timed_out = true;
         } else if (v >= (1 << 30)) {
-          int nl = __hip_atomic_load(nlam_out + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          avail = m < nl;
-          if (avail) lv = __hip_atomic_load(lams + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) {
+            int nl = __hip_atomic_load(nlam_out + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            avail = m < nl;
+            if (avail) lv = __hip_atomic_load(lams + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+          }
+        } else if (lam_reg) {
+          avail = 1;
+          lv = readlane_d(m < 64 ? lam_lo : lam_hi, m & 63);
         } else {
           avail = 1;
-          lv = __hip_atomic_load(lampub + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0)
+            lv = __hip_atomic_load(lampub + (int64_t)pr.ulam_src * L + m, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        savail = avail;
-        slam = lv;
+        if (lane == 0) {
+          savail = avail;
+          slam = lv;
+        }
       }
       __syncthreads();
       const int avail = savail;
-      alm = slam / ysq;
-      __syncthreads();
+      alm = slam / ysq;     // savail / slam are next written after this lambda's barriers
       if (!avail) break;
     } else if (m == 0) {
       alm = BIGL;
@@ -1476,6 +1501,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
     }
 #ifdef ENET_PROF
     const unsigned long long tpass0_ = wall_clock64();
+    if (tid == 0) sprof[0][29] += tpass0_ - tlam0_;   // [29]: lambda start -> first pass
 #endif
     while (npass < maxit) {
       ++npass;
@@ -1488,21 +1514,24 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       }
     }
 #ifdef ENET_PROF
-    if (tid == 0) sprof[0][5] += wall_clock64() - tpass0_;   // [5]: wall ticks inside passes
+    const unsigned long long tpend_ = wall_clock64();
+    if (tid == 0) sprof[0][5] += tpend_ - tpass0_;   // [5]: wall ticks inside passes
 #endif
     double* ap = apath + ((int64_t)q * L + m) * p;
     for (int k = tid; k < p; k += NTH) ap[k] = sa[k];
     rsq = wave_sum(rsq_l);
-    if (tid == 0) sdl = rsq;
+    if (tid == 0) srsq = rsq;
     __syncthreads();
-    const double rsq_all = sdl;
-    __syncthreads();
+    const double rsq_all = srsq;   // srsq is next written after the next lambda's barriers
     if (tid == 0) {
       lams[(int64_t)q * L + m] = alm * ysq;
       rsqs[(int64_t)q * L + m] = rsq_all;
       if (!is_fold && m == 2)   // glmnet reports lambda_0 extrapolated from lambda_1, lambda_2
         lams[(int64_t)q * L] = lambda0_extrap(lams[(int64_t)q * L + 1], alm * ysq);
-      if (!is_fold && m >= 2) publish(m + 1);
+      // a count only (the folds read the sequence published at lambda 1, and lams[] only
+      // after the releasing FINAL): no wait for this lambda's stores
+      if (!is_fold && m >= 2)
+        __hip_atomic_store(progress + q, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     m_out = m + 1;
     if (tid == 0) snpass_ring[m & 3] = npass;
@@ -1510,6 +1539,9 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       if (rsq_all - rsq_prev < 1e-5 * rsq_all || rsq_all > 0.999) break;
     }
     rsq_prev = rsq_all;
+#ifdef ENET_PROF
+    if (tid == 0) sprof[0][30] += wall_clock64() - tpend_;   // [30]: last pass -> lambda end
+#endif
   }
   if (is_fold) {
     // lambdas computed past the end of the source's path: back to their launch state
@@ -1524,11 +1556,11 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (v < 0) timed_out = true;
-      savail = v < 0 ? m_out
+      snl_final = v < 0 ? m_out
                      : __hip_atomic_load(nlam_out + pr.ulam_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    const int nl = savail;
+    const int nl = snl_final;
     if (m_out > nl) {
       ATE_DASSERT(m_out - nl <= FOLD_LEAD + 1);
       for (int mm = nl; mm < m_out; ++mm) {
