@@ -569,7 +569,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   // loop-carried state leaves the pull waves' code the whole register budget (no spills).
   // sCn2[2][64 * 64], sCorr[64 * 64] (C[t rows][tn cols], fp32 C): in s_union above
   __shared__ __attribute__((aligned(16))) float sdall[64];         // wave 0: block t's deltas
-  __shared__ int svis[8], snv, sblk_any[8];
+  __shared__ int svis[8], snv, sblk_any[8], svis_id[8];
   __shared__ double sdl;
   __shared__ double srsq;                 // a lambda's R^2 (apart from sdl: fewer barriers)
   __shared__ int snl_final;               // fold: the source's final count
@@ -607,6 +607,7 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
   }
   for (int e = tid; e < TMAX * PMAX; e += NTH) (&sds[0][0])[e] = 0.0;
   for (int k = tid; k < PMAX; k += NTH) sslot[k] = -1;
+  if (tid < 8) svis_id[tid] = tid;
   if (tid == 0) { sever_n = 0; sncache = 0; spub = 0; sarr = 0; sfetch0 = 0; }
   __syncthreads();
   const int nlam = pr.ulam_src >= 0 ? L : pr.nlam_req;
@@ -913,37 +914,43 @@ __global__ __launch_bounds__(NTH) void enet_path_kernel(
       return r;
     }
     double dlx_l = 0.0;
-    for (int t = wid; t < T; t += NW) {     // blocks holding an active coordinate
-      const bool a = full || ((sflag[t * 64 + lane] & 3) == 3);
-      const uint64_t b = __builtin_amdgcn_ballot_w64(a);
-      if (lane == 0) sblk_any[t] = b != 0;
+    // a full pass visits every block (no list, no barriers); an active pass the blocks
+    // holding an active coordinate
+    int nv = T;
+    if (!full) {
+      for (int t = wid; t < T; t += NW) {
+        const bool a = (sflag[t * 64 + lane] & 3) == 3;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(a);
+        if (lane == 0) sblk_any[t] = b != 0;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int c = 0;
+        for (int t = 0; t < T; ++t)
+          if (sblk_any[t]) svis[c++] = t;
+        snv = c;
+      }
+      __syncthreads();
+      nv = snv;
     }
-    __syncthreads();
-    if (tid == 0) {
-      int nv = 0;
-      for (int t = 0; t < T; ++t)
-        if (sblk_any[t]) svis[nv++] = t;
-      snv = nv;
-    }
-    __syncthreads();
-    const int nv = snv;
+    const int* vl = full ? svis_id : svis;          // identity list: written at kernel start
     if (nv == 0) {
       PROF_ADD(13, 1ull);                  // [12]: mode-L passes with visits, [13]: empty
       return 0.0;
     }
     PROF_T(tp0_);
     PROF_ADD(12, 1ull);
-    if (ready != svis[0]) pull(svis[0]);   // else: brought up to date by the last visit
+    if (ready != vl[0]) pull(vl[0]);       // else: brought up to date by the last visit
     ready = -1;
     PROF_T(tp1_);
     PROF_ADD(0, tp1_ - tp0_);
     PROF_ADD(8, tp1_ - tp0_);
     for (int v = 0; v < nv; ++v) {
-      const int t = svis[v];
+      const int t = vl[v];
       const int vpar = v & 1;
       // the last visit prefetches block 0, the first block of the next pass whenever
       // that pass is a full pass or block 0 holds an active coordinate (checked there)
-      const int tn = v + 1 < nv ? svis[v + 1] : (t != 0 ? 0 : -1);
+      const int tn = v + 1 < nv ? vl[v + 1] : (t != 0 ? 0 : -1);
       if (v + 1 == nv) ready = tn;
       const int k = t * 64 + lane;
       PROF_T(ta_);
