@@ -16,6 +16,7 @@ COUNT (one packed buffer per phase), the right trade on point-to-point xGMI.
 from __future__ import annotations
 
 import os
+import sys
 import threading
 
 import torch
@@ -262,6 +263,22 @@ def local_device() -> int:
     return int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
 
 
+def default_backend() -> str:
+    """RCCL ("nccl") with one rank per GPU; gloo without a GPU, or when the node runs more
+    ranks than it has GPUs: RCCL refuses two ranks on one device at communicator init
+    ("Duplicate GPU detected", measured on a one-GPU MI355X box, profiles/r05_rccl)."""
+    if not torch.cuda.is_available():
+        return "gloo"
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    ndev = torch.cuda.device_count()
+    if local > ndev:
+        if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+            print(f"[comm] {local} ranks on {ndev} GPU(s): RCCL needs one rank per GPU, "
+                  "using gloo (host-staged collectives)", file=sys.stderr, flush=True)
+        return "gloo"
+    return "nccl"
+
+
 def from_env():
     """TorchComm if launched under torch.distributed.run (WORLD_SIZE>1), else LocalComm."""
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -269,8 +286,7 @@ def from_env():
         if not dist.is_initialized():
             # ATE_DIST_BACKEND=gloo: host-staged collectives (e.g. several ranks sharing one
             # GPU in a rehearsal); default RCCL ("nccl") when a GPU is visible
-            backend = os.environ.get("ATE_DIST_BACKEND") or \
-                ("nccl" if torch.cuda.is_available() else "gloo")
+            backend = os.environ.get("ATE_DIST_BACKEND") or default_backend()
             # RCCL errors (a failed peer, a timed-out collective) abort the process
             # instead of leaving the other ranks blocked
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")

@@ -365,3 +365,18 @@ def test_bench_emulated_rank_share():
     assert out["config"]["dgp"] == "tutorial"
     assert out["config"]["n_kept"] == 6000 and out["config"]["n_generated"] > 6000
     assert np.isfinite(out["ate"]) and out["value"] > 0
+
+
+def test_default_backend_one_rank_per_gpu(monkeypatch):
+    """RCCL refuses two ranks on one GPU ("Duplicate GPU detected", profiles/r05_rccl):
+    more local ranks than GPUs selects gloo, one rank per GPU keeps RCCL."""
+    from ate_replication_causalml_amd.parallel import comm as C
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert C.default_backend() == "gloo"
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert C.default_backend() == "nccl"
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    assert C.default_backend() == "gloo"
