@@ -39,6 +39,7 @@ from .dgp import DgpParams, selection_flags
 
 SEL_BR = 16384            # generated rows per selection block (csrc/dgp.hip SEL_BR)
 KEEP_FRACTION_GUESS = 0.16
+MAX_SEL_BLOCKS = 1 << 20   # 1.7e10 generated rows: far past any config (config 5: 4.2e8)
 
 
 def r_round(x: float) -> int:
@@ -133,6 +134,8 @@ def plan_selection(n_keep: int, seed: int, params: DgpParams, comm=None, device=
     every block itself: the same integers)."""
     if not (0 < pt <= 1 and 0 < pc <= 1):
         raise ValueError("pt, pc must be in (0, 1]")
+    if int(n_keep) < 1:
+        raise ValueError(f"n_keep must be >= 1, got {n_keep}")
     fl = _Flags(seed, params, compat, device)
     r, w = (comm.rank, comm.world_size) if comm is not None else (0, 1)
     ct = np.zeros(0, np.int64)
@@ -141,6 +144,10 @@ def plan_selection(n_keep: int, seed: int, params: DgpParams, comm=None, device=
     while True:
         # blocks to have counted: enough for n_keep at the keep fraction seen so far (+3 %)
         want = int(np.ceil(n_keep / guess * 1.03 / SEL_BR)) + 1
+        if want > MAX_SEL_BLOCKS:
+            # every rank sees the same counts, so every rank raises here together
+            raise ValueError(f"the selection keeps too few rows: {n_keep} kept rows would "
+                             f"need more than {MAX_SEL_BLOCKS * SEL_BR} generated rows")
         have = len(ct)
         if want > have:
             n_new = want - have

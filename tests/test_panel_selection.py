@@ -185,3 +185,12 @@ def test_emulated_comm_shapes():
     assert len(c.all_gather(t)) == 4 and c.emulated
     with pytest.raises(ValueError):
         EmulatedComm(4, 4)
+
+
+def test_plan_selection_rejects_degenerate_requests():
+    from ate_replication_causalml_amd.data import panel_selection as PS
+    from ate_replication_causalml_amd.data.dgp import TUTORIAL
+    with pytest.raises(ValueError):
+        PS.plan_selection(0, 1, TUTORIAL)
+    with pytest.raises(ValueError):
+        PS.plan_selection(10, 1, TUTORIAL, pt=0.0)
