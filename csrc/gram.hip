@@ -269,6 +269,11 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // (profiles/r05_gram_sync)
 #define GRAM_PRELOAD 1
 #endif
+#ifndef GRAM_PRIO
+// 1: s_setprio 1 for waves 4-7 of the paired-tile kernel (see gram_bf16_pair_kernel).
+// Tile kernel 2.60 -> 2.56-2.57 ms, same bits (profiles/r05_gram_sync, r05_s43)
+#define GRAM_PRIO 1
+#endif
 #ifndef GRAM_DIAG
 #define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA,
                       // 3 = 1 with only the off-diagonal tile's workgroups (each K-step
@@ -537,6 +542,12 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   const int bbuf = type == 0 ? 1 : region;
   const int base = tri ? 128 + (wid - 4) * 36 : wid * 32;
   float* out = slab + ((int64_t)c * ntiles + t) * (PAIR_SLOTS * 256) + (int64_t)base * 256;
+#if GRAM_PRIO
+  // the second-dispatched half (waves 4-7: the triangle waves of a diagonal pair, the
+  // heavier role) loses VALU / LDS issue arbitration to the older half on every stage;
+  // one static priority raise for it (uniform branch: readfirstlane)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
   if (tri)
     pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
   else
