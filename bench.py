@@ -228,7 +228,14 @@ def measure(args, comm, device, dgp, n_total, slot_comms_cache):
             return phases
         if gram_stream is not None:
             to_gram, to_fit, done = split_streams(i)
-            return [Collective(to_gram), phases[0], Collective(to_fit), *phases[1:],
+            g0 = phases[0]
+            if os.environ.get("ATE_BENCH_EAGER_GRAM", "1") == "1":
+                # the one-kernel Gram phase as a plain launch, not a one-node graph: the
+                # fit's reduce and the next Gram start ~55-65 us after the tile kernel ends
+                # instead of ~110-130 us (tutorial 3.30 -> 3.24-3.25 ms/step, same bits;
+                # profiles/r05_eg)
+                g0 = Collective(in_slot(phases[0], i))
+            return [Collective(to_gram), g0, Collective(to_fit), *phases[1:],
                     Collective(done)]
         return [Collective(wait_prev_gram), phases[0], Collective(record_gram), *phases[1:]]
 
