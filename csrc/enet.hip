@@ -1684,8 +1684,9 @@ ATE_API int ate_enet_coef(const void* apath, const void* probs, int nprob, int p
 // ------------------------------------------------------------------ K09 CV loss from held-out Gram
 // For fold problem q (trained without segment hold[q]) and every lambda m:
 // cvraw[q][m] = SSE / n_hold using the raw held-out Gram G[hold] (panel columns).
-// The nonzero coefficients are compacted first (ordered ballot scan), so the quadratic
-// form costs nnz^2 instead of p^2 — LASSO paths are sparse over most lambdas.
+// Rows of the held-out Gram outside every support of the chunk are skipped (LASSO paths
+// are sparse over most lambdas); a wave's next row is in flight while it applies the
+// current one.
 // One workgroup per (fold problem, chunk of CVL lambdas): every entry of the held-out
 // Gram is read ONCE per chunk and applied to all CVL coefficient vectors, which each lane
 // keeps in registers for its own columns j = lane + 64 k (dense: zeros off the support).
@@ -1710,6 +1711,7 @@ __global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
   const int yc = ycol_of_prob[q];
   __shared__ double sbeta[CVL][PMAX];
   __shared__ int sxc[PMAX];
+  __shared__ unsigned char snz[PMAX];
   __shared__ double sred[4][3 * CVL];
   for (int e = tid; e < CVL * PMAX; e += 256) {
     const int m = e / PMAX, j = e % PMAX;
@@ -1717,6 +1719,13 @@ __global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
     sbeta[m][j] = ok ? coef[((int64_t)q * L + m0 + m) * (p + 1) + 1 + j] : 0.0;
   }
   for (int j = tid; j < PMAX; j += 256) sxc[j] = j < p ? xcols[j] : xcols[0];
+  __syncthreads();
+  for (int j = tid; j < PMAX; j += 256) {
+    bool any = false;
+#pragma unroll
+    for (int m = 0; m < CVL; ++m) any |= sbeta[m][j] != 0.0;
+    snz[j] = any;                                   // row j inside some support
+  }
   __syncthreads();
   double bl[CVK][CVL];          // this lane's columns
 #pragma unroll
@@ -1742,15 +1751,26 @@ __global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
       }
     }
   }
-  for (int a = wid; a < p; a += 4) {
-    bool any = false;
-#pragma unroll
-    for (int m = 0; m < CVL; ++m) any |= sbeta[m][a] != 0.0;
-    if (!any) continue;                              // row outside every support (uniform)
+  // rows a = wid, wid + 4, ... inside some support of the chunk, in order; the next such
+  // row's Gram entries are loaded while the current row is applied (same arithmetic)
+  auto next_row = [&](int a) {
+    while (a < p && !snz[a]) a += 4;
+    return a;
+  };
+  auto load_row = [&](int a, double* g) {
     const double* Gr = Gh + (int64_t)sxc[a] * P;
-    double g[CVK];
 #pragma unroll
     for (int k = 0; k < CVK; ++k) g[k] = (k * 64 + lane < p) ? Gr[cl[k]] : 0.0;
+  };
+  double gn[CVK];
+  int a = next_row(wid);
+  if (a < p) load_row(a, gn);
+  while (a < p) {
+    double g[CVK];
+#pragma unroll
+    for (int k = 0; k < CVK; ++k) g[k] = gn[k];
+    const int an = next_row(a + 4);
+    if (an < p) load_row(an, gn);
 #pragma unroll
     for (int m = 0; m < CVL; ++m) {
       double t = 0.0;
@@ -1758,6 +1778,7 @@ __global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
       for (int k = 0; k < CVK; ++k) t = fma(g[k], bl[k][m], t);
       quad[m] = fma(sbeta[m][a], t, quad[m]);
     }
+    a = an;
   }
 #pragma unroll
   for (int m = 0; m < CVL; ++m) {
