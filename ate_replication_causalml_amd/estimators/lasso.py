@@ -289,6 +289,37 @@ def dml_residual_terms(pan, coef: torch.Tensor, rows: int = 1 << 20) -> torch.Te
     return torch.cat(out)
 
 
+_TRI: dict = {}
+
+
+def _tri_index(P: int, device):
+    """Flat indices of the upper triangle (i <= j) of a P x P matrix and of the mirrored
+    entries (j, i), row-major, cached per (P, device)."""
+    key = (P, str(device))
+    t = _TRI.get(key)
+    if t is None:
+        i, j = np.triu_indices(P)
+        t = (torch.as_tensor(i * P + j, dtype=torch.int64).to(device),
+             torch.as_tensor(j * P + i, dtype=torch.int64).to(device))
+        _TRI[key] = t
+    return t
+
+
+def allreduce_sym_(comm, t: torch.Tensor) -> torch.Tensor:
+    """In-place sum over ranks of a stack of symmetric P x P matrices (``t``: [..., P, P],
+    contiguous), moving only the upper triangles (half the ring bytes of a full
+    all-reduce); the lower triangle is mirrored from the reduced upper one, so the result
+    is exactly symmetric."""
+    P = t.shape[-1]
+    up, lo = _tri_index(P, t.device)
+    v = t.view(-1, P * P)
+    buf = v.index_select(1, up)
+    comm.all_reduce_(buf)
+    v.index_copy_(1, up, buf)
+    v.index_copy_(1, lo, buf)
+    return t
+
+
 def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G=None,
                shard_paths=True, exact=False):
     """The cross-fit DML-PLR step as phases for utils.graphs.SegmentedStep:
@@ -411,6 +442,17 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
             return st
         return Collective(f, capturable=cap)     # RCCL: captured inside the step's graph
 
+    def reduce_sym(name):
+        # C01 on the upper triangles only: the fold Grams are symmetric (csrc/gram.hip writes
+        # every entry once and mirrors it), so half the bytes cross the ring; the lower
+        # triangle is mirrored back from the reduced upper one
+        _tri_index(pan.P, pan.device)            # built here, never inside a capture
+
+        def f(st):
+            allreduce_sym_(comm, st[name])
+            return st
+        return Collective(f, capturable=cap)
+
     if exact:
         phases = [phase_gram, phase_gram_reduce]
         if dist:
@@ -433,7 +475,7 @@ def dml_phases(pan, folds: int, lambda_rule="min", comm=None, seg_counts=None, G
         return phases
     phases = [phase_gram, phase_gram_reduce]
     if dist:
-        phases.append(reduce("G"))
+        phases.append(reduce_sym("G"))
     if sharded:
         phases += [phase_fit_sharded, reduce("coef"), phase_resid]
     else:

@@ -380,3 +380,25 @@ def test_default_backend_one_rank_per_gpu(monkeypatch):
     assert C.default_backend() == "nccl"
     monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
     assert C.default_backend() == "gloo"
+
+
+def test_allreduce_sym_matches_full_allreduce():
+    """C01 moves only the upper triangles of the symmetric fold Grams; the result equals a
+    full all-reduce of symmetric inputs and is exactly symmetric."""
+    from ate_replication_causalml_amd.estimators.lasso import allreduce_sym_
+    P, nseg, world = 7, 3, 3
+
+    def stack(r):
+        g = torch.Generator().manual_seed(r)
+        a = torch.randn(nseg, P, P, dtype=torch.float64, generator=g)
+        return a + a.transpose(1, 2)
+
+    def body(c):
+        t = stack(c.rank)
+        full = t.clone()
+        c.all_reduce_(full)
+        allreduce_sym_(c, t)
+        return t, full
+    for t, full in run_simulated(world, body):
+        assert torch.equal(t, t.transpose(1, 2))
+        assert torch.allclose(t, full, rtol=0, atol=1e-12)
