@@ -1687,7 +1687,8 @@ ATE_API int ate_enet_coef(const void* apath, const void* probs, int nprob, int p
 // Rows of the held-out Gram outside every support of the chunk are skipped (LASSO paths
 // are sparse over most lambdas); a wave's next row is in flight while it applies the
 // current one.
-// One workgroup per (fold problem, chunk of CVL lambdas): every entry of the held-out
+// One workgroup per (fold problem, chunk of CVL lambdas), densest chunks dispatched first:
+// every entry of the held-out
 // Gram is read ONCE per chunk and applied to all CVL coefficient vectors, which each lane
 // keeps in registers for its own columns j = lane + 64 k (dense: zeros off the support).
 // quad_m = b_m' Gxx b_m accumulates per lane as sum_a b_m[a] * sum_{j in lane} G[a][j] b_m[j];
@@ -1700,7 +1701,10 @@ __global__ __launch_bounds__(256) void enet_cvloss_gauss_kernel(
     const int* __restrict__ xcols, int p, int ones_col, const int* __restrict__ ycol_of_prob,
     const double* __restrict__ coef, const int* __restrict__ nlam_out, int L, int q0,
     double* __restrict__ cvraw) {
-  const int q = q0 + blockIdx.y, m0 = blockIdx.x * CVL;
+  // grid (problem, chunk), chunks dispatched densest first: the last lambdas (largest
+  // supports) start in the first round, so the workgroups past one round of the chip are
+  // the sparse early-lambda chunks that skip most rows
+  const int q = q0 + blockIdx.x, m0 = (gridDim.y - 1 - blockIdx.y) * CVL;
   const int nl = nlam_out[q];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (m0 >= nl) {
@@ -1818,7 +1822,7 @@ ATE_API int ate_enet_cvloss_gauss(const void* G, int P, const void* hold, const 
                                   void* stream) {
   if (p > PMAX) return -1;
   if (nprob <= 0) return 0;
-  hipLaunchKernelGGL(enet_cvloss_gauss_kernel, dim3((L + CVL - 1) / CVL, nprob), dim3(256), 0,
+  hipLaunchKernelGGL(enet_cvloss_gauss_kernel, dim3(nprob, (L + CVL - 1) / CVL), dim3(256), 0,
                      (hipStream_t)stream, (const double*)G, P, (const int*)hold,
                      (const int*)xcols, p, ones_col, (const int*)ycol_of_prob,
                      (const double*)coef, (const int*)nlam_out, L, q0, (double*)cvraw);
