@@ -270,9 +270,11 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #define GRAM_PRELOAD 1
 #endif
 #ifndef GRAM_PRIO
-// 1: s_setprio 1 for waves 4-7 of the paired-tile kernel (see gram_bf16_pair_kernel).
-// Tile kernel 2.60 -> 2.56-2.57 ms, same bits (profiles/r05_gram_sync, r05_s43)
-#define GRAM_PRIO 1
+// s_setprio 1 for waves 4-7 of the paired-tile kernel (see gram_bf16_pair_kernel):
+// 1 = in every workgroup, 2 = in diagonal-pair workgroups only (their waves 4-7 are the
+// heavier triangle waves; the off-diagonal tile's waves are symmetric). Tile kernel, one
+// box: none 2.66-2.67, 1: 2.60, 2: 2.57 ms, same bits (profiles/r05_gram_sync)
+#define GRAM_PRIO 2
 #endif
 #ifndef GRAM_DIAG
 #define GRAM_DIAG 0   // timing-only builds (tools/gram_diag.py): 1 = no MFMA work, 2 = no DMA,
@@ -545,8 +547,12 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
 #if GRAM_PRIO
   // the second-dispatched half (waves 4-7: the triangle waves of a diagonal pair, the
   // heavier role) loses VALU / LDS issue arbitration to the older half on every stage;
-  // one static priority raise for it (uniform branch: readfirstlane)
+  // one static priority raise for it (uniform branches: readfirstlane, type)
+#if GRAM_PRIO == 2
+  if (type != 0 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#else
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
 #endif
   if (tri)
     pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
