@@ -338,3 +338,25 @@ def test_weighted_gram_bitwise_repeatable(gpu, dtype):
     Gs = [gram(pan, w=w).clone() for _ in range(3)]
     assert all(torch.equal(Gs[0], g) for g in Gs[1:])
     assert torch.equal(Gs[0], Gs[0].transpose(1, 2))
+
+
+def test_bench_eager_gram_matches_graph_gram(gpu):
+    """bench.py --stagger 2: the in-flight Gram as a plain launch on the Gram stream (the
+    default, ATE_BENCH_EAGER_GRAM=1) and as a one-node graph give the same ATE/SE bits."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for eg in ("0", "1"):
+        env = dict(os.environ, ATE_BENCH_EAGER_GRAM=eg)
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--rows", "1e6",
+                            "--steps", "2", "--warmup", "1", "--parity", "0", "--also-rct", "0"],
+                           capture_output=True, text=True, env=env, timeout=200)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        d = json.loads(line)
+        assert d["inflight"] == 3 and d["config"]["stagger"]
+        out[eg] = (d["ate_hex"], d["se_hex"])
+    assert out["0"] == out["1"]
