@@ -22,18 +22,19 @@ history there. ``--also-rct 1`` (default) then measures the same step on the RCT
 (``--dgp rct``: W independent of X, every coordinate of the W path moves -- the path
 solver's worst case) and reports it under ``"rct"``.
 
-Three cross-fits are in flight at every world size (``--inflight 3``): ``ms_per_step`` is
-the wall time per completed cross-fit (throughput); ``single_fit_ms`` in the JSON is the
-latency of one cross-fit alone (SURVEY.md §7.5 protocol: median of >= 5 single-call
-replays, each bracketed by device syncs; ``single_fit_rows_per_s`` = N / that). The Grams
-of all fits run back to back on one low-priority stream; each fit's path solve / residual
-pass / score runs on its own high-priority stream beside the next fit's Gram
-(``--stagger 2``). The panel uses the 64-row blocked layout (``--blocked 1``). With RCCL
-the all-reduces (C01 Gram stack, C08 coefficients, C06 moments) are captured inside the
-fit's graph (utils/graphs.SegmentedStep), so a fit is the same two graph launches at every
-world size; if capture of the collectives fails they run eagerly between graph segments
-and the JSON says so (``collectives_captured``). Each in-flight fit owns an RCCL
-communicator (``communicators``).
+Timed step (the metric of record): ONE ``ate_dml`` call on the resident
+panel, captured as the library runs it (one stream, the default Gram plan). The K timed
+steps are K such calls back to back on one stream; stream order serialises them, so no
+two fits overlap. ``value`` = N / ms_per_step. ``single_fit_ms`` is the median of >= 5
+replays each bracketed by device syncs (the §7.5 latency). The panel uses the 64-row
+blocked layout (``--blocked 1``). With RCCL the all-reduces (C01 Gram stack, C08
+coefficients, C06 moments) are captured inside the call's graph
+(utils/graphs.SegmentedStep); if capture of the collectives fails they run eagerly between
+graph segments and the JSON says so (``collectives_captured``).
+
+Secondary, reported under ``throughput_inflight`` and never as ``value``: ``--inflight 3``
+identical calls overlapped on streams (each fit's Gram on one low-priority stream beside
+another fit's latency-bound path solve), with a check that they return the same bits.
 
 Parity (``--parity 1``, untimed): the same kept rows as a float64 panel, fp64 Gram and
 fp64 path solves; the JSON reports |dATE| / SE_f64 and the relative SE difference.
@@ -93,61 +94,34 @@ def parse():
     ap.add_argument("--blocked", type=int, default=1,
                     help="1: 64-row blocked panel layout (one contiguous HBM run per Gram "
                          "K-step, ops/panel.py); 0: column-major")
-    ap.add_argument("--stagger", type=int, default=2,
-                    help="1: a fit's Gram waits for the previous fit's Gram (event between "
-                         "the streams); 2: the Grams of all fits run on one low-priority "
-                         "stream and the rest of each fit on its own high-priority stream")
     ap.add_argument("--exact", type=int, default=0,
                     help="1: world-size-invariant exact reduction mode (block-aligned row "
                          "shards, int64-limb Gram all-reduce, exact score moments: the same "
                          "ATE / SE bits at every world size; estimators/lasso.dml_phases)")
     ap.add_argument("--inflight", type=int, default=-1,
-                    help="independent cross-fits in flight (one hipGraph + stream + Gram "
-                         "workspace each); every timed step is still one complete DML-ATE")
+                    help="secondary throughput block: identical cross-fits in flight (one "
+                         "hipGraph + stream + Gram workspace each); 1 = skip")
     return ap.parse_args()
 
 
-def measure(args, comm, device, dgp, n_total, slot_comms_cache):
-    """Build the ``dgp`` panel, capture the in-flight fits, time ``args.steps`` steps and
-    the single-call latency. Returns a dict (and the panel, for the parity refit)."""
+def measure_inflight(args, comm, device, pan, inflight, fit_phases, agree, slot_comms_cache,
+                     sync, single):
+    """Secondary number: ``inflight`` independent cross-fits in flight (one hipGraph +
+    stream + Gram workspace each, slots 1..inflight). The CV path solve is a latency-bound
+    recurrence on few CUs, so another fit's HBM-bound Gram runs beside it. The fits are
+    the same call on the same panel (identical bits, checked): this is the throughput of
+    back-to-back calls, NOT the metric of record (that is the single call).
+    Returns a dict for the JSON's "inflight" block."""
     import torch
-    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
-    from ate_replication_causalml_amd.estimators.lasso import (EXACT_BLOCK, dml_phases,
-                                                               global_seg_counts)
-    from ate_replication_causalml_amd.ops.gram import plan_slot
     from ate_replication_causalml_amd.parallel import comm as C
     from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
-    world, rank = comm.world_size, comm.rank
-
-    def sync():
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-
-    sync()
-    t_gen = time.perf_counter()
-    pan = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed, dtype=args.dtype,
-                          blocked=bool(args.blocked) and args.dtype == "bf16",
-                          device=device, rank=rank, world=world,
-                          align=EXACT_BLOCK if args.exact else 0, dgp=dgp,
-                          comm=comm if world > 1 else None)
-    sync()
-    t_gen = time.perf_counter() - t_gen
-    seg_counts = global_seg_counts(pan, comm)   # fold sizes: data layout, fixed across steps
-    use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
-    # Independent cross-fits in flight at EVERY world size (same setting for the whole
-    # 1/2/4/8 curve): the CV path solve is a latency-bound serial recurrence that fills few
-    # CUs, so another fit's HBM-bound Gram runs beside it on its own stream.
-    inflight = 3 if args.inflight < 0 else max(1, args.inflight)
-    # One RCCL communicator per in-flight fit. The fits' graphs replay side by side on their
-    # own streams; collectives of ONE communicator must never run concurrently (their
-    # kernels share the communicator's channel buffers, and captured graphs replayed on
-    # different streams carry no order between them), while each fit's own collectives
-    # stay in stream order on its private communicator. gloo (CPU) ops are synchronous
-    # calls: one communicator serves every slot. Made once per process (reused by the
-    # second measurement).
+    world = comm.world_size
+    # One RCCL communicator per in-flight fit: collectives of ONE communicator must never
+    # run concurrently (their kernels share its channel buffers, and graphs replayed on
+    # different streams carry no order between them). Made once per process.
     if "slots" not in slot_comms_cache:
         slot_comms = [comm] * inflight
-        if world > 1 and inflight > 1 and isinstance(comm, C.TorchComm) and comm.capturable:
+        if world > 1 and isinstance(comm, C.TorchComm) and comm.capturable:
             import torch.distributed as tdist
             slot_comms = [comm] + [C.TorchComm(tdist.new_group(list(range(world))))
                                    for _ in range(inflight - 1)]
@@ -155,54 +129,19 @@ def measure(args, comm, device, dgp, n_total, slot_comms_cache):
                 c.barrier()             # create each communicator now, outside any capture
         slot_comms_cache["slots"] = slot_comms
     slot_comms = slot_comms_cache["slots"]
-    if inflight > 1:
-        # Gram workgroup count beside another fit's path solve: 1024 for two fits in
-        # lockstep (profiles/r01_bench/wg_inflight.log); staggered, 824-4096 are within 3 %
-        # and 2048 is the default (profiles/r02_overlap/stagger_sweep.log)
-        os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024" if not args.stagger else "2048")
-
-    def in_slot(ph, i):
-        if isinstance(ph, Collective):
-            return ph
-
-        def f(st):
-            with plan_slot(i):  # eager calls too: never share another fit's workspace
-                return ph(st)
-        return f
-
-    # Stagger: with two fits started together on two streams, the two Grams share the chip
-    # and then the two path solves leave it mostly idle, a lockstep that persists (both
-    # fits are identical). --stagger 1: one event orders the Grams across the streams (fit
-    # k's Gram starts when fit k-1's has finished). --stagger 2 (default): the Grams of all
-    # fits run on one low-priority stream, each fit's remaining phases on its own
-    # high-priority stream, so its path solve gets CUs ahead of the next Gram's
-    # workgroups. The hooks are eager phases between the captured graphs (the fit is split
-    # into a Gram-tile graph and a reduce/path/residual/score graph).
-    gram_done = {"ev": None}
-
-    def wait_prev_gram(st):
-        if gram_done["ev"] is not None:
-            torch.cuda.current_stream().wait_event(gram_done["ev"])
-        return st
-
-    def record_gram(st):
-        ev = torch.cuda.Event()
-        ev.record()
-        gram_done["ev"] = ev
-        return st
-
-    gram_stream = None
-    fit_streams = []
+    # Gram workgroup count beside another fit's path solve (staggered: 824-4096 within 3 %,
+    # 2048 the default; profiles/r02_overlap/stagger_sweep.log)
+    os.environ.setdefault("ATE_GRAM_PAIR_WG", "2048")
+    # --stagger 2: the Grams of all fits run on one low-priority stream, each fit's remaining
+    # phases on its own high-priority stream, so its path solve gets CUs ahead of the next
+    # Gram's workgroups (eager stream hooks between the Gram graph and the rest)
+    lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
+        else (0, -1)
+    gram_stream = torch.cuda.Stream(device, priority=lo)
+    fit_streams = [torch.cuda.Stream(device, priority=hi) for _ in range(inflight)]
     fit_done = [None] * inflight
-    if args.stagger == 2 and inflight > 1 and device.type == "cuda":
-        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") \
-            else (0, -1)
-        gram_stream = torch.cuda.Stream(device, priority=lo)
-        fit_streams = [torch.cuda.Stream(device, priority=hi) for _ in range(inflight)]
 
-    def split_streams(i):
-        # Gram of fit i on the shared low-priority stream (after fit i's previous solve
-        # has consumed the previous Gram), the rest on fit i's high-priority stream
+    def hooks(i):
         def to_gram(st):
             if fit_done[i] is not None:
                 gram_stream.wait_event(fit_done[i])
@@ -223,83 +162,165 @@ def measure(args, comm, device, dgp, n_total, slot_comms_cache):
             return st
         return to_gram, to_fit, done
 
-    def staggered(phases, i):
-        if not (args.stagger and inflight > 1 and device.type == "cuda"):
-            return phases
-        if gram_stream is not None:
-            to_gram, to_fit, done = split_streams(i)
-            g0 = phases[0]
-            if os.environ.get("ATE_BENCH_EAGER_GRAM", "1") == "1":
-                # the one-kernel Gram phase as a plain launch, not a one-node graph: the
-                # fit's reduce and the next Gram start ~55-65 us after the tile kernel ends
-                # instead of ~110-130 us (tutorial 3.30 -> 3.24-3.25 ms/step, same bits;
-                # profiles/r05_eg)
-                g0 = Collective(in_slot(phases[0], i))
-            return [Collective(to_gram), g0, Collective(to_fit), *phases[1:],
-                    Collective(done)]
-        return [Collective(wait_prev_gram), phases[0], Collective(record_gram), *phases[1:]]
-
     def make_run(i):
-        # device phases and RCCL collectives (world > 1) captured together; the stream
-        # hooks of the stagger stay eager between the Gram graph and the rest
-        with plan_slot(i):      # private Gram workspace per in-flight fit
-            phases = [in_slot(ph, i) for ph in staggered(
-                dml_phases(pan, args.folds, "min", comm=slot_comms[i], seg_counts=seg_counts,
-                           exact=bool(args.exact)), i)]
+        slot = i + 1
+        phases = fit_phases(slot, slot_comms[i])
+        to_gram, to_fit, done = hooks(i)
+        # the one-kernel Gram phase as a plain launch, not a one-node graph: the fit's
+        # reduce and the next Gram start ~55-65 us earlier (profiles/r05_eg)
+        g0 = Collective(phases[0]) if os.environ.get("ATE_BENCH_EAGER_GRAM", "1") == "1" \
+            else phases[0]
+        phases = [Collective(to_gram), g0, Collective(to_fit), *phases[1:], Collective(done)]
+        return SegmentedStep(phases, graph=True, agree=agree if world > 1 else None)
 
-            def agree(ok):
-                t = torch.tensor([float(ok)], device=device)
-                comm.all_reduce_min_(t)
-                return bool(t.item())
-            try:
-                return SegmentedStep(phases, graph=use_graph,
-                                     agree=agree if world > 1 else None), None
-            except Exception as e:  # noqa: BLE001 - reported, then every rank goes eager
-                torch.cuda.synchronize()
-                return SegmentedStep(phases, graph=False, warmup=0), repr(e)
-
-    runs, errors = [], []
-    home = torch.cuda.current_stream() if device.type == "cuda" else None
-    for i in range(inflight):
-        r, err = make_run(i)
-        if home is not None:
+    home = torch.cuda.current_stream()
+    runs = []
+    try:
+        for i in range(inflight):
+            runs.append(make_run(i))
             torch.cuda.set_stream(home)     # stream-switching phases leave another current
-        runs.append(r)
-        errors.append(err)
-    ok = torch.tensor([float(all(r.graphed for r in runs) if use_graph else 0)], device=device)
-    cc = torch.tensor([float(all(r.collectives_captured for r in runs))], device=device)
-    comm.all_reduce_min_(cc)
-    comm.all_reduce_min_(ok)
-    graphed = bool(ok.item())
-    if use_graph and not graphed:
-        # every rank falls back the same way: one eager fit at a time under slot 0's plan
-        print(f"[bench] rank {rank}: graph capture unavailable ({errors}); eager, inflight 1",
-              flush=True)
-        with plan_slot(0):
-            runs = [SegmentedStep(dml_phases(pan, args.folds, "min", comm=comm,
-                                             seg_counts=seg_counts, exact=bool(args.exact)),
-                                  graph=False, warmup=0)]
-    graphs_per_fit = runs[0].graph_count
-    # world 1 has no collectives; at world > 1: whether every rank captured them
-    collectives_captured = bool(cc.item()) if world > 1 and graphed else None
-    streams = [torch.cuda.Stream(device) if device.type == "cuda" and len(runs) > 1 else None
-               for _ in runs]
+        ok = agree(all(r.graphed for r in runs))
+    except Exception as e:  # noqa: BLE001 - the secondary block is skipped, not fatal
+        torch.cuda.set_stream(home)
+        sync()
+        print(f"[bench] in-flight block skipped: {e!r}", flush=True)
+        ok = agree(False)
+    finally:
+        os.environ.pop("ATE_GRAM_PAIR_WG", None)
+    if not ok:
+        return None
+    streams = [torch.cuda.Stream(device) for _ in runs]
 
     def run_step(k):
         i = k % len(runs)
-        if streams[i] is None:
-            return runs[i]()["res"]
         with torch.cuda.stream(streams[i]):
             return runs[i]()["res"]
 
+    for k in range(max(args.warmup, len(runs))):
+        run_step(k)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    outs = []
+    for k in range(args.steps):
+        r = run_step(k)
+        if k >= args.steps - len(runs):
+            outs.append(r)
+    sync()
+    comm.barrier()
+    sync()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    comm.all_reduce_max_(el)
+    ms = float(el.item()) / args.steps * 1e3
+    outs = [o.detach().cpu() for o in outs]
+    ref = single()["res"].detach().cpu()
+    ate, se = (float(v) for v in outs[0])
+    del runs
+    return {"inflight": inflight, "ms_per_fit": ms, "rows_per_s": pan_rows(pan, comm) / (ms / 1e3),
+            # the fits share one Gram plan (2048 workgroups: other row chunks than the single
+            # call's plan, so other fp32 partial sums): equal to each other bit for bit, to the
+            # single call up to the chunking's rounding
+            "fits_agree": all(bool(torch.equal(o, outs[0])) for o in outs),
+            "ate_hex": ate.hex(), "se_hex": se.hex(),
+            "abs_diff_ate_vs_single": abs(ate - float(ref[0])),
+            "rel_diff_se_vs_single": abs(se - float(ref[1])) / abs(float(ref[1])),
+            "stagger": True,
+            "communicators": len({id(c) for c in slot_comms}),
+            "note": "throughput of identical back-to-back calls overlapped on streams; not "
+                    "the metric of record"}
+
+
+def pan_rows(pan, comm):
+    import numpy as np
+    from ate_replication_causalml_amd.estimators.lasso import global_seg_counts
+    return float(np.asarray(global_seg_counts(pan, comm)).sum())
+
+
+def measure(args, comm, device, dgp, n_total, slot_comms_cache):
+    """Build the ``dgp`` panel, capture one ate_dml call, time ``args.steps`` calls back to
+    back (the metric of record) and the median single-call latency, then the secondary
+    in-flight throughput. Returns a dict (and the panel, for the parity refit)."""
+    import torch
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import (EXACT_BLOCK, dml_phases,
+                                                               global_seg_counts)
+    from ate_replication_causalml_amd.ops.gram import plan_slot
+    from ate_replication_causalml_amd.utils.graphs import Collective, SegmentedStep
+    world, rank = comm.world_size, comm.rank
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    sync()
+    t_gen = time.perf_counter()
+    pan = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed, dtype=args.dtype,
+                          blocked=bool(args.blocked) and args.dtype == "bf16",
+                          device=device, rank=rank, world=world,
+                          align=EXACT_BLOCK if args.exact else 0, dgp=dgp,
+                          comm=comm if world > 1 else None)
+    sync()
+    t_gen = time.perf_counter() - t_gen
+    seg_counts = global_seg_counts(pan, comm)   # fold sizes: data layout, fixed across steps
+    use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
+    exact = bool(args.exact)
+
+    def agree(ok):
+        t = torch.tensor([float(ok)], device=device)
+        comm.all_reduce_min_(t)
+        return bool(t.item())
+
+    def in_slot(ph, i):
+        if isinstance(ph, Collective):
+            return ph
+
+        def f(st):
+            with plan_slot(i):  # eager calls too: never share another fit's workspace
+                return ph(st)
+        return f
+
+    def fit_phases(slot, c):
+        return [in_slot(ph, slot) for ph in dml_phases(
+            pan, args.folds, "min", comm=c, seg_counts=seg_counts, exact=exact)]
+
+    # ---- the metric of record (SURVEY.md §7.5): ONE ate_dml call as the library runs it --
+    # its own captured step on one stream, the default Gram plan (whole rounds of
+    # workgroups), slot 0's workspace. The K timed steps are K such calls back to back on
+    # one stream (each call's Gram depends on nothing of the previous call's, but stream
+    # order serialises them: no two fits overlap).
+    saved = os.environ.pop("ATE_GRAM_PAIR_WG", None)
+    try:
+        with plan_slot(0):
+            try:
+                single = SegmentedStep(fit_phases(0, comm), graph=use_graph,
+                                       agree=agree if world > 1 else None)
+                err0 = None
+            except Exception as e:  # noqa: BLE001 - reported, then every rank goes eager
+                sync()
+                single, err0 = None, repr(e)
+    finally:
+        if saved is not None:
+            os.environ["ATE_GRAM_PAIR_WG"] = saved
+    graphed = agree(single is not None and single.graphed) if use_graph else False
+    if single is None or (use_graph and not graphed):
+        # every rank falls back the same way
+        print(f"[bench] rank {rank}: graph capture unavailable ({err0}); eager", flush=True)
+        del single
+        with plan_slot(0):
+            single = SegmentedStep(fit_phases(0, comm), graph=False, warmup=0)
+    graphs_per_fit = single.graph_count
+    # world 1 has no collectives; at world > 1: whether every rank captured them
+    collectives_captured = agree(single.collectives_captured) if world > 1 and graphed else None
+
     for k in range(args.warmup):
-        res = run_step(k)
+        res = single()["res"]
     sync()
     comm.barrier()
     sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        res = run_step(k)
+        res = single()["res"]
     sync()
     comm.barrier()
     sync()
@@ -307,59 +328,46 @@ def measure(args, comm, device, dgp, n_total, slot_comms_cache):
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
     comm.all_reduce_max_(el)
     elapsed = float(el.item())
-    # latency of ONE cross-fit alone (no overlap), SURVEY.md §7.5: median of >= 5 replays of
-    # one ate_dml call as the library runs it -- its own captured step on one stream with the
-    # default Gram plan (whole rounds of workgroups), not the throughput fits' split-stream
-    # graphs and their overlap-tuned plan
-    lat_step, lat_kind = None, "throughput fit 0"
-    if device.type == "cuda" and graphed:
-        saved = os.environ.pop("ATE_GRAM_PAIR_WG", None)
-        try:
-            with plan_slot(len(runs)):
-                lat_step = SegmentedStep(
-                    [in_slot(ph, len(runs)) for ph in dml_phases(
-                        pan, args.folds, "min", comm=comm, seg_counts=seg_counts,
-                        exact=bool(args.exact))], graph=True)
-            lat_kind = f"own step ({lat_step.graph_count} graph(s), default Gram plan)"
-        finally:
-            if saved is not None:
-                os.environ["ATE_GRAM_PAIR_WG"] = saved
+    ate, se = [float(v) for v in res.detach().cpu()]
+    if not (math.isfinite(ate) and math.isfinite(se)):
+        from ate_replication_causalml_amd.utils.guards import NumericalError
+        raise NumericalError(f"bench step returned ate={ate} se={se} (truncated CV fold path?)")
+    ms = elapsed / args.steps * 1e3
+    # latency of one call alone, each replay bracketed by device syncs (and a barrier):
+    # median of >= 5 replays, the slowest rank per replay
     nlat = max(5, min(args.steps, 11))
     lats = []
     for k in range(nlat):
         sync()
         comm.barrier()
         t1 = time.perf_counter()
-        if lat_step is not None:
-            lat_step()
-        else:
-            run_step(0)
+        single()
         sync()
         lats.append(time.perf_counter() - t1)
     lat_t = torch.tensor(lats, dtype=torch.float64, device=device)
-    comm.all_reduce_max_(lat_t)                     # per replay: the slowest rank
+    comm.all_reduce_max_(lat_t)
     lats = sorted(float(v) for v in lat_t.cpu())
     lat = lats[len(lats) // 2]
-    ate, se = [float(v) for v in res.detach().cpu()]
-    if not (math.isfinite(ate) and math.isfinite(se)):
-        from ate_replication_causalml_amd.utils.guards import NumericalError
-        raise NumericalError(f"bench step returned ate={ate} se={se} (truncated CV fold path?)")
-    ms = elapsed / args.steps * 1e3
+
+    inflight = 3 if args.inflight < 0 else max(1, args.inflight)
+    inflight_out = None
+    if inflight > 1 and device.type == "cuda" and graphed:
+        inflight_out = measure_inflight(args, comm, device, pan, inflight, fit_phases, agree,
+                                        slot_comms_cache, sync, single)
     out = {
         "dgp": dgp, "ms_per_step": ms, "rows_per_s": n_total / (ms / 1e3),
         "single_fit_ms": lat * 1e3, "single_fit_ms_all": [round(v * 1e3, 4) for v in lats],
-        "single_fit_step": lat_kind, "single_fit_rows_per_s": n_total / lat,
+        "single_fit_rows_per_s": n_total / lat,
         "ate": ate, "se": se, "ate_hex": ate.hex(), "se_hex": se.hex(),
         "n_kept": n_total, "n_generated": int(pan.n_generated) * 1,
-        "panel_gen_s": t_gen, "hipgraph": graphed, "inflight": len(runs),
-        "graphs_per_fit": graphs_per_fit, "collectives_captured": collectives_captured,
-        "communicators": len({id(c) for c in slot_comms}),
+        "panel_gen_s": t_gen, "hipgraph": graphed, "graphs_per_fit": graphs_per_fit,
+        "collectives_captured": collectives_captured,
         "layout": "blocked64" if pan.blocked else "colmajor",
-        "stagger": bool(args.stagger and len(runs) > 1 and device.type == "cuda"),
+        "inflight": inflight_out,
     }
     if world > 1 and pan.selection is not None:
         out["n_generated"] = int(pan.selection.n_gen)
-    del runs, lat_step
+    del single
     return out, pan, seg_counts
 
 
@@ -461,25 +469,23 @@ def main():
                 "dgp": args.dgp,
                 "n_kept": n_total,
                 "n_generated": main_m["n_generated"],
-                "inflight": main_m["inflight"],
                 "layout": main_m["layout"],
-                "stagger": main_m["stagger"],
+                "timed_step": "one ate_dml call (SURVEY.md 7.5), calls back to back on one "
+                              "stream, no two fits overlapping",
             },
             "ate": main_m["ate"],
             "se": main_m["se"],
             "ate_hex": main_m["ate_hex"],
             "se_hex": main_m["se_hex"],
             "hipgraph": main_m["hipgraph"],
-            "inflight": main_m["inflight"],
             "single_fit_ms": main_m["single_fit_ms"],
             "single_fit_ms_all": main_m["single_fit_ms_all"],
-            "single_fit_step": main_m["single_fit_step"],
             "single_fit_rows_per_s": main_m["single_fit_rows_per_s"],
             "graphs_per_fit": main_m["graphs_per_fit"],
             "exact": bool(args.exact),
             "collectives_captured": main_m["collectives_captured"],
-            "communicators": main_m["communicators"],
             "panel_gen_s": main_m["panel_gen_s"],
+            "throughput_inflight": main_m["inflight"],
             "parity": parity,
             "rct": None if rct is None else {k: rct[k] for k in (
                 "ms_per_step", "rows_per_s", "single_fit_ms", "single_fit_ms_all",

@@ -341,8 +341,9 @@ def test_weighted_gram_bitwise_repeatable(gpu, dtype):
 
 
 def test_bench_eager_gram_matches_graph_gram(gpu):
-    """bench.py --stagger 2: the in-flight Gram as a plain launch on the Gram stream (the
-    default, ATE_BENCH_EAGER_GRAM=1) and as a one-node graph give the same ATE/SE bits."""
+    """bench.py's in-flight block: the Gram as a plain launch on the Gram stream (the
+    default, ATE_BENCH_EAGER_GRAM=1) and as a one-node graph give the same ATE/SE bits, the
+    in-flight fits agree with each other and with the timed single call."""
     import json
     import os
     import subprocess
@@ -357,6 +358,11 @@ def test_bench_eager_gram_matches_graph_gram(gpu):
         assert r.returncode == 0, r.stderr[-2000:]
         line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
         d = json.loads(line)
-        assert d["inflight"] == 3 and d["config"]["stagger"]
-        out[eg] = (d["ate_hex"], d["se_hex"])
+        inf = d["throughput_inflight"]
+        assert inf["inflight"] == 3 and inf["stagger"]
+        assert inf["fits_agree"]                   # the three in-flight fits: same bits
+        # another Gram chunking than the single call: equal up to fp32 partial-sum rounding
+        assert inf["abs_diff_ate_vs_single"] <= 1e-3 * d["se"]
+        assert inf["rel_diff_se_vs_single"] <= 1e-4
+        out[eg] = (inf["ate_hex"], inf["se_hex"])
     assert out["0"] == out["1"]

@@ -16,6 +16,6 @@ import json, sys
 a = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 b = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 print(f"world {sys.argv[3]}: ranks ate={a['ate']!r} se={a['se']!r} | one process ate={b['ate']!r} se={b['se']!r} | "
-      f"diff {abs(a['ate'] - b['ate']):.2e} {abs(a['se'] - b['se']):.2e} | hipgraph {a['hipgraph']} inflight {a['inflight']}")
+      f"diff {abs(a['ate'] - b['ate']):.2e} {abs(a['se'] - b['se']):.2e} | hipgraph {a['hipgraph']} inflight {a.get('throughput_inflight')}")
 PY
 done

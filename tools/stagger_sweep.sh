@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: drives the round-2..5 bench, whose --stagger flag was removed in round 6 when
+#  the in-flight fits became the secondary "throughput_inflight" block)
 # Bench step with / without cross-stream Gram staggering and over Gram workgroup counts,
 # then a kernel trace of the default (staggered) step for tools/timeline.py.
 set -o pipefail
