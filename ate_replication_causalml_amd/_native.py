@@ -31,6 +31,7 @@ c_double = ctypes.c_double
 _SIGS = {
     "ate_gram_bf16": "pliipipipipppp",
     "ate_gram_bf16_pair": "pllipippipippipp",
+    "ate_gram_bf16_tri": "pllippipippipp",
     "ate_gram_f32": "plippipipippppp",
     "ate_gram_f64": "plippipipippppp",
     "ate_gram_tile_sizes": "pppp",

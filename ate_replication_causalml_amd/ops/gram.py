@@ -29,6 +29,12 @@ TARGET_WG = 2048   # workgroups per launch (>= 8 per CU on 256 CUs)
 # stages fetch half cache lines; profiles/r01_pmc/gram_variant*.txt.)
 GRAM_KERNEL = os.environ.get("ATE_GRAM_KERNEL", "pair")
 PAIR_SLOTS = 272
+# P == 512 (p <= 505 covariates, the bench shape): ATE_GRAM_TRI=1 selects the split-triangle
+# kernel (csrc/gram.hip gram_bf16_tri_kernel: 864 instead of 1024 column reads per chunk).
+# Measured and NOT the default (profiles/r06_gram): equal to the paired-tile kernel alone
+# (2.54-2.56 vs 2.52-2.56 ms) and 0.45 ms slower inside the single ate_dml call (2.73 vs 2.29)
+TRI_SLOTS, TRI_SPLIT = 288, 22
+GRAM_TRI = os.environ.get("ATE_GRAM_TRI", "0") == "1"
 PLAN_CACHE_MAX = int(os.environ.get("ATE_GRAM_PLAN_CACHE", 8))
 
 _plan_cache: dict = {}
@@ -59,6 +65,7 @@ class GramPlan:
             raise ValueError("weighted Gram needs an fp32/fp64 panel")
         P = panel.P
         self.pair = bf16 and P % (2 * BF16_TILE_BIG) == 0 and GRAM_KERNEL == "pair"
+        self.tri = self.pair and P == 512 and GRAM_TRI
         if bf16:
             T = BF16_TILE_BIG if P % BF16_TILE_BIG == 0 else BF16_TILE
         else:
@@ -67,7 +74,9 @@ class GramPlan:
         if P % T:
             raise ValueError(f"panel P={P} must be a multiple of {T}")
         nt = P // T
-        if self.pair:
+        if self.tri:
+            tiles, blocks = [(0, 0, 0, 0), (0, 0, 1, 0)], tri_blocks()
+        elif self.pair:
             tiles, blocks = _pair_tiles(nt)
         else:
             tiles = [(a, b) for a in range(nt) for b in range(a, nt)]
@@ -133,7 +142,7 @@ class GramPlan:
         self.chunks = torch.from_numpy(ch.view(np.uint8).copy()).to(dev)
         self.seg_chunk0 = torch.tensor(seg_chunk0, dtype=torch.int32, device=dev)
         slab_dtype = torch.float32 if panel.dtype != torch.float64 else torch.float64
-        per_tile = PAIR_SLOTS * 256 if self.pair else T * T
+        per_tile = (TRI_SLOTS if self.tri else PAIR_SLOTS) * 256 if self.pair else T * T
         self.slab = torch.empty(self.nchunks * ntiles * per_tile, dtype=slab_dtype, device=dev)
         self.G = torch.empty((panel.nseg, P, P), dtype=torch.float64, device=dev)
         self.Gx = torch.empty((2, panel.nseg, P, P), dtype=torch.int64, device=dev) \
@@ -218,6 +227,40 @@ def _pair_tiles(nt: int):
                         idx += 1
         blocks.append(tb)
     return tiles, blocks
+
+
+def tri_roles():
+    """Wave roles of the split-triangle kernel (csrc/gram.hip gram_bf16_tri_kernel, same
+    order): per workgroup type, per wave, (fragment column blocks, block list as pairs of
+    fragment indices). Mirrors RoleRect / RoleTri / RoleMix."""
+    def rect(a0, na, b0, nb):
+        return ([a0 + f for f in range(na)] + [b0 + f for f in range(nb)],
+                [(m, na + n) for m in range(na) for n in range(nb)])
+
+    def tri(s0, s):
+        return [s0 + f for f in range(s)], [(m, n) for m in range(s) for n in range(m, s)]
+    mix_blocks = [(0, n) for n in range(1, 6)] + [
+        (1 + 5 * g + m, 1 + 5 * g + n) for g in range(2) for m in range(5) for n in range(m, 5)]
+    t0 = [tri(0, 8), tri(8, 8), rect(0, 4, 8, 8), rect(4, 4, 8, 8), rect(0, 6, 16, 6),
+          rect(6, 5, 16, 6), rect(11, 5, 16, 6), tri(16, 6)]
+    t1 = [rect(0, 7, 22, 5), rect(7, 7, 22, 5), rect(14, 7, 22, 5), rect(0, 7, 27, 5),
+          rect(7, 7, 27, 5), rect(14, 7, 27, 5), rect(21, 6, 27, 5),
+          ([21 + f for f in range(11)], mix_blocks)]
+    return [t0, t1]
+
+
+def tri_blocks():
+    """Slab block table [2][TRI_SLOTS] of 16-column Gram blocks (I, J) for the
+    split-triangle kernel: wave w of a workgroup writes its k-th block to slot 36 w + k."""
+    out = []
+    for roles in tri_roles():
+        tb = [(-1, -1)] * TRI_SLOTS
+        for w, (fc, bl) in enumerate(roles):
+            assert len(bl) <= 36
+            for k, (a, b) in enumerate(bl):
+                tb[w * 36 + k] = (fc[a], fc[b])
+        out.append(tb)
+    return out
 
 
 def plan_for(panel: DevicePanel, weighted=False, exact=False) -> GramPlan:
@@ -305,6 +348,12 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
     G = pl.G if out is None else out
     Gx = pl.Gx.data_ptr() if exact else None
     s = _stream()
+    if X.dtype == torch.bfloat16 and pl.tri:
+        cs, bs = panel.strides()
+        _native.call("ate_gram_bf16_tri", X.data_ptr(), cs, bs, panel.P, pl.blocks.data_ptr(),
+                     pl.chunks.data_ptr(), pl.nchunks, pl.seg_chunk0.data_ptr(), panel.nseg,
+                     pl.slab.data_ptr(), G.data_ptr(), _STAGES[stage], Gx, s)
+        return pl.Gx if exact else G
     if X.dtype == torch.bfloat16 and pl.pair:
         cs, bs = panel.strides()
         _native.call("ate_gram_bf16_pair", X.data_ptr(), cs, bs, panel.P, pl.tiles.data_ptr(),
@@ -363,7 +412,7 @@ def _gram_cpu_exact(panel, w):
 
 def gram_reference(panel: DevicePanel, w=None) -> torch.Tensor:
     """Plain fp64 PyTorch reference of the same op (for numerics tests)."""
-    X = panel.data.double().cpu()
+    X = panel.colmajor().double().cpu()
     wv = None if w is None else w.double().cpu()
     out = []
     for (r0, r1) in panel.seg_bounds:

@@ -568,6 +568,214 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
 #endif
 }
 
+// ------------------------------------------------------------------ bf16 split-triangle kernel
+// P == 512 (32 column blocks of 16). Two workgroups per row chunk, both on one XCD:
+//   type 0 ("T"): stages columns 0..351 (22 blocks) and computes the upper triangle of blocks
+//                 I <= J < 22 (253 blocks);
+//   type 1 ("R"): stages all 512 columns and computes every block with J >= 22 (rows 0..21 x
+//                 cols 22..31 and the triangle 22..31: 275 blocks).
+// The paired-tile kernel's two workgroups each stage all 512 columns (the second reader of
+// every byte hits L2 on the first one's fetch); here only 352 of them are read twice, so a
+// chunk moves 864 column-reads into LDS instead of 1024 (-16 %) for the same 528 blocks.
+// Each wave owns a fixed role (a rectangle of A x B blocks, a triangle, or the one mixed role),
+// described at compile time by its fragment columns and block list; roles hold <= 36 blocks.
+constexpr int TRI_SLOTS = 288;            // slab blocks per (chunk, workgroup): 8 waves x 36
+constexpr int TRI_SPLIT = 22;             // column blocks staged by the type-0 workgroup
+
+template <int NF> struct FragCols { int c[NF]; };
+template <int NB> struct BlockPairs { int a[NB], b[NB]; };
+
+// rect<A0, NA, B0, NB>: fragments A0.., then B0..; block m*NB + n = (A0 + m, B0 + n)
+template <int A0, int NA, int B0, int NB>
+struct RoleRect {
+  static constexpr int NF = NA + NB, NBK = NA * NB;
+  static constexpr FragCols<NF> fc() {
+    FragCols<NF> r{};
+    for (int f = 0; f < NF; ++f) r.c[f] = f < NA ? A0 + f : B0 + (f - NA);
+    return r;
+  }
+  static constexpr BlockPairs<NBK> bp() {
+    BlockPairs<NBK> r{};
+    for (int m = 0; m < NA; ++m)
+      for (int n = 0; n < NB; ++n) { r.a[m * NB + n] = m; r.b[m * NB + n] = NA + n; }
+    return r;
+  }
+};
+// tri<S0, S>: fragments S0..S0+S-1 serve as A and B; blocks (m, n), m <= n, row-major
+template <int S0, int S>
+struct RoleTri {
+  static constexpr int NF = S, NBK = S * (S + 1) / 2;
+  static constexpr FragCols<NF> fc() {
+    FragCols<NF> r{};
+    for (int f = 0; f < NF; ++f) r.c[f] = S0 + f;
+    return r;
+  }
+  static constexpr BlockPairs<NBK> bp() {
+    BlockPairs<NBK> r{};
+    int i = 0;
+    for (int m = 0; m < S; ++m)
+      for (int n = m; n < S; ++n) { r.a[i] = m; r.b[i] = n; ++i; }
+    return r;
+  }
+};
+// the mixed role of type 1: fragments 21..31; (21, 22..26), triangle 22..26, triangle 27..31
+struct RoleMix {
+  static constexpr int NF = 11, NBK = 35;
+  static constexpr FragCols<NF> fc() {
+    FragCols<NF> r{};
+    for (int f = 0; f < NF; ++f) r.c[f] = 21 + f;
+    return r;
+  }
+  static constexpr BlockPairs<NBK> bp() {
+    BlockPairs<NBK> r{};
+    int i = 0;
+    for (int n = 1; n <= 5; ++n) { r.a[i] = 0; r.b[i] = n; ++i; }
+    for (int g = 0; g < 2; ++g)
+      for (int m = 0; m < 5; ++m)
+        for (int n = m; n < 5; ++n) { r.a[i] = 1 + 5 * g + m; r.b[i] = 1 + 5 * g + n; ++i; }
+    return r;
+  }
+};
+
+// One wave's whole K-loop in its role. The workgroup stages NPC 8-column pieces (columns
+// 0 .. 8 NPC - 1) per 64-row stage by LDS-DMA, double buffered; every wave issues its share
+// of the pieces, computes the current stage, waits for its own pieces of the next one and
+// meets the others at the barrier. PRE: both 32-row halves' fragments read before the MFMAs
+// (only where registers allow: 4 NBK + 8 NF <= 224).
+template <class R, int NSTG>
+__device__ __forceinline__ void tri_role(const bf16_t* __restrict__ X, int64_t cs, int64_t bs,
+                                         const Chunk& ch, int npc, bf16_t* lds_raw,
+                                         float* __restrict__ out) {
+  constexpr int NF = R::NF, NBK = R::NBK;
+  constexpr FragCols<NF> FC = R::fc();
+  constexpr BlockPairs<NBK> BP = R::bp();
+  constexpr bool PRE = 4 * NBK + 8 * NF <= 224;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int stage_elems = npc * 8 * GK;
+  const int mine = (npc - wid + 7) >> 3;          // LDS-DMA pieces this wave issues per stage
+  f32x4 acc[NBK];
+#pragma unroll
+  for (int i = 0; i < NBK; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int st, int64_t i0) {
+    bf16_t* dst = lds_raw + st * stage_elems;
+    const bf16_t* Xk = X + (i0 >> 6) * bs;
+    for (int q = wid; q < npc; q += 8) {
+      const int col = q * 8 + (lane >> 3);
+      const int cc = (lane & 7) ^ (col & 7);
+      glds16(Xk + (int64_t)col * cs + cc * 8, dst + q * 8 * GK);
+    }
+  };
+  auto frag = [&](const bf16_t* P_, int col, int cc) {
+    return *reinterpret_cast<const bf16x8*>(&P_[col * GK + ((cc ^ (col & 7)) << 3)]);
+  };
+  const int64_t nsteps = (ch.row1 - ch.row0) / GK;
+#pragma unroll
+  for (int j = 0; j < NSTG - 1; ++j)
+    if (j < nsteps) stage(j, ch.row0 + j * GK);
+  for (int64_t s = 0; s < nsteps; ++s) {
+    // stage s landed (this wave's pieces; at most the later stages' are outstanding), then
+    // the barrier: every wave's pieces of stage s landed, stage s - 1 consumed by every wave
+    // (raw s_barrier, not __syncthreads(): its fence would drain every LDS-DMA in flight,
+    // including the later stages'; lgkmcnt(0) retires this wave's reads of stage s - 1, whose
+    // buffer the DMA issued after the barrier overwrites)
+    if constexpr (NSTG > 2) {
+      const int64_t left = nsteps - 1 - s;
+      if (left > 0) wait_vmcnt((NSTG - 2) * mine);
+      else __builtin_amdgcn_s_waitcnt(0x0F70);
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (s + NSTG - 1 < nsteps) stage((int)((s + NSTG - 1) % NSTG), ch.row0 + (s + NSTG - 1) * GK);
+    const bf16_t* S_ = lds_raw + (int)(s % NSTG) * stage_elems;
+    if constexpr (PRE) {
+      bf16x8 fr[2][NF];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int cc = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int f = 0; f < NF; ++f) fr[kk][f] = frag(S_, FC.c[f] * 16 + (lane & 15), cc);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int b = 0; b < NBK; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kk][BP.a[b]], fr[kk][BP.b[b]],
+                                                           acc[b], 0, 0, 0);
+      // the first half's reads, then the second half's reads one per MFMA of the first half
+      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NBK - NF, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int cc = kk * 4 + (lane >> 4);
+        bf16x8 fr[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) fr[f] = frag(S_, FC.c[f] * 16 + (lane & 15), cc);
+#pragma unroll
+        for (int b = 0; b < NBK; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[BP.a[b]], fr[BP.b[b]], acc[b],
+                                                           0, 0, 0);
+      }
+    }
+  }
+  // lane-major 16x16 block images, one dwordx4 store per block (as the paired-tile kernel)
+#pragma unroll
+  for (int i = 0; i < NBK; ++i)
+    *reinterpret_cast<f32x4*>(out + i * 256 + lane * 4) = acc[i];
+}
+
+#ifndef GRAM_TRI_NSTG0
+// LDS stages of the type-0 workgroup (352 columns x 64 rows = 44 KB each): 3 = two stages in
+// flight while one is multiplied (132 KB); the type-1 workgroup's 64 KB stages fit only 2
+#define GRAM_TRI_NSTG0 3
+#endif
+constexpr int TRI_LDS = (GRAM_TRI_NSTG0 * TRI_SPLIT * 16 > 2 * 512 ? GRAM_TRI_NSTG0 * TRI_SPLIT * 16
+                                                                   : 2 * 512) * GK;
+
+__global__ __launch_bounds__(512) void gram_bf16_tri_kernel(
+    const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const Chunk* __restrict__ chunks,
+    int nchunks, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[TRI_LDS];   // 128 / 132 KB
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int c = L >> 1, type = L & 1;
+  ATE_DASSERT(c < nchunks);
+  const Chunk ch = chunks[c];
+  ATE_DASSERT(ch.row0 >= 0 && ch.row0 <= ch.row1 && ch.row0 % GK == 0 && ch.row1 % GK == 0);
+  const int wid = threadIdx.x >> 6;
+  float* out = slab + ((int64_t)c * 2 + type) * (TRI_SLOTS * 256) + (int64_t)wid * 36 * 256;
+  if (type == 0) {
+    constexpr int npc = TRI_SPLIT * 2;          // 352 columns = 44 pieces of 8
+    switch (wid) {
+      case 0: tri_role<RoleTri<0, 8>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      case 1: tri_role<RoleTri<8, 8>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      case 2: tri_role<RoleRect<0, 4, 8, 8>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      case 3: tri_role<RoleRect<4, 4, 8, 8>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      case 4: tri_role<RoleRect<0, 6, 16, 6>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      case 5: tri_role<RoleRect<6, 5, 16, 6>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      case 6: tri_role<RoleRect<11, 5, 16, 6>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+      default: tri_role<RoleTri<16, 6>, GRAM_TRI_NSTG0>(X, cs, bs, ch, npc, lds, out); break;
+    }
+  } else {
+    constexpr int npc = 64;                     // all 512 columns
+    switch (wid) {
+      case 0: tri_role<RoleRect<0, 7, 22, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      case 1: tri_role<RoleRect<7, 7, 22, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      case 2: tri_role<RoleRect<14, 7, 22, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      case 3: tri_role<RoleRect<0, 7, 27, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      case 4: tri_role<RoleRect<7, 7, 27, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      case 5: tri_role<RoleRect<14, 7, 27, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      case 6: tri_role<RoleRect<21, 6, 27, 5>, 2>(X, cs, bs, ch, npc, lds, out); break;
+      default: tri_role<RoleMix, 2>(X, cs, bs, ch, npc, lds, out); break;
+    }
+  }
+}
+
 // Exact (world-size-invariant) reduction: a chunk partial v is split into two int64 limbs
 // of fixed scale, hi = floor(v 2^24), lo = rint((v 2^24 - hi) 2^32) (both exact in fp64),
 // and the limbs of all chunks are summed as integers -- associative, so the rank that
@@ -583,15 +791,16 @@ __device__ __forceinline__ void gram_limbs(double v, long long& hi, long long& l
 // side = row), (-1, -1) = unused slot. Blocks with I == J are full 16x16 diagonal blocks: only
 // their r <= c entries are written (plus mirror), so every Gram entry has ONE writer.
 __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const int2* __restrict__ blocks,
-                                        int ntiles, const int* __restrict__ seg_chunk0, int nseg,
-                                        int P, double* __restrict__ G, long long* __restrict__ Gx) {
-  const int64_t per = (int64_t)ntiles * PAIR_SLOTS * 256;
+                                        int ntiles, int slots, const int* __restrict__ seg_chunk0,
+                                        int nseg, int P, double* __restrict__ G,
+                                        long long* __restrict__ Gx) {
+  const int64_t per = (int64_t)ntiles * slots * 256;
   const int64_t total = (int64_t)nseg * per;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     const int s = (int)(e / per);
     const int64_t rem = e % per;
-    const int tb = (int)(rem >> 8);                 // tile * PAIR_SLOTS + slot
+    const int tb = (int)(rem >> 8);                 // tile * slots + slot
     const int ln = (int)(rem & 255) >> 2;           // lane-major image (pair_wave epilogue)
     const int r = ((ln >> 4) << 2) | (int)(rem & 3), cl = ln & 15;
     const int2 bl = blocks[tb];
@@ -664,8 +873,29 @@ ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, con
   if (what & 2) {
     const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
     hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
-                       (const float*)slab, (const int2*)blocks, ntiles, (const int*)seg_chunk0,
-                       nseg, P, (double*)G, (long long*)Gx);
+                       (const float*)slab, (const int2*)blocks, ntiles, PAIR_SLOTS,
+                       (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx);
+    ATE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// Split-triangle Gram (P == 512): what as ate_gram_bf16_pair; blocks = [2][TRI_SLOTS] int2.
+ATE_API int ate_gram_bf16_tri(const void* X, int64_t cs, int64_t bs, int P, const void* blocks,
+                              const void* chunks, int nchunks, const void* seg_chunk0, int nseg,
+                              void* slab, void* G, int what, void* Gx, void* stream) {
+  if (P != 512 || what < 1 || what > 3) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  if (what & 1) {
+    hipLaunchKernelGGL(gram_bf16_tri_kernel, dim3(nchunks * 2), dim3(512), 0, s,
+                       (const bf16_t*)X, cs, bs, (const Chunk*)chunks, nchunks, (float*)slab);
+    ATE_CHECK_LAUNCH();
+  }
+  if (what & 2) {
+    const int64_t total = (int64_t)nseg * 2 * TRI_SLOTS * 256;
+    hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+                       (const float*)slab, (const int2*)blocks, 2, TRI_SLOTS,
+                       (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx);
     ATE_CHECK_LAUNCH();
   }
   return 0;

@@ -71,6 +71,37 @@ def test_gram_pair_kernel_vs_tile256(gpu, monkeypatch, p):
     assert torch.equal(G0, G0.transpose(1, 2))
 
 
+@pytest.mark.parametrize("blocked", [False, True])
+def test_gram_tri_kernel_vs_pair(gpu, monkeypatch, blocked):
+    """Split-triangle kernel (P == 512, csrc/gram.hip gram_bf16_tri_kernel) vs the paired-tile
+    kernel vs fp64, on a column-major and on a 64-row blocked panel; symmetric, every block
+    written once (the slab table covers the triangle: tests/test_gram_plan.py)."""
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    if blocked:
+        pan = synthetic_panel(40000, p=480, folds=5, seed=5, dtype="bf16", blocked=True,
+                              device=gpu)
+    else:
+        rs = np.random.RandomState(5)
+        n = 7000
+        pan = build_panel(rs.randn(n, 400), rs.rand(n), rs.randint(0, 2, n),
+                          folds=rs.randint(0, 5, n), dtype="bf16", device=gpu)
+    assert pan.P == 512
+    gram_op._plan_cache.clear()
+    monkeypatch.setattr(gram_op, "GRAM_TRI", True)
+    assert gram_op.plan_for(pan).tri
+    Gt = gram_op.gram(pan).clone()
+    gram_op._plan_cache.clear()
+    monkeypatch.setattr(gram_op, "GRAM_TRI", False)
+    assert not gram_op.plan_for(pan).tri
+    Gp = gram_op.gram(pan).clone()
+    gram_op._plan_cache.clear()
+    ref = gram_op.gram_reference(pan).to(gpu)
+    scale = ref.abs().max()
+    assert ((Gt - ref).abs().max() / scale) < 2e-6
+    assert ((Gt - Gp).abs().max() / scale) < 2e-6
+    assert torch.equal(Gt, Gt.transpose(1, 2))
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_weighted_gram_kernel(gpu, dtype):
     rs = np.random.RandomState(1)

@@ -43,3 +43,20 @@ def test_pair_chunks_small_segments():
     _check(segs, 64, chunks, c0)
     # a segment shorter than its chunk count gets one chunk per K-step
     assert [c0[s + 1] - c0[s] for s in range(3)] == [1, 5, 2]
+
+
+def test_tri_blocks_cover_the_upper_triangle_once():
+    """Split-triangle kernel (P == 512): the slab table names every 16-column block I <= J of
+    the 32 x 32 block triangle exactly once; the type-0 workgroup only blocks of the first 22
+    columns blocks (the 352 columns it stages), every wave at most 36 blocks."""
+    from ate_replication_causalml_amd.ops.gram import TRI_SLOTS, TRI_SPLIT, tri_blocks, tri_roles
+    tb = tri_blocks()
+    assert len(tb) == 2 and all(len(t) == TRI_SLOTS for t in tb)
+    used = [b for t in tb for b in t if b[0] >= 0]
+    assert sorted(used) == [(i, j) for i in range(32) for j in range(i, 32)]
+    assert all(j < TRI_SPLIT for i, j in tb[0] if i >= 0)
+    for roles in tri_roles():
+        assert len(roles) == 8
+        for fc, bl in roles:
+            assert len(bl) <= 36 and len(set(fc)) == len(fc)
+            assert all(fc[a] <= fc[b] for a, b in bl)

@@ -1,5 +1,5 @@
 """Run the bf16 Gram kernel alone on the N=1e7, p=500 bench panel (A/B of the 256-tile
-kernel variants, and for PMC profiling). Usage: gram_only.py [N] [pair|tile256 ...]; ATE_BLOCKED=0 for a column-major panel"""
+kernel variants, and for PMC profiling). Usage: gram_only.py [N] [tri|pair|tile256 ...]; ATE_BLOCKED=0 for a column-major panel"""
 import os
 import sys
 
@@ -17,7 +17,9 @@ pan = synthetic_panel(n, p=500, folds=5, seed=1991, dtype="bf16", device=torch.d
 ref = None
 stage = os.environ.get("ATE_GRAM_STAGE", "all")   # "tiles": the tile kernel alone (no slab reduce)
 for v in variants:
-    gram_mod.GRAM_KERNEL = v
+    # "tri": the split-triangle kernel (P == 512); "pair": the paired-tile kernel
+    gram_mod.GRAM_KERNEL = "pair" if v == "tri" else v
+    gram_mod.GRAM_TRI = v == "tri"
     gram_mod._plan_cache.clear()
     for _ in range(3):
         G = gram_mod.gram(pan)
