@@ -26,6 +26,7 @@ import torch
 
 from ..models import gbdt as G
 from ..ops import stats as S
+from ..ops.linalg import logistic
 from ..parallel import rng
 from .common import as_np, read_result, resolve_device
 
@@ -44,7 +45,7 @@ def _response(m, dev):
     """Raw boosting scores of every row -> response on ``dev`` (no host copy for GPU fits)."""
     f = m.scores if isinstance(m.scores, torch.Tensor) else torch.from_numpy(np.asarray(m.scores))
     f = f.to(dev, torch.float64)
-    return torch.sigmoid(f) if m.loss == "logistic" else f
+    return logistic(f) if m.loss == "logistic" else f
 
 
 def _all_ranks_have(ck, stage, dkey, dist, dev):

@@ -25,7 +25,7 @@ import torch
 
 from .. import _native
 from ..models import forest as F
-from ..ops.linalg import logistic_irls
+from ..ops.linalg import logistic, logistic_irls
 from ..ops.panel import build_panel
 from ..ops.scan import compact_rows
 from ..parallel import rng
@@ -73,7 +73,7 @@ def _glm_fit_predict(Xd, tr_idx, ytr_host, ho_idx, dev):
     fit = logistic_irls(pan, cols, pan.cols["Y"], pan.cols["z"])
     beta = torch.nan_to_num(fit.beta.double(), nan=0.0).to(dev)
     eta = beta[0] + Xd.index_select(0, ho_idx) @ beta[1:]
-    return torch.sigmoid(eta)
+    return logistic(eta)
 
 
 def _gbdt_fit_predict(y, train, ho, Xb, edges, dev, seed, gbdt_kw):
@@ -86,7 +86,7 @@ def _gbdt_fit_predict(y, train, ho, Xb, edges, dev, seed, gbdt_kw):
                    train=train if be == "gpu" else train.cpu().numpy(), seed=seed, backend=be,
                    edges=edges, Xb=Xb, **(gbdt_kw or {}))
     f = torch.as_tensor(m.scores, dtype=torch.float64).to(dev)[ho]
-    return torch.sigmoid(f) if loss == "logistic" else f
+    return logistic(f) if loss == "logistic" else f
 
 
 _NAMES = ("e", "mu1", "mu0")

@@ -18,6 +18,17 @@ from .panel import DevicePanel, dtype_code
 LM_TOL = 1e-7
 
 
+def logistic(x: torch.Tensor) -> torch.Tensor:
+    """1 / (1 + exp(-x)) with a result that depends on each element alone. On the CPU,
+    torch.sigmoid's vectorised body and its scalar tail round differently, so the same row
+    got a different last bit depending on where a rank's shard ended (world 8, found by
+    tests/test_world8.py); exp and the division are exact per element in every lane. GPU
+    tensors keep torch.sigmoid (no tail path: one formula per element)."""
+    if x.is_cuda:
+        return torch.sigmoid(x)
+    return torch.reciprocal(1.0 + torch.exp(-x))
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -138,7 +149,7 @@ def predict(panel: DevicePanel, cols, beta: torch.Tensor, override_idx: int = -1
             X[override_idx] = override_val
         b = torch.nan_to_num(beta.double(), nan=0.0)
         eta = b @ X
-        return torch.sigmoid(eta) if lk else eta
+        return logistic(eta) if lk else eta
     out = out if out is not None else torch.empty(panel.ld, dtype=torch.float64, device=panel.device)
     _native.call("ate_predict", dtype_code(panel.data), panel.data.data_ptr(), panel.cm_ld, panel.ld,
                  cols_t.data_ptr(), beta.data_ptr(), cols_t.numel(), override_idx, override_val, lk,

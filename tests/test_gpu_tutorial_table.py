@@ -1,16 +1,17 @@
-"""The tutorial's 14-row table on the synthetic DGP against the PUBLISHED table's
-pattern (ate_replication.md:118,157,233,317). R and the real CSV are absent,
-so values cannot match exactly; the DGP is calibrated (data/dgp.py TUTORIAL,
-tests/test_dgp_calibration.py) and what the published report shows, this test holds:
+"""The tutorial's 14-row table on the synthetic DGP against the PUBLISHED table
+(reference/published.py: /root/reference/ate_replication.md:118,157,233,294,317; SURVEY.md
+§6). R and the real CSV are absent, so values cannot match exactly; the DGP is calibrated
+(data/dgp.py TUTORIAL, tests/test_dgp_calibration.py) and on it, through the HIP kernels:
 
-* the selection transform drops ~41,062 of 50,000 rows (within 2 %);
-* the RCT oracle sits near 0.096 and selection bias drives the naive difference to ~0;
-* the outcome-model family (Direct Method, DR with logistic PS, Belloni, residual
-  balancing, causal forest) recovers the oracle to within a few hundredths;
-* Propensity_Weighting (published 0.064) lands below the oracle and
-  Propensity_Weighting_LASSOPS (0.011) below it; Double ML (0.052) in [0.03, 0.08];
-* the reference's DR-RF (counterfactual quirk Q6, ate_functions.R:160-164) and the usual
-  LASSO stay near the naive value (published 0.004 and 0.025)."""
+* every row with a published CI lands inside that CI (digitised, +-0.001);
+* the CI-less LASSO rows (ate_functions.R:107,129) within 0.03 of the published points
+  (Usual LASSO sits at the band's edge: tests/test_tutorial_table.py says why);
+* the selection transform drops 41,062 +- 2 % of 50,000 rows;
+* the causal forest's printed "incorrect" mean-CATE line, 0.083 (SE 0.198), in sign and
+  magnitude;
+* the reference's orderings: selection bias drives the naive difference to ~0, the
+  LASSO-PS IPW below the logistic-PS IPW, the DR-RF quirk (Q6) near the naive value.
+The CPU twin (fp64 T-ref + host forest engine) is tests/test_tutorial_table.py."""
 import math
 
 import pytest
@@ -18,23 +19,18 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_replicate_table_matches_published_pattern(gpu):
+def test_replicate_table_matches_published(gpu):
     import ate_replication_causalml_amd as ate
     from ate_replication_causalml_amd.config import ReplicateConfig
+    from ate_replication_causalml_amd.reference import published as P
     rep = ate.replicate(config=ReplicateConfig())
     v = {r.method: (r.ate, r.se) for r in rep.results}
     assert len(v) == 14
+    cf = [r for r in rep.results if r.method == "Causal Forest(GRF)"][0]
+    msgs = P.check_table(v, rep.n_dropped, (cf.diagnostics["ate_bad"], cf.diagnostics["se_bad"]))
+    assert msgs == [], msgs
     oracle = v["oracle"][0]
-    assert 0.08 < oracle < 0.12
     assert abs(v["naive"][0]) < 0.03 and v["naive"][0] < oracle - 0.06
-    for m in ("Direct Method", "Doubly Robust with logistic regression PS", "Belloni et.al",
-              "residual_balancing", "Causal Forest(GRF)"):
-        assert abs(v[m][0] - oracle) < 0.035, (m, v[m], oracle)
-        assert 0.003 < v[m][1] < 0.03
-    for m in ("Doubly Robust with Random Forest PS", "Usual LASSO"):
-        assert v[m][0] < oracle - 0.05, (m, v[m], oracle)
     assert math.isnan(v["Single-equation LASSO"][1]) and math.isnan(v["Usual LASSO"][1])
-    assert v["Propensity_Weighting"][0] < oracle
-    assert v["Propensity_Weighting_LASSOPS"][0] < v["Propensity_Weighting"][0]
-    assert 0.03 <= v["Double Machine Learning"][0] <= 0.08
-    assert abs(rep.n_dropped - 41_062) <= 0.02 * 41_062, rep.n_dropped
+    assert v["Propensity_Weighting_LASSOPS"][0] < v["Propensity_Weighting"][0] < oracle
+    assert v["Doubly Robust with Random Forest PS"][0] < oracle - 0.05
