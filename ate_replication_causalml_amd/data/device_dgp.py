@@ -97,6 +97,9 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
             n_total, seed, params, comm=pcomm, device=pan.data.device, compat=compat)
         if sel.n_keep != n_total or sel.seed != seed:
             raise ValueError("selection plan does not match (n_total, seed)")
+        if sel.compat != compat or sel.params != params:
+            raise ValueError(f"selection plan made for compat={sel.compat!r} / other DGP "
+                             f"parameters, not compat={compat!r}")
         gids = kept_gids(sel, slices, device=pan.data.device)
     offs = np.concatenate([[0], np.cumsum([c for _, c in slices])])
     if pan.data.is_cuda:

@@ -58,11 +58,12 @@ class DgpParams:
     factor_load: float = 0.6
 
     def device_block(self) -> np.ndarray:
-        """The float32[18] parameter block of csrc/dgp.hip (load_params)."""
+        """The float64[18] parameter block of csrc/dgp.hip (load_params: the selection
+        rule's parameters used at full precision, the rest rounded to fp32 there)."""
         fl = self.factor_load
         return np.array([self.intercept, *self.b_hist, self.b_latent, self.tau_logit,
                          self.p_treat, *self.hist_thresh, self.hist_latent, self.yob_latent,
-                         fl, np.sqrt(1 - fl ** 2)], dtype=np.float32)
+                         fl, np.sqrt(1 - fl ** 2)], dtype=np.float64)
 
 
 # The scaled-config panels (data/device_dgp.synthetic_panel, the bench) and the HIP

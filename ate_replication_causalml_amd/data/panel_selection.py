@@ -24,8 +24,11 @@ function of (seed, g)) before any panel row is written:
 
 Every rank derives the same n_gen / thresholds / kept set from the same integers, so the
 union of the shards is the same data set at every world size. On a CPU panel the flags
-come from the float64 host twin (dgp.selection_flags); on the GPU from the float32 device
-draws (the values the panel stores).
+come from the host (dgp.selection_flags), on the GPU from the device kernels: both compute
+the draws the rule reads in fp64 with the same formulas (csrc/dgp.hip core_draws, no FMA
+contraction), so a CPU panel and a GPU panel of the same (N, seed) keep the same rows
+(tests/test_gpu_panel_selection.py; a flag could differ only for a draw within an ulp of a
+threshold, where the two log / cos implementations may round differently).
 """
 from __future__ import annotations
 

@@ -3,6 +3,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+
+#include <vector>
 
 #define ATE_API extern "C" __attribute__((visibility("default")))
 
@@ -127,4 +130,82 @@ inline int grid_for(int64_t n, int block, int cap = 2048) {
 #define ATE_DASSERT(cond) do { } while (0)
 #endif
 
-#define ATE_CHECK_LAUNCH() do { hipError_t e_ = hipGetLastError(); if (e_ != hipSuccess) return (int)e_; } while (0)
+// ---------------------------------------------------------------- launch errors
+// Every kernel launch goes through ATE_LAUNCH: hipLaunchKernelGGL between a check of the
+// error state BEFORE it and one AFTER it. A failed launch is recorded as "hipErrorName
+// (code): description" with its entry point, file and line, and the entry point's next
+// ATE_CHECK_LAUNCH returns the HIP error code; ate_last_error (csrc/errors.hip) hands the
+// text to the host, where _native.call puts it in its exception. An error left pending by an
+// EARLIER HIP call (another library's, or an ignored one) is not this launch's: ATE_LAUNCH
+// clears it first and records it separately as stale (ate_last_stale_error), so it cannot
+// be reported under this entry point's name (the unexplained "ate_forest_fit_exact failed
+// with status 1" of round 5 was such a report: profiles/r05_debug/README.md).
+namespace ate {
+struct LaunchError {
+  int code = 0;
+  bool pending = false;        // recorded by a launch, not yet returned by ATE_CHECK_LAUNCH
+  char msg[512] = {0};
+};
+inline thread_local LaunchError g_launch_error, g_stale_error;
+
+inline void record_error(LaunchError& slot, hipError_t e, const char* what, const char* func,
+                         const char* file, int line) {
+  slot.code = (int)e;
+  snprintf(slot.msg, sizeof(slot.msg), "%s (%d): %s; %s in %s at %s:%d", hipGetErrorName(e),
+           (int)e, hipGetErrorString(e), what, func, file, line);
+}
+inline void launch_pre(const char* func, const char* file, int line) {
+  const hipError_t e = hipGetLastError();   // returns AND clears the pending error
+  if (e != hipSuccess)
+    record_error(g_stale_error, e, "pending before a launch (an earlier HIP call's)", func,
+                 file, line);
+}
+inline void launch_post(const char* func, const char* file, int line) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess && !g_launch_error.pending) {
+    record_error(g_launch_error, e, "kernel launch failed", func, file, line);
+    g_launch_error.pending = true;
+  }
+}
+inline int take_launch_error() {
+  if (!g_launch_error.pending) return 0;
+  g_launch_error.pending = false;
+  return g_launch_error.code;
+}
+}  // namespace ate
+
+// Launch shapes of the heavy kernels (block size, dynamic LDS), registered next to each
+// kernel: the debug build checks them against the compiled kernels' attributes at library
+// load (ate_check_kernel_resources, csrc/errors.hip; _native.hip() under ATE_DEBUG=1).
+namespace ate {
+struct KernelShape {
+  const void* fn;
+  const char* name;
+  int threads, dyn_lds;
+};
+inline std::vector<KernelShape>& kernel_shapes() {
+  static std::vector<KernelShape> v;
+  return v;
+}
+struct KernelShapeReg {
+  KernelShapeReg(const void* f, const char* n, int t, int d) { kernel_shapes().push_back({f, n, t, d}); }
+};
+}  // namespace ate
+#define ATE_CAT2(a, b) a##b
+#define ATE_CAT(a, b) ATE_CAT2(a, b)
+#define ATE_KERNEL_SHAPE(name, threads, dyn_lds, ...)                                   \
+  static ate::KernelShapeReg ATE_CAT(ate_kshape_, __LINE__)((const void*)(__VA_ARGS__), \
+                                                              name, threads, dyn_lds);
+
+#define ATE_LAUNCH(...)                                   \
+  do {                                                    \
+    ate::launch_pre(__func__, __FILE__, __LINE__);        \
+    hipLaunchKernelGGL(__VA_ARGS__);                      \
+    ate::launch_post(__func__, __FILE__, __LINE__);       \
+  } while (0)
+
+#define ATE_CHECK_LAUNCH()                                \
+  do {                                                    \
+    const int e_ = ate::take_launch_error();              \
+    if (e_ != 0) return e_;                               \
+  } while (0)

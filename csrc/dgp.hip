@@ -29,10 +29,16 @@ struct DgpP {
   float intercept, b_hist[5], b_latent, tau_logit, p_treat, thr[5], hist_latent, yob_latent,
       factor_load, factor_rest;
   int uniform_b;      // all b_hist equal: eta uses b * (sum of history bits)
+  // the selection rule's parameters at full precision (core_draws works in fp64)
+  double p_treat_d, thr_d[5], hist_latent_d, yob_latent_d;
 };
 
-DgpP load_params(const float* a) {
+DgpP load_params(const double* a) {
   DgpP P;
+  P.p_treat_d = a[8];
+  for (int k = 0; k < 5; ++k) P.thr_d[k] = a[9 + k];
+  P.hist_latent_d = a[14];
+  P.yob_latent_d = a[15];
   P.intercept = a[0];
   for (int k = 0; k < 5; ++k) P.b_hist[k] = a[1 + k];
   P.b_latent = a[6];
@@ -58,24 +64,44 @@ __device__ __forceinline__ float dgp_uniform(uint64_t seed, uint32_t stream, uin
   u32x4 w = rand4(seed, P_DGP, stream, idx);
   return (float)(w.x >> 8) * (1.0f / 16777216.0f);
 }
+// fp64 twins with the host's exact formulas (parallel/rng.py normal_pair / uniform): the
+// draws the selection rule reads are computed in fp64 on both sides, so the CPU and the GPU
+// panel keep the same rows (a flag can differ only where a draw lies within an ulp of a
+// threshold)
+__device__ __forceinline__ double dgp_normal_d(uint64_t seed, uint32_t stream, uint64_t idx) {
+#pragma clang fp contract(off)
+  u32x4 w = rand4(seed, P_DGP, stream, idx);
+  const double u1 = ((double)(w.x >> 8) + 1.0) * (1.0 / 16777217.0);
+  const double u2 = (double)(w.y >> 8) * (1.0 / 16777216.0);
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+__device__ __forceinline__ double dgp_uniform_d(uint64_t seed, uint32_t stream, uint64_t idx) {
+  u32x4 w = rand4(seed, P_DGP, stream, idx);
+  return (double)(w.x >> 8) * (1.0 / 16777216.0);
+}
 
 // The draws the selection rule reads (one definition for the fill and both selection
 // passes, so a kept row's stored values are exactly the ones its flag was computed from)
 struct Core {
-  float yob, city, latent, w;
+  double yob, city, latent;
+  float w;
   int hist;          // bit k = vote-history column k (g2000, g2002, p2000, p2002, p2004)
 };
 
+// fp64, no FMA contraction: the operations of data/dgp.py selection_flags / raw_columns in
+// their order (x + a * b as a product, then a sum)
 __device__ __forceinline__ Core core_draws(uint64_t seed, uint64_t g, const DgpP& P) {
+#pragma clang fp contract(off)
   Core c;
-  c.yob = dgp_normal(seed, 0, g);      // individual covariates (j < 3): the raw N(0,1) draw
-  c.city = dgp_normal(seed, 1, g);
-  c.latent = dgp_normal(seed, 41, g) + P.yob_latent * c.yob;
+  c.yob = dgp_normal_d(seed, 0, g);    // individual covariates (j < 3): the raw N(0,1) draw
+  c.city = dgp_normal_d(seed, 1, g);
+  c.latent = dgp_normal_d(seed, 41, g) + P.yob_latent_d * c.yob;
   c.hist = 0;
 #pragma unroll
   for (int k = 0; k < 5; ++k)
-    c.hist |= (dgp_normal(seed, 50 + k, g) + P.hist_latent * c.latent > P.thr[k]) ? (1 << k) : 0;
-  c.w = dgp_uniform(seed, 61, g) < P.p_treat ? 1.f : 0.f;
+    c.hist |= (dgp_normal_d(seed, 50 + k, g) + P.hist_latent_d * c.latent > P.thr_d[k])
+                  ? (1 << k) : 0;
+  c.w = dgp_uniform_d(seed, 61, g) < P.p_treat_d ? 1.f : 0.f;
   return c;
 }
 
@@ -86,10 +112,10 @@ __device__ __forceinline__ Core core_draws(uint64_t seed, uint64_t g, const DgpP
 __device__ __forceinline__ int sel_flag(const Core& c, int last) {
   const int h = c.hist;
   if (c.w == 1.f) {
-    const bool d = (h & 0xF) != 0 || ((h >> last) & 1) || c.city > 2.f || c.yob > 2.f;
+    const bool d = (h & 0xF) != 0 || ((h >> last) & 1) || c.city > 2.0 || c.yob > 2.0;
     return d ? 1 : 0;
   }
-  const bool d = (h & 0x1F) != 0x1F || c.city < -2.f || c.yob < -2.f;
+  const bool d = (h & 0x1F) != 0x1F || c.city < -2.0 || c.yob < -2.0;
   return d ? 2 : 0;
 }
 
@@ -107,6 +133,12 @@ __device__ __forceinline__ void put<bf16_t>(bf16_t* X, int64_t cs, int64_t bs, i
                                             float v) {
   X[pidx(c, i, cs, bs)] = f32_to_bf16_rne(v);
 }
+// an fp64 core draw: stored at the panel's precision (fp64 panels keep every bit)
+template <typename T>
+__device__ __forceinline__ void put_d(T* X, int64_t cs, int64_t bs, int c, int64_t i, double v) {
+  if constexpr (sizeof(T) == 8) X[pidx(c, i, cs, bs)] = (T)v;
+  else put(X, cs, bs, c, i, (float)v);
+}
 
 template <typename T>
 __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64_t row0, int64_t count,
@@ -121,8 +153,8 @@ __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64
     const float f = dgp_normal(seed, 40, g);
     int c = 0;
     put(X, cs, bs, c++, i, 1.0f);
-    put(X, cs, bs, c++, i, cr.yob);
-    put(X, cs, bs, c++, i, cr.city);
+    put_d(X, cs, bs, c++, i, cr.yob);
+    put_d(X, cs, bs, c++, i, cr.city);
     for (int j = 2; j < 15; ++j) {
       float z = dgp_normal(seed, j, g);
       put(X, cs, bs, c++, i, j < 3 ? z : FL * f + FS * z);
@@ -144,7 +176,7 @@ __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64
     }
     const float w = cr.w;
     const float hterm = P.uniform_b ? P.b_hist[0] * hsum : hb;
-    const float eta = P.intercept + hterm + P.b_latent * cr.latent + P.tau_logit * w;
+    const float eta = P.intercept + hterm + P.b_latent * (float)cr.latent + P.tau_logit * w;
     const float y = dgp_uniform(seed, 62, g) < 1.0f / (1.0f + expf(-eta)) ? 1.f : 0.f;
     put(X, cs, bs, c++, i, w);
     put(X, cs, bs, c++, i, y);
@@ -259,23 +291,23 @@ __global__ __launch_bounds__(NT) void sel_gen_mark_kernel(uint64_t seed, DgpP P,
 
 }  // namespace
 
-// params: float[18] (data/dgp.py DgpParams.device_block). dtype 1 f32, 2 f64, 3 bf16.
+// params: double[18] (data/dgp.py DgpParams.device_block). dtype 1 f32, 2 f64, 3 bf16.
 // gids: optional int64 generated-row ids of the count rows (else gid0 + r).
 ATE_API int ate_dgp_fill(int dtype, void* X, int64_t cs, int64_t bs, int64_t row0, int64_t count,
                          int64_t gid0, const void* gids, uint64_t seed, int p_extra, int hi_lo,
                          const void* params, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const DgpP P = load_params((const float*)params);
+  const DgpP P = load_params((const double*)params);
   const int64_t* gl = (const int64_t*)gids;
   dim3 grid(grid_for(count, 256, 8192)), block(256);
   if (dtype == 1)
-    hipLaunchKernelGGL(dgp_fill_kernel<float>, grid, block, 0, s, (float*)X, cs, bs, row0, count, gid0,
+    ATE_LAUNCH(dgp_fill_kernel<float>, grid, block, 0, s, (float*)X, cs, bs, row0, count, gid0,
                        gl, seed, p_extra, hi_lo, P);
   else if (dtype == 2)
-    hipLaunchKernelGGL(dgp_fill_kernel<double>, grid, block, 0, s, (double*)X, cs, bs, row0, count,
+    ATE_LAUNCH(dgp_fill_kernel<double>, grid, block, 0, s, (double*)X, cs, bs, row0, count,
                        gid0, gl, seed, p_extra, hi_lo, P);
   else if (dtype == 3)
-    hipLaunchKernelGGL(dgp_fill_kernel<bf16_t>, grid, block, 0, s, (bf16_t*)X, cs, bs, row0, count,
+    ATE_LAUNCH(dgp_fill_kernel<bf16_t>, grid, block, 0, s, (bf16_t*)X, cs, bs, row0, count,
                        gid0, gl, seed, p_extra, hi_lo, P);
   else
     return -1;
@@ -289,8 +321,8 @@ ATE_API int ate_sel_block_rows() { return SEL_BR; }
 ATE_API int ate_sel_gen_count(uint64_t seed, const void* params, int last, int64_t b0, int64_t nblk,
                               int64_t n_lim, void* cnt, void* stream) {
   if (nblk <= 0) return 0;
-  const DgpP P = load_params((const float*)params);
-  hipLaunchKernelGGL(sel_gen_count_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,
+  const DgpP P = load_params((const double*)params);
+  ATE_LAUNCH(sel_gen_count_kernel, dim3((unsigned)nblk), dim3(NT), 0, (hipStream_t)stream,
                      seed, P, last, b0, n_lim, (int64_t*)cnt);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -299,8 +331,8 @@ ATE_API int ate_sel_gen_count(uint64_t seed, const void* params, int last, int64
 ATE_API int ate_sel_gen_flags(uint64_t seed, const void* params, int last, int64_t g0, int64_t count,
                               void* flags, void* stream) {
   if (count <= 0) return 0;
-  const DgpP P = load_params((const float*)params);
-  hipLaunchKernelGGL(sel_gen_flags_kernel, dim3(grid_for(count, NT, 4096)), dim3(NT), 0,
+  const DgpP P = load_params((const double*)params);
+  ATE_LAUNCH(sel_gen_flags_kernel, dim3(grid_for(count, NT, 4096)), dim3(NT), 0,
                      (hipStream_t)stream, seed, P, last, g0, count, (uint8_t*)flags);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -311,8 +343,8 @@ ATE_API int ate_sel_gen_mark(uint64_t seed, const void* params, int last, const 
                              int64_t thr_t, int64_t thr_c, const void* sl, int ns, void* out,
                              int64_t cap, void* stream) {
   if (nl <= 0) return 0;
-  const DgpP P = load_params((const float*)params);
-  hipLaunchKernelGGL(sel_gen_mark_kernel, dim3((unsigned)nl), dim3(NT), 0, (hipStream_t)stream,
+  const DgpP P = load_params((const double*)params);
+  ATE_LAUNCH(sel_gen_mark_kernel, dim3((unsigned)nl), dim3(NT), 0, (hipStream_t)stream,
                      seed, P, last, (const int64_t*)blk, thr_t, thr_c, (const int64_t*)sl, ns,
                      (int64_t*)out, cap);
   ATE_CHECK_LAUNCH();

@@ -137,11 +137,11 @@ static int dml_resid_t(const void* X, int64_t ld, const void* xcols, int p, cons
                        int nbx, void* partial, void* moments, hipStream_t s) {
   size_t sh = (size_t)2 * (p + 1) * sizeof(double) + (size_t)p * sizeof(int);
   dim3 grid(nbx, nseg);
-  hipLaunchKernelGGL((dml_resid_kernel<T, 4>), grid, dim3(256), sh, s, (const T*)X, ld,
+  ATE_LAUNCH((dml_resid_kernel<T, 4>), grid, dim3(256), sh, s, (const T*)X, ld,
                      (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
                      w0, w1, vcol, (double*)partial);
   ATE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
+  ATE_LAUNCH(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
                      (double*)moments);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -306,11 +306,11 @@ ATE_API int ate_dml_resid_moments(int dtype, const void* X, int64_t cs, int64_t 
   if (dtype == 3) {
     size_t sh = (size_t)2 * (p + 1) * sizeof(float) + (size_t)p * sizeof(int);
     dim3 grid(nbx, nseg);
-    hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), sh, s, (const bf16_t*)X, cs, bs,
+    ATE_LAUNCH(dml_resid_bf16_kernel, grid, dim3(256), sh, s, (const bf16_t*)X, cs, bs,
                        (const int*)xcols, p, (const Seg*)segs, nseg, (const double*)coef, y0, y1,
                        w0, w1, vcol, (double*)partial, 0, (const int64_t*)nullptr);
     ATE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
+    ATE_LAUNCH(sum7_kernel, dim3(1), dim3(256), 0, s, (const double*)partial, nbx * nseg,
                        (double*)moments);
     ATE_CHECK_LAUNCH();
     return 0;
@@ -328,7 +328,7 @@ ATE_API int ate_dml_resid_exact(const void* X, int64_t cs, int64_t bs, const voi
   if (mode < 1 || mode > 2) return -1;
   size_t shm = (size_t)2 * (p + 1) * sizeof(float) + (size_t)p * sizeof(int);
   dim3 grid(nbx, nseg);
-  hipLaunchKernelGGL(dml_resid_bf16_kernel, grid, dim3(256), shm, (hipStream_t)stream,
+  ATE_LAUNCH(dml_resid_bf16_kernel, grid, dim3(256), shm, (hipStream_t)stream,
                      (const bf16_t*)X, cs, bs, (const int*)xcols, p, (const Seg*)segs, nseg,
                      (const double*)coef, y0, y1, w0, w1, vcol, (double*)partial, mode,
                      (const int64_t*)sh);

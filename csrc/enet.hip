@@ -115,7 +115,7 @@ ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, 
                              void* C, int c_f32, void* g, void* xm, void* xs, void* ju, void* ym,
                              void* ys, void* nobs, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(enet_prep_stats_kernel, dim3((p + ny + 255) / 256, ntrain), dim3(256), 0, st,
+  ATE_LAUNCH(enet_prep_stats_kernel, dim3((p + ny + 255) / 256, ntrain), dim3(256), 0, st,
                      (const double*)G, nseg, P, (const unsigned char*)masks, (const int*)xcols,
                      p, ones_col, (const int*)ycols, ny, (double*)xm, (double*)xs,
                      (unsigned char*)ju, (double*)ym, (double*)ys, (double*)nobs);
@@ -124,13 +124,13 @@ ATE_API int ate_enet_prepare(const void* G, int nseg, int P, const void* masks, 
   dim3 grid(grid_for(total, 256, 512), ntrain);
   const int ldc = (p + 63) / 64 * 64;   // padded row stride (C buffer must be zeroed)
   if (c_f32)
-    hipLaunchKernelGGL(enet_prepare_kernel<float>, grid, dim3(256), 0, st, (const double*)G, nseg,
+    ATE_LAUNCH(enet_prepare_kernel<float>, grid, dim3(256), 0, st, (const double*)G, nseg,
                        P, (const unsigned char*)masks, (const int*)xcols, p, ldc,
                        (const int*)ycols, ny, (const double*)xm, (const double*)xs,
                        (const unsigned char*)ju, (const double*)ym, (const double*)ys,
                        (const double*)nobs, (float*)C, (double*)g);
   else
-    hipLaunchKernelGGL(enet_prepare_kernel<double>, grid, dim3(256), 0, st, (const double*)G, nseg,
+    ATE_LAUNCH(enet_prepare_kernel<double>, grid, dim3(256), 0, st, (const double*)G, nseg,
                        P, (const unsigned char*)masks, (const int*)xcols, p, ldc,
                        (const int*)ycols, ny, (const double*)xm, (const double*)xs,
                        (const unsigned char*)ju, (const double*)ym, (const double*)ys,
@@ -284,7 +284,7 @@ __global__ void enet_isa_selftest_kernel(double* out) {
 }
 
 ATE_API int ate_enet_isa_selftest(void* out, void* stream) {
-  hipLaunchKernelGGL(enet_isa_selftest_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+  ATE_LAUNCH(enet_isa_selftest_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
                      (double*)out);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -1610,6 +1610,11 @@ extern "C" __attribute__((visibility("default"))) int ate_enet_prof_reset() {
 }
 #endif
 
+ATE_KERNEL_SHAPE("enet_path_kernel<float, lasso>", NTH, 0, enet_path_kernel<float, true>)
+ATE_KERNEL_SHAPE("enet_path_kernel<float, enet>", NTH, 0, enet_path_kernel<float, false>)
+ATE_KERNEL_SHAPE("enet_path_kernel<double, lasso>", NTH, 0, enet_path_kernel<double, true>)
+ATE_KERNEL_SHAPE("enet_path_kernel<double, enet>", NTH, 0, enet_path_kernel<double, false>)
+
 ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny, const void* ju,
                           const void* ys, const void* vp, const void* probs, int nprob,
                           double alpha, double flmin, double thr, int maxit, void* apath,
@@ -1625,7 +1630,7 @@ ATE_API int ate_enet_path(const void* C, int c_f32, const void* g, int p, int ny
   const char* sm = getenv("ATE_ENET_SPIN_MAX");
   const long spin_max = sm ? atol(sm) : (1l << 26);
 #define LAUNCH_C(CTT, LS)                                                                      \
-  hipLaunchKernelGGL((enet_path_kernel<CTT, LS>), dim3(nwg), dim3(NTH), 0, s, (const CTT*)C,   \
+  ATE_LAUNCH((enet_path_kernel<CTT, LS>), dim3(nwg), dim3(NTH), 0, s, (const CTT*)C,   \
                      (const double*)g, p, ny, (const unsigned char*)ju, (const double*)ys,     \
                      (const double*)vp, (const EnetProblem*)probs, nprob, alpha, flmin, thr,   \
                      maxit, (double*)apath, (double*)lams, (double*)rsqs, (int*)nlam_out,     \
@@ -1672,7 +1677,7 @@ __global__ void enet_coef_kernel(const double* __restrict__ apath, const EnetPro
 ATE_API int ate_enet_coef(const void* apath, const void* probs, int nprob, int p, int ny, int L,
                           const void* nlam_out, const void* xm, const void* xs, const void* ju,
                           const void* ym, const void* ys, void* coef, void* stream) {
-  hipLaunchKernelGGL(enet_coef_kernel, dim3(L, nprob), dim3(128), 0, (hipStream_t)stream,
+  ATE_LAUNCH(enet_coef_kernel, dim3(L, nprob), dim3(128), 0, (hipStream_t)stream,
                      (const double*)apath, (const EnetProblem*)probs, nprob, p, ny, L,
                      (const int*)nlam_out, (const double*)xm, (const double*)xs,
                      (const unsigned char*)ju, (const double*)ym, (const double*)ys,
@@ -1822,7 +1827,7 @@ ATE_API int ate_enet_cvloss_gauss(const void* G, int P, const void* hold, const 
                                   void* stream) {
   if (p > PMAX) return -1;
   if (nprob <= 0) return 0;
-  hipLaunchKernelGGL(enet_cvloss_gauss_kernel, dim3(nprob, (L + CVL - 1) / CVL), dim3(256), 0,
+  ATE_LAUNCH(enet_cvloss_gauss_kernel, dim3(nprob, (L + CVL - 1) / CVL), dim3(256), 0,
                      (hipStream_t)stream, (const double*)G, P, (const int*)hold,
                      (const int*)xcols, p, ones_col, (const int*)ycol_of_prob,
                      (const double*)coef, (const int*)nlam_out, L, q0, (double*)cvraw);
@@ -1920,7 +1925,7 @@ ATE_API int ate_cv_select(const void* cvraw, const void* fold_probs, const void*
                           int nfull, const void* nlam_full, int L, void* cvm, void* cvsd, void* sel,
                           const void* fold_npass, int nfp, void* stream) {
   if (L > 256) return -1;
-  hipLaunchKernelGGL(cv_select_kernel, dim3(nfull), dim3(64), 0, (hipStream_t)stream,
+  ATE_LAUNCH(cv_select_kernel, dim3(nfull), dim3(64), 0, (hipStream_t)stream,
                      (const double*)cvraw, (const int*)fold_probs, (const double*)nfold, K, nfull,
                      (const int*)nlam_full, L, (double*)cvm, (double*)cvsd, (int*)sel,
                      (const int*)fold_npass, nfp);
@@ -1946,7 +1951,7 @@ __global__ void enet_pick_kernel(const double* __restrict__ coef, const int* __r
 ATE_API int ate_enet_pick(const void* coef, const void* sel, int p, int L, int nfull,
                           void* out_min, void* out_1se, const void* fold_npass, int nfp,
                           void* stream) {
-  hipLaunchKernelGGL(enet_pick_kernel, dim3(nfull, 2), dim3(128), 0, (hipStream_t)stream,
+  ATE_LAUNCH(enet_pick_kernel, dim3(nfull, 2), dim3(128), 0, (hipStream_t)stream,
                      (const double*)coef, (const int*)sel, p, L, nfull, (double*)out_min,
                      (double*)out_1se, (const int*)fold_npass, nfp);
   ATE_CHECK_LAUNCH();

@@ -688,6 +688,13 @@ __global__ __launch_bounds__(64 * NW, MINW) void forest_grow_kernel(
   }
 }
 
+#ifndef FOREST_W4_MINW
+#define FOREST_W4_MINW 4   // 4 waves/SIMD: 4 trees per CU, ~48 VGPRs spilled; vs 3: config 4
+#endif                     // 0.616 -> 0.597 s, tutorial causal forest 124 -> 114 ms, same trees
+ATE_KERNEL_SHAPE("forest_grow_kernel<4>", 256, 0, forest_grow_kernel<4, FOREST_W4_MINW>)
+ATE_KERNEL_SHAPE("forest_grow_kernel<8>", 512, 0, forest_grow_kernel<8, 4>)
+ATE_KERNEL_SHAPE("forest_grow_kernel<16>", 1024, 0, forest_grow_kernel<16, 4>)
+
 ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, const void* r1,
                            const void* r2, int cap, void* feat, void* thr, void* left, void* val,
                            void* nnodes, void* inbag, void* est, void* scratch, int nw,
@@ -704,14 +711,11 @@ ATE_API int ate_forest_fit(const void* fpp, const void* Xb, const void* ycls, co
   if (w == 0) w = fp.ntree <= 256 ? 16 : fp.ntree <= 1024 ? 8 : 4;
   hipStream_t s = (hipStream_t)stream;
 #define ATE_FOREST_LAUNCH(NWV, MINW)                                                              \
-  hipLaunchKernelGGL((forest_grow_kernel<NWV, MINW>), dim3(fp.ntree), dim3(64 * NWV), 0, s, fp,   \
+  ATE_LAUNCH((forest_grow_kernel<NWV, MINW>), dim3(fp.ntree), dim3(64 * NWV), 0, s, fp,   \
                      (const uint8_t*)Xb, (const uint8_t*)ycls, (const int64_t*)r1,                 \
                      (const int64_t*)r2, cap, (int32_t*)feat, (int32_t*)thr, (int32_t*)left,      \
                      (double*)val, (int32_t*)nnodes, (uint8_t*)inbag, (int64_t*)est,              \
                      (char*)scratch)
-#ifndef FOREST_W4_MINW
-#define FOREST_W4_MINW 4   // 4 waves/SIMD: 4 trees per CU, ~48 VGPRs spilled; vs 3: config 4
-#endif                     // 0.616 -> 0.597 s, tutorial causal forest 124 -> 114 ms, same trees
   if (w == 4) ATE_FOREST_LAUNCH(4, FOREST_W4_MINW);
   else if (w == 8) ATE_FOREST_LAUNCH(8, 4);
   else if (w == 16) ATE_FOREST_LAUNCH(16, 4);
@@ -921,7 +925,7 @@ ATE_API int ate_forest_pack(const void* fpp, int cap, const void* feat, const vo
                             const void* left, const void* nnodes, const void* est, void* packed,
                             void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
-  hipLaunchKernelGGL(forest_pack_kernel, dim3(ate::grid_for((int64_t)fp.ntree * cap, 256, 4096)),
+  ATE_LAUNCH(forest_pack_kernel, dim3(ate::grid_for((int64_t)fp.ntree * cap, 256, 4096)),
                      dim3(256), 0, (hipStream_t)stream, fp, cap, (const int32_t*)feat,
                      (const int32_t*)thr, (const int32_t*)left, (const int32_t*)nnodes,
                      (const int64_t*)est, (int2*)packed);
@@ -948,19 +952,19 @@ static int forest_predict_impl(const ForestParams& fp, int n2, int cap, const vo
       const int nt = min(tchunk, fp.ntree - t0);
       leaf(dim3(rb, nt), t0);
       if (fp.kind != 2)
-        hipLaunchKernelGGL(forest_vote_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
+        ATE_LAUNCH(forest_vote_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
                            (const int32_t*)leaves, (const double*)val, (const int64_t*)est,
                            (int64_t*)state);
       else if (pass == 0)
-        hipLaunchKernelGGL(forest_cate1_kernel, dim3(rb), dim3(256), 0, st, n2, cap, t0, nt,
+        ATE_LAUNCH(forest_cate1_kernel, dim3(rb), dim3(256), 0, st, n2, cap, t0, nt,
                            (const int32_t*)leaves, (const int64_t*)est, (int64_t*)state);
       else
-        hipLaunchKernelGGL(forest_cate2_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
+        ATE_LAUNCH(forest_cate2_kernel, dim3(rb), dim3(256), 0, st, fp, n2, cap, t0, nt,
                            (const int32_t*)leaves, (const int64_t*)est, (int64_t*)state);
     }
   }
   if (phases & 4)
-    hipLaunchKernelGGL(forest_final_kernel, dim3(rb), dim3(256), 0, st, fp, n2,
+    ATE_LAUNCH(forest_final_kernel, dim3(rb), dim3(256), 0, st, fp, n2,
                        (const int64_t*)state, (double*)out);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -974,7 +978,7 @@ ATE_API int ate_forest_predict(const void* fpp, const void* Xb, int n2, int oob,
   hipStream_t st = (hipStream_t)stream;
   return forest_predict_impl(fp, n2, cap, val, est, leaves, tchunk, state, out, phases, st,
                              [&](dim3 g, int t0) {
-    hipLaunchKernelGGL(forest_leaf_kernel, g, dim3(256), 0, st, fp, (const uint8_t*)Xb, n2, oob,
+    ATE_LAUNCH(forest_leaf_kernel, g, dim3(256), 0, st, fp, (const uint8_t*)Xb, n2, oob,
                        cap, t0, (const int2*)packed, (const uint8_t*)inbag, (int32_t*)leaves);
   });
 }
@@ -990,7 +994,7 @@ ATE_API int ate_forest_predict16(const void* fpp, const void* Xb, int n2, int oo
   hipStream_t st = (hipStream_t)stream;
   return forest_predict_impl(fp, n2, cap, val, est, leaves, tchunk, state, out, phases, st,
                              [&](dim3 g, int t0) {
-    hipLaunchKernelGGL(forest_leaf16_kernel, g, dim3(256), 0, st, fp, (const uint16_t*)Xb, n2, oob,
+    ATE_LAUNCH(forest_leaf16_kernel, g, dim3(256), 0, st, fp, (const uint16_t*)Xb, n2, oob,
                        cap, t0, (const int32_t*)feat, (const int32_t*)thr, (const int32_t*)left,
                        (const uint8_t*)inbag, (const int64_t*)est, (int32_t*)leaves);
   });
@@ -1022,7 +1026,7 @@ __global__ __launch_bounds__(256) void bin_kernel(const double* __restrict__ X, 
 ATE_API int ate_bin_matrix(const void* X, int64_t n, int p, const void* edges, const void* nedges,
                            void* out, void* stream) {
   dim3 grid(ate::grid_for(n, 256, 512), p);
-  hipLaunchKernelGGL(bin_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const double*)X, n, p,
+  ATE_LAUNCH(bin_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const double*)X, n, p,
                      (const double*)edges, (const int*)nedges, (uint8_t*)out);
   ATE_CHECK_LAUNCH();
   return 0;

@@ -1101,6 +1101,9 @@ __global__ __launch_bounds__(XT, EXACT_MINWG) void forest_exact_kernel(
 
 }  // namespace
 
+ATE_KERNEL_SHAPE("forest_exact_kernel<lane>", XT, 0, forest_exact_kernel<true>)
+ATE_KERNEL_SHAPE("forest_exact_kernel<lists>", XT, 0, forest_exact_kernel<false>)
+
 ATE_API int64_t ate_forest_exact_scratch_bytes(int n, int p, int mc, int ntree) {
   return tree_bytes(n, p, mc) * (int64_t)ntree;
 }
@@ -1118,7 +1121,7 @@ ATE_API int ate_forest_fit_exact(const void* fpp, int tbeg, int nchunk, int mc, 
   if (tbeg < 0 || nchunk < 1 || tbeg + nchunk > fp.ntree) return -1;
   if (mc < 1 || mc > fp.n) return -1;
   auto kern = fp.mtry <= SMALL_MTRY ? forest_exact_kernel<true> : forest_exact_kernel<false>;
-  hipLaunchKernelGGL(kern, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
+  ATE_LAUNCH(kern, dim3(nchunk), dim3(XT), 0, (hipStream_t)stream, fp, tbeg,
                      mc, (const uint16_t*)Xb, (const uint32_t*)order, (const double*)vals, ldv, (const int32_t*)nval,
                      (const uint8_t*)ycls, (const int64_t*)r1, (const int64_t*)r2, cap,
                      (int32_t*)feat, (int32_t*)thr, (int32_t*)left, (double*)val, (int32_t*)nnodes,

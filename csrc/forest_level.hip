@@ -991,7 +991,7 @@ static LvArgs lv_args(const LvHost& h) {
 ATE_API int ate_lv_boot(const void* fpp, void* w, void* stream) {
   const ForestParams fp = *(const ForestParams*)fpp;
   const int gx = std::min(4096, (fp.n + 255) / 256);
-  hipLaunchKernelGGL(lv_boot_kernel, dim3(gx, fp.ntree), dim3(256), 0, (hipStream_t)stream, fp,
+  ATE_LAUNCH(lv_boot_kernel, dim3(gx, fp.ntree), dim3(256), 0, (hipStream_t)stream, fp,
                      (int32_t*)w);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -1001,7 +1001,7 @@ ATE_API int ate_lv_boot(const void* fpp, void* w, void* stream) {
 ATE_API int ate_lv_classify(const void* cur, int ncur_ub, const void* nsplit, int t2, int t3,
                             void* lists, void* counts, void* stream) {
   if (ncur_ub <= 0) return 0;
-  hipLaunchKernelGGL(lv_classify_kernel, dim3((ncur_ub + 255) / 256), dim3(256), 0,
+  ATE_LAUNCH(lv_classify_kernel, dim3((ncur_ub + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, (const LNode*)cur, ncur_ub, (const int32_t*)nsplit, t2,
                      t3, (int32_t*)lists, (int32_t*)counts);
   ATE_CHECK_LAUNCH();
@@ -1021,26 +1021,26 @@ ATE_API int ate_lv_decide(const void* hp, const void* small, int nsmall, const v
   const LvArgs a = lv_args(h);
   hipStream_t st = (hipStream_t)stream;
   if (nsmall)
-    hipLaunchKernelGGL(lv_small_kernel, dim3((nsmall + 3) / 4), dim3(256), 0, st, a,
+    ATE_LAUNCH(lv_small_kernel, dim3((nsmall + 3) / 4), dim3(256), 0, st, a,
                        (const int32_t*)small, nsmall);
   for (int c = 0; c < 2; ++c) {
     const int cnt = c == 0 ? nmid : nmid2;
     const int32_t* L = (const int32_t*)(c == 0 ? mid : mid2);
     if (!cnt) continue;
     if (h.fp.kind == 0)
-      hipLaunchKernelGGL((lv_mid_kernel<uint32_t, 24, 1>), dim3(cnt), dim3(256), 0, st, a, L);
+      ATE_LAUNCH((lv_mid_kernel<uint32_t, 24, 1>), dim3(cnt), dim3(256), 0, st, a, L);
     else
-      hipLaunchKernelGGL((lv_mid_kernel<int64_t, LV_FG, 4>), dim3(cnt), dim3(256), 0, st, a, L);
+      ATE_LAUNCH((lv_mid_kernel<int64_t, LV_FG, 4>), dim3(cnt), dim3(256), 0, st, a, L);
   }
   if (nbig) {
     const int32_t* B = (const int32_t*)big;
-    hipLaunchKernelGGL(lv_big_draw_kernel, dim3((nbig + 3) / 4), dim3(256), 0, st, a, B, nbig,
+    ATE_LAUNCH(lv_big_draw_kernel, dim3((nbig + 3) / 4), dim3(256), 0, st, a, B, nbig,
                        (int16_t*)drawn, (int32_t*)nfo);
-    hipLaunchKernelGGL(lv_big_hist_kernel, dim3(nitems, ngroups), dim3(256), 0, st, a,
+    ATE_LAUNCH(lv_big_hist_kernel, dim3(nitems, ngroups), dim3(256), 0, st, a,
                        (const int32_t*)item_slot, (const int32_t*)item_q0,
                        (const int32_t*)item_q1, B, (const int16_t*)drawn, (const int32_t*)nfo,
                        (int64_t*)hist, fs);
-    hipLaunchKernelGGL(lv_big_split_kernel, dim3(nbig), dim3(256), 0, st, a, B, nbig,
+    ATE_LAUNCH(lv_big_split_kernel, dim3(nbig), dim3(256), 0, st, a, B, nbig,
                        (const int16_t*)drawn, (const int32_t*)nfo, (const int64_t*)hist, fs);
   }
   ATE_CHECK_LAUNCH();
@@ -1056,13 +1056,13 @@ ATE_API int ate_lv_partition(const void* hp, const void* l1, int n1, const void*
   const LvArgs a = lv_args(h);
   hipStream_t st = (hipStream_t)stream;
   if (n1)
-    hipLaunchKernelGGL(lv_part_wave_kernel, dim3((n1 + 3) / 4), dim3(256), 0, st, a,
+    ATE_LAUNCH(lv_part_wave_kernel, dim3((n1 + 3) / 4), dim3(256), 0, st, a,
                        (const int32_t*)l1, n1);
   if (n2)
-    hipLaunchKernelGGL(lv_part_wave_kernel, dim3((n2 + 3) / 4), dim3(256), 0, st, a,
+    ATE_LAUNCH(lv_part_wave_kernel, dim3((n2 + 3) / 4), dim3(256), 0, st, a,
                        (const int32_t*)l2, n2);
   if (nitems)
-    hipLaunchKernelGGL(lv_part_count_kernel, dim3(nitems), dim3(256), 0, st, a,
+    ATE_LAUNCH(lv_part_count_kernel, dim3(nitems), dim3(256), 0, st, a,
                        (const int32_t*)item_slot, (const int32_t*)item_q0,
                        (const int32_t*)item_q1, (const int32_t*)plist, (int32_t*)icnt);
   ATE_CHECK_LAUNCH();
@@ -1076,7 +1076,7 @@ ATE_API int ate_lv_scatter(const void* hp, const void* plist, const void* item_s
   const LvHost& h = *(const LvHost*)hp;
   const LvArgs a = lv_args(h);
   if (nitems)
-    hipLaunchKernelGGL(lv_part_scatter_kernel, dim3(nitems), dim3(256), 0, (hipStream_t)stream, a,
+    ATE_LAUNCH(lv_part_scatter_kernel, dim3(nitems), dim3(256), 0, (hipStream_t)stream, a,
                        (const int32_t*)item_slot, (const int32_t*)item_q0,
                        (const int32_t*)item_q1, (const int32_t*)plist, (const int32_t*)ipre,
                        (const int32_t*)nlb);
@@ -1091,11 +1091,11 @@ ATE_API int ate_lv_children(const void* hp, int ncur, const void* excl, void* br
   const LvArgs a = lv_args(h);
   hipStream_t st = (hipStream_t)stream;
   const int g = (ncur + 255) / 256;
-  hipLaunchKernelGGL(lv_tree_base_kernel, dim3(g), dim3(256), 0, st, a.cur, ncur,
+  ATE_LAUNCH(lv_tree_base_kernel, dim3(g), dim3(256), 0, st, a.cur, ncur,
                      (const int32_t*)excl, (int32_t*)brank);
-  hipLaunchKernelGGL(lv_children_kernel, dim3(g), dim3(256), 0, st, a, ncur, (const int32_t*)excl,
+  ATE_LAUNCH(lv_children_kernel, dim3(g), dim3(256), 0, st, a, ncur, (const int32_t*)excl,
                      (const int32_t*)brank, (int32_t*)next_id, (LNode*)nxt);
-  hipLaunchKernelGGL(lv_next_id_kernel, dim3(g), dim3(256), 0, st, a.cur, ncur,
+  ATE_LAUNCH(lv_next_id_kernel, dim3(g), dim3(256), 0, st, a.cur, ncur,
                      (const int32_t*)excl, a.dec, (const int32_t*)brank, (int32_t*)next_id);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -1104,7 +1104,7 @@ ATE_API int ate_lv_children(const void* hp, int ncur, const void* excl, void* br
 ATE_API int ate_lv_transpose(const void* src, int p, int n, void* dst, int ldr, void* stream) {
   if (ldr % 16 || ldr < p) return -1;
   dim3 grid((n + 255) / 256, (p + 63) / 64);
-  hipLaunchKernelGGL(lv_transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+  ATE_LAUNCH(lv_transpose_kernel, grid, dim3(256), 0, (hipStream_t)stream,
                      (const uint8_t*)src, p, n, (uint8_t*)dst, ldr);
   ATE_CHECK_LAUNCH();
   return 0;

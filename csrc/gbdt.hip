@@ -765,7 +765,7 @@ static void gbdt_launch_apply(const uint8_t* Xr, int64_t ldr, int64_t n, int ntr
                               const int32_t* feat, const int32_t* thr, const double* value,
                               double* f, hipStream_t st) {
   const int RW = gbdt_apply_rows(ldr);
-  hipLaunchKernelGGL(gbdt_apply_kernel, dim3((unsigned)((n + RW - 1) / RW)), dim3(NT),
+  ATE_LAUNCH(gbdt_apply_kernel, dim3((unsigned)((n + RW - 1) / RW)), dim3(NT),
                      (size_t)RW * ldr, st, Xr, ldr, n, RW, ntree, M, feat, thr, value, f);
 }
 
@@ -840,6 +840,9 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
   *nwg = wg;
 }
 
+ATE_KERNEL_SHAPE("gbdt_hist_kernel<compact>", NTH, 0, gbdt_hist_kernel<true>)
+ATE_KERNEL_SHAPE("gbdt_hist_kernel<full>", NTH, 0, gbdt_hist_kernel<false>)
+
 // compile-time limits the host side sizes its buffers with (models/gbdt.py checks them)
 ATE_API int ate_gbdt_limits(void* out) {
   int* o = static_cast<int*>(out);
@@ -894,7 +897,7 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
     double* vt = a.value + (int64_t)s.t * M;
     if (s.d == 0 && !s.resume) {
       s.cur = 0;                                          // ping-pong index of idx/gh/seg
-      hipLaunchKernelGGL(gbdt_grad_kernel, dim3((unsigned)((a.n_train + 4 * NT - 1) / (4 * NT))),
+      ATE_LAUNCH(gbdt_grad_kernel, dim3((unsigned)((a.n_train + 4 * NT - 1) / (4 * NT))),
                          dim3(NT), 0, st, a.loss, a.f, a.y, a.idx[0], a.n_train, a.gh[0],
                          a.seg[0]);
     }
@@ -908,12 +911,12 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
         if (s.resume == 0) {
           int64_t CH, nwg;
           gbdt_hist_geom(a.n_train, a.p, d, a.rule, &CH, &nwg);
-          hipLaunchKernelGGL(hmode ? gbdt_hist_kernel<true> : gbdt_hist_kernel<false>,
+          ATE_LAUNCH(hmode ? gbdt_hist_kernel<true> : gbdt_hist_kernel<false>,
                              dim3((unsigned)nwg), dim3(NTH), 0, st, a.Xr,
                              a.ldr, a.idx[cur], a.gh[cur], a.seg[cur], a.tot, a.rule, nn, a.p, d,
                              CH, ydim, a.slab, hmode, a.loss);
           const int64_t perP = 512LL * nr * hp;
-          hipLaunchKernelGGL(gbdt_hist_reduce_kernel,
+          ATE_LAUNCH(gbdt_hist_reduce_kernel,
                              dim3((unsigned)std::min<int64_t>((perP + NT - 1) / NT, 256), nn),
                              dim3(NT), 0, st, a.slab, a.seg[cur], a.tot, a.rule, nn, a.p, d, CH,
                              ydim, a.Hs, nr, hp);
@@ -925,11 +928,11 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
           }
         }
         if (s.resume <= 1) {
-          if (d == 0) hipLaunchKernelGGL(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, Hsrc, hp, a.tot);
-          hipLaunchKernelGGL(gbdt_expand_kernel,
+          if (d == 0) ATE_LAUNCH(gbdt_root_kernel, dim3(1), dim3(NT), 0, st, Hsrc, hp, a.tot);
+          ATE_LAUNCH(gbdt_expand_kernel,
                              dim3((unsigned)std::min<int64_t>((per + NT - 1) / NT, 128), nsl),
                              dim3(NT), 0, st, Hsrc, Hp, Hc, a.seg[cur], a.tot, ft, a.rule, hp, d);
-          hipLaunchKernelGGL(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc,
+          ATE_LAUNCH(gbdt_split_search_kernel, dim3(nn, ydim_s), dim3(NTS), 0, st, Hc,
                              hp, hc, joff, d, a.depth, a.lam, a.min_child, a.tot, ft, a.cand);
           if (sliced) {
             ATE_CHECK_LAUNCH();
@@ -940,18 +943,18 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
         }
         s.resume = 0;
       }
-      hipLaunchKernelGGL(gbdt_split_final_kernel, dim3(nn), dim3(64), 0, st,
+      ATE_LAUNCH(gbdt_split_final_kernel, dim3(nn), dim3(64), 0, st,
                          sliced ? a.candg : a.cand, ydim_s, nr, (int64_t)nn * ydim_s, d,
                          a.depth, a.min_gain, a.lam, a.lr, a.tot, ft, th, vt);
       if (d + 1 < a.depth) {
         const int nb = 2 * nn + 1;
         const int W = (int)((a.n_train + a.R - 1) / a.R);
-        hipLaunchKernelGGL(gbdt_part_count_kernel, dim3(W), dim3(NT), 0, st, a.Xr, a.ldr,
+        ATE_LAUNCH(gbdt_part_count_kernel, dim3(W), dim3(NT), 0, st, a.Xr, a.ldr,
                            a.idx[cur], a.n_train, a.seg[cur], nn, d, ft, th, a.R, W, a.bkt,
                            a.cnt);
-        hipLaunchKernelGGL(gbdt_part_scan_kernel, dim3(nb), dim3(NT), 0, st, a.cnt, W, a.base,
+        ATE_LAUNCH(gbdt_part_scan_kernel, dim3(nb), dim3(NT), 0, st, a.cnt, W, a.base,
                            a.btot);
-        hipLaunchKernelGGL(gbdt_part_scatter_kernel, dim3(W), dim3(NT), 0, st, a.idx[cur],
+        ATE_LAUNCH(gbdt_part_scatter_kernel, dim3(W), dim3(NT), 0, st, a.idx[cur],
                            a.gh[cur], a.bkt, a.n_train, nb, a.R, W, a.base, a.btot,
                            a.idx[cur ^ 1], a.gh[cur ^ 1], a.seg[cur ^ 1]);
         s.cur ^= 1;
@@ -964,7 +967,7 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
       return -3;
     {
       const int64_t g = std::min<int64_t>((a.n + NT * WALK_U - 1) / (NT * WALK_U), 256 * 16);
-      hipLaunchKernelGGL(gbdt_walk_kernel, dim3((unsigned)g), dim3(NT), 0, st, a.Xr, a.ldr, a.n,
+      ATE_LAUNCH(gbdt_walk_kernel, dim3((unsigned)g), dim3(NT), 0, st, a.Xr, a.ldr, a.n,
                          a.depth, M, ft, th, vt, a.f);
     }
   }
@@ -1051,12 +1054,12 @@ ATE_API int ate_gbdt_bin_panel(const void* X, int dtype, int64_t ld, const void*
   dim3 grid(ate::grid_for(nreal, 256, 4096), (p + 15) / 16);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 0)
-    hipLaunchKernelGGL(gbdt_bin_panel_kernel<uint16_t>, grid, dim3(256), 0, st,
+    ATE_LAUNCH(gbdt_bin_panel_kernel<uint16_t>, grid, dim3(256), 0, st,
                        (const uint16_t*)X, ld, (const int*)xcols, p, (const int64_t*)seg_r0,
                        (const int64_t*)seg_n, (const int64_t*)seg_c0, nseg, nreal,
                        (const double*)edges, (const int*)nedges, (uint8_t*)out, ldr);
   else if (dtype == 1)
-    hipLaunchKernelGGL(gbdt_bin_panel_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ld,
+    ATE_LAUNCH(gbdt_bin_panel_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ld,
                        (const int*)xcols, p, (const int64_t*)seg_r0, (const int64_t*)seg_n,
                        (const int64_t*)seg_c0, nseg, nreal, (const double*)edges,
                        (const int*)nedges, (uint8_t*)out, ldr);

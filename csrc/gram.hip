@@ -856,6 +856,11 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
   }
 }
 
+ATE_KERNEL_SHAPE("gram_bf16_pair_kernel", 512, 0, gram_bf16_pair_kernel)
+ATE_KERNEL_SHAPE("gram_bf16_tri_kernel", 512, 0, gram_bf16_tri_kernel)
+ATE_KERNEL_SHAPE("gram_bf16_256_kernel", 512, 0, gram_bf16_256_kernel)
+ATE_KERNEL_SHAPE("gram_bf16_kernel", 256, 0, gram_bf16_kernel)
+
 // what: 1 = tile kernel (slab partials), 2 = fixed-order slab reduce into G, 3 = both.
 // Split so a caller can run the reduce on another stream than the next tile kernel.
 ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, const void* tiles, int ntiles,
@@ -865,14 +870,14 @@ ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, con
   if (P % (2 * GT) || what < 1 || what > 3) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (what & 1) {
-  hipLaunchKernelGGL(gram_bf16_pair_kernel, dim3(nchunks * ntiles), dim3(512), 0, s,
+  ATE_LAUNCH(gram_bf16_pair_kernel, dim3(nchunks * ntiles), dim3(512), 0, s,
                      (const bf16_t*)X, cs, bs, (const int4*)tiles, ntiles, (const Chunk*)chunks,
                      nchunks, (float*)slab);
   ATE_CHECK_LAUNCH();
   }
   if (what & 2) {
     const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
-    hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+    ATE_LAUNCH(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                        (const float*)slab, (const int2*)blocks, ntiles, PAIR_SLOTS,
                        (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx);
     ATE_CHECK_LAUNCH();
@@ -887,13 +892,13 @@ ATE_API int ate_gram_bf16_tri(const void* X, int64_t cs, int64_t bs, int P, cons
   if (P != 512 || what < 1 || what > 3) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (what & 1) {
-    hipLaunchKernelGGL(gram_bf16_tri_kernel, dim3(nchunks * 2), dim3(512), 0, s,
+    ATE_LAUNCH(gram_bf16_tri_kernel, dim3(nchunks * 2), dim3(512), 0, s,
                        (const bf16_t*)X, cs, bs, (const Chunk*)chunks, nchunks, (float*)slab);
     ATE_CHECK_LAUNCH();
   }
   if (what & 2) {
     const int64_t total = (int64_t)nseg * 2 * TRI_SLOTS * 256;
-    hipLaunchKernelGGL(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+    ATE_LAUNCH(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                        (const float*)slab, (const int2*)blocks, 2, TRI_SLOTS,
                        (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx);
     ATE_CHECK_LAUNCH();
@@ -1039,18 +1044,18 @@ ATE_API int ate_gram_bf16(const void* X, int64_t ld, int P, int tile,
   int nwg = nchunks * ntiles;
   if (tile == GT) {
     if (P % GT) return -1;
-    hipLaunchKernelGGL(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
+    ATE_LAUNCH(gram_bf16_256_kernel, dim3(nwg), dim3(512), 0, s, (const bf16_t*)X, ld,
                        (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
   } else if (tile == BT) {
     if (P % BT) return -1;
-    hipLaunchKernelGGL(gram_bf16_kernel, dim3(nwg), dim3(256), 0, s, (const bf16_t*)X, ld,
+    ATE_LAUNCH(gram_bf16_kernel, dim3(nwg), dim3(256), 0, s, (const bf16_t*)X, ld,
                        (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks, (float*)slab);
   } else {
     return -1;
   }
   ATE_CHECK_LAUNCH();
   int64_t total = (int64_t)nseg * ntiles * tile * tile;
-  hipLaunchKernelGGL(gram_reduce_kernel<float>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+  ATE_LAUNCH(gram_reduce_kernel<float>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                      (const float*)slab, tile, (const int2*)tiles, ntiles, (const int*)seg_chunk0,
                      nseg, P, (double*)G, (const int*)nullptr, (long long*)Gx);
   ATE_CHECK_LAUNCH();
@@ -1064,12 +1069,12 @@ static int gram_small(const void* X, int64_t ld, int P, const void* w, const voi
   if (P % FT) return -1;
   hipStream_t s = (hipStream_t)stream;
   int nwg = nchunks * ntiles;
-  hipLaunchKernelGGL(gram_small_kernel<T>, dim3(nwg), dim3(256), 0, s, (const T*)X, ld,
+  ATE_LAUNCH(gram_small_kernel<T>, dim3(nwg), dim3(256), 0, s, (const T*)X, ld,
                      (const T*)w, (const int2*)tiles, ntiles, (const Chunk*)chunks, nchunks,
                      (T*)slab, (const int*)done);
   ATE_CHECK_LAUNCH();
   int64_t total = (int64_t)nseg * ntiles * FT * FT;
-  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
+  ATE_LAUNCH(gram_reduce_kernel<T>, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                      (const T*)slab, FT, (const int2*)tiles, ntiles, (const int*)seg_chunk0,
                      nseg, P, (double*)G, (const int*)done, (long long*)Gx);
   ATE_CHECK_LAUNCH();

@@ -131,7 +131,7 @@ ATE_API int ate_chol_solve(const void* G, int P, const void* cols, int k, int rc
   double* L = (double*)work;
   double* Linv = L + (int64_t)k * k;
   size_t sh = (size_t)3 * k * sizeof(double);
-  hipLaunchKernelGGL(chol_solve_kernel, dim3(1), dim3(1024), sh, (hipStream_t)stream,
+  ATE_LAUNCH(chol_solve_kernel, dim3(1), dim3(1024), sh, (hipStream_t)stream,
                      (const double*)G, P, (const int*)cols, k, rcol, (const double*)rhs_vec, tol,
                      L, Linv, (double*)beta, (double*)invdiag, (double*)aux, (const int*)done,
                      (const int*)nullptr);
@@ -147,7 +147,7 @@ ATE_API int ate_chol_solve_k(const void* G, int P, const void* cols, int k, cons
   double* L = (double*)work;
   double* Linv = L + (int64_t)k * k;
   size_t sh = (size_t)3 * k * sizeof(double);
-  hipLaunchKernelGGL(chol_solve_kernel, dim3(1), dim3(1024), sh, (hipStream_t)stream,
+  ATE_LAUNCH(chol_solve_kernel, dim3(1), dim3(1024), sh, (hipStream_t)stream,
                      (const double*)G, P, (const int*)cols, k, rcol, (const double*)nullptr, tol,
                      L, Linv, (double*)beta, (double*)invdiag, (double*)aux, (const int*)nullptr,
                      (const int*)kdev);
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(1024) void spd_solve_kernel(const double* __restric
 ATE_API int ate_spd_solve_batched(const void* K, const void* r, int A, int k, void* work, void* x,
                                   void* stream) {
   if (A <= 0 || k <= 0 || k > 4096) return -1;
-  hipLaunchKernelGGL(spd_solve_kernel, dim3(A), dim3(256), (size_t)k * sizeof(double),
+  ATE_LAUNCH(spd_solve_kernel, dim3(A), dim3(256), (size_t)k * sizeof(double),
                      (hipStream_t)stream, (const double*)K, (const double*)r, k, (double*)work,
                      (double*)x);
   ATE_CHECK_LAUNCH();
@@ -261,7 +261,7 @@ __global__ void predict_kernel(const T* __restrict__ X, int64_t ld, int64_t n, c
 template <typename T>
 static int predict_t(const void* X, int64_t ld, int64_t n, const void* cols, const void* beta, int k,
                      int ov_idx, double ov_val, int link, void* out, void* stream) {
-  hipLaunchKernelGGL(predict_kernel<T>, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+  ATE_LAUNCH(predict_kernel<T>, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
                      (const T*)X, ld, n, (const int*)cols, (const double*)beta, k, ov_idx, ov_val,
                      link, (double*)out);
   ATE_CHECK_LAUNCH();
@@ -352,7 +352,7 @@ template <typename T>
 static int irls_update_t(void* X, int64_t ld, int64_t n, const void* cols, const void* beta, int k,
                          int ycol, int vcol, int zcol, int first, void* eta, void* mu, void* w,
                          void* dev_partial, int nb, const void* done, void* stream) {
-  hipLaunchKernelGGL(irls_update_kernel<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (T*)X, ld,
+  ATE_LAUNCH(irls_update_kernel<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (T*)X, ld,
                      n, (const int*)cols, (const double*)beta, k, ycol, vcol, zcol, first,
                      (double*)eta, (double*)mu, (T*)w, (double*)dev_partial, (const int*)done);
   ATE_CHECK_LAUNCH();
@@ -374,7 +374,7 @@ ATE_API int ate_irls_update(int dtype, void* X, int64_t ld, int64_t n, const voi
 
 ATE_API int ate_irls_check(const void* dev_partial, int nb, int first, double eps, int maxit,
                            void* state, void* done, void* stream) {
-  hipLaunchKernelGGL(irls_check_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
+  ATE_LAUNCH(irls_check_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
                      (const double*)dev_partial, nb, first, eps, maxit, (double*)state, (int*)done);
   ATE_CHECK_LAUNCH();
   return 0;

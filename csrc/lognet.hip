@@ -550,21 +550,26 @@ int launch_path(const void* X, int64_t ld, const int* xcols, int p, int ycol, co
                 int L, double* a0, double* beta, double* lam, double* dev, int* nlam_out,
                 int* npass, int* progress, double* lampub, hipStream_t st) {
   if (p <= 24)
-    hipLaunchKernelGGL((lognet_path_kernel<T, 24, 512>), dim3(nprob), dim3(512), 0, st, (const T*)X,
+    ATE_LAUNCH((lognet_path_kernel<T, 24, 512>), dim3(nprob), dim3(512), 0, st, (const T*)X,
                        ld, xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
                        nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   else if (p <= 32)
-    hipLaunchKernelGGL((lognet_path_kernel<T, 32, NT>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
+    ATE_LAUNCH((lognet_path_kernel<T, 32, NT>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
                        xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
                        nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   else
-    hipLaunchKernelGGL((lognet_path_kernel<T, 96, NT>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
+    ATE_LAUNCH((lognet_path_kernel<T, 96, NT>), dim3(nprob), dim3(NT), 0, st, (const T*)X, ld,
                        xcols, p, ycol, segs, nseg, masks, vp, alpha, flmin, thresh, maxit, ulam,
                        nlam_in, L, a0, beta, lam, dev, nlam_out, npass, progress, lampub);
   return 0;
 }
 
 }  // namespace
+
+ATE_KERNEL_SHAPE("lognet_path_kernel<double, 24>", 512, 0, lognet_path_kernel<double, 24, 512>)
+ATE_KERNEL_SHAPE("lognet_path_kernel<float, 24>", 512, 0, lognet_path_kernel<float, 24, 512>)
+ATE_KERNEL_SHAPE("lognet_path_kernel<double, 32>", NT, 0, lognet_path_kernel<double, 32, NT>)
+ATE_KERNEL_SHAPE("lognet_path_kernel<double, 96>", NT, 0, lognet_path_kernel<double, 96, NT>)
 
 // dt: 1 = fp32 panel, 2 = fp64 panel. segs: int64 [nseg][2] real-row ranges.
 ATE_API int ate_lognet_path(int dt, const void* X, int64_t ld, const void* xcols, int p, int ycol,
@@ -594,12 +599,12 @@ ATE_API int ate_lognet_cvloss(int dt, const void* X, int64_t ld, const void* xco
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(nprob, L);
   if (dt == 2)
-    hipLaunchKernelGGL(lognet_cvloss_kernel<double>, grid, dim3(NT), 0, st, (const double*)X, ld,
+    ATE_LAUNCH(lognet_cvloss_kernel<double>, grid, dim3(NT), 0, st, (const double*)X, ld,
                        (const int*)xcols, p, ycol, (const int64_t*)segs, (const int*)hold,
                        (const double*)a0, (const double*)beta, (const int*)nlam, L,
                        (double*)cvraw);
   else
-    hipLaunchKernelGGL(lognet_cvloss_kernel<float>, grid, dim3(NT), 0, st, (const float*)X, ld,
+    ATE_LAUNCH(lognet_cvloss_kernel<float>, grid, dim3(NT), 0, st, (const float*)X, ld,
                        (const int*)xcols, p, ycol, (const int64_t*)segs, (const int*)hold,
                        (const double*)a0, (const double*)beta, (const int*)nlam, L,
                        (double*)cvraw);

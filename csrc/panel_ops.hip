@@ -61,10 +61,10 @@ template <typename T>
 int xtv_launch(const void* X, int64_t ld, const int* xcols, int p, const double* v,
                const int8_t* grp, int64_t n, int A, double* out, hipStream_t st) {
   if (A == 1)
-    hipLaunchKernelGGL((xtv_kernel<T, 1>), dim3(p), dim3(NT), 0, st, (const T*)X, ld, xcols, v,
+    ATE_LAUNCH((xtv_kernel<T, 1>), dim3(p), dim3(NT), 0, st, (const T*)X, ld, xcols, v,
                        grp, n, out, p);
   else if (A == 2)
-    hipLaunchKernelGGL((xtv_kernel<T, 2>), dim3(p), dim3(NT), 0, st, (const T*)X, ld, xcols, v,
+    ATE_LAUNCH((xtv_kernel<T, 2>), dim3(p), dim3(NT), 0, st, (const T*)X, ld, xcols, v,
                        grp, n, out, p);
   else
     return -1;
@@ -95,11 +95,11 @@ ATE_API int ate_panel_xv(int dt, const void* X, int64_t ld, const void* xcols, i
   if (sh > 64 * 1024) return -1;
   dim3 grid(ate::grid_for(n, NT, 2048));
   if (dt == 2)
-    hipLaunchKernelGGL(xv_kernel<double>, grid, dim3(NT), sh, st, (const double*)X, ld,
+    ATE_LAUNCH(xv_kernel<double>, grid, dim3(NT), sh, st, (const double*)X, ld,
                        (const int*)xcols, p, (const double*)V, A, (const int8_t*)grp, n,
                        (double*)out);
   else
-    hipLaunchKernelGGL(xv_kernel<float>, grid, dim3(NT), sh, st, (const float*)X, ld,
+    ATE_LAUNCH(xv_kernel<float>, grid, dim3(NT), sh, st, (const float*)X, ld,
                        (const int*)xcols, p, (const double*)V, A, (const int8_t*)grp, n,
                        (double*)out);
   ATE_CHECK_LAUNCH();

@@ -108,12 +108,12 @@ ATE_API int ate_col_moments(const void* X, int64_t ld, int64_t n, int p, void* p
   hipStream_t st = (hipStream_t)stream;
   const dim3 g(CHUNKS, p), fb((p + 63) / 64);
   for (int mode = 0; mode < 2; ++mode) {
-    hipLaunchKernelGGL(colmom_partial_kernel, g, dim3(NT), 0, st, (const double*)X, ld, n, mode,
+    ATE_LAUNCH(colmom_partial_kernel, g, dim3(NT), 0, st, (const double*)X, ld, n, mode,
                        (const double*)mean, (double*)part);
-    hipLaunchKernelGGL(colmom_final_kernel, fb, dim3(64), 0, st, (const double*)part, p, mode,
+    ATE_LAUNCH(colmom_final_kernel, fb, dim3(64), 0, st, (const double*)part, p, mode,
                        (double*)mom);
     if (mode == 0)
-      hipLaunchKernelGGL(colmom_mean_kernel, fb, dim3(64), 0, st, (const double*)mom, p,
+      ATE_LAUNCH(colmom_mean_kernel, fb, dim3(64), 0, st, (const double*)mom, p,
                          (double*)mean);
   }
   ATE_CHECK_LAUNCH();
@@ -123,7 +123,7 @@ ATE_API int ate_col_moments(const void* X, int64_t ld, int64_t n, int p, void* p
 ATE_API int ate_standardize(void* X, int64_t ld, int64_t n, int p, const void* mom,
                             const void* sel, void* stream) {
   if (p < 1 || ld < n) return -1;
-  hipLaunchKernelGGL(standardize_kernel, dim3(grid_for(n, NT, 256), p), dim3(NT), 0,
+  ATE_LAUNCH(standardize_kernel, dim3(grid_for(n, NT, 256), p), dim3(NT), 0,
                      (hipStream_t)stream, (double*)X, ld, n, (const double*)mom,
                      (const uint8_t*)sel);
   ATE_CHECK_LAUNCH();
@@ -133,7 +133,7 @@ ATE_API int ate_standardize(void* X, int64_t ld, int64_t n, int p, const void* m
 ATE_API int ate_interactions(const void* X, int64_t ldx, int64_t n, int p, void* out, int64_t ldo,
                              void* stream) {
   if (p < 1 || (int64_t)p * (p + 1) > 65535 || ldx < n || ldo < n) return -1;
-  hipLaunchKernelGGL(interactions_kernel, dim3(grid_for(n, NT, 64), p * (p + 1)), dim3(NT), 0,
+  ATE_LAUNCH(interactions_kernel, dim3(grid_for(n, NT, 64), p * (p + 1)), dim3(NT), 0,
                      (hipStream_t)stream, (const double*)X, ldx, n, p, (double*)out, ldo);
   ATE_CHECK_LAUNCH();
   return 0;

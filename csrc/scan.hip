@@ -116,9 +116,9 @@ template <typename T>
 int launch_scan(const T* in, int64_t n, T* out, T* part, T* tot, hipStream_t st) {
   if (n <= 0) return 0;
   const int64_t nt = (n + STILE - 1) / STILE;
-  hipLaunchKernelGGL(scan_tile_sum_kernel<T>, dim3((unsigned)nt), dim3(SNT), 0, st, in, n, part);
-  hipLaunchKernelGGL(scan_parts_kernel<T>, dim3(1), dim3(SNT), 0, st, part, nt, tot);
-  hipLaunchKernelGGL(scan_apply_kernel<T>, dim3((unsigned)nt), dim3(SNT), 0, st, in, n,
+  ATE_LAUNCH(scan_tile_sum_kernel<T>, dim3((unsigned)nt), dim3(SNT), 0, st, in, n, part);
+  ATE_LAUNCH(scan_parts_kernel<T>, dim3(1), dim3(SNT), 0, st, part, nt, tot);
+  ATE_LAUNCH(scan_apply_kernel<T>, dim3((unsigned)nt), dim3(SNT), 0, st, in, n,
                      (const T*)part, out);
   ATE_CHECK_LAUNCH();
   return 0;

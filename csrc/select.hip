@@ -142,13 +142,13 @@ ATE_API int ate_select_compact(const void* X, int64_t n, const void* W, const vo
   int* cnt = (int*)scratch;
   int* kcnt = cnt + 2 * nblk;
   int* tail = kcnt + nblk;        // thr[2], total
-  hipLaunchKernelGGL(sel_count_kernel, dim3(nblk), dim3(NT), 0, st, (const double*)X, n,
+  ATE_LAUNCH(sel_count_kernel, dim3(nblk), dim3(NT), 0, st, (const double*)X, n,
                      (const double*)W, c, (uint8_t*)flags, cnt);
-  hipLaunchKernelGGL(sel_offsets_kernel, dim3(1), dim3(NT), 0, st, cnt, nblk, pt, pc, tail);
-  hipLaunchKernelGGL(sel_drop_kernel, dim3(nblk), dim3(NT), 0, st, (const uint8_t*)flags, n, cnt,
+  ATE_LAUNCH(sel_offsets_kernel, dim3(1), dim3(NT), 0, st, cnt, nblk, pt, pc, tail);
+  ATE_LAUNCH(sel_drop_kernel, dim3(nblk), dim3(NT), 0, st, (const uint8_t*)flags, n, cnt,
                      tail, (uint8_t*)keep, kcnt);
-  hipLaunchKernelGGL(sel_koff_kernel, dim3(1), dim3(NT), 0, st, kcnt, nblk, tail + 2);
-  hipLaunchKernelGGL(sel_compact_kernel, dim3(nblk), dim3(NT), 0, st, (const uint8_t*)keep, n,
+  ATE_LAUNCH(sel_koff_kernel, dim3(1), dim3(NT), 0, st, kcnt, nblk, tail + 2);
+  ATE_LAUNCH(sel_compact_kernel, dim3(nblk), dim3(NT), 0, st, (const uint8_t*)keep, n,
                      kcnt, (int64_t*)out);
   ATE_CHECK_LAUNCH();
   return 0;

@@ -40,9 +40,9 @@ __global__ void slab_sum_kernel(const double* __restrict__ partial, int nb, doub
 template <int NV, class F>
 static int rowreduce(F f, int64_t n, double* partial, double* out, hipStream_t s) {
   int nb = grid_for(n, RB, RGRID);
-  hipLaunchKernelGGL((rowreduce_kernel<NV, F>), dim3(nb), dim3(RB), 0, s, f, n, partial);
+  ATE_LAUNCH((rowreduce_kernel<NV, F>), dim3(nb), dim3(RB), 0, s, f, n, partial);
   ATE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(slab_sum_kernel<NV>, dim3(1), dim3(64), 0, s, partial, nb, out);
+  ATE_LAUNCH(slab_sum_kernel<NV>, dim3(1), dim3(64), 0, s, partial, nb, out);
   ATE_CHECK_LAUNCH();
   return 0;
 }
@@ -77,7 +77,7 @@ static int naive_t(const void* y, const void* w, const void* valid, int64_t n, v
   GroupMoments<T> f{(const T*)y, (const T*)w, (const T*)valid};
   int rc = rowreduce<6>(f, n, (double*)partial, (double*)moments, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(naive_finalize_kernel, dim3(1), dim3(1), 0, s, (const double*)moments,
+  ATE_LAUNCH(naive_finalize_kernel, dim3(1), dim3(1), 0, s, (const double*)moments,
                      (double*)res);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -135,10 +135,10 @@ __global__ void clip_apply_kernel(double* __restrict__ p, int64_t n, const doubl
 ATE_API int ate_clip_propensity(void* p, const void* valid, int64_t n, void* partial, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int nb = grid_for(n, RB, RGRID);
-  hipLaunchKernelGGL(clip_minmax_kernel, dim3(nb), dim3(RB), 0, s, (const double*)p,
+  ATE_LAUNCH(clip_minmax_kernel, dim3(nb), dim3(RB), 0, s, (const double*)p,
                      (const double*)valid, n, (double*)partial);
   ATE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(clip_apply_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, (double*)p, n,
+  ATE_LAUNCH(clip_apply_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, (double*)p, n,
                      (const double*)partial, nb);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -179,7 +179,7 @@ ATE_API int ate_aipw(const void* w, const void* y, const void* p, const void* mu
                 (const double*)mu1, (const double*)valid, sign};
   int rc = rowreduce<6>(f, n, (double*)partial, (double*)moments, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(aipw_finalize_kernel, dim3(1), dim3(1), 0, s, (const double*)moments,
+  ATE_LAUNCH(aipw_finalize_kernel, dim3(1), dim3(1), 0, s, (const double*)moments,
                      (double*)res);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -224,7 +224,7 @@ ATE_API int ate_dml_moments(const void* yr, const void* wr, const void* valid, i
 }
 
 ATE_API int ate_dml_finalize(const void* moments, int mode, void* res, void* stream) {
-  hipLaunchKernelGGL(dml_finalize_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
+  ATE_LAUNCH(dml_finalize_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
                      (const double*)moments, mode, (double*)res);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void boot_poisson_kernel(
 ATE_API int ate_boot_multinomial(const void* e1, const void* e2, int64_t n, uint64_t seed, int b0,
                                  int B, void* taus, void* stream) {
   if (n > 0xFFFFFFFFll) return -1;
-  hipLaunchKernelGGL(boot_multinomial_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream,
+  ATE_LAUNCH(boot_multinomial_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream,
                      (const double*)e1, (const double*)e2, n, seed, b0, (double*)taus);
   ATE_CHECK_LAUNCH();
   return 0;
@@ -310,7 +310,7 @@ ATE_API int ate_boot_multinomial(const void* e1, const void* e2, int64_t n, uint
 ATE_API int ate_boot_poisson(const void* e1, const void* e2, int64_t n, uint64_t seed, int b0,
                              int B, int64_t row_offset, int nb, void* partial, void* stream) {
   dim3 grid(nb, (B + 63) / 64);
-  hipLaunchKernelGGL(boot_poisson_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+  ATE_LAUNCH(boot_poisson_kernel, grid, dim3(256), 0, (hipStream_t)stream,
                      (const double*)e1, (const double*)e2, n, seed, b0, B, row_offset,
                      (double*)partial);
   ATE_CHECK_LAUNCH();

@@ -102,6 +102,26 @@ def test_gram_tri_kernel_vs_pair(gpu, monkeypatch, blocked):
     assert torch.equal(Gt, Gt.transpose(1, 2))
 
 
+def test_invalid_launch_is_named(gpu):
+    """A launch the runtime refuses (2,048 work-items per block) surfaces as NativeError
+    with the HIP error's name, the entry point and the launch site (csrc/errors.hip), and
+    leaves no error pending for the next op. Under ATE_DEBUG=1 the load-time resource check
+    of the registered heavy kernels ran and passed."""
+    import torch
+    from ate_replication_causalml_amd import _native
+    with pytest.raises(_native.NativeError) as ei:
+        _native.call("ate_debug_bad_launch", 2048, torch.cuda.current_stream().cuda_stream)
+    msg = str(ei.value)
+    assert "hipError" in msg and "ate_debug_bad_launch" in msg and "errors.hip" in msg, msg
+    assert ei.value.status > 0
+    _native.call("ate_debug_bad_launch", 64, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rep = _native.kernel_resource_report()
+    if _native.hip_library_path().name.endswith("_debug.so"):
+        assert rep and "FAIL" not in rep and "forest_exact_kernel" in rep, rep
+    print(msg)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
 def test_weighted_gram_kernel(gpu, dtype):
     rs = np.random.RandomState(1)

@@ -34,8 +34,11 @@ def test_two_ranks_on_one_gpu_match_one_process(gpu):
     assert two["hipgraph"] and two["n_gpus"] == 2
     assert two["throughput_inflight"]["inflight"] == 3
     assert two["throughput_inflight"]["fits_agree"]
-    assert two["ate"] == pytest.approx(ref["ate"], rel=1e-9, abs=1e-12)
-    assert two["se"] == pytest.approx(ref["se"], rel=1e-9)
+    # default (non-exact) mode: each rank's Gram chunks hold other rows than the one
+    # process's, so the fp32 chunk partials round differently (~1e-9 relative in the ATE);
+    # the bitwise world-size comparison is the exact mode's (test below)
+    assert two["ate"] == pytest.approx(ref["ate"], rel=1e-7, abs=1e-12)
+    assert two["se"] == pytest.approx(ref["se"], rel=1e-7)
 
 
 @pytest.mark.parametrize("cols,c04,ranks", [(40, "sliced", 2), (37, "sliced", 2),

@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _device_rows(n, gpu, seed):
-    """The first n generated rows of the tutorial model, unselected (float32 draws)."""
+    """The first n generated rows of the tutorial model, unselected (the rule's draws in
+    fp64, the rest in fp32)."""
     return synthetic_panel(n, p=21, folds=1, seed=seed, dtype="f64", device=gpu,
                            dgp="tutorial-rct")
 
@@ -37,13 +38,42 @@ def test_device_selection_equals_host_transform(gpu, compat):
     got = kept_gids(sel, [(0, N)], device=gpu).cpu().numpy()
     assert len(want) == N
     assert np.array_equal(got, want)
-    # the selected panel stores exactly those rows (same float32 draws)
+    # the selected panel stores exactly those rows (same draws)
     pan = synthetic_panel(N, p=21, folds=5, seed=seed, dtype="f64", device=gpu, dgp="tutorial",
                           selection=sel)
     m = (pan.row_index >= 0).cpu()
     rows = pan.row_index.cpu()[m]
     Xp = pan.colmajor().cpu()[:, m]
     assert torch.equal(Xp, torch.from_numpy(Xc[:, got[rows.numpy()]]))
+
+
+def test_cpu_and_gpu_panels_keep_the_same_rows(gpu):
+    """The selection rule's draws are fp64 on both sides (csrc/dgp.hip core_draws /
+    dgp_normal_d, the formulas of data/dgp.py selection_flags without FMA contraction), so a
+    CPU panel (host flags) and a GPU panel (device flags) of the same (N, seed) analyse the
+    SAME df_mod: equal n_generated, thresholds, per-block counts and kept rows at N = 2e5,
+    seed 21; the stored rule columns (yob, city: fp64 panels) agree to the last few ulps of
+    log / cos, the vote history and W exactly."""
+    N, seed = 200_000, 21
+    sg = plan_selection(N, seed, dgp.TUTORIAL, device=gpu)
+    sc = plan_selection(N, seed, dgp.TUTORIAL, device="cpu")
+    assert (sg.n_gen, sg.thr_t, sg.thr_c, sg.cand_t, sg.cand_c) == \
+        (sc.n_gen, sc.thr_t, sc.thr_c, sc.cand_t, sc.cand_c)
+    for f in ("blk_ct", "blk_cc", "blk_kept"):
+        np.testing.assert_array_equal(getattr(sg, f), getattr(sc, f))
+    kg = kept_gids(sg, [(0, N)], device=gpu).cpu().numpy()
+    kc = kept_gids(sc, [(0, N)]).numpy()
+    np.testing.assert_array_equal(kg, kc)
+    n = 30_000
+    pg = synthetic_panel(n, p=21, folds=5, seed=seed, dtype="f64", device=gpu, dgp="tutorial")
+    pc = synthetic_panel(n, p=21, folds=5, seed=seed, dtype="f64", device="cpu", dgp="tutorial")
+    np.testing.assert_array_equal(pg.gen_ids.cpu().numpy(), pc.gen_ids.numpy())
+    Xg, Xc = pg.colmajor().cpu().numpy(), pc.colmajor().numpy()
+    for c in ("x0", "x1"):                                  # yob, city
+        j = pg.cols[c]
+        np.testing.assert_allclose(Xg[j], Xc[j], rtol=1e-13, atol=1e-13)
+    for c in ["W"] + [f"x{16 + k}" for k in range(5)]:      # W and the vote history
+        np.testing.assert_array_equal(Xg[pg.cols[c]], Xc[pc.cols[c]])
 
 
 def test_device_selection_sharded_slices(gpu):
