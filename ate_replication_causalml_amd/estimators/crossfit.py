@@ -420,7 +420,7 @@ def causal_forest_bootstrap(Y, W, X, num_trees=2000, B=1000, seed=12345, boot_se
         # everything that changes the forest outputs: the resolved split engine, the
         # orthogonalisation forests' little-bag size, the causal split rule and a format tag
         # (an older checkpoint of binned / group-2 / unbalanced-split forests must not load)
-        sp = F.resolve_splits("auto", len(Yn))
+        sp = F.resolve_splits("auto", len(Yn), Xn.shape[1])
         key = fingerprint(Yn, Wn, Xn, np.array([num_trees, seed, nuisance_trees or 0]),
                           np.frombuffer(f"v{CF_CKPT_VERSION}|{sp}|ng1|{F.CAUSAL_SPLIT_RULE}"
                                         .encode(), dtype=np.uint8))

@@ -62,7 +62,7 @@ def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, fores
     thresholds), "binned" = 256-bin histograms, "auto" = exact up to 65536 rows."""
     dev = resolve_device(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
-    splits = F.resolve_splits(splits, len(Yn))
+    splits = F.resolve_splits(splits, len(Yn), Xn.shape[1])
     from ..parallel.comm import capturable
     if graph and capturable(comm) and dev.type == "cuda":
         # one hipGraph launch: outcome IRLS + counterfactual predictions, the propensity
@@ -182,7 +182,7 @@ def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, device=None, comm=Non
     Bins (256-bin edges or the exact mode's value table) come from ALL rows."""
     be = _backend(device)
     Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
-    splits = F.resolve_splits(splits, len(Yn))
+    splits = F.resolve_splits(splits, len(Yn), Xn.shape[1])
     edges = F.exact_bins(Xn) if splits == "exact" else F.bin_edges(Xn)
     kw = dict(backend=be, edges=edges, splits=splits)
     if comm is not None and comm.world_size > 1:
@@ -208,7 +208,7 @@ def double_ml(Y, W, X, num_trees=100, seed=123, method="Double Machine Learning"
     n = len(as_np(Y))
     h = n // 2
     dev = resolve_device(device)
-    splits = F.resolve_splits(splits, n)
+    splits = F.resolve_splits(splits, n, as_np(X).shape[1])
     if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
         # one hipGraph launch: the four forests, their predictions on all rows and both
         # residual-on-residual fits, over the binned matrix (edges from the data)
@@ -238,7 +238,7 @@ def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest
     grf); "textbook": W.hat clipped to [1e-6, 1 - 1e-6]."""
     dev = resolve_device(device)
     clip = None if compat == "reference" else F.AIPW_TEXTBOOK_CLIP
-    splits = F.resolve_splits(splits, len(as_np(Y)))
+    splits = F.resolve_splits(splits, len(as_np(Y)), as_np(X).shape[1])
     if graph and (comm is None or comm.world_size == 1) and dev.type == "cuda":
         # one hipGraph launch: Y.hat / W.hat OOB regression forests, the honest causal
         # forest on the centred data, its OOB CATEs and the AIPW average effect

@@ -184,11 +184,28 @@ class DeviceExactBins:
         raise ValueError("a device-only exact bin table cannot bin new rows; pass binned rows")
 
 
-def resolve_splits(splits: str, n: int) -> str:
+# "auto" keeps exact splits only while a tree's per-feature row lists stay small: the exact
+# engine's scratch holds two [p][in-bag rows] uint32 lists per tree (csrc/forest_exact.hip
+# tree_bytes), 8 p n bytes -- 5 MB at the tutorial's p = 21, n = 3e4, but 268 MB per tree at
+# p = 512, n = 65,536, where a 1-GiB launch cap would hold ~3 trees.
+EXACT_AUTO_LIST_BYTES = 64 << 20
+
+
+def exact_list_bytes(n: int, p: int) -> int:
+    """Bytes of a tree's two per-feature row lists in the exact engine (in-bag rows <= n)."""
+    return 8 * int(p) * int(n)
+
+
+def resolve_splits(splits: str, n: int, p: int | None = None) -> str:
     """"auto": randomForest's exact splits when the rows fit the uint16 value ranks
-    (n <= 65536, the tutorial scale), else the 256-bin histogram engine."""
+    (n <= 65536, the tutorial scale) and, given ``p``, a tree's row lists fit
+    ``EXACT_AUTO_LIST_BYTES``; else the 256-bin histogram engine."""
     if splits == "auto":
-        return "exact" if n <= EXACT_MAX_ROWS else "binned"
+        if n > EXACT_MAX_ROWS:
+            return "binned"
+        if p is not None and exact_list_bytes(n, p) > EXACT_AUTO_LIST_BYTES:
+            return "binned"
+        return "exact"
     if splits not in ("binned", "exact"):
         raise ValueError(f"splits must be 'auto', 'binned' or 'exact', got {splits!r}")
     return splits
@@ -580,6 +597,11 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
         est = torch.zeros(ntree * cap * 5, dtype=torch.int64, device=dev) if need_est else None
         mc = exact_mcap(n, sampling, max(1, group), sample_fraction, bool(honesty))
         per = _native.hip().ate_forest_exact_scratch_bytes(n, p, mc, 1)
+        if per > 4 * EXACT_AUTO_LIST_BYTES:
+            import warnings
+            warnings.warn(f"exact-split forest with p = {p}, {mc} in-bag rows: {per >> 20} MB "
+                          "of scratch per tree, few trees per launch; splits='binned' (or "
+                          "'auto') suits wide panels", RuntimeWarning, stacklevel=3)
         # trees per launch: two resident per CU, so a launch wants >= 512 of them and as
         # few tails as possible. A 1-GiB scratch cap held 264 trees of 5e4 rows (half the CUs
         # idle, a tail per launch; config 4 2.53 s); when 1 GiB cannot hold the whole forest
@@ -607,6 +629,15 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
                          val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
                          scratch.data_ptr(), s)
         del scratch
+        if not torch.cuda.is_current_stream_capturing():
+            # a tree whose in-bag count exceeded the host's bound mc returns nnodes = -1
+            # (csrc/forest_exact.hip; exact_mcap is exact, so never expected): an empty tree
+            # must not pass silently (inside a graph capture the check runs on the eager
+            # first call of the estimator instead)
+            bad = int((nnodes < 0).sum())
+            if bad:
+                raise RuntimeError(f"exact forest: {bad} of {ntree} trees overflowed the in-bag "
+                                   f"bound mc = {mc} (models/forest.exact_mcap)")
         return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, est, None, None, Xb,
                       exact=eb)
     Xbn = np.ascontiguousarray(h(Xb), dtype=np.uint16)
@@ -663,7 +694,7 @@ def regression_forest(X, y, num_trees=2000, honesty=True, min_node=5, alpha=0.05
     return fit_forest(X, KIND_REG, r1=y, ntree=num_trees, mtry=grf_mtry(p), min_node=min_node,
                       sampling=1, honesty=honesty, group=group, mtry_poisson=True, alpha=alpha,
                       sample_fraction=sample_fraction, seed=seed, backend=backend,
-                      splits=resolve_splits(splits, X.shape[0]), edges=edges)
+                      splits=resolve_splits(splits, X.shape[0], X.shape[1]), edges=edges)
 
 
 @dataclass
@@ -690,7 +721,7 @@ def causal_forest(X, Y, W, num_trees=2000, honesty=True, min_node=5, alpha=0.05,
     Y = np.asarray(Y, dtype=np.float64)
     W = np.asarray(W, dtype=np.float64)
     nt = nuisance_trees or max(50, num_trees // 4)
-    splits = resolve_splits(splits, X.shape[0])
+    splits = resolve_splits(splits, X.shape[0], X.shape[1])
     edges = exact_bins(X) if splits == "exact" else bin_edges(X)
     p = X.shape[1]
     grf = dict(mtry=grf_mtry(p), min_node=min_node, sampling=1, honesty=honesty,

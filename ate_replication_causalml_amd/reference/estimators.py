@@ -204,7 +204,7 @@ def aipw_rf(Y, W, X, num_trees=100, bootstrap_se=False, B=1000, seed=1991, fores
     Y, W, X = _arr(Y), _arr(W), _arr(X)
     mu0, mu1 = outcome_logit_mu(Y, W, X, counterfactual_quirk=(compat == "reference"))
     rf = rf_classifier_fit(X, W, num_trees=num_trees, seed=forest_seed,
-                           splits=resolve_splits(splits, len(Y)))
+                           splits=resolve_splits(splits, len(Y), X.shape[1]))
     p = clip_propensity(rf.oob_proba())
     return _aipw_result(method, W, Y, p, mu0, mu1, bootstrap_se, B, seed, compat,
                         n_oob_nan=int(np.isnan(rf.oob_proba()).sum()))
@@ -278,7 +278,7 @@ def chernozhukov(Y, W, X, idx1, idx2, num_trees, seed=123, splits="auto"):
     """One DML half (ate_functions.R:332-369, Q14/Q15); bins from all rows."""
     from ..models import forest as F
     Y, W, X = _arr(Y), _arr(W), _arr(X)
-    splits = F.resolve_splits(splits, len(Y))
+    splits = F.resolve_splits(splits, len(Y), X.shape[1])
     edges = F.exact_bins(X) if splits == "exact" else F.bin_edges(X)
     rf1 = F.fit_forest(X[idx1], F.KIND_CLASS, y=W[idx1], ntree=num_trees, seed=seed,
                        backend="cpu", edges=edges, splits=splits)

@@ -377,7 +377,7 @@ def main():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from ate_replication_causalml_amd.parallel import comm as C
     from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
-    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    from ate_replication_causalml_amd.estimators.lasso import EXACT_BLOCK, dml_crossfit_panel
     from ate_replication_causalml_amd.ops.gram import clear_plans
 
     comm = C.from_env()
@@ -413,6 +413,7 @@ def main():
         t2 = time.perf_counter()
         pan64 = synthetic_panel(n_total, p=args.p, folds=args.folds, seed=args.seed,
                                 dtype="f64", device=device, rank=rank, world=world,
+                                align=EXACT_BLOCK if args.exact else 0,
                                 dgp=args.dgp, selection=pan.selection)
         r64 = dml_crossfit_panel(pan64, args.folds, "min", comm=comm, seg_counts=seg_counts)[0]
         a64, s64 = [float(v) for v in r64.detach().cpu()]

@@ -343,3 +343,17 @@ def test_aipw_average_effect_clipping_is_a_textbook_option():
     w_c = np.clip(w_hat, 1e-6, 1 - 1e-6)
     g = (W - w_hat) / (w_c * (1 - w_c)) * Y
     assert np.isclose(tb_est, g.mean(), rtol=1e-12)
+
+
+def test_auto_splits_bound_the_exact_list_scratch():
+    """"auto" picks exact splits up to 65,536 rows only while a tree's two per-feature row
+    lists (8 p n bytes) stay within EXACT_AUTO_LIST_BYTES: the tutorial's p = 21 keeps
+    exact splits, a 512-column panel of 65,536 rows (268 MB of lists per tree) goes to the
+    histogram engine; explicit choices are kept."""
+    assert F.resolve_splits("auto", 9_416, 21) == "exact"
+    assert F.resolve_splits("auto", 65_536, 128) == "exact"
+    assert F.resolve_splits("auto", 65_536, 512) == "binned"
+    assert F.resolve_splits("auto", 70_000, 5) == "binned"
+    assert F.resolve_splits("auto", 65_536) == "exact"          # p unknown: rows only
+    assert F.resolve_splits("exact", 65_536, 512) == "exact"
+    assert F.exact_list_bytes(65_536, 512) == 268_435_456

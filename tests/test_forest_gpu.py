@@ -71,10 +71,38 @@ def test_device_forest_estimators_match_host(gpu, tutorial):
     Y, W, X = m.Y, m.W, m.X
     for f in (lambda d: DF.aipw_rf(Y, W, X, num_trees=60, device=d),
               lambda d: DF.double_ml(Y, W, X, num_trees=40, device=d),
-              lambda d: DF.causal_forest_ate(Y, W, X, num_trees=80, device=d, compat="textbook")):
+              lambda d: DF.causal_forest_ate(Y, W, X, num_trees=80, device=d, compat="textbook"),
+              # the default (compat="reference", W.hat unclipped; here in [0.07, 0.26])
+              lambda d: DF.causal_forest_ate(Y, W, X, num_trees=80, device=d)):
         a, b = f(gpu), f("cpu")
+        assert np.isfinite(a.ate) and np.isfinite(a.se)
         assert a.ate == pytest.approx(b.ate, rel=1e-9, abs=1e-12)
         assert a.se == pytest.approx(b.se, rel=1e-9, abs=1e-12)
+        for k in ("w_hat_min", "w_hat_max"):
+            if k in a.diagnostics:
+                assert a.diagnostics[k] == pytest.approx(b.diagnostics[k], rel=1e-12)
+
+
+def test_causal_forest_default_compat_overlap(gpu, tutorial):
+    """compat="reference" (grf: W.hat not clipped). The tutorial df_mod keeps W.hat inside
+    (0, 1): the bootstrap SE path agrees with the host. Tiny orthogonalisation forests (12
+    trees) on the toy data leave W.hat at exactly 0 for some rows: then the AIPW scores are
+    infinite on both devices, as in grf, and the overlap warning fires on both."""
+    import warnings
+    from ate_replication_causalml_amd.estimators import crossfit as CF
+    _, m, _ = tutorial
+    a = CF.causal_forest_bootstrap(m.Y, m.W, m.X, num_trees=24, B=64, device=gpu)
+    b = CF.causal_forest_bootstrap(m.Y, m.W, m.X, num_trees=24, B=64, device="cpu")
+    assert np.isfinite(a.ate) and np.isfinite(a.se) and a.se > 0
+    assert a.ate == pytest.approx(b.ate, rel=1e-9) and a.se == pytest.approx(b.se, rel=1e-8)
+    X, W, Y = _data(2000)
+    for dev in (gpu, "cpu"):
+        with warnings.catch_warnings(record=True) as ws:
+            warnings.simplefilter("always")
+            r = CF.causal_forest_bootstrap(Y, W, X, num_trees=24, nuisance_trees=12, B=64,
+                                           device=dev)
+        assert any("poor overlap" in str(w.message) for w in ws), dev
+        assert not np.isfinite(r.ate), (dev, r)
 
 
 def test_crossfit_and_cf_bootstrap_gpu_match_host(gpu):

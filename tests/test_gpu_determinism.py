@@ -29,12 +29,16 @@ def _cases(dev):
         "aipw_rf": lambda: forest.aipw_rf(Yb, W, X, num_trees=40, device=dev, graph=False),
         "causal_forest": lambda: forest.causal_forest_ate(Yc, W, X, num_trees=100, device=dev,
                                                           graph=False, compat="textbook"),
+        # the production default: grf's AIPW without clipping W.hat (here in [0.15, 0.80])
+        "causal_forest_reference": lambda: forest.causal_forest_ate(Yc, W, X, num_trees=100,
+                                                                    device=dev, graph=False),
         "residual_balance": lambda: balance.residual_balance(Yc, W, X, device=dev),
     }
 
 
 @pytest.mark.parametrize("name", ["ols", "aipw_glm", "lasso_single", "dml", "aipw_rf",
-                                  "causal_forest", "residual_balance"])
+                                  "causal_forest", "causal_forest_reference",
+                                  "residual_balance"])
 def test_estimator_bit_reproducible(gpu, name):
     fn = _cases(gpu)[name]
     vals = {repr((r.ate, r.se)) for r in (fn() for _ in range(3))}

@@ -34,6 +34,9 @@ CASES = {
         Yb, W, X, num_trees=40, device=dev, graph=g),
     "causal_forest": lambda L, X, W, Yc, Yb, dev, g: _forest().causal_forest_ate(
         Yc, W, X, num_trees=200, device=dev, graph=g, compat="textbook"),
+    # the default compat="reference": the clip=None graph body (6 outputs incl. W.hat range)
+    "causal_forest_reference": lambda L, X, W, Yc, Yb, dev, g: _forest().causal_forest_ate(
+        Yc, W, X, num_trees=200, device=dev, graph=g),
     "lasso_single": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_single(
         Yc, W, X, device=dev, graph=g),
     "lasso_usual": lambda L, X, W, Yc, Yb, dev, g: _lasso().lasso_usual(

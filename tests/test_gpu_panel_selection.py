@@ -40,7 +40,7 @@ def test_device_selection_equals_host_transform(gpu, compat):
     assert np.array_equal(got, want)
     # the selected panel stores exactly those rows (same draws)
     pan = synthetic_panel(N, p=21, folds=5, seed=seed, dtype="f64", device=gpu, dgp="tutorial",
-                          selection=sel)
+                          selection=sel, compat=compat)
     m = (pan.row_index >= 0).cpu()
     rows = pan.row_index.cpu()[m]
     Xp = pan.colmajor().cpu()[:, m]
