@@ -330,7 +330,10 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
     // stage s landed: at most the later stages' loads are outstanding
     const int64_t later = nsteps - 1 - s < PNS - 2 ? nsteps - 1 - s : PNS - 2;
     wait_vmcnt((int)later * per);
-    __syncthreads();                                    // ... in every wave; stage s-1 consumed
+    // ... in every wave; stage s-1 consumed. A raw s_barrier: __syncthreads()'s fence would
+    // drain every LDS-DMA in flight (the later stages' too) and undo the ring (round 6: the
+    // rings measured in round 5 had that drain)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (s + PNS - 1 < nsteps) stage((int)((s + PNS - 1) % PNS), ch.row0 + (s + PNS - 1) * PKS);
     const int cur = (int)(s % PNS);
     const bf16_t* As = buf(cur, abuf);
