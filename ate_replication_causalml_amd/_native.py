@@ -67,6 +67,7 @@ _SIGS = {
     "ate_gram_bf16": "pliipipipipppp",
     "ate_gram_bf16_pair": "pllipippipippipp",
     "ate_gram_bf16_tri": "pllippipippipp",
+    "ate_gram_pair_bal": "",
     "ate_last_error": "pi",
     "ate_last_stale_error": "pi",
     "ate_clear_errors": "",

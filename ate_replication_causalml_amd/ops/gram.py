@@ -77,7 +77,7 @@ class GramPlan:
         if self.tri:
             tiles, blocks = [(0, 0, 0, 0), (0, 0, 1, 0)], tri_blocks()
         elif self.pair:
-            tiles, blocks = _pair_tiles(nt)
+            tiles, blocks = _pair_tiles(nt, bal=bool(_native.hip().ate_gram_pair_bal()))
         else:
             tiles = [(a, b) for a in range(nt) for b in range(a, nt)]
         ntiles = len(tiles)
@@ -184,11 +184,14 @@ def _cu_count(dev) -> int:
         return 256
 
 
-def _pair_tiles(nt: int):
+def _pair_tiles(nt: int, bal: bool = True):
     """Tile list (a, b, type, 0) and slab block table for the paired-tile kernel
     (csrc/gram.hip gram_bf16_pair_kernel): every diagonal pair (a, b) follows the
     off-diagonal tile (a, b) that streams the same columns; remaining off-diagonal tiles
-    after. Returns (tiles, blocks[ntiles][PAIR_SLOTS] of 16-column block (I, J))."""
+    after. Returns (tiles, blocks[ntiles][PAIR_SLOTS] of 16-column block (I, J)).
+    ``bal`` (the library's GRAM_BAL, ate_gram_pair_bal): in a diagonal pair every wave holds
+    34 blocks -- each triangle wave's last two, (6, 7) and (7, 7) of its triangle, are
+    computed by the rectangle wave of the same region and half."""
     tiles = []
     for a in range(0, nt - 1, 2):
         tiles.append((a, a + 1, 0, 0))
@@ -207,6 +210,7 @@ def _pair_tiles(nt: int):
                     for n in range(4):
                         tb[w * 32 + m * 4 + n] = (a * 16 + wr * 8 + m, b * 16 + wc * 4 + n)
         else:
+            rs, ts = (34, 34) if bal else (32, 36)     # blocks per rectangle / triangle wave
             for w in range(4):                         # rectangles rows 0-7 x cols 8-15
                 region, half = w >> 1, w & 1
                 if typ == 2 and region == 1:
@@ -214,7 +218,11 @@ def _pair_tiles(nt: int):
                 base = (a if region == 0 else b) * 16
                 for m in range(8):
                     for n in range(4):
-                        tb[w * 32 + m * 4 + n] = (base + m, base + 8 + half * 4 + n)
+                        tb[w * rs + m * 4 + n] = (base + m, base + 8 + half * 4 + n)
+                if bal:                                # the triangle's (6, 7), (7, 7)
+                    t0 = base + half * 8
+                    tb[w * rs + 32] = (t0 + 6, t0 + 7)
+                    tb[w * rs + 33] = (t0 + 7, t0 + 7)
             for w in range(4):                         # triangles I <= J in 0-7 / 8-15
                 region, half = w >> 1, w & 1
                 if typ == 2 and region == 1:
@@ -223,7 +231,8 @@ def _pair_tiles(nt: int):
                 idx = 0
                 for m in range(8):
                     for n in range(m, 8):
-                        tb[128 + w * 36 + idx] = (base + m, base + n)
+                        if idx < ts:
+                            tb[4 * rs + w * ts + idx] = (base + m, base + n)
                         idx += 1
         blocks.append(tb)
     return tiles, blocks

@@ -288,16 +288,63 @@ __device__ __forceinline__ int tri_index(int m, int n) {   // m <= n < 8, row-ma
   return m * 8 - (m * (m - 1)) / 2 + (n - m);
 }
 
-// One wave role for the whole K-loop: TRI = triangle wave (8 fragments as both A and B,
-// 36 blocks), else rectangle wave (8 A + 4 B fragments, 32 blocks). Each instantiation
-// keeps only its own accumulators live; every wave runs the same number of barriers.
-template <bool TRI>
+#ifndef GRAM_BAL
+// 1: the diagonal-pair workgroup's eight waves hold 34 blocks each instead of 32 (rectangle)
+// and 36 (triangle): each triangle wave's last two blocks, (6, 7) and (7, 7) of its 8-block
+// triangle, move to the rectangle wave of the same region and half, which already holds
+// both fragments (half 0: A fragments 6, 7; half 1: B fragments 2, 3 = blocks 14, 15). Every
+// block still sums the same K sequence: the Gram bits do not change.
+#define GRAM_BAL 0
+#endif
+constexpr int PAIR_RECT = 0, PAIR_RECT_D0 = 1, PAIR_TRI = 2, PAIR_RECT_D1 = 3;
+template <int MODE> struct PairRole {
+  static constexpr bool TRI = MODE == PAIR_TRI;
+  static constexpr int NB = MODE == PAIR_RECT ? 32 : GRAM_BAL ? 34 : TRI ? 36 : 32;
+};
+
+// The MFMAs of one 32-deep k-step of a wave role: a rectangle (8 A x 4 B fragments, plus the
+// two balanced-away triangle blocks in a diagonal-pair workgroup) or a triangle (8 fragments
+// as A and B, blocks m <= n in tri_index order, the last two dropped under GRAM_BAL).
+template <int MODE>
+__device__ __forceinline__ void pair_mfma(f32x4* acc, const bf16x8* af, const bf16x8* bfr) {
+  if constexpr (MODE != PAIR_TRI) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m * 4 + n],
+                                                                 0, 0, 0);
+    if constexpr (GRAM_BAL && MODE == PAIR_RECT_D0) {
+      acc[32] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[6], af[7], acc[32], 0, 0, 0);
+      acc[33] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[7], af[7], acc[33], 0, 0, 0);
+    }
+    if constexpr (GRAM_BAL && MODE == PAIR_RECT_D1) {
+      acc[32] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[2], bfr[3], acc[32], 0, 0, 0);
+      acc[33] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[3], bfr[3], acc[33], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = m; n < 8; ++n)
+        if (tri_index(m, n) < PairRole<MODE>::NB)
+          acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              af[m], af[n], acc[tri_index(m, n)], 0, 0, 0);
+  }
+}
+
+// One wave role for the whole K-loop (MODE: PAIR_TRI = triangle wave, else a rectangle wave;
+// PAIR_RECT_D0 / D1 = the rectangle waves of a diagonal-pair workgroup, halves 0 / 1). Each
+// instantiation keeps only its own accumulators live; every wave runs the same number of
+// barriers.
+template <int MODE>
 __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t cs, int64_t bs, int a0,
                                           int b0, bool haveB, bool idle, int abuf, int bbuf,
                                           int arow0, int bcol0, const Chunk& ch,
                                           bf16_t* lds_raw, float* __restrict__ out,
                                           bool second) {
-  constexpr int NB = TRI ? 36 : 32;
+  constexpr bool TRI = PairRole<MODE>::TRI;
+  constexpr int NB = PairRole<MODE>::NB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   f32x4 acc[NB];
 #pragma unroll
@@ -346,22 +393,12 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
         for (int m = 0; m < 8; ++m) af[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
 #pragma unroll
         for (int n = 0; n < 4; ++n) bfr[n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-#pragma unroll
-          for (int n = 0; n < 4; ++n)
-            acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n],
-                                                                      acc[m * 4 + n], 0, 0, 0);
+        pair_mfma<MODE>(acc, af, bfr);
       } else {
         bf16x8 fr[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m) fr[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-#pragma unroll
-          for (int n = m; n < 8; ++n)
-            acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                fr[m], fr[n], acc[tri_index(m, n)], 0, 0, 0);
+        pair_mfma<MODE>(acc, fr, fr);
       }
     }
   }
@@ -412,13 +449,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
           for (int n = 0; n < 4; ++n) bfr[kk][n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int m = 0; m < 8; ++m)
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-              acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][m], bfr[kk][n],
-                                                                        acc[m * 4 + n], 0, 0, 0);
+        for (int kk = 0; kk < 2; ++kk) pair_mfma<MODE>(acc, af[kk], bfr[kk]);
         // schedule: the first half's 12 reads, then the second half's 12 reads one per
         // MFMA of the first half, then the remaining MFMAs (mask 0x100 DS read, 0x008 MFMA)
         __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
@@ -427,7 +458,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 52, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 12, 0);
       } else {
         bf16x8 fr[2][8];
 #pragma unroll
@@ -437,20 +468,14 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
           for (int m = 0; m < 8; ++m) fr[kk][m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
         }
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int m = 0; m < 8; ++m)
-#pragma unroll
-            for (int n = m; n < 8; ++n)
-              acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  fr[kk][m], fr[kk][n], acc[tri_index(m, n)], 0, 0, 0);
+        for (int kk = 0; kk < 2; ++kk) pair_mfma<MODE>(acc, fr[kk], fr[kk]);
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 64, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 8, 0);
       }
     }
 #else
@@ -464,22 +489,12 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
           for (int m = 0; m < 8; ++m) af[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
 #pragma unroll
           for (int n = 0; n < 4; ++n) bfr[n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
-#pragma unroll
-          for (int m = 0; m < 8; ++m)
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-              acc[m * 4 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n],
-                                                                        acc[m * 4 + n], 0, 0, 0);
+          pair_mfma<MODE>(acc, af, bfr);
         } else {
           bf16x8 fr[8];
 #pragma unroll
           for (int m = 0; m < 8; ++m) fr[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
-#pragma unroll
-          for (int m = 0; m < 8; ++m)
-#pragma unroll
-            for (int n = m; n < 8; ++n)
-              acc[tri_index(m, n)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  fr[m], fr[n], acc[tri_index(m, n)], 0, 0, 0);
+          pair_mfma<MODE>(acc, fr, fr);
         }
       }
     }
@@ -545,7 +560,8 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   else { arow0 = half * 128; bcol0 = half * 128; }
   const int abuf = type == 0 ? 0 : region;
   const int bbuf = type == 0 ? 1 : region;
-  const int base = tri ? 128 + (wid - 4) * 36 : wid * 32;
+  constexpr int RS = PairRole<PAIR_RECT_D0>::NB, TS = PairRole<PAIR_TRI>::NB;  // 34 / 34 (32 / 36)
+  const int base = type == 0 ? wid * 32 : tri ? 4 * RS + (wid - 4) * TS : wid * RS;
   float* out = slab + ((int64_t)c * ntiles + t) * (PAIR_SLOTS * 256) + (int64_t)base * 256;
 #if GRAM_PRIO
   // the second-dispatched half (waves 4-7: the triangle waves of a diagonal pair, the
@@ -558,9 +574,13 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
 #endif
 #endif
   if (tri)
-    pair_wave<true>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
+    pair_wave<PAIR_TRI>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, true);
+  else if (type == 0)
+    pair_wave<PAIR_RECT>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, false);
+  else if (half == 0)
+    pair_wave<PAIR_RECT_D0>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, true);
   else
-    pair_wave<false>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, type != 0);
+    pair_wave<PAIR_RECT_D1>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, true);
 #ifdef GRAM_CLOCK
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -887,6 +907,10 @@ ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, con
   }
   return 0;
 }
+
+// The slab layout of the paired-tile kernel's diagonal-pair workgroups (ops/gram.py
+// _pair_tiles reads it): 1 = 34 blocks per wave (GRAM_BAL), 0 = 32 / 36.
+ATE_API int ate_gram_pair_bal() { return GRAM_BAL; }
 
 // Split-triangle Gram (P == 512): what as ate_gram_bf16_pair; blocks = [2][TRI_SLOTS] int2.
 ATE_API int ate_gram_bf16_tri(const void* X, int64_t cs, int64_t bs, int P, const void* blocks,

@@ -60,3 +60,16 @@ def test_tri_blocks_cover_the_upper_triangle_once():
         for fc, bl in roles:
             assert len(bl) <= 36 and len(set(fc)) == len(fc)
             assert all(fc[a] <= fc[b] for a, b in bl)
+
+
+@pytest.mark.parametrize("nt", [2, 3, 4])
+@pytest.mark.parametrize("bal", [True, False])
+def test_pair_tiles_cover_the_upper_triangle_once(nt, bal):
+    """Paired-tile slab table (csrc/gram.hip gram_bf16_pair_kernel): every 16-column block
+    I <= J once, for the balanced (34 / 34 blocks per diagonal-pair wave, GRAM_BAL) and the
+    unbalanced (32 / 36) wave roles."""
+    from ate_replication_causalml_amd.ops.gram import PAIR_SLOTS, _pair_tiles
+    tiles, blocks = _pair_tiles(nt, bal)
+    assert all(len(t) == PAIR_SLOTS for t in blocks)
+    used = [b for t in blocks for b in t if b[0] >= 0]
+    assert sorted(used) == [(i, j) for i in range(16 * nt) for j in range(i, 16 * nt)]
