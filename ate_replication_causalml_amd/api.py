@@ -206,10 +206,21 @@ def ate_double_ml(Y, W, X, num_trees=100, method="Double Machine Learning", run=
 
 
 def ate_dml(Y, W, X, folds=5, lambda_rule="min", method="DML cross-fit (LASSO)",
-            run=None) -> AteResult:
-    """K-fold cross-fit partially linear DML with CV-LASSO nuisances (north-star)."""
+            run=None, repeats=1, aggregate="median") -> AteResult:
+    """K-fold cross-fit partially linear DML with CV-LASSO nuisances (north-star).
+    ``repeats`` > 1: repeated cross-fitting over that many distinct K-fold partitions
+    (Chernozhukov et al. 2018 §3.4), ``aggregate`` "median" (default) or "mean"; the
+    partitions share one Gram pass (estimators/lasso.dml_repeated_phases)."""
     run = _run(run)
-    with trace("ate_dml", folds=folds):
+    with trace("ate_dml", folds=folds, repeats=repeats):
+        if repeats > 1:
+            if _ref(run):
+                from .reference import estimators as R
+                return R.dml_plr_lasso_repeated(Y, W, X, folds, repeats, run.seed, lambda_rule,
+                                                aggregate)
+            from .estimators import lasso as DL
+            return DL.dml_plr_lasso_repeated(Y, W, X, folds, repeats, run.seed, lambda_rule,
+                                             aggregate, device=run.device(), dtype=run.dtype)
         if _ref(run):
             from .reference import estimators as R
             return R.dml_plr_lasso(Y, W, X, folds=folds, seed=run.seed, lambda_rule=lambda_rule,

@@ -500,6 +500,117 @@ def dml_crossfit_panel(pan, folds: int, lambda_rule="min", G=None, comm=None, se
     return st["res"], st["mom"], st.get("cv")
 
 
+# ---------------------------------------------------------------- repeated cross-fitting
+def micro_fold_map(K: int, s: int) -> np.ndarray:
+    """Fold of each of the K*K micro-segments m = K a + b under partition s: (a + s b) mod K.
+    Every partition puts K micro-segments in every fold; for prime K the partitions
+    s = 0..K-1 are pairwise distinct (two of them share one micro-segment per fold pair)."""
+    a, b = np.divmod(np.arange(K * K), K)
+    return (a + s * b) % K
+
+
+def median_aggregate(theta: torch.Tensor, se: torch.Tensor, how: str = "median"):
+    """Chernozhukov et al. (2018) §3.4, Definition 3.3: theta = median of the S split
+    estimates, SE^2 = median of SE_s^2 + (theta_s - theta)^2 ("mean": the means). Medians of
+    an even count average the two middle values. Device tensors in, [2] out (capturable)."""
+    def med(v):
+        v = torch.sort(v).values
+        n = v.shape[0]
+        return v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
+    if how == "mean":
+        t = theta.mean()
+        return torch.stack([t, torch.sqrt((se * se + (theta - t) ** 2).mean())])
+    t = med(theta)
+    return torch.stack([t, torch.sqrt(med(se * se + (theta - t) ** 2))])
+
+
+def dml_repeated_phases(pan, folds: int, repeats: int, lambda_rule="min", comm=None,
+                        seg_counts=None, aggregate="median"):
+    """Repeated K-fold cross-fitting (Chernozhukov et al. 2018 §3.4): ``repeats`` = S
+    distinct K-fold partitions of the rows, one DML-PLR fit per partition, median-aggregated.
+    The panel holds K*K micro-segments (segment m = K a + b); partition s puts micro-segment m
+    in fold (a + s b) mod K (micro_fold_map). So ONE Gram pass gives every partition's fold
+    Grams: the K*K micro-Gram stack (K01, C01) is summed per partition into its K fold
+    Grams (a [K, K*K] 0/1 matrix times the stack, fp64), and each partition runs its CV-LASSO
+    paths (K08/K09) and the residual pass with its fold coefficients spread over the
+    micro-segments. Phases as dml_phases (SegmentedStep captures them: one graph at world 1);
+    the result state holds "res" [2] (the aggregate) and "splits" [S, 2]. Reference:
+    the split-and-average DML of /root/reference/ate_functions.R:372-389, generalised."""
+    from ..utils.graphs import Collective
+    K, Sn = folds, repeats
+    if pan.nseg != K * K:
+        raise ValueError(f"repeated cross-fitting needs K*K = {K * K} micro-segments, the panel "
+                         f"has {pan.nseg}")
+    if not 1 <= Sn <= K:
+        raise ValueError(f"repeats must be in 1..{K} (distinct partitions of K*K micro-segments)")
+    dist = comm is not None and comm.world_size > 1
+    if seg_counts is None:
+        seg_counts = global_seg_counts(pan, comm) if dist else np.asarray(pan.seg_nreal)
+    counts = np.asarray(seg_counts, dtype=np.float64)
+    dev = pan.device
+    maps = [micro_fold_map(K, s) for s in range(Sn)]
+    M = [const(np.eye(K)[m].T.copy(), torch.float64, dev) for m in maps]       # [K, K*K]
+    fold_counts = [np.bincount(m, weights=counts, minlength=K) for m in maps]
+    mi = [const(m, torch.int64, dev) for m in maps]
+    full_sets = [[j for j in range(K) if j != k] for k in range(K)]
+    ycols = [pan.cols["Y"], pan.cols["W"]]
+    P = pan.P
+    cap = bool(getattr(comm, "capturable", False))
+
+    def phase_gram(_):
+        return {"G": gram(pan, stage="tiles")}
+
+    def phase_gram_reduce(st):
+        return {"G": gram(pan, stage="reduce", out=st["G"])}
+
+    def phase_split(s):
+        def f(st):
+            Gs = (M[s] @ st["G"].view(K * K, P * P)).view(K, P, P)
+            cv = cv_enet_gaussian(Gs, pan, pan.xcols, ycols, full_sets=full_sets,
+                                  seg_counts=fold_counts[s])
+            coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1)
+            coef_m = coef.double().index_select(0, mi[s]).contiguous()
+            return {**st, f"mom{s}": dml_residual_moments(pan, coef_m)}
+        return f
+
+    def phase_final(st):
+        res = torch.stack([S.dml_finalize(st[f"mom{s}"], "plr") for s in range(Sn)])
+        return {**st, "splits": res, "res": median_aggregate(res[:, 0], res[:, 1], aggregate)}
+
+    def reduce(name):
+        def f(st):
+            comm.all_reduce_(st[name])
+            return st
+        return Collective(f, capturable=cap)
+
+    def reduce_sym(name):
+        _tri_index(P, dev)
+
+        def f(st):
+            allreduce_sym_(comm, st[name])
+            return st
+        return Collective(f, capturable=cap)
+
+    phases = [phase_gram, phase_gram_reduce]
+    if dist:
+        phases.append(reduce_sym("G"))
+    for s in range(Sn):
+        phases.append(phase_split(s))
+        if dist:
+            phases.append(reduce(f"mom{s}"))
+    phases.append(phase_final)
+    return phases
+
+
+def dml_repeated_panel(pan, folds: int, repeats: int, lambda_rule="min", comm=None,
+                       seg_counts=None, aggregate="median"):
+    """Eager run of dml_repeated_phases: (aggregate [2], splits [S, 2])."""
+    st = None
+    for ph in dml_repeated_phases(pan, folds, repeats, lambda_rule, comm, seg_counts, aggregate):
+        st = ph(st)
+    return st["res"], st["splits"]
+
+
 def _exact_resid(pan, coef: torch.Tensor, mode: int, sh) -> torch.Tensor:
     """Exact-mode passes of the fused bf16 residual kernel (csrc/dml.hip): mode 1 ->
     per-block max |term| [blocks * 7] fp64; mode 2 -> per-block int64 limb sums
@@ -576,6 +687,36 @@ def _dml_graphed(pan, folds, lambda_rule, dist=None):
     if dist is not None and dist.world > 1:
         counts = tuple(global_seg_counts(pan, dist.comm).tolist())   # host ints, outside
     return estimator_graphs.run("dml_plr", _dml_body, (pan,), folds, lambda_rule, dist, counts)
+
+
+def _dml_repeated_body(pan, folds, repeats, lambda_rule, aggregate):
+    st = None
+    for ph in dml_repeated_phases(pan, folds, repeats, lambda_rule, aggregate=aggregate):
+        st = ph(st)
+    return torch.cat([st["res"], st["splits"].reshape(-1)])
+
+
+def dml_plr_lasso_repeated(Y, W, X, folds=5, repeats=3, seed=1991, lambda_rule="min",
+                           aggregate="median", method="DML cross-fit (LASSO, repeated)",
+                           device=None, dtype="f64", graph=True):
+    """``repeats`` = S distinct K-fold cross-fits, median-aggregated (dml_repeated_phases).
+    Rows go to K*K micro-segments by a balanced Philox assignment (parallel.rng.fold_ids
+    with K*K groups); partition s is micro_fold_map(K, s). On a GPU the whole call (one
+    Gram pass, S path solves and residual passes, the aggregate) is one captured graph.
+    Matches reference.estimators.dml_plr_lasso_repeated. diagnostics["splits"]: the S
+    (ATE, SE) pairs."""
+    dev = resolve_device(device)
+    Yn, Wn, Xn = as_np(Y), as_np(W), as_np(X)
+    micro = rng.fold_ids(len(Yn), folds * folds, seed, 0)
+    pan = build_panel(Xn, Wn, Yn, folds=micro, dtype=dtype, device=dev)
+    if graph and pan.data.is_cuda:
+        out, g = estimator_graphs.run("dml_repeated", _dml_repeated_body, (pan,), folds, repeats,
+                                      lambda_rule, aggregate)
+    else:
+        out, g = _dml_repeated_body(pan, folds, repeats, lambda_rule, aggregate), False
+    v = out.detach().double().cpu().numpy()
+    return AteResult.make(method, v[0], v[1], n=len(Yn), repeats=repeats, aggregate=aggregate,
+                          splits=v[2:].reshape(repeats, 2).tolist(), hipgraph=g)
 
 
 def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min", method="DML cross-fit (LASSO)",

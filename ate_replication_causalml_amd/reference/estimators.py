@@ -323,14 +323,16 @@ def causal_forest_ate(Y, W, X, num_trees=2000, seed=12345, method="Causal Forest
 
 # ---------------------------------------------------------------- K-fold DML (north star)
 def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min",
-                  method="DML cross-fit (LASSO)"):
+                  method="DML cross-fit (LASSO)", fold_ids=None):
     """Partially-linear DML with K-fold cross-fitting and CV-LASSO nuisances.
 
     For held-out fold k the nuisances E[Y|X], E[W|X] are gaussian LASSO fits on
     the other K-1 folds, with lambda chosen by (K-1)-fold CV over those same
-    folds (so every Gram the GPU needs is a sum of per-fold Grams)."""
+    folds (so every Gram the GPU needs is a sum of per-fold Grams). ``fold_ids``:
+    an explicit fold of every row (default: the Philox assignment)."""
     Y, W, X = _arr(Y), _arr(W), _arr(X)
-    fid = rng.fold_ids(len(Y), folds, seed, stream=0)
+    fid = rng.fold_ids(len(Y), folds, seed, stream=0) if fold_ids is None else \
+        np.asarray(fold_ids, dtype=np.int64)
     yr = np.empty_like(Y)
     wr = np.empty_like(W)
     for k in range(folds):
@@ -343,6 +345,27 @@ def dml_plr_lasso(Y, W, X, folds=5, seed=1991, lambda_rule="min",
             s = "lambda.min" if lambda_rule == "min" else "lambda.1se"
             out[te] = target[te] - cv.predict(X[te], s=s)
     return dml_from_residuals(yr, wr, method)
+
+
+def dml_plr_lasso_repeated(Y, W, X, folds=5, repeats=3, seed=1991, lambda_rule="min",
+                           aggregate="median", method="DML cross-fit (LASSO, repeated)"):
+    """Repeated cross-fitting (Chernozhukov et al. 2018 §3.4, median method): S = repeats
+    K-fold partitions built from K*K micro-groups (group m = K a + b of a balanced Philox
+    assignment; partition s puts it in fold (a + s b) mod K), one DML fit per partition,
+    theta = median(theta_s), SE^2 = median(SE_s^2 + (theta_s - theta)^2) ("mean": means)."""
+    Y, W, X = _arr(Y), _arr(W), _arr(X)
+    micro = rng.fold_ids(len(Y), folds * folds, seed, stream=0)
+    a, b = np.divmod(micro, folds)
+    th, se = [], []
+    for s in range(repeats):
+        r = dml_plr_lasso(Y, W, X, folds, seed, lambda_rule, method, fold_ids=(a + s * b) % folds)
+        th.append(r.ate)
+        se.append(r.se)
+    th, se = np.array(th), np.array(se)
+    agg = np.median if aggregate == "median" else np.mean
+    t = float(agg(th))
+    return AteResult.make(method, t, float(np.sqrt(agg(se * se + (th - t) ** 2))),
+                          n=len(Y), repeats=repeats, splits=np.stack([th, se], 1).tolist())
 
 
 def dml_from_residuals(yr, wr, method):
