@@ -65,7 +65,7 @@ c_double = ctypes.c_double
 # name -> argtypes (restype int). 'p' pointer, 'i' int32, 'l' int64, 'u' uint64, 'd' double
 _SIGS = {
     "ate_gram_bf16": "pliipipipipppp",
-    "ate_gram_bf16_pair": "pllipippipippipp",
+    "ate_gram_bf16_pair": "pllipippipippippp",
     "ate_gram_bf16_tri": "pllippipippipp",
     "ate_gram_pair_bal": "",
     "ate_last_error": "pi",
@@ -100,7 +100,7 @@ _SIGS = {
     "ate_dml_resid_exact": "pllpipipiiiiiiippp",
     "ate_lognet_path": "iplpiipipipdddippippppppppp",
     "ate_lognet_cvloss": "iplpiippipppipp",
-    "ate_dgp_fill": "iplllllp" + "uiipp",
+    "ate_dgp_fill": "iplllllp" + "uiipppp",
     "ate_sel_block_rows": "",
     "ate_sel_gen_count": "upilllpp",
     "ate_sel_gen_flags": "upillpp",

@@ -22,6 +22,8 @@ Two data-generating processes (``dgp=``):
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -52,6 +54,39 @@ def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1, align: 
     return out
 
 
+# One-byte columns (csrc/gram.hip, the paired-tile Gram's byte path): a P = 512 blocked bf16
+# panel on the GPU keeps its {0, 1}-valued columns (one, the 6 tutorial binaries, every 4th
+# extra covariate, W, Y and their hi / lo halves, padding) in physical columns 384..511 and a
+# one-byte copy of those 128 columns beside the panel (DevicePanel.bytes8). Estimators see
+# the same names -> columns map (pan.cols / pan.xcols); the Gram streams 896 instead of
+# 1,024 bytes per row. Measured slower than the all-bf16 read (profiles/r06_gram/README.md:
+# 4.79 vs 4.64 ms per ate_dml call), so it is opt-in: ATE_PANEL_BYTES=1. Off: the
+# generator's column order, no byte copy.
+BYTE_COL0 = 384
+BYTE_PANEL = os.environ.get("ATE_PANEL_BYTES", "0") == "1"
+
+
+def _binary_names(p: int) -> set:
+    """Generator columns whose values are exactly 0 or 1 (csrc/dgp.hip dgp_fill_kernel)."""
+    out = {"one", "W", "Y", "W_hi", "W_lo", "Y_hi", "Y_lo"}
+    out |= {f"x{j}" for j in range(15, min(21, p))}                    # sex + vote history
+    out |= {f"x{j}" for j in range(21, p) if (j - 21) % 4 == 3}        # binary extras
+    return out
+
+
+def byte_column_order(names: list, p: int, P: int):
+    """Physical column order for the one-byte path: the continuous columns first, then the
+    binary ones, so that physical columns BYTE_COL0..P-1 are all binary or padding. None
+    when the panel does not have that shape (P != 512, or too few binary columns)."""
+    if P != 512:
+        return None
+    binary = _binary_names(p)
+    cont = [nm for nm in names if nm not in binary]
+    if len(cont) > BYTE_COL0:
+        return None
+    return cont + [nm for nm in names if nm in binary]
+
+
 def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991,
                     dtype: str = "bf16", device="cpu", rank: int = 0, world: int = 1,
                     blocked: bool = False, align: int = 0, dgp: str = "rct", comm=None,
@@ -80,8 +115,16 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
     cpad = 128 if dtype == "bf16" else 64
     P = (len(names) + cpad - 1) // cpad * cpad
     pan = empty_panel([c for _, c in slices], P, dtype=dtype, device=device, blocked=blocked)
-    pan.cols = {nm: i for i, nm in enumerate(names)}
+    order = byte_column_order(names, p, P) if (
+        hi_lo and blocked and pan.data.is_cuda and BYTE_PANEL) else None
+    pan.cols = {nm: i for i, nm in enumerate(names if order is None else order)}
     pan.xcols = [pan.cols[f"x{j}"] for j in range(p)]
+    pcol = None
+    if order is not None:
+        pcol = torch.as_tensor([pan.cols[nm] for nm in names], dtype=torch.int16,
+                               device=pan.data.device)
+        pan.bytes8 = torch.zeros((pan.ld // 64, P - BYTE_COL0, 64), dtype=torch.uint8,
+                                 device=pan.data.device)
     # global (kept) row ids of this shard (panel order)
     rid = torch.full((pan.ld,), -1, dtype=torch.int64, device=device)
     for (g0, cnt), (r0, _) in zip(slices, pan.seg_bounds):
@@ -109,7 +152,8 @@ def synthetic_panel(n_total: int, p: int = 500, folds: int = 5, seed: int = 1991
             gp = 0 if gids is None or cnt == 0 else gids[int(offs[k]):].data_ptr()
             _native.call("ate_dgp_fill", dtype_code(pan.data), pan.data.data_ptr(),
                          *pan.strides(), int(r0), cnt, g0, gp, seed, p_extra, int(hi_lo),
-                         pblk.ctypes.data, s)
+                         pblk.ctypes.data, None if pcol is None else pcol.data_ptr(),
+                         None if pcol is None else pan.bytes8.data_ptr(), s)
     else:
         cm = torch.zeros((pan.P, pan.ld), dtype=pan.data.dtype) if blocked else pan.data
         for k, ((g0, cnt), (r0, _)) in enumerate(zip(slices, pan.seg_bounds)):

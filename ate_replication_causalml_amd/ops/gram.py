@@ -35,6 +35,11 @@ PAIR_SLOTS = 272
 # (2.54-2.56 vs 2.52-2.56 ms) and 0.45 ms slower inside the single ate_dml call (2.73 vs 2.29)
 TRI_SLOTS, TRI_SPLIT = 288, 22
 GRAM_TRI = os.environ.get("ATE_GRAM_TRI", "0") == "1"
+# Panels that carry one-byte copies of their {0, 1} columns (DevicePanel.bytes8: physical
+# columns 384..511 of a P = 512 blocked bf16 panel) stream those to the paired-tile Gram as
+# bytes (csrc/gram.hip): 896 instead of 1,024 bytes per row, the same Gram bits.
+# ATE_GRAM_BYTES=0 reads them as bf16 (A/B).
+BYTE_COLS = os.environ.get("ATE_GRAM_BYTES", "1") == "1"
 PLAN_CACHE_MAX = int(os.environ.get("ATE_GRAM_PLAN_CACHE", 8))
 
 _plan_cache: dict = {}
@@ -365,10 +370,11 @@ def gram(panel: DevicePanel, w: torch.Tensor | None = None, done: torch.Tensor |
         return pl.Gx if exact else G
     if X.dtype == torch.bfloat16 and pl.pair:
         cs, bs = panel.strides()
+        x8 = getattr(panel, "bytes8", None)
         _native.call("ate_gram_bf16_pair", X.data_ptr(), cs, bs, panel.P, pl.tiles.data_ptr(),
                      pl.ntiles, pl.blocks.data_ptr(), pl.chunks.data_ptr(), pl.nchunks,
                      pl.seg_chunk0.data_ptr(), panel.nseg, pl.slab.data_ptr(), G.data_ptr(),
-                     _STAGES[stage], Gx, s)
+                     _STAGES[stage], Gx, None if x8 is None or not BYTE_COLS else x8.data_ptr(), s)
         return pl.Gx if exact else G
     if stage == "reduce":
         return pl.Gx if exact else G

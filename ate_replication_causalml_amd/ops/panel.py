@@ -50,6 +50,10 @@ class DevicePanel:
     # rows counted from the segment start, the same blocks at every world size
     # (data/device_dgp.fold_slices(align=...)); 0 = not block-aligned
     exact_block: int = 0
+    # one-byte copy of physical columns 384..P-1 when they are all {0, 1}-valued (P = 512
+    # blocked bf16 panels from data/device_dgp.synthetic_panel): [ld/64, 128, 64] uint8, 0x3F
+    # for 1; the paired-tile Gram streams it instead of those bf16 columns (csrc/gram.hip)
+    bytes8: torch.Tensor | None = None
 
     @property
     def P(self):

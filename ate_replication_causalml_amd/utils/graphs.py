@@ -261,7 +261,8 @@ def layout_key(*inputs):
         k = (tuple(t.shape), t.dtype, str(t.device))
         if not isinstance(x, torch.Tensor):
             k += (x.n, tuple(sorted(x.cols.items())), tuple(map(tuple, x.seg_bounds)),
-                  tuple(int(c) for c in x.seg_nreal), bool(getattr(x, "identity", False)))
+                  tuple(int(c) for c in x.seg_nreal), bool(getattr(x, "identity", False)),
+                  getattr(x, "bytes8", None) is not None)
         key.append(k)
     return tuple(key)
 
@@ -280,6 +281,8 @@ class _Captured:
         for s, x in zip(self.inputs, inputs):
             if x is not s and x is not None:
                 _data(s).copy_(_data(x))
+                if getattr(x, "bytes8", None) is not None:      # a panel's one-byte columns
+                    s.bytes8.copy_(x.bytes8)
 
     def __call__(self, inputs):
         self.load(inputs)
@@ -382,6 +385,8 @@ class GraphCache:
                 for s, x in zip(static, inputs):
                     if x is not s and x is not None:
                         _data(s).copy_(_data(x))
+                        if getattr(x, "bytes8", None) is not None:
+                            s.bytes8.copy_(x.bytes8)
                 g = _Captured(body, static, static_args, warmup=1)
             except Exception as e:  # noqa: BLE001 - fall back to eager, but say why
                 print(f"[graphs] {name}: capture failed, running eagerly: {e}", flush=True)

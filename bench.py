@@ -362,7 +362,8 @@ def measure(args, comm, device, dgp, n_total, slot_comms_cache):
         "n_kept": n_total, "n_generated": int(pan.n_generated) * 1,
         "panel_gen_s": t_gen, "hipgraph": graphed, "graphs_per_fit": graphs_per_fit,
         "collectives_captured": collectives_captured,
-        "layout": "blocked64" if pan.blocked else "colmajor",
+        "layout": ("blocked64" if pan.blocked else "colmajor") +
+                  ("+bytes8" if getattr(pan, "bytes8", None) is not None else ""),
         "inflight": inflight_out,
     }
     if world > 1 and pan.selection is not None:

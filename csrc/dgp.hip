@@ -140,10 +140,17 @@ __device__ __forceinline__ void put_d(T* X, int64_t cs, int64_t bs, int c, int64
   else put(X, cs, bs, c, i, (float)v);
 }
 
+// Column c of the generator's order (one, x0..x{p-1}, W, Y[, W_hi, W_lo, Y_hi, Y_lo]) is
+// stored at physical column pcol[c] (null: c). X8 (bf16 panels, data/device_dgp.py): the
+// one-byte copy of physical columns X8_COL0.. (all {0, 1}-valued), [row block][128][64],
+// byte 0x3F for 1 (csrc/gram.hip reads it as bf16 0.5 and scales back).
+constexpr int X8_COL0 = 384;
+
 template <typename T>
 __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64_t row0, int64_t count,
                                 int64_t gid0, const int64_t* __restrict__ gids, uint64_t seed,
-                                int p_extra, int hi_lo, DgpP P) {
+                                int p_extra, int hi_lo, DgpP P, const int16_t* __restrict__ pcol,
+                                uint8_t* __restrict__ X8) {
   const float FL = P.factor_load, FS = P.factor_rest;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < count;
        r += (int64_t)gridDim.x * blockDim.x) {
@@ -152,39 +159,49 @@ __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64
     const Core cr = core_draws(seed, g, P);
     const float f = dgp_normal(seed, 40, g);
     int c = 0;
-    put(X, cs, bs, c++, i, 1.0f);
-    put_d(X, cs, bs, c++, i, cr.yob);
-    put_d(X, cs, bs, c++, i, cr.city);
+    auto phys = [&](int cl) { return pcol != nullptr ? (int)pcol[cl] : cl; };
+    auto emit = [&](float v) {
+      const int pc = phys(c++);
+      put(X, cs, bs, pc, i, v);
+      if (X8 != nullptr && pc >= X8_COL0) {
+        ATE_DASSERT(v == 0.f || v == 1.f);
+        X8[(i >> 6) * (128 * 64) + (pc - X8_COL0) * 64 + (i & 63)] = v != 0.f ? 0x3F : 0;
+      }
+    };
+    emit(1.0f);
+    ATE_DASSERT(phys(1) < X8_COL0 || X8 == nullptr);
+    put_d(X, cs, bs, phys(c++), i, cr.yob);
+    put_d(X, cs, bs, phys(c++), i, cr.city);
     for (int j = 2; j < 15; ++j) {
       float z = dgp_normal(seed, j, g);
-      put(X, cs, bs, c++, i, j < 3 ? z : FL * f + FS * z);
+      emit(j < 3 ? z : FL * f + FS * z);
     }
     const float sex = dgp_uniform(seed, 60, g) < 0.5f ? 1.f : 0.f;
-    put(X, cs, bs, c++, i, sex);
+    emit(sex);
     float hsum = 0.f, hb = 0.f;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const float h = ((cr.hist >> k) & 1) ? 1.f : 0.f;
       hsum += h;
       hb += P.b_hist[k] * h;
-      put(X, cs, bs, c++, i, h);
+      emit(h);
     }
     for (int j = 0; j < p_extra; ++j) {
       float z = dgp_normal(seed, 100 + j, g);
       float v = (j % 4 == 3) ? (z > 0.f ? 1.f : 0.f) : FL * f + FS * z;
-      put(X, cs, bs, c++, i, v);
+      emit(v);
     }
     const float w = cr.w;
     const float hterm = P.uniform_b ? P.b_hist[0] * hsum : hb;
     const float eta = P.intercept + hterm + P.b_latent * (float)cr.latent + P.tau_logit * w;
     const float y = dgp_uniform(seed, 62, g) < 1.0f / (1.0f + expf(-eta)) ? 1.f : 0.f;
-    put(X, cs, bs, c++, i, w);
-    put(X, cs, bs, c++, i, y);
+    emit(w);
+    emit(y);
     if (hi_lo) {  // binary -> hi exact, lo 0
-      put(X, cs, bs, c++, i, w);
-      put(X, cs, bs, c++, i, 0.f);
-      put(X, cs, bs, c++, i, y);
-      put(X, cs, bs, c++, i, 0.f);
+      emit(w);
+      emit(0.f);
+      emit(y);
+      emit(0.f);
     }
   }
 }
@@ -293,22 +310,26 @@ __global__ __launch_bounds__(NT) void sel_gen_mark_kernel(uint64_t seed, DgpP P,
 
 // params: double[18] (data/dgp.py DgpParams.device_block). dtype 1 f32, 2 f64, 3 bf16.
 // gids: optional int64 generated-row ids of the count rows (else gid0 + r).
+// pcol: int16 physical column of each generator column (null: identity); X8: the one-byte
+// copy of physical columns 384..511 (null: none; bf16 panels only).
 ATE_API int ate_dgp_fill(int dtype, void* X, int64_t cs, int64_t bs, int64_t row0, int64_t count,
                          int64_t gid0, const void* gids, uint64_t seed, int p_extra, int hi_lo,
-                         const void* params, void* stream) {
+                         const void* params, const void* pcol, void* X8, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const DgpP P = load_params((const double*)params);
   const int64_t* gl = (const int64_t*)gids;
+  const int16_t* pc = (const int16_t*)pcol;
   dim3 grid(grid_for(count, 256, 8192)), block(256);
+  if (X8 != nullptr && dtype != 3) return -1;
   if (dtype == 1)
     ATE_LAUNCH(dgp_fill_kernel<float>, grid, block, 0, s, (float*)X, cs, bs, row0, count, gid0,
-                       gl, seed, p_extra, hi_lo, P);
+                       gl, seed, p_extra, hi_lo, P, pc, (uint8_t*)nullptr);
   else if (dtype == 2)
     ATE_LAUNCH(dgp_fill_kernel<double>, grid, block, 0, s, (double*)X, cs, bs, row0, count,
-                       gid0, gl, seed, p_extra, hi_lo, P);
+                       gid0, gl, seed, p_extra, hi_lo, P, pc, (uint8_t*)nullptr);
   else if (dtype == 3)
     ATE_LAUNCH(dgp_fill_kernel<bf16_t>, grid, block, 0, s, (bf16_t*)X, cs, bs, row0, count,
-                       gid0, gl, seed, p_extra, hi_lo, P);
+                       gid0, gl, seed, p_extra, hi_lo, P, pc, (uint8_t*)X8);
   else
     return -1;
   ATE_CHECK_LAUNCH();

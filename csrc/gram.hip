@@ -337,12 +337,32 @@ __device__ __forceinline__ void pair_mfma(f32x4* acc, const bf16x8* af, const bf
 // PAIR_RECT_D0 / D1 = the rectangle waves of a diagonal-pair workgroup, halves 0 / 1). Each
 // instantiation keeps only its own accumulators live; every wave runs the same number of
 // barriers.
-template <int MODE>
+// One-byte columns (X8 != null; P == 512): physical columns 384..511 -- tile b's second half,
+// the panel's {0, 1}-valued columns (data/device_dgp.synthetic_panel puts them there) -- are
+// also kept as bytes, [row block][128 columns][64 rows], byte 0x3F for 1. The B image of a
+// stage then holds tile b's columns 0..127 as bf16 and 128..255 as bytes (24 KB instead of
+// 32: a chunk streams 896 instead of 1,024 bytes per row). A byte column's 16-row chunk p
+// sits at slot p ^ ((column >> 2) & 3) (conflict-free ds_read_b64 over 32 lanes); v_perm puts
+// each byte into the high byte of a bf16 (0x3F00 = 0.5), so the MFMA products are exact
+// halves and the slab reduce scales them back by 2 per byte column: the same Gram bits.
+__device__ __forceinline__ bf16x8 bytes_to_bf16x8(uint2 d) {
+  uint4 w;
+  w.x = __builtin_amdgcn_perm(0u, d.x, 0x010C000Cu);
+  w.y = __builtin_amdgcn_perm(0u, d.x, 0x030C020Cu);
+  w.z = __builtin_amdgcn_perm(0u, d.y, 0x010C000Cu);
+  w.w = __builtin_amdgcn_perm(0u, d.y, 0x030C020Cu);
+  return __builtin_bit_cast(bf16x8, w);
+}
+constexpr int PAIR_BYTE0 = 384;   // first one-byte column (P == 512)
+
+// BYTES: the launch streams one-byte columns (X8 != null); BY: this wave's B fragments
+// (rectangle) or all its fragments (triangle) are byte columns.
+template <int MODE, bool BYTES, bool BY>
 __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t cs, int64_t bs, int a0,
                                           int b0, bool haveB, bool idle, int abuf, int bbuf,
                                           int arow0, int bcol0, const Chunk& ch,
                                           bf16_t* lds_raw, float* __restrict__ out,
-                                          bool second) {
+                                          bool second, const uint8_t* __restrict__ X8) {
   constexpr bool TRI = PairRole<MODE>::TRI;
   constexpr int NB = PairRole<MODE>::NB;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -354,6 +374,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
   // 16-byte pieces per column, piece p stored at slot p ^ ((col >> 1) & 3) (8 consecutive
   // lanes of a fragment read hit 8 distinct 16-byte bank groups)
   (void)second;
+  (void)X8;   // one-byte columns: the double-buffered path only
   auto buf = [&](int st, int side) { return lds_raw + (st * 2 + side) * (GT * PKS); };
   auto stage = [&](int st, int64_t i0) {
 #pragma unroll
@@ -409,6 +430,31 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
   const int qw = (GRAM_CROSS == 1 && second) ? ((wid + 4) & 7) : wid;
   const bool bfirst = GRAM_CROSS == 2 && second && haveB;
   auto stage = [&](int st, int64_t i0) {
+    if constexpr (BYTES) {
+      // A: 32 pieces of 8 bf16 columns (4 per wave); B: 16 pieces of its bf16 half (2 per
+      // wave) and 8 pieces of 16 byte columns (1 per wave)
+      const bf16_t* Xk0 = X + (i0 >> 6) * bs;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = wid * 4 + r;
+        const int col = q * 8 + (lane >> 3);
+        const int cc = (lane & 7) ^ (col & 7);
+        glds16(Xk0 + cc * 8 + (int64_t)(a0 + col) * cs, &lds[st][0][q * 8 * GK]);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int q = wid * 2 + r;
+        const int col = q * 8 + (lane >> 3);
+        const int cc = (lane & 7) ^ (col & 7);
+        glds16(Xk0 + cc * 8 + (int64_t)(b0 + col) * cs, &lds[st][1][q * 8 * GK]);
+      }
+      const int cb = wid * 16 + (lane >> 2);                  // byte column 0..127
+      const int pc = (lane & 3) ^ ((cb >> 2) & 3);             // its 16-row chunk this lane moves
+      glds16(X8 + (i0 >> 6) * (128 * GK) + cb * GK + pc * 16,
+             reinterpret_cast<bf16_t*>(reinterpret_cast<uint8_t*>(&lds[st][1][128 * GK]) +
+                                       wid * 1024));
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = qw * 4 + r;
@@ -423,6 +469,15 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
   auto frag = [&](const bf16_t* P_, int col, int cc) {
     return *reinterpret_cast<const bf16x8*>(&P_[col * GK + ((cc ^ (col & 7)) << 3)]);
   };
+  // a byte column's raw fragment (image column col >= 128: byte column col - 128), rows
+  // cc * 8 .. cc * 8 + 7 of the stage (bytes_to_bf16x8: the MFMA operand); frag8 converted
+  auto raw8 = [&](const bf16_t* P_, int col, int cc) {
+    const int cb = col - 128;
+    const uint8_t* b8 = reinterpret_cast<const uint8_t*>(P_ + 128 * GK);
+    const int slot = (cc >> 1) ^ ((cb >> 2) & 3);
+    return *reinterpret_cast<const uint2*>(b8 + cb * GK + slot * 16 + (cc & 1) * 8);
+  };
+  auto frag8 = [&](const bf16_t* P_, int col, int cc) { return bytes_to_bf16x8(raw8(P_, col, cc)); };
   const int64_t nsteps = (ch.row1 - ch.row0) / GK;
   if (nsteps > 0) stage(0, ch.row0);
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
@@ -438,7 +493,69 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
     // every fragment of the stage (both 32-row halves) read from LDS up front, then the
     // MFMAs: the waits on LDS leave the MFMA chains of the stage
     if (!idle && GRAM_DIAG != 1 && GRAM_DIAG != 3) {
-      if constexpr (!TRI) {
+      if constexpr (BY && !TRI) {
+        // byte B fragments: read raw for both halves (2 VGPRs each), converted per half just
+        // ahead of its MFMAs; the second half's conversion interleaved with the first half's
+        // MFMAs (mask 0x002 VALU)
+        bf16x8 af[2][8];
+        uint2 braw[2][4];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int cc = kk * 4 + (lane >> 4);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) af[kk][m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) braw[kk][n] = raw8(Bs, bcol0 + n * 16 + (lane & 15), cc);
+        }
+        bf16x8 b0v[4], b1v[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) b0v[n] = bytes_to_bf16x8(braw[0][n]);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) b1v[n] = bytes_to_bf16x8(braw[1][n]);
+        pair_mfma<MODE>(acc, af[0], b0v);
+        pair_mfma<MODE>(acc, af[1], b1v);
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);     // half 0 reads
+        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);     // half 0 conversion
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {                          // half 1 reads beside
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // half 0's MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {                          // half 1 conversion beside
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // the next MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 28, 0);
+      } else if constexpr (BY) {
+        uint2 fraw[2][8];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int cc = kk * 4 + (lane >> 4);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) fraw[kk][m] = raw8(As, arow0 + m * 16 + (lane & 15), cc);
+        }
+        bf16x8 f0[8], f1[8];
+#pragma unroll
+        for (int m = 0; m < 8; ++m) f0[m] = bytes_to_bf16x8(fraw[0][m]);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) f1[m] = bytes_to_bf16x8(fraw[1][m]);
+        pair_mfma<MODE>(acc, f0, f0);
+        pair_mfma<MODE>(acc, f1, f1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 24, 0);
+      } else if constexpr (!TRI) {
         bf16x8 af[2][8], bfr[2][4];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -488,12 +605,16 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
 #pragma unroll
           for (int m = 0; m < 8; ++m) af[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
 #pragma unroll
-          for (int n = 0; n < 4; ++n) bfr[n] = frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
+          for (int n = 0; n < 4; ++n)
+            bfr[n] = BY ? frag8(Bs, bcol0 + n * 16 + (lane & 15), cc)
+                        : frag(Bs, bcol0 + n * 16 + (lane & 15), cc);
           pair_mfma<MODE>(acc, af, bfr);
         } else {
           bf16x8 fr[8];
 #pragma unroll
-          for (int m = 0; m < 8; ++m) fr[m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
+          for (int m = 0; m < 8; ++m)
+            fr[m] = BY ? frag8(As, arow0 + m * 16 + (lane & 15), cc)
+                       : frag(As, arow0 + m * 16 + (lane & 15), cc);
           pair_mfma<MODE>(acc, fr, fr);
         }
       }
@@ -528,9 +649,11 @@ extern "C" __attribute__((visibility("default"))) int ate_gram_clock_reset() {
 }
 #endif
 
+template <bool BYTES>
 __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
     const bf16_t* __restrict__ X, int64_t cs, int64_t bs, const int4* __restrict__ tiles, int ntiles,
-    const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab) {
+    const Chunk* __restrict__ chunks, int nchunks, float* __restrict__ slab,
+    const uint8_t* __restrict__ X8) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[PAIR_LDS];   // 128 KB (ring: up to 160)
 #ifdef GRAM_CLOCK
   const unsigned long long gc0 = clock64(), gw0 = wall_clock64();
@@ -573,14 +696,17 @@ __global__ __launch_bounds__(512) void gram_bf16_pair_kernel(
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
 #endif
 #endif
-  if (tri)
-    pair_wave<PAIR_TRI>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, true);
-  else if (type == 0)
-    pair_wave<PAIR_RECT>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, false);
-  else if (half == 0)
-    pair_wave<PAIR_RECT_D0>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, true);
-  else
-    pair_wave<PAIR_RECT_D1>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, bcol0, ch, lds, out, true);
+  // byte fragments: tile b's columns 128..255 (type 0: the waves of B columns 128..255;
+  // type 1, tile b: the rectangle waves' B and the second triangle)
+  const bool by = BYTES && (type == 0 ? (wid & 3) >= 2 : region == 1 && (!tri || half == 1));
+  ATE_DASSERT(!BYTES || (X8 != nullptr && ntiles == 2 && b0 == 256));
+#define PAIR_WAVE(M, B) pair_wave<M, BYTES, B>(X, cs, bs, a0, b0, haveB, idle, abuf, bbuf, arow0, \
+                                               bcol0, ch, lds, out, type != 0, X8)
+  if (tri) { if (by) PAIR_WAVE(PAIR_TRI, BYTES); else PAIR_WAVE(PAIR_TRI, false); }
+  else if (type == 0) { if (by) PAIR_WAVE(PAIR_RECT, BYTES); else PAIR_WAVE(PAIR_RECT, false); }
+  else if (half == 0) { if (by) PAIR_WAVE(PAIR_RECT_D0, BYTES); else PAIR_WAVE(PAIR_RECT_D0, false); }
+  else { if (by) PAIR_WAVE(PAIR_RECT_D1, BYTES); else PAIR_WAVE(PAIR_RECT_D1, false); }
+#undef PAIR_WAVE
 #ifdef GRAM_CLOCK
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -813,10 +939,12 @@ __device__ __forceinline__ void gram_limbs(double v, long long& hi, long long& l
 // blocks: [ntiles][PAIR_SLOTS] int2 (I, J) = 16-column block coordinates of the Gram (I: A
 // side = row), (-1, -1) = unused slot. Blocks with I == J are full 16x16 diagonal blocks: only
 // their r <= c entries are written (plus mirror), so every Gram entry has ONE writer.
+// byte0: first one-byte column (their slab partials are halves: scaled back by 2 per byte
+// column, exactly), P when there are none.
 __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const int2* __restrict__ blocks,
                                         int ntiles, int slots, const int* __restrict__ seg_chunk0,
                                         int nseg, int P, double* __restrict__ G,
-                                        long long* __restrict__ Gx) {
+                                        long long* __restrict__ Gx, int byte0) {
   const int64_t per = (int64_t)ntiles * slots * 256;
   const int64_t total = (int64_t)nseg * per;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
@@ -834,6 +962,7 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
     const float* src = slab + rem;
     const int a = bl.x * 16 + r, b = bl.y * 16 + cl;
     ATE_DASSERT(s < nseg && c0 >= 0 && c0 <= c1 && a >= 0 && a < P && b >= 0 && b < P);
+    const double sc = (a >= byte0 ? 2.0 : 1.0) * (b >= byte0 ? 2.0 : 1.0);
     if (Gx) {                                       // exact mode: int64 limbs
       long long hs = 0, ls = 0;
       int ci = c0;
@@ -844,14 +973,14 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           long long h, l;
-          gram_limbs((double)v[u], h, l);
+          gram_limbs((double)v[u] * sc, h, l);
           hs += h;
           ls += l;
         }
       }
       for (; ci < c1; ++ci) {
         long long h, l;
-        gram_limbs((double)src[(int64_t)ci * per], h, l);
+        gram_limbs((double)src[(int64_t)ci * per] * sc, h, l);
         hs += h;
         ls += l;
       }
@@ -873,36 +1002,46 @@ __global__ void gram_pair_reduce_kernel(const float* __restrict__ slab, const in
       for (int u = 0; u < 8; ++u) acc += (double)v[u];
     }
     for (; ci < c1; ++ci) acc += (double)src[(int64_t)ci * per];
+    acc *= sc;
     double* Gs = G + (int64_t)s * P * P;
     Gs[(int64_t)a * P + b] = acc;
     Gs[(int64_t)b * P + a] = acc;
   }
 }
 
-ATE_KERNEL_SHAPE("gram_bf16_pair_kernel", 512, 0, gram_bf16_pair_kernel)
+ATE_KERNEL_SHAPE("gram_bf16_pair_kernel", 512, 0, gram_bf16_pair_kernel<false>)
+ATE_KERNEL_SHAPE("gram_bf16_pair_kernel<bytes>", 512, 0, gram_bf16_pair_kernel<true>)
 ATE_KERNEL_SHAPE("gram_bf16_tri_kernel", 512, 0, gram_bf16_tri_kernel)
 ATE_KERNEL_SHAPE("gram_bf16_256_kernel", 512, 0, gram_bf16_256_kernel)
 ATE_KERNEL_SHAPE("gram_bf16_kernel", 256, 0, gram_bf16_kernel)
 
 // what: 1 = tile kernel (slab partials), 2 = fixed-order slab reduce into G, 3 = both.
 // Split so a caller can run the reduce on another stream than the next tile kernel.
+// X8: the one-byte copies of columns 384..511 (P == 512 only), or null.
 ATE_API int ate_gram_bf16_pair(const void* X, int64_t cs, int64_t bs, int P, const void* tiles, int ntiles,
                                const void* blocks, const void* chunks, int nchunks,
                                const void* seg_chunk0, int nseg, void* slab, void* G, int what,
-                               void* Gx, void* stream) {
+                               void* Gx, const void* X8, void* stream) {
   if (P % (2 * GT) || what < 1 || what > 3) return -1;
+  if (X8 != nullptr && (P != 512 || ntiles != 2 || GRAM_RING)) return -1;
   hipStream_t s = (hipStream_t)stream;
   if (what & 1) {
-  ATE_LAUNCH(gram_bf16_pair_kernel, dim3(nchunks * ntiles), dim3(512), 0, s,
-                     (const bf16_t*)X, cs, bs, (const int4*)tiles, ntiles, (const Chunk*)chunks,
-                     nchunks, (float*)slab);
+  if (X8 != nullptr)
+    ATE_LAUNCH(gram_bf16_pair_kernel<true>, dim3(nchunks * ntiles), dim3(512), 0, s,
+               (const bf16_t*)X, cs, bs, (const int4*)tiles, ntiles, (const Chunk*)chunks,
+               nchunks, (float*)slab, (const uint8_t*)X8);
+  else
+    ATE_LAUNCH(gram_bf16_pair_kernel<false>, dim3(nchunks * ntiles), dim3(512), 0, s,
+               (const bf16_t*)X, cs, bs, (const int4*)tiles, ntiles, (const Chunk*)chunks,
+               nchunks, (float*)slab, (const uint8_t*)nullptr);
   ATE_CHECK_LAUNCH();
   }
   if (what & 2) {
     const int64_t total = (int64_t)nseg * ntiles * PAIR_SLOTS * 256;
     ATE_LAUNCH(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                        (const float*)slab, (const int2*)blocks, ntiles, PAIR_SLOTS,
-                       (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx);
+                       (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx,
+                       X8 != nullptr ? PAIR_BYTE0 : P);
     ATE_CHECK_LAUNCH();
   }
   return 0;
@@ -927,7 +1066,7 @@ ATE_API int ate_gram_bf16_tri(const void* X, int64_t cs, int64_t bs, int P, cons
     const int64_t total = (int64_t)nseg * 2 * TRI_SLOTS * 256;
     ATE_LAUNCH(gram_pair_reduce_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s,
                        (const float*)slab, (const int2*)blocks, 2, TRI_SLOTS,
-                       (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx);
+                       (const int*)seg_chunk0, nseg, P, (double*)G, (long long*)Gx, P);
     ATE_CHECK_LAUNCH();
   }
   return 0;

@@ -102,6 +102,60 @@ def test_gram_tri_kernel_vs_pair(gpu, monkeypatch, blocked):
     assert torch.equal(Gt, Gt.transpose(1, 2))
 
 
+def test_byte_columns_gram_same_bits(gpu, monkeypatch):
+    """One-byte columns (data/device_dgp.synthetic_panel: the {0, 1} columns in physical
+    columns 384..511 plus a byte copy; csrc/gram.hip streams the copy as bf16 halves and the
+    reduce scales back): the Gram equals the all-bf16 read BIT FOR BIT (default and exact
+    mode), the byte copy holds exactly the panel's columns, and the DML-ATE is unchanged."""
+    from ate_replication_causalml_amd.data import device_dgp
+    from ate_replication_causalml_amd.data.device_dgp import BYTE_COL0, synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    monkeypatch.setattr(device_dgp, "BYTE_PANEL", True)
+    pan = synthetic_panel(40000, p=500, folds=5, seed=5, dtype="bf16", blocked=True,
+                          device=gpu, dgp="tutorial", align=4096)
+    assert pan.P == 512 and pan.bytes8 is not None
+    Xc = pan.colmajor()
+    b = pan.bytes8.permute(1, 0, 2).reshape(512 - BYTE_COL0, -1)
+    assert torch.equal(b, (Xc[BYTE_COL0:] != 0).to(torch.uint8) * 0x3F)
+    assert torch.all((Xc[BYTE_COL0:] == 0) | (Xc[BYTE_COL0:] == 1))
+    res = {}
+    for on in (True, False):
+        monkeypatch.setattr(gram_op, "BYTE_COLS", on)
+        gram_op._plan_cache.clear()
+        G = gram_op.gram(pan).clone()
+        GX = gram_op.gram(pan, exact=True).clone()
+        r, _, _ = dml_crossfit_panel(pan, 5)
+        res[on] = (G, GX, r.cpu())
+    gram_op._plan_cache.clear()
+    assert torch.equal(res[True][0], res[False][0])
+    assert torch.equal(res[True][1], res[False][1])
+    assert torch.equal(res[True][2], res[False][2])
+    ref = gram_op.gram_reference(pan).to(gpu)
+    assert ((res[True][0] - ref).abs().max() / ref.abs().max()) < 2e-6
+
+
+def test_byte_column_order_matches_generator_order(gpu, monkeypatch):
+    """The byte panel's physical column order only relabels columns: its DML-ATE equals the
+    generator-order panel's (the default, ATE_PANEL_BYTES=0) to rounding, and every named column holds the
+    same values."""
+    from ate_replication_causalml_amd.data import device_dgp
+    from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel
+    kw = dict(p=500, folds=5, seed=9, dtype="bf16", blocked=True, device=gpu, dgp="tutorial")
+    monkeypatch.setattr(device_dgp, "BYTE_PANEL", True)
+    a = device_dgp.synthetic_panel(30000, **kw)
+    monkeypatch.setattr(device_dgp, "BYTE_PANEL", False)
+    b = device_dgp.synthetic_panel(30000, **kw)
+    assert a.bytes8 is not None and b.bytes8 is None and a.cols != b.cols
+    Xa, Xb = a.colmajor(), b.colmajor()
+    for nm in ("x0", "x15", "x24", "x499", "W", "Y", "W_hi", "Y_lo", "one"):
+        assert torch.equal(Xa[a.cols[nm]], Xb[b.cols[nm]]), nm
+    ra = dml_crossfit_panel(a, 5)[0].cpu()
+    gram_op._plan_cache.clear()
+    rb = dml_crossfit_panel(b, 5)[0].cpu()
+    gram_op._plan_cache.clear()
+    assert torch.allclose(ra, rb, rtol=1e-9, atol=1e-12), (ra, rb)
+
+
 def test_invalid_launch_is_named(gpu):
     """A launch the runtime refuses (2,048 work-items per block) surfaces as NativeError
     with the HIP error's name, the entry point and the launch site (csrc/errors.hip), and
@@ -417,3 +471,22 @@ def test_bench_eager_gram_matches_graph_gram(gpu):
         assert inf["rel_diff_se_vs_single"] <= 1e-4
         out[eg] = (inf["ate_hex"], inf["se_hex"])
     assert out["0"] == out["1"]
+
+
+def test_repeated_dml_gpu_matches_host_and_graph(gpu):
+    """Repeated cross-fitting (3 partitions from one 25-segment Gram pass) on the GPU: equal
+    to the host run of the same device pipeline, and its captured-graph replays (2nd and
+    3rd call) equal the eager first call."""
+    from ate_replication_causalml_amd.estimators import lasso as L
+    rs = np.random.RandomState(8)
+    n, p = 6000, 30
+    X = rs.randn(n, p)
+    W = (rs.rand(n) < 1 / (1 + np.exp(-X[:, 0]))).astype(float)
+    Y = X[:, 1] + 0.5 * W + rs.randn(n)
+    c = L.dml_plr_lasso_repeated(Y, W, X, 5, 3, device="cpu")
+    outs = [L.dml_plr_lasso_repeated(Y, W, X, 5, 3, device=gpu) for _ in range(3)]
+    assert [o.diagnostics["hipgraph"] for o in outs] == [False, True, True]
+    for o in outs:
+        assert o.ate == pytest.approx(c.ate, rel=1e-9) and o.se == pytest.approx(c.se, rel=1e-9)
+        np.testing.assert_allclose(o.diagnostics["splits"], c.diagnostics["splits"], rtol=1e-9)
+    assert outs[1].ate == outs[0].ate and outs[2].se == outs[0].se

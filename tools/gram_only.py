@@ -7,6 +7,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from ate_replication_causalml_amd.data.device_dgp import synthetic_panel  # noqa: E402
+from ate_replication_causalml_amd.data import device_dgp  # noqa: E402
+
+device_dgp.BYTE_PANEL = True      # the byte copy, so that pair / pair16 A/B both run
 from ate_replication_causalml_amd.ops import gram as gram_mod  # noqa: E402
 
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else int(1e7)
@@ -18,8 +21,9 @@ ref = None
 stage = os.environ.get("ATE_GRAM_STAGE", "all")   # "tiles": the tile kernel alone (no slab reduce)
 for v in variants:
     # "tri": the split-triangle kernel (P == 512); "pair": the paired-tile kernel
-    gram_mod.GRAM_KERNEL = "pair" if v == "tri" else v
+    gram_mod.GRAM_KERNEL = "pair" if v in ("tri", "pair16") else v
     gram_mod.GRAM_TRI = v == "tri"
+    gram_mod.BYTE_COLS = v != "pair16"      # pair16: the panel's byte columns read as bf16
     gram_mod._plan_cache.clear()
     for _ in range(3):
         G = gram_mod.gram(pan)

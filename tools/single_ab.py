@@ -1,7 +1,7 @@
 """A/B of the single ate_dml call (bench.py's timed step) over Gram kernels on ONE panel:
 the panel is generated once, each variant's step is captured and timed in alternation
 (K calls back to back, R rounds), so box-to-box and clock drift cancel out.
-Usage: single_ab.py [tri,pair] [rounds] [calls]   (variants: tri | pair)"""
+Usage: single_ab.py [tri,pair] [rounds] [calls]   (variants: tri | pair | pair16)"""
 import os
 import sys
 import time
@@ -10,6 +10,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from ate_replication_causalml_amd.data.device_dgp import synthetic_panel  # noqa: E402
+from ate_replication_causalml_amd.data import device_dgp  # noqa: E402
+
+device_dgp.BYTE_PANEL = True      # the byte copy, so that pair / pair16 A/B both run
 from ate_replication_causalml_amd.estimators.lasso import dml_phases, global_seg_counts  # noqa: E402
 from ate_replication_causalml_amd.ops import gram as gram_mod  # noqa: E402
 from ate_replication_causalml_amd.parallel.comm import LocalComm  # noqa: E402
@@ -23,14 +26,20 @@ pan = synthetic_panel(int(1e7), p=500, folds=5, seed=1991, dtype="bf16", blocked
                       dgp=os.environ.get("ATE_DGP", "tutorial"))
 seg = global_seg_counts(pan, LocalComm())
 steps = {}
-for i, v in enumerate(variants):
+def _select(v):
     gram_mod.GRAM_TRI = v == "tri"
+    gram_mod.BYTE_COLS = v != "pair16"      # pair16: the byte columns read as bf16
+
+
+for i, v in enumerate(variants):
+    _select(v)
     with gram_mod.plan_slot(10 + i):
         steps[v] = SegmentedStep(dml_phases(pan, 5, "min", seg_counts=seg), graph=True)
 times = {v: [] for v in variants}
 res = {}
 for r in range(rounds):
     for v in variants:
+        _select(v)      # the captured steps launch with their own settings; eager kept in sync
         for _ in range(3):
             steps[v]()
         torch.cuda.synchronize()
