@@ -59,11 +59,10 @@ def fold_slices(n_total: int, folds: int, rank: int = 0, world: int = 1, align: 
 # extra covariate, W, Y and their hi / lo halves, padding) in physical columns 384..511 and a
 # one-byte copy of those 128 columns beside the panel (DevicePanel.bytes8). Estimators see
 # the same names -> columns map (pan.cols / pan.xcols); the Gram streams 896 instead of
-# 1,024 bytes per row. Measured slower than the all-bf16 read (profiles/r06_gram/README.md:
-# 4.79 vs 4.64 ms per ate_dml call), so it is opt-in: ATE_PANEL_BYTES=1. Off: the
-# generator's column order, no byte copy.
+# 1,024 bytes per row (profiles/r06_gram/README.md: 4.47 vs 4.54 ms per ate_dml call, the
+# same bits). ATE_PANEL_BYTES=0: the generator's column order, no byte copy.
 BYTE_COL0 = 384
-BYTE_PANEL = os.environ.get("ATE_PANEL_BYTES", "0") == "1"
+BYTE_PANEL = os.environ.get("ATE_PANEL_BYTES", "1") == "1"
 
 
 def _binary_names(p: int) -> set:

@@ -143,8 +143,14 @@ __device__ __forceinline__ void put_d(T* X, int64_t cs, int64_t bs, int c, int64
 // Column c of the generator's order (one, x0..x{p-1}, W, Y[, W_hi, W_lo, Y_hi, Y_lo]) is
 // stored at physical column pcol[c] (null: c). X8 (bf16 panels, data/device_dgp.py): the
 // one-byte copy of physical columns X8_COL0.. (all {0, 1}-valued), [row block][128][64],
-// byte 0x3F for 1 (csrc/gram.hip reads it as bf16 0.5 and scales back).
+// byte 0x3F for 1 (csrc/gram.hip reads it as bf16 0.5 and scales back). Inside a column's
+// 64 bytes, 16-byte piece q holds rows 8q..8q+7 then 32+8q..32+8q+7: the two 8-row groups
+// one MFMA lane needs from a 64-row stage, so the Gram reads both with one ds_read_b128.
 constexpr int X8_COL0 = 384;
+__device__ __forceinline__ int x8_pos(int64_t i) {
+  const int r = (int)(i & 63);
+  return ((r >> 3) & 3) * 16 + (r >> 5) * 8 + (r & 7);
+}
 
 template <typename T>
 __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64_t row0, int64_t count,
@@ -165,7 +171,7 @@ __global__ void dgp_fill_kernel(T* __restrict__ X, int64_t cs, int64_t bs, int64
       put(X, cs, bs, pc, i, v);
       if (X8 != nullptr && pc >= X8_COL0) {
         ATE_DASSERT(v == 0.f || v == 1.f);
-        X8[(i >> 6) * (128 * 64) + (pc - X8_COL0) * 64 + (i & 63)] = v != 0.f ? 0x3F : 0;
+        X8[(i >> 6) * (128 * 64) + (pc - X8_COL0) * 64 + x8_pos(i)] = v != 0.f ? 0x3F : 0;
       }
     };
     emit(1.0f);

@@ -341,10 +341,12 @@ __device__ __forceinline__ void pair_mfma(f32x4* acc, const bf16x8* af, const bf
 // the panel's {0, 1}-valued columns (data/device_dgp.synthetic_panel puts them there) -- are
 // also kept as bytes, [row block][128 columns][64 rows], byte 0x3F for 1. The B image of a
 // stage then holds tile b's columns 0..127 as bf16 and 128..255 as bytes (24 KB instead of
-// 32: a chunk streams 896 instead of 1,024 bytes per row). A byte column's 16-row chunk p
-// sits at slot p ^ ((column >> 2) & 3) (conflict-free ds_read_b64 over 32 lanes); v_perm puts
-// each byte into the high byte of a bf16 (0x3F00 = 0.5), so the MFMA products are exact
-// halves and the slab reduce scales them back by 2 per byte column: the same Gram bits.
+// 32: a chunk streams 896 instead of 1,024 bytes per row). A byte column's 16-byte piece q
+// (rows 8q..8q+7 and 32+8q..32+8q+7, csrc/dgp.hip x8_pos) sits at slot q ^ ((column >> 1) & 2):
+// lane l reads both MFMA halves' rows of its column with one ds_read_b128, conflict-free over
+// that instruction's 16-lane groups. v_perm puts each byte into the high byte of a bf16
+// (0x3F00 = 0.5), so the MFMA products are exact halves and the slab reduce scales them back
+// by 2 per byte column: the same Gram bits.
 __device__ __forceinline__ bf16x8 bytes_to_bf16x8(uint2 d) {
   uint4 w;
   w.x = __builtin_amdgcn_perm(0u, d.x, 0x010C000Cu);
@@ -449,7 +451,7 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
         glds16(Xk0 + cc * 8 + (int64_t)(b0 + col) * cs, &lds[st][1][q * 8 * GK]);
       }
       const int cb = wid * 16 + (lane >> 2);                  // byte column 0..127
-      const int pc = (lane & 3) ^ ((cb >> 2) & 3);             // its 16-row chunk this lane moves
+      const int pc = (lane & 3) ^ ((cb >> 1) & 2);             // its 16-byte piece this lane moves
       glds16(X8 + (i0 >> 6) * (128 * GK) + cb * GK + pc * 16,
              reinterpret_cast<bf16_t*>(reinterpret_cast<uint8_t*>(&lds[st][1][128 * GK]) +
                                        wid * 1024));
@@ -469,15 +471,21 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
   auto frag = [&](const bf16_t* P_, int col, int cc) {
     return *reinterpret_cast<const bf16x8*>(&P_[col * GK + ((cc ^ (col & 7)) << 3)]);
   };
-  // a byte column's raw fragment (image column col >= 128: byte column col - 128), rows
-  // cc * 8 .. cc * 8 + 7 of the stage (bytes_to_bf16x8: the MFMA operand); frag8 converted
-  auto raw8 = [&](const bf16_t* P_, int col, int cc) {
+  // a byte column's raw fragments (image column col >= 128: byte column col - 128): both
+  // halves of the stage for lane l, rows 8r..8r+7 (.xy) and 32+8r..32+8r+7 (.zw), r = l >> 4.
+  // (Round 6 first read each half with its own ds_read_b64 from a 16-row-chunk layout; the
+  // compiler paired those into ds_read2st64_b64, which banks mod 32 over 16 lanes: 4e7
+  // conflict cycles per launch, profiles/r06_pmc.)
+  auto raw16 = [&](const bf16_t* P_, int col) {
     const int cb = col - 128;
     const uint8_t* b8 = reinterpret_cast<const uint8_t*>(P_ + 128 * GK);
-    const int slot = (cc >> 1) ^ ((cb >> 2) & 3);
-    return *reinterpret_cast<const uint2*>(b8 + cb * GK + slot * 16 + (cc & 1) * 8);
+    const int slot = (lane >> 4) ^ ((cb >> 1) & 2);
+    return *reinterpret_cast<const uint4*>(b8 + cb * GK + slot * 16);
   };
-  auto frag8 = [&](const bf16_t* P_, int col, int cc) { return bytes_to_bf16x8(raw8(P_, col, cc)); };
+  auto frag8 = [&](const bf16_t* P_, int col, int cc) {
+    const uint4 w = raw16(P_, col);
+    return bytes_to_bf16x8(cc >= 4 ? make_uint2(w.z, w.w) : make_uint2(w.x, w.y));
+  };
   const int64_t nsteps = (ch.row1 - ch.row0) / GK;
   if (nsteps > 0) stage(0, ch.row0);
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
@@ -494,30 +502,30 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
     // MFMAs: the waits on LDS leave the MFMA chains of the stage
     if (!idle && GRAM_DIAG != 1 && GRAM_DIAG != 3) {
       if constexpr (BY && !TRI) {
-        // byte B fragments: read raw for both halves (2 VGPRs each), converted per half just
-        // ahead of its MFMAs; the second half's conversion interleaved with the first half's
-        // MFMAs (mask 0x002 VALU)
+        // byte B fragments: one 16-byte read per column holds both halves' rows, converted
+        // per half just ahead of its MFMAs; the second half's conversion interleaved with the
+        // first half's MFMAs (mask 0x002 VALU)
         bf16x8 af[2][8];
-        uint2 braw[2][4];
+        uint4 braw[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) braw[n] = raw16(Bs, bcol0 + n * 16 + (lane & 15));
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
           const int cc = kk * 4 + (lane >> 4);
 #pragma unroll
           for (int m = 0; m < 8; ++m) af[kk][m] = frag(As, arow0 + m * 16 + (lane & 15), cc);
-#pragma unroll
-          for (int n = 0; n < 4; ++n) braw[kk][n] = raw8(Bs, bcol0 + n * 16 + (lane & 15), cc);
         }
         bf16x8 b0v[4], b1v[4];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) b0v[n] = bytes_to_bf16x8(braw[0][n]);
+        for (int n = 0; n < 4; ++n) b0v[n] = bytes_to_bf16x8(make_uint2(braw[n].x, braw[n].y));
 #pragma unroll
-        for (int n = 0; n < 4; ++n) b1v[n] = bytes_to_bf16x8(braw[1][n]);
+        for (int n = 0; n < 4; ++n) b1v[n] = bytes_to_bf16x8(make_uint2(braw[n].z, braw[n].w));
         pair_mfma<MODE>(acc, af[0], b0v);
         pair_mfma<MODE>(acc, af[1], b1v);
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);     // half 0 reads
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);     // B (both halves) + A half 0
         __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);     // half 0 conversion
 #pragma unroll
-        for (int i = 0; i < 12; ++i) {                          // half 1 reads beside
+        for (int i = 0; i < 8; ++i) {                           // A half 1 reads beside
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // half 0's MFMAs
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
@@ -526,35 +534,26 @@ __device__ __forceinline__ void pair_wave(const bf16_t* __restrict__ X, int64_t 
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // the next MFMAs
           __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 28, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 24, 0);
       } else if constexpr (BY) {
-        uint2 fraw[2][8];
+        uint4 fraw[8];
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int cc = kk * 4 + (lane >> 4);
-#pragma unroll
-          for (int m = 0; m < 8; ++m) fraw[kk][m] = raw8(As, arow0 + m * 16 + (lane & 15), cc);
-        }
+        for (int m = 0; m < 8; ++m) fraw[m] = raw16(As, arow0 + m * 16 + (lane & 15));
         bf16x8 f0[8], f1[8];
 #pragma unroll
-        for (int m = 0; m < 8; ++m) f0[m] = bytes_to_bf16x8(fraw[0][m]);
+        for (int m = 0; m < 8; ++m) f0[m] = bytes_to_bf16x8(make_uint2(fraw[m].x, fraw[m].y));
 #pragma unroll
-        for (int m = 0; m < 8; ++m) f1[m] = bytes_to_bf16x8(fraw[1][m]);
+        for (int m = 0; m < 8; ++m) f1[m] = bytes_to_bf16x8(make_uint2(fraw[m].z, fraw[m].w));
         pair_mfma<MODE>(acc, f0, f0);
         pair_mfma<MODE>(acc, f1, f1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);      // both halves' reads
+        __builtin_amdgcn_sched_group_barrier(0x002, 32, 0);     // half 0 conversion
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        for (int i = 0; i < 16; ++i) {                          // half 1 conversion beside
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // half 0's MFMAs
           __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 24, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB - 16, 0);
       } else if constexpr (!TRI) {
         bf16x8 af[2][8], bfr[2][4];
 #pragma unroll

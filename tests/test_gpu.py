@@ -115,7 +115,10 @@ def test_byte_columns_gram_same_bits(gpu, monkeypatch):
                           device=gpu, dgp="tutorial", align=4096)
     assert pan.P == 512 and pan.bytes8 is not None
     Xc = pan.colmajor()
-    b = pan.bytes8.permute(1, 0, 2).reshape(512 - BYTE_COL0, -1)
+    r = torch.arange(64, device=gpu)                 # byte position of row r (csrc/dgp.hip x8_pos)
+    pos = ((r >> 3) & 3) * 16 + (r >> 5) * 8 + (r & 7)
+    assert torch.equal(torch.sort(pos).values, r)
+    b = pan.bytes8[:, :, pos].permute(1, 0, 2).reshape(512 - BYTE_COL0, -1)
     assert torch.equal(b, (Xc[BYTE_COL0:] != 0).to(torch.uint8) * 0x3F)
     assert torch.all((Xc[BYTE_COL0:] == 0) | (Xc[BYTE_COL0:] == 1))
     res = {}
@@ -136,7 +139,7 @@ def test_byte_columns_gram_same_bits(gpu, monkeypatch):
 
 def test_byte_column_order_matches_generator_order(gpu, monkeypatch):
     """The byte panel's physical column order only relabels columns: its DML-ATE equals the
-    generator-order panel's (the default, ATE_PANEL_BYTES=0) to rounding, and every named column holds the
+    generator-order panel's (ATE_PANEL_BYTES=0) to rounding, and every named column holds the
     same values."""
     from ate_replication_causalml_amd.data import device_dgp
     from ate_replication_causalml_amd.estimators.lasso import dml_crossfit_panel

@@ -10,6 +10,7 @@ step() { local n=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$n.log" 2
 for s in "$@"; do
   case $s in
     tests) step tests 1200 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
+    testsall) step testsall 1200 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread ;;
     debugtests) ATE_DEBUG=1 step debugtests 1200 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
     bench) step bench 400 python -u bench.py ;;
     smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
