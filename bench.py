@@ -83,6 +83,10 @@ def parse():
     # the BASELINE config and rows/s measures the data-parallel design. The CV-LASSO
     # path solve is O(p^2 * lambdas) and independent of N, so at a fixed total N it is
     # an Amdahl term every rank repeats (use --scaling strong to measure that).
+    ap.add_argument("--repeats", type=int, default=3,
+                    help="> 1 (world 1): also time ate_dml(repeats=S) -- S distinct K-fold "
+                         "partitions of K*K micro-segments from one Gram pass, median-aggregated "
+                         "(JSON key 'repeated'; secondary, not the metric of record)")
     ap.add_argument("--scaling", default="weak", choices=["strong", "weak"])
     ap.add_argument("--seed", type=int, default=1991)
     ap.add_argument("--graph", type=int, default=-1,
@@ -372,6 +376,49 @@ def measure(args, comm, device, dgp, n_total, slot_comms_cache):
     return out, pan, seg_counts
 
 
+def measure_repeated(args, comm, device, n_total, selection):
+    """Repeated cross-fitting (estimators/lasso.dml_repeated_phases; Chernozhukov et al. 2018
+    §3.4): the same kept rows in K*K micro-segments, ONE captured call = one Gram pass, S
+    partitions' CV-LASSO paths and residual passes, the median aggregate. Timed like the
+    main step (min(steps, 10) calls back to back after the warmup). Secondary: its
+    fits_rows_per_s counts S fits per call, and the S split ATEs differ (distinct work)."""
+    import torch
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.lasso import (dml_repeated_phases,
+                                                               global_seg_counts)
+    from ate_replication_causalml_amd.ops.gram import plan_slot
+    from ate_replication_causalml_amd.utils.graphs import SegmentedStep
+    K, S = args.folds, args.repeats
+    pan = synthetic_panel(n_total, p=args.p, folds=K * K, seed=args.seed, dtype=args.dtype,
+                          blocked=bool(args.blocked) and args.dtype == "bf16", device=device,
+                          dgp=args.dgp, selection=selection)
+    seg = global_seg_counts(pan, comm)
+    use_graph = device.type == "cuda" if args.graph < 0 else bool(args.graph)
+    with plan_slot(0):
+        step = SegmentedStep(dml_repeated_phases(pan, K, S, "min", seg_counts=seg),
+                             graph=use_graph)
+    for _ in range(args.warmup):
+        st = step()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    n = max(1, min(args.steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st = step()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / n * 1e3
+    ate, se = [float(v) for v in st["res"].detach().cpu()]
+    splits = [[float(a), float(b)] for a, b in st["splits"].detach().cpu()]
+    out = {"repeats": S, "folds": K, "micro_segments": K * K, "aggregate": "median",
+           "ms_per_call": ms, "rows_per_s": n_total / (ms / 1e3),
+           "fits_rows_per_s": S * n_total / (ms / 1e3), "ate": ate, "se": se,
+           "splits": splits, "splits_distinct": len({a for a, _ in splits}) == S,
+           "hipgraph": bool(step.graphed), "calls_timed": n}
+    del step, pan
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -429,6 +476,11 @@ def main():
                   "tolerance": "|dATE| <= 0.01 SE_f64 and |dSE| <= 1e-3 SE_f64",
                   "seconds": time.perf_counter() - t2}
         del pan64
+        clear_plans()
+    repeated = None
+    if args.repeats > 1 and world == 1 and not emulate:
+        clear_plans()
+        repeated = measure_repeated(args, comm, device, n_total, pan.selection)
         clear_plans()
     del pan
     rct = None
@@ -489,6 +541,7 @@ def main():
             "panel_gen_s": main_m["panel_gen_s"],
             "throughput_inflight": main_m["inflight"],
             "parity": parity,
+            "repeated": repeated,
             "rct": None if rct is None else {k: rct[k] for k in (
                 "ms_per_step", "rows_per_s", "single_fit_ms", "single_fit_ms_all",
                 "single_fit_rows_per_s", "ate", "se", "ate_hex", "se_hex", "hipgraph",

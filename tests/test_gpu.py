@@ -451,7 +451,10 @@ def test_weighted_gram_bitwise_repeatable(gpu, dtype):
 def test_bench_eager_gram_matches_graph_gram(gpu):
     """bench.py's in-flight block: the Gram as a plain launch on the Gram stream (the
     default, ATE_BENCH_EAGER_GRAM=1) and as a one-node graph give the same ATE/SE bits, the
-    in-flight fits agree with each other and with the timed single call."""
+    in-flight fits agree with each other and with the timed single call. The repeated
+    cross-fitting block (3 partitions of 25 micro-segments, one graph) reports 3 distinct
+    split ATEs whose median is the aggregate, and partition 0 (micro-segment m -> fold
+    m // 5: the main panel's folds) matches the single call up to Gram chunking."""
     import json
     import os
     import subprocess
@@ -473,6 +476,11 @@ def test_bench_eager_gram_matches_graph_gram(gpu):
         assert inf["abs_diff_ate_vs_single"] <= 1e-3 * d["se"]
         assert inf["rel_diff_se_vs_single"] <= 1e-4
         out[eg] = (inf["ate_hex"], inf["se_hex"])
+        rep = d["repeated"]
+        assert rep["repeats"] == 3 and rep["hipgraph"] and rep["splits_distinct"]
+        a = sorted(s[0] for s in rep["splits"])
+        assert rep["ate"] == a[1]
+        assert abs(rep["splits"][0][0] - d["ate"]) <= 1e-3 * d["se"]
     assert out["0"] == out["1"]
 
 

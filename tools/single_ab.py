@@ -1,7 +1,8 @@
 """A/B of the single ate_dml call (bench.py's timed step) over Gram kernels on ONE panel:
 the panel is generated once, each variant's step is captured and timed in alternation
 (K calls back to back, R rounds), so box-to-box and clock drift cancel out.
-Usage: single_ab.py [tri,pair] [rounds] [calls]   (variants: tri | pair | pair16)"""
+Usage: single_ab.py [tri,pair] [rounds] [calls]   (variants: tri | pair | pair16, with an
+optional @rN suffix: the paired Gram's plan built for N whole rounds of workgroups)"""
 import os
 import sys
 import time
@@ -27,8 +28,13 @@ pan = synthetic_panel(int(1e7), p=500, folds=5, seed=1991, dtype="bf16", blocked
 seg = global_seg_counts(pan, LocalComm())
 steps = {}
 def _select(v):
+    v, _, r = v.partition("@r")
     gram_mod.GRAM_TRI = v == "tri"
     gram_mod.BYTE_COLS = v != "pair16"      # pair16: the byte columns read as bf16
+    if r:
+        os.environ["ATE_GRAM_ROUNDS"] = r
+    else:
+        os.environ.pop("ATE_GRAM_ROUNDS", None)
 
 
 for i, v in enumerate(variants):
