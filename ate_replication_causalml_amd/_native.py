@@ -125,6 +125,8 @@ _SIGS = {
     "ate_lv_transpose": "piipip",
     "ate_gbdt_bin_panel": "pilpipppilpppl" + "p",
     "ate_gbdt_slab_entries": "liii",
+    "ate_gbdt_slab2_entries": "li",
+    "ate_gbdt_pair_root": "pppplllp",
     "ate_gbdt_apply": "plliipppp" + "p",
     "ate_panel_xv": "iplpipiplpp",
     "ate_col_moments": "pllipppp",
@@ -137,6 +139,7 @@ _SIGS = {
 }
 _RESTYPE = {"ate_forest_scratch_bytes": ctypes.c_int64,
             "ate_forest_exact_scratch_bytes": ctypes.c_int64, "ate_gbdt_slab_entries": ctypes.c_int64,
+            "ate_gbdt_slab2_entries": ctypes.c_int64,
             "ate_scan_parts": ctypes.c_int64}
 _CT = {"p": c_void_p, "i": c_int, "l": c_int64, "u": c_uint64, "d": c_double}
 

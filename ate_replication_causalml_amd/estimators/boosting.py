@@ -98,9 +98,24 @@ def _fit_pair(fit, jobs, dev, dists):
         return list(ex.map(run, range(2)))
 
 
-def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent=False):
+def _pair_fitter(kw):
+    """fit_pair for _crossfit on the GPU: models/gbdt.fit_gbdt_pair with the fits' settings
+    (None when ATE_GBDT_FUSED_ROOT=0: the two fits of a fold run one after the other)."""
+    if not G.FUSED_ROOT:
+        return None
+    opts = {k: kw[k] for k in ("n_trees", "depth", "lr", "lam", "min_child")}
+
+    def fit_pair(jobs, d):
+        (ty, ly, tr), (tw, lw, _) = jobs
+        return G.fit_gbdt_pair([ty, tw], [ly, lw], tr, kw["Xb"], kw["edges"], dist=d, **opts)
+    return fit_pair
+
+
+def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent=False, fit_pair=None):
     """Held-out predictions of E[Y|X], E[W|X] for every fold (device tensors). ``fit(target,
-    loss, train, dist)``. ``concurrent`` (GPU): a fold's two fits run side by side on two
+    loss, train, dist)``. ``fit_pair(jobs, dist)`` (GPU, models/gbdt.fit_gbdt_pair): a fold's
+    two fits in lockstep with one fused root-histogram pass per tree pair (the same trees).
+    ``concurrent`` (GPU): a fold's two fits run side by side on two
     streams, the second with a duplicated communicator -- the same bits, but slower on the
     config-5 shard (1.31 vs 1.18 s for 20 trees: the histogram kernels fill the GPU alone and
     two of them contend for L2; profiles/r04_cfg5), so off by default."""
@@ -121,6 +136,8 @@ def _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent=False):
             # held-out predictions = the trainer's running scores of the rows it skipped
             if pair:
                 my, mw = _fit_pair(fit, [(y, ly, ~ho), (w, lw, ~ho)], dev, [dist, d2])
+            elif fit_pair is not None:
+                my, mw = fit_pair([(y, ly, ~ho), (w, lw, ~ho)], dist)
             else:
                 my, mw = fit(y, ly, ~ho, dist), fit(w, lw, ~ho, dist)
             py = torch.where(ho, _response(my, dev), torch.zeros_like(y))
@@ -157,7 +174,8 @@ def dml_plr_gbdt(Y, W, X, folds=5, n_trees=100, depth=6, lr=0.1, lam=1.0, min_ch
 
     dkey = _data_key(checkpoint, Yn, Wn, Xn, np.array([folds, n_trees, depth, lr, lam,
                                                        min_child, seed, fold_stream], float))
-    ey, ew = _crossfit(y, w, fid_t, folds, fit, dev, dist, checkpoint, dkey)
+    ey, ew = _crossfit(y, w, fid_t, folds, fit, dev, dist, checkpoint, dkey,
+                       fit_pair=_pair_fitter(kw) if backend == "gpu" else None)
     mom = S.dml_moments_exact(y - ey, w - ew, dist)
     return read_result(S.dml_finalize(mom, "plr"), method,
                        n=dist.n_total if dist is not None else n)
@@ -263,7 +281,8 @@ def dml_plr_gbdt_panel(pan, n_trees=100, depth=6, lr=0.1, lam=1.0, min_child=1.0
         from .crossfit import _panel_key
         dkey = _panel_key(pan, data_key, pan.n, len(pan.xcols), n_trees, depth, lr, lam,
                           min_child, edge_rows)
-    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent)
+    ey, ew = _crossfit(y, w, fid, K, fit, dev, dist, checkpoint, dkey, concurrent,
+                       fit_pair=_pair_fitter(kw))
     mom = S.dml_moments_exact(y - ey, w - ew, dist)
     n_all = dist.n_total if dist is not None else pan.n
     return read_result(S.dml_finalize(mom, "plr"), method, n=n_all, trees=n_trees, depth=depth)

@@ -228,9 +228,10 @@ class FitArgs(ctypes.Structure):
 
 
 class RunState(ctypes.Structure):
-    """Mirror of csrc/gbdt.hip::GbdtRunState (resumable position of a fit)."""
+    """Mirror of csrc/gbdt.hip::GbdtRunState (resumable position of a fit; t_stop > 0 ends
+    the run after tree t_stop - 1, for the lockstep pair fits)."""
     _fields_ = [("t", ctypes.c_int), ("d", ctypes.c_int), ("cur", ctypes.c_int),
-                ("resume", ctypes.c_int), ("red_count", ctypes.c_int64)]
+                ("resume", ctypes.c_int), ("red_count", ctypes.c_int64), ("t_stop", ctypes.c_int)]
 
 
 MAXB = 2 ** (MAX_DEPTH - 1) + 1    # csrc/gbdt.hip MAXB: partition buckets + retired
@@ -313,84 +314,179 @@ def _fit_gpu(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min
              dist, dev):
     """y: [n] targets, train: [n] bool (numpy or device tensors: the HBM-panel path keeps
     them on the device)."""
-    yt = torch.as_tensor(y, device=dev, dtype=torch.float64)
-    trn = torch.as_tensor(train, device=dev, dtype=torch.bool)
-    n = yt.numel()
-    order = torch.cat([torch.nonzero(trn).flatten(), torch.nonzero(~trn).flatten()])
-    n_train = int(trn.sum())
-    base = exact_base(yt[order[:n_train]], n_train, loss, dist)
-    M = 2 ** (depth + 1) - 1
-    f = torch.full((n,), base, dtype=torch.float64, device=dev)
-    feat = torch.full((n_trees, M), -2, dtype=torch.int32, device=dev)
-    thr = torch.zeros((n_trees, M), dtype=torch.int32, device=dev)
-    value = torch.zeros((n_trees, M), dtype=torch.float64, device=dev)
-    if n_train == 0 or n_trees == 0:
-        # a rank may hold no training rows; it still has to join every collective
-        if dist is not None and dist.world > 1 and n_trees:
-            raise ValueError("row-sharded GBDT needs training rows on every rank")
-        return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu", f)
-    i32 = dict(dtype=torch.int32, device=dev)
-    i64 = dict(dtype=torch.int64, device=dev)
-    R = max(1024, -(-n_train // 1024))
-    R = -(-R // 256) * 256
-    W = -(-n_train // R)
-    idx = [order[:n_train].to(torch.int32).contiguous(), torch.empty(n_train, **i32)]
-    gh = [torch.empty(n_train, **i64), torch.empty(n_train, **i64)]
-    bkt = torch.empty(n_train, dtype=torch.uint8, device=dev)
-    cntb = torch.empty(MAXB * W, **i32)
-    baseb = torch.empty(MAXB * W, **i32)
-    btot = torch.empty(MAXB, **i32)
-    seg = [torch.zeros(MAXB + 1, **i32), torch.zeros(MAXB + 1, **i32)]
-    tot = torch.zeros(2 * M, **i64)
-    # rule 1 (hessian child rule + a pause per level for the histogram all-reduce) for
-    # every row-sharded fit, world 1 included (the same code path as world W)
-    rule = 0 if dist is None else 1
-    # world W > 1: feature-sliced C04 (reduce-scatter of the level histograms, split search
-    # on this rank's pw features, all-gather of the candidates; csrc/gbdt.hip header)
-    nr, pw = c04_slices(p, dist) if rule == 1 else (1, p)
-    rk = dist.rank if nr > 1 else 0
-    slots = max(1, 2 ** (depth - 2))
-    H = [torch.empty(2 ** (depth - 1) * 512 * pw, **i64) for _ in range(2)]
-    Hs = torch.empty(slots * 512 * nr * pw, **i64)
-    Hl = torch.empty(slots * 512 * pw, **i64) if nr > 1 else None
-    cap = int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule))
-    slab = torch.empty(cap, **i64)
-    ncand = (1 << max(depth - 1, 0)) * (-(-pw // 8)) * 4                     # 32-B Cand
-    cand = torch.empty(ncand, **i64)
-    candg = torch.empty(nr * ncand, **i64) if nr > 1 else None
-    P = ctypes.c_void_p
-    a = FitArgs(Xr=Xr.data_ptr(), ldr=ldr, n=n, n_train=n_train, p=p, depth=depth,
-                n_trees=n_trees, loss=LOSS[loss], rule=rule, W=W, lam=lam,
-                min_gain=min_gain, lr=lr, min_child=int(np.rint(min_child * ref.FIX)), R=R,
-                y=yt.data_ptr(), f=f.data_ptr(), bkt=bkt.data_ptr(), cnt=cntb.data_ptr(),
-                base=baseb.data_ptr(), btot=btot.data_ptr(), tot=tot.data_ptr(),
-                feat=feat.data_ptr(), thr=thr.data_ptr(), value=value.data_ptr(),
-                Hs=Hs.data_ptr(), slab=slab.data_ptr(), slab_cap=cap, cand=cand.data_ptr(),
-                nr=nr, rk=rk, pw=pw, pl=min(pw, p - rk * pw),
-                Hl=Hl.data_ptr() if Hl is not None else None,
-                candg=candg.data_ptr() if candg is not None else None)
-    a.idx = (P * 2)(idx[0].data_ptr(), idx[1].data_ptr())
-    a.gh = (P * 2)(gh[0].data_ptr(), gh[1].data_ptr())
-    a.seg = (P * 2)(seg[0].data_ptr(), seg[1].data_ptr())
-    a.H = (P * 2)(H[0].data_ptr(), H[1].data_ptr())
-    st = RunState()
-    run = _native.hip().ate_gbdt_run
-    while True:
-        # the stepper enqueues a level's kernels on the current stream; a row-sharded fit
-        # pauses after each level's compact histograms, which are all-reduced (C04) -- or,
-        # feature-sliced, reduce-scattered, and after the slice's split search its
-        # candidates all-gathered -- on the same stream: no host callback, no host sync
-        rc = run(ctypes.addressof(a), ctypes.addressof(st),
-                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-        if rc == 0:
-            break
-        if rc not in (1, 2) or dist is None or (rc == 2 and nr == 1):
-            raise RuntimeError(f"ate_gbdt_run failed with status {rc}")
-        m = st.red_count
-        if rc == 1 and nr == 1:
-            dist.sum_(Hs[:m])
+    fs = _GpuFit(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
+                 edges, dist, dev)
+    if not fs.empty:
+        fs.drive(dist)
+    return fs.model()
+
+
+class _GpuFit:
+    """One device fit: its buffers, the native argument block (csrc/gbdt.hip GbdtFitArgs)
+    and the stepper position. ``slab_min``: slab entries to allocate at least (the fused
+    root pass of fit_gbdt_pair writes fit A's slab)."""
+
+    def __init__(self, Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child,
+                 min_gain, edges, dist, dev, slab_min=0):
+        self._init(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
+                   edges, dist, dev, slab_min)
+
+    def model(self):
+        return GbdtModel(self.feat, self.thr, self.value, self.base, self.loss, self.depth,
+                         self.edges, "gpu", self.f)
+
+    def drive(self, dist):
+        """Run the stepper from its position until it returns 0, servicing the row-sharded
+        fit's pauses: level histograms all-reduced (C04) -- or, feature-sliced, reduce-
+        scattered, and after the slice's split search the candidates all-gathered -- on the
+        same stream (no host callback, no host sync)."""
+        a, st, nr = self.a, self.st, self.nr
+        run = _native.hip().ate_gbdt_run
+        while True:
+            rc = run(ctypes.addressof(a), ctypes.addressof(st),
+                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc == 0:
+                break
+            if rc not in (1, 2) or dist is None or (rc == 2 and nr == 1):
+                raise RuntimeError(f"ate_gbdt_run failed with status {rc}")
+            self.reduce(dist, rc, st.red_count)
+
+    def reduce(self, dist, rc, m):
+        if rc == 1 and self.nr == 1:
+            dist.sum_(self.Hs[:m])
         elif rc == 1:
-            dist.comm.reduce_scatter_(Hl[:m // nr], Hs[:m])
+            dist.comm.reduce_scatter_(self.Hl[:m // self.nr], self.Hs[:m])
         else:
-            dist.comm.all_gather_into_(candg[:nr * m], cand[:m])
-    return GbdtModel(feat, thr, value, base, loss, depth, edges, "gpu", f)
+            dist.comm.all_gather_into_(self.candg[:self.nr * m], self.cand[:m])
+
+    def _init(self, Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
+              edges, dist, dev, slab_min):
+        yt = torch.as_tensor(y, device=dev, dtype=torch.float64)
+        trn = torch.as_tensor(train, device=dev, dtype=torch.bool)
+        n = yt.numel()
+        order = torch.cat([torch.nonzero(trn).flatten(), torch.nonzero(~trn).flatten()])
+        n_train = int(trn.sum())
+        base = exact_base(yt[order[:n_train]], n_train, loss, dist)
+        M = 2 ** (depth + 1) - 1
+        self.loss, self.depth, self.edges, self.base, self.n_train = loss, depth, edges, base, n_train
+        self.f = torch.full((n,), base, dtype=torch.float64, device=dev)
+        self.feat = torch.full((n_trees, M), -2, dtype=torch.int32, device=dev)
+        self.thr = torch.zeros((n_trees, M), dtype=torch.int32, device=dev)
+        self.value = torch.zeros((n_trees, M), dtype=torch.float64, device=dev)
+        self.empty = n_train == 0 or n_trees == 0
+        if self.empty:
+            # a rank may hold no training rows; it still has to join every collective
+            if dist is not None and dist.world > 1 and n_trees:
+                raise ValueError("row-sharded GBDT needs training rows on every rank")
+            return
+        i32 = dict(dtype=torch.int32, device=dev)
+        i64 = dict(dtype=torch.int64, device=dev)
+        R = max(1024, -(-n_train // 1024))
+        R = -(-R // 256) * 256
+        W = -(-n_train // R)
+        self.idx = [order[:n_train].to(torch.int32).contiguous(), torch.empty(n_train, **i32)]
+        self.gh = [torch.empty(n_train, **i64), torch.empty(n_train, **i64)]
+        self.yt, self.bkt = yt, torch.empty(n_train, dtype=torch.uint8, device=dev)
+        self.cntb = torch.empty(MAXB * W, **i32)
+        self.baseb = torch.empty(MAXB * W, **i32)
+        self.btot = torch.empty(MAXB, **i32)
+        self.seg = [torch.zeros(MAXB + 1, **i32), torch.zeros(MAXB + 1, **i32)]
+        self.tot = torch.zeros(2 * M, **i64)
+        # rule 1 (hessian child rule + a pause per level for the histogram all-reduce) for
+        # every row-sharded fit, world 1 included (the same code path as world W)
+        rule = 0 if dist is None else 1
+        # world W > 1: feature-sliced C04 (reduce-scatter of the level histograms, split
+        # search on this rank's pw features, all-gather of the candidates; csrc/gbdt.hip)
+        nr, pw = c04_slices(p, dist) if rule == 1 else (1, p)
+        self.nr, self.pw, self.rule = nr, pw, rule
+        rk = dist.rank if nr > 1 else 0
+        slots = max(1, 2 ** (depth - 2))
+        self.H = [torch.empty(2 ** (depth - 1) * 512 * pw, **i64) for _ in range(2)]
+        self.Hs = torch.empty(slots * 512 * nr * pw, **i64)
+        self.Hl = torch.empty(slots * 512 * pw, **i64) if nr > 1 else None
+        cap = max(int(_native.hip().ate_gbdt_slab_entries(n_train, p, depth, rule)), int(slab_min))
+        self.slab = torch.empty(cap, **i64)
+        ncand = (1 << max(depth - 1, 0)) * (-(-pw // 8)) * 4                 # 32-B Cand
+        self.cand = torch.empty(ncand, **i64)
+        self.candg = torch.empty(nr * ncand, **i64) if nr > 1 else None
+        P = ctypes.c_void_p
+        a = FitArgs(Xr=Xr.data_ptr(), ldr=ldr, n=n, n_train=n_train, p=p, depth=depth,
+                    n_trees=n_trees, loss=LOSS[loss], rule=rule, W=W, lam=lam,
+                    min_gain=min_gain, lr=lr, min_child=int(np.rint(min_child * ref.FIX)), R=R,
+                    y=yt.data_ptr(), f=self.f.data_ptr(), bkt=self.bkt.data_ptr(),
+                    cnt=self.cntb.data_ptr(), base=self.baseb.data_ptr(),
+                    btot=self.btot.data_ptr(), tot=self.tot.data_ptr(),
+                    feat=self.feat.data_ptr(), thr=self.thr.data_ptr(),
+                    value=self.value.data_ptr(), Hs=self.Hs.data_ptr(),
+                    slab=self.slab.data_ptr(), slab_cap=cap, cand=self.cand.data_ptr(),
+                    nr=nr, rk=rk, pw=pw, pl=min(pw, p - rk * pw),
+                    Hl=self.Hl.data_ptr() if self.Hl is not None else None,
+                    candg=self.candg.data_ptr() if self.candg is not None else None)
+        a.idx = (P * 2)(self.idx[0].data_ptr(), self.idx[1].data_ptr())
+        a.gh = (P * 2)(self.gh[0].data_ptr(), self.gh[1].data_ptr())
+        a.seg = (P * 2)(self.seg[0].data_ptr(), self.seg[1].data_ptr())
+        a.H = (P * 2)(self.H[0].data_ptr(), self.H[1].data_ptr())
+        self.a, self.st = a, RunState()
+
+
+# Lockstep pair fits with a fused root histogram pass (fit_gbdt_pair); ATE_GBDT_FUSED_ROOT=0
+# fits a pair one after the other (the A/B of profiles/r06_cfg5)
+FUSED_ROOT = __import__("os").environ.get("ATE_GBDT_FUSED_ROOT", "1") == "1"
+
+
+def _two_ranges(rows):
+    """(a0, n0, a1) when the ascending row list ``rows`` is rows a0 .. a0 + n0 - 1 followed by
+    a1, a1 + 1, ... (a fold's complement on a fold-segmented panel), else (0, -1, 0): the
+    fused root pass then computes each position's row instead of loading it."""
+    n = rows.numel()
+    if n == 0:
+        return 0, -1, 0
+    brk = torch.nonzero(rows[1:] - rows[:-1] != 1).flatten()
+    if brk.numel() > 1:
+        return 0, -1, 0
+    n0 = int(brk[0]) + 1 if brk.numel() else n
+    return int(rows[0]), n0, int(rows[n0]) if n0 < n else int(rows[0]) + n0
+
+
+def fit_gbdt_pair(ys, losses, train, Xb, edges, dist=None, n_trees=100, depth=6, lr=0.1,
+                  lam=1.0, min_child=1.0, min_gain=0.0):
+    """Two device fits on the SAME training rows and binned panel -- a DML fold's E[Y|X] and
+    E[W|X] (estimators/boosting._crossfit) -- in lockstep, tree by tree. Level 0 of both trees
+    comes from ONE pass over the rows' bins (csrc/gbdt.hip ate_gbdt_pair_root: four-channel
+    LDS histograms, gbdt_hist2_kernel); levels 1.. and the score walk are each fit's own
+    stepper. Every histogram is an exact integer sum, so the trees, scores and held-out
+    predictions are the bits of two fit_gbdt calls (tests/test_gbdt_gpu.py). With ``dist``
+    each fit's root histogram is all-reduced / reduce-scattered (C04) as in the stepper.
+    Returns the two GbdtModels."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    _check_limits()
+    Xr, ldr = Xb
+    p = len(edges[0])
+    if depth < 1 or depth > MAX_DEPTH:
+        raise ValueError(f"depth must be in [1, {MAX_DEPTH}]")
+    trn = torch.as_tensor(train, device=dev, dtype=torch.bool)
+    n_train = int(trn.sum())
+    cap2 = int(_native.hip().ate_gbdt_slab2_entries(max(n_train, 1), p)) if n_train else 0
+    fits = [_GpuFit(Xr, ldr, p, ys[0], trn, losses[0], n_trees, depth, lr, lam, min_child,
+                    min_gain, edges, dist, dev, slab_min=cap2),
+            _GpuFit(Xr, ldr, p, ys[1], trn, losses[1], n_trees, depth, lr, lam, min_child,
+                    min_gain, edges, dist, dev)]
+    A, B = fits
+    if A.empty or B.empty:
+        for fs in fits:
+            if not fs.empty:
+                fs.drive(dist)
+        return A.model(), B.model()
+    idx_root = A.idx[0].clone()          # the training rows in row order (any order: same trees)
+    gh2 = torch.empty(2 * A.n_train, dtype=torch.int64, device=dev)
+    a0, n0, a1 = _two_ranges(idx_root)
+    for t in range(n_trees):
+        s = torch.cuda.current_stream().cuda_stream
+        _native.call("ate_gbdt_pair_root", ctypes.addressof(A.a), ctypes.addressof(B.a),
+                     idx_root.data_ptr(), gh2.data_ptr(), a0, n0, a1, s)
+        for fs in fits:
+            if fs.rule == 1:                 # the root's compact histogram (C04)
+                fs.reduce(dist, 1, 512 * fs.nr * fs.pw)
+            fs.st.t, fs.st.d, fs.st.cur, fs.st.resume, fs.st.t_stop = t, 0, 0, 1, t + 1
+            fs.drive(dist)
+    return A.model(), B.model()

@@ -95,7 +95,8 @@ __global__ __launch_bounds__(NT) void gbdt_grad_kernel(int loss, const double* _
                                                        const double* __restrict__ y,
                                                        const int32_t* __restrict__ idx,
                                                        int64_t n_train, int64_t* __restrict__ gh,
-                                                       int32_t* __restrict__ seg) {
+                                                       int32_t* __restrict__ seg,
+                                                       int64_t* __restrict__ gh2 = nullptr) {
   if (blockIdx.x == 0 && threadIdx.x == 0) { seg[0] = 0; seg[1] = (int32_t)n_train; }
   const int64_t q0 = (blockIdx.x * (int64_t)NT * 4) + threadIdx.x;
   int32_t ii[4];
@@ -117,7 +118,9 @@ __global__ __launch_bounds__(NT) void gbdt_grad_kernel(int loss, const double* _
       g = s - yv[u];
       h = fmax(s * (1.0 - s), 1e-16);
     }
-    gh[q] = gbdt_pack(loss, llrint(g * GFIX), llrint(h * GFIX));
+    const int64_t v = gbdt_pack(loss, llrint(g * GFIX), llrint(h * GFIX));
+    gh[q] = v;
+    if (gh2) gh2[2 * q] = v;      // the fused root pass's interleaved (fit A, fit B) pairs
   }
 }
 
@@ -368,6 +371,158 @@ __global__ __launch_bounds__(NT) void gbdt_hist_reduce_kernel(
       v3 += sp[(i + 3) * stride];
     }
     for (; i < c; ++i) v0 += sp[i * stride];
+    *dst = (int64_t)(v0 + v1 + v2 + v3);
+  }
+}
+
+// ---- fused root histogram of two fits on the same training rows (ate_gbdt_pair_root) ----
+// A fold's E[Y|X] and E[W|X] fits (config 5) histogram the same rows at level 0; trained in
+// lockstep, tree by tree, one pass reads each row's bins once for both and accumulates four
+// channels (G_A, H_A, G_B, H_B). 16 features per workgroup keep the four-channel image at
+// 128 KB of LDS: [bin][channel][slot(f)], slot(f) = (f & 3) * FQ2 + (f >> 2). Lane = (row r16
+// of 16, dword l4 of 4). A u64 atomic lands on banks 2 (16 ch + 4 q + l4) mod 64 = 32 (ch & 1)
+// + 8 q + 2 l4: in a 32-lane group (8 rows) the rotation rot = r16 & 3 separates 4 rows
+// through q, and the other 4 (bsw = (r16 >> 2) & 1) add the channel of the opposite parity
+// first (H before G), so every atomic instruction is conflict-free whatever the bins. The
+// integer sums are the two separate passes' bits (profiles/r06_cfg5: the separate pass is
+// latency-bound between its bin gathers and the LDS atomic queue, LDS array 52 % busy).
+constexpr int FB2 = 16, FQ2 = FB2 / 4, NTH2 = 1024;
+constexpr int SLAB2 = 4 * 256 * FB2;   // u64 entries of one workgroup's image (128 KB)
+#ifndef GBDT_U2
+#define GBDT_U2 4
+#endif
+
+// gh2: the two fits' packed (g, h) of position q at gh2[2q], gh2[2q + 1] (one 16-byte load).
+// RANGES: the training rows are rows a0 .. a0 + n0 - 1 then a1 .. (a DML fold's complement
+// on a fold-segmented panel): the row of a position is computed, no idx load.
+template <bool RANGES>
+__global__ __launch_bounds__(NTH2) void gbdt_hist2_kernel(
+    const uint8_t* __restrict__ Xr, int64_t ldr, const int32_t* __restrict__ idx,
+    const longlong2* __restrict__ gh2, int a0, int n0, int a1, int n_train, int p, int CH,
+    int nchunk, int ydim2, u64* __restrict__ slab, int lossA, int lossB) {
+  __shared__ u64 sh[SLAB2];
+  const int bid = blockIdx.x;
+  // chunk c on XCD c % 8 with its ydim2 feature blocks back to back (gbdt_hist_kernel)
+  const int xq = bid >> 3;
+  const int chunk = (xq / ydim2) * 8 + (bid & 7), yb = xq % ydim2;
+  if (chunk >= nchunk) return;                               // uniform: spare workgroup
+  const int s = chunk * CH, e = min(n_train, s + CH);
+  const int j0 = yb * FB2, nf = min(FB2, p - j0);
+  ATE_DASSERT(s < e && nf > 0 && yb < ydim2);
+  {
+    ulonglong2* z = reinterpret_cast<ulonglong2*>(sh);
+    for (int t = threadIdx.x; t < SLAB2 / 2; t += NTH2) z[t] = make_ulonglong2(0, 0);
+  }
+  __syncthreads();
+  const int l4 = threadIdx.x % FQ2, r16 = (threadIdx.x / FQ2) % 16, w = threadIdx.x >> 6;
+  const int rot = r16 & 3, bsw = (r16 >> 2) & 1;
+  const uint32_t* xw = reinterpret_cast<const uint32_t*>(Xr + j0) + l4;
+  const int64_t ldw = ldr >> 2;
+  constexpr int U = GBDT_U2, RPI = U * (NTH2 / FQ2);
+  const int last = e - 1;
+  const bool wok = 4 * l4 < nf;
+  auto pos = [&](int base, int u) { return base + (u * (NTH2 / 64) + w) * 16 + r16; };
+  auto row_of = [&](int q) { return q < n0 ? a0 + q : a1 + (q - n0); };
+  // software pipeline as gbdt_hist_kernel: positions two iterations ahead (idx path), (g, h,
+  // bins) one
+  int32_t iiA[U], iiB[U];
+  longlong2 gA[U];
+  uint32_t bA[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    iiA[u] = RANGES ? row_of(min(pos(s, u), last)) : idx[min(pos(s, u), last)];
+    iiB[u] = RANGES ? row_of(min(pos(s + RPI, u), last)) : idx[min(pos(s + RPI, u), last)];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    gA[u] = gh2[min(pos(s, u), last)];
+    bA[u] = xw[(int64_t)iiA[u] * ldw];
+  }
+  auto step = [&](int base, auto tail_tag) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    auto at = [&](int q) { return TAIL ? min(q, last) : q; };
+    longlong2 nA[U];
+    uint32_t bB[U];
+    int32_t iiC[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      nA[u] = gh2[at(pos(base + RPI, u))];
+      bB[u] = xw[(int64_t)iiB[u] * ldw];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      iiC[u] = RANGES ? row_of(at(pos(base + 2 * RPI, u))) : idx[at(pos(base + 2 * RPI, u))];
+    if (wok) {                                                // padding words add nothing
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (TAIL && pos(base, u) > last) continue;            // rows past the chunk
+        u64 ga, ha, gb, hb;
+        gbdt_unpack(lossA, gA[u].x, ga, ha);
+        gbdt_unpack(lossB, gA[u].y, gb, hb);
+        const u64 x0 = bsw ? ha : ga, x1 = bsw ? ga : ha;
+        const u64 x2 = bsw ? hb : gb, x3 = bsw ? gb : hb;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = (k + rot) & 3;
+          const uint32_t bin = __builtin_amdgcn_ubfe(bA[u], 8 * q, 8);
+          u64* e0 = sh + ((bin * 4 * FB2) | (q * FQ2 + l4));
+          u64* pa = e0 + bsw * FB2;                           // channel bsw (then 2 + bsw)
+          u64* pb = e0 + (bsw ^ 1) * FB2;                     // channel 1 - bsw (then 3 - bsw)
+          atomicAdd(pa, x0);
+          atomicAdd(pb, x1);
+          atomicAdd(pa + 2 * FB2, x2);
+          atomicAdd(pb + 2 * FB2, x3);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      iiA[u] = iiB[u];
+      gA[u] = nA[u];
+      bA[u] = bB[u];
+      iiB[u] = iiC[u];
+    }
+  };
+  int base = s;
+  for (; base + 3 * RPI <= e; base += RPI) step(base, std::false_type{});
+  for (; base < e; base += RPI) step(base, std::true_type{});
+  __syncthreads();
+  ulonglong2* dst = reinterpret_cast<ulonglong2*>(slab + ((int64_t)chunk * ydim2 + yb) * SLAB2);
+  const ulonglong2* src = reinterpret_cast<const ulonglong2*>(sh);
+  for (int t = threadIdx.x; t < SLAB2 / 2; t += NTH2) dst[t] = src[t];
+}
+
+// Root histograms of both fits from the fused images: fit m (blockIdx.y) gets channels 2m
+// (G) and 2m + 1 (H), summed over the chunks, in gbdt_hist_reduce_kernel's compact layout
+// (slot 0; rank-block-major [nr][1][512][pw] when feature-sliced).
+__global__ __launch_bounds__(NT) void gbdt_hist2_reduce_kernel(
+    const u64* __restrict__ slab, int nchunk, int p, int ydim2, int64_t* __restrict__ HsA,
+    int64_t* __restrict__ HsB, int nr, int pw) {
+  const int m = blockIdx.y;
+  int64_t* Hs = m ? HsB : HsA;
+  const int P = nr * pw;
+  const int64_t per = 512LL * P;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < per; t += (int64_t)gridDim.x * NT) {
+    const int cb = (int)(t / P), j = (int)(t - (int64_t)cb * P);
+    const int r = j / pw;
+    int64_t* dst = Hs + ((int64_t)r * 512 + cb) * pw + (j - r * pw);
+    if (j >= p) {
+      *dst = 0;
+      continue;
+    }
+    const int yb = j / FB2, fl = j - yb * FB2;
+    const int ch = 2 * m + (cb >> 8), bin = cb & 255;
+    const u64* sp = slab + (int64_t)yb * SLAB2 + (bin * 4 + ch) * FB2 + ((fl & 3) * FQ2 + (fl >> 2));
+    const int64_t stride = (int64_t)ydim2 * SLAB2;
+    u64 v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    int i = 0;
+    for (; i + 4 <= nchunk; i += 4) {
+      v0 += sp[i * stride];
+      v1 += sp[(i + 1) * stride];
+      v2 += sp[(i + 2) * stride];
+      v3 += sp[(i + 3) * stride];
+    }
+    for (; i < nchunk; ++i) v0 += sp[i * stride];
     *dst = (int64_t)(v0 + v1 + v2 + v3);
   }
 }
@@ -813,6 +968,7 @@ struct GbdtFitArgs {
 struct GbdtRunState {
   int t, d, cur, resume;
   int64_t red_count;
+  int t_stop;             // > 0: return 0 once tree t_stop - 1 is done (lockstep pair fits)
 };
 
 // chunk length and (upper bound of the) workgroup count of level d's histogram
@@ -840,6 +996,19 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
   *nwg = wg;
 }
 
+// fused root pass (gbdt_hist2_kernel): chunk length, chunk count, workgroups
+static void gbdt_hist2_geom(int64_t n_train, int p, int64_t* CH, int64_t* nchunk, int64_t* nwg) {
+  const int ydim2 = (p + FB2 - 1) / FB2;
+  const int64_t target = std::max<int64_t>(512, (n_train * ydim2 + 32767) / 32768);
+  int64_t ch = (n_train * ydim2 + target - 1) / target;
+  ch = std::max<int64_t>(1024, (ch + 255) / 256 * 256);
+  *CH = ch;
+  *nchunk = (n_train + ch - 1) / ch;
+  *nwg = (*nchunk + 7) / 8 * 8 * ydim2;
+}
+
+ATE_KERNEL_SHAPE("gbdt_hist2_kernel<idx>", NTH2, 0, gbdt_hist2_kernel<false>)
+ATE_KERNEL_SHAPE("gbdt_hist2_kernel<ranges>", NTH2, 0, gbdt_hist2_kernel<true>)
 ATE_KERNEL_SHAPE("gbdt_hist_kernel<compact>", NTH, 0, gbdt_hist_kernel<true>)
 ATE_KERNEL_SHAPE("gbdt_hist_kernel<full>", NTH, 0, gbdt_hist_kernel<false>)
 
@@ -860,6 +1029,62 @@ ATE_API int64_t ate_gbdt_slab_entries(int64_t n_train, int p, int depth, int rul
     m = std::max(m, wg);
   }
   return m * SLAB;
+}
+
+// slab entries the fused root pass of a pair of fits needs (in fit A's slab)
+ATE_API int64_t ate_gbdt_slab2_entries(int64_t n_train, int p) {
+  int64_t ch, nc, wg;
+  gbdt_hist2_geom(n_train, p, &ch, &nc, &wg);
+  return wg * SLAB2;
+}
+
+// Level 0 of tree t of two fits A, B on the same training rows, in lockstep
+// (models/gbdt.fit_gbdt_pair): both fits' positions reset to idx_root (any order gives the
+// same trees: every histogram is an exact integer sum), both gradients, ONE fused root
+// histogram pass, and the compact root histograms of each fit written to its Hs. The caller
+// then (rule 1) all-reduces / reduce-scatters each fit's 512 * nr * pw entries and resumes each
+// stepper at (t, d = 0, cur = 0, resume = 1, t_stop = t + 1).
+// gh2: [2 n_train] int64 scratch (the interleaved pairs); a0 / n0 / a1: the training rows as
+// two ranges (rows a0 .. a0 + n0 - 1, then from a1; idx_root must list them in that order),
+// or n0 < 0: read positions -> rows from idx_root.
+ATE_API int ate_gbdt_pair_root(const void* args_a, const void* args_b, const void* idx_root,
+                               void* gh2, int64_t a0, int64_t n0, int64_t a1, void* stream) {
+  const GbdtFitArgs& A = *static_cast<const GbdtFitArgs*>(args_a);
+  const GbdtFitArgs& B = *static_cast<const GbdtFitArgs*>(args_b);
+  hipStream_t st = (hipStream_t)stream;
+  if (A.Xr != B.Xr || A.ldr != B.ldr || A.n != B.n || A.n_train != B.n_train || A.p != B.p ||
+      A.rule != B.rule || A.nr != B.nr || A.pw != B.pw || A.depth < 1 || B.depth < 1 ||
+      (A.ldr & 31) || A.n_train < 1 || A.n_train >= (1LL << 31))
+    return -1;
+  if (A.slab_cap < ate_gbdt_slab2_entries(A.n_train, A.p)) return -5;
+  const bool sliced = A.nr > 1;
+  const int hp = sliced ? A.pw : A.p, nr = sliced ? A.nr : 1;
+  const size_t bytes = (size_t)A.n_train * sizeof(int32_t);
+  if (hipMemcpyAsync(A.idx[0], idx_root, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(B.idx[0], idx_root, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return -3;
+  const dim3 gg((unsigned)((A.n_train + 4 * NT - 1) / (4 * NT)));
+  if (!gh2 || (n0 >= 0 && (a0 < 0 || n0 > A.n_train || a1 < a0 + n0 ||
+                           a1 + (A.n_train - n0) > A.n)))
+    return -1;
+  int64_t* g2 = static_cast<int64_t*>(gh2);
+  ATE_LAUNCH(gbdt_grad_kernel, gg, dim3(NT), 0, st, A.loss, A.f, A.y, A.idx[0], A.n_train,
+             A.gh[0], A.seg[0], g2);
+  ATE_LAUNCH(gbdt_grad_kernel, gg, dim3(NT), 0, st, B.loss, B.f, B.y, B.idx[0], B.n_train,
+             B.gh[0], B.seg[0], g2 + 1);
+  int64_t CH, nchunk, nwg;
+  gbdt_hist2_geom(A.n_train, A.p, &CH, &nchunk, &nwg);
+  const int ydim2 = (A.p + FB2 - 1) / FB2;
+  const bool ranges = n0 >= 0;
+  ATE_LAUNCH(ranges ? gbdt_hist2_kernel<true> : gbdt_hist2_kernel<false>, dim3((unsigned)nwg),
+             dim3(NTH2), 0, st, A.Xr, A.ldr, A.idx[0], reinterpret_cast<const longlong2*>(g2),
+             (int)a0, (int)n0, (int)a1, (int)A.n_train, A.p, (int)CH, (int)nchunk, ydim2, A.slab,
+             A.loss, B.loss);
+  const int64_t perP = 512LL * nr * hp;
+  ATE_LAUNCH(gbdt_hist2_reduce_kernel, dim3((unsigned)std::min<int64_t>((perP + NT - 1) / NT, 256), 2),
+             dim3(NT), 0, st, A.slab, (int)nchunk, A.p, ydim2, A.Hs, B.Hs, nr, hp);
+  ATE_CHECK_LAUNCH();
+  return 0;
 }
 
 // Runs the fit from the position in *state to completion (returns 0), or until a
@@ -891,7 +1116,8 @@ ATE_API int ate_gbdt_run(const void* args, void* state, void* stream) {
   // 8 G atomics only, 16 H atomics as u32
   const char* hm = getenv("ATE_GBDT_HIST_MODE");
   const int hmode = hm ? atoi(hm) : 0;
-  for (; s.t < a.n_trees; ++s.t, s.d = 0) {
+  const int t_end = s.t_stop > 0 ? std::min(s.t_stop, a.n_trees) : a.n_trees;
+  for (; s.t < t_end; ++s.t, s.d = 0) {
     int32_t* ft = a.feat + (int64_t)s.t * M;
     int32_t* th = a.thr + (int64_t)s.t * M;
     double* vt = a.value + (int64_t)s.t * M;

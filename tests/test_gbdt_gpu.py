@@ -159,3 +159,49 @@ def test_dml_gbdt_panel_matches_host_arrays(gpu):
     finally:
         R.fold_ids = orig
     assert a.ate == pytest.approx(b.ate, abs=1e-12) and a.se == pytest.approx(b.se, rel=1e-10)
+
+
+@pytest.mark.parametrize("mode", ["single", "world1", "sliced", "ranges"])
+def test_gbdt_pair_fused_root_equals_two_fits(gpu, mode):
+    """fit_gbdt_pair (a fold's two fits in lockstep, level 0 of both from ONE fused
+    four-channel histogram pass, csrc/gbdt.hip gbdt_hist2_kernel) grows the trees of two
+    fit_gbdt calls bit for bit: squared + logistic targets, p = 70 (a partial 16-feature
+    block), depth 6; single device (rule 0), a one-rank row-sharded context (rule 1, root
+    histogram all-reduced) and an emulated rank 0 of 2 (feature-sliced C04: root histogram
+    reduce-scattered); "ranges": training rows in two runs (a fold's complement), the
+    variant that computes each position's row instead of loading it."""
+    from ate_replication_causalml_amd.parallel.comm import EmulatedComm, LocalComm
+    from ate_replication_causalml_amd.parallel.dist import DistContext
+    X, y = _wide()
+    yb = (y > 0.4).astype(float)
+    r = np.arange(len(y))
+    tr = torch.as_tensor((r < 5000) | (r >= 9000) if mode == "ranges" else r % 5 != 2,
+                         device=gpu)
+    assert (G._two_ranges(torch.nonzero(tr).flatten().to(torch.int32))[1] >= 0) == (mode == "ranges")
+    edges = G.global_bin_edges(X, None)
+    Xb = G.binned(X, edges, gpu)
+    dist = {"single": None, "world1": DistContext(LocalComm(), 0, len(y)),
+            "sliced": DistContext(EmulatedComm(0, 2), 0, len(y)), "ranges": None}[mode]
+    ty = torch.as_tensor(y, device=gpu)
+    tw = torch.as_tensor(yb, device=gpu)
+    kw = dict(n_trees=5, depth=6, lr=0.3)
+    pa, pb = G.fit_gbdt_pair([ty, tw], ["squared", "logistic"], tr, Xb, edges, dist=dist, **kw)
+    sa = G.fit_gbdt(None, ty, loss="squared", train=tr, dist=dist, edges=edges, Xb=Xb, **kw)
+    sb = G.fit_gbdt(None, tw, loss="logistic", train=tr, dist=dist, edges=edges, Xb=Xb, **kw)
+    for p_, s_ in ((pa, sa), (pb, sb)):
+        assert torch.equal(p_.feat, s_.feat) and torch.equal(p_.thr, s_.thr)
+        assert torch.equal(p_.value, s_.value) and torch.equal(p_.scores, s_.scores)
+        assert int((p_.feat >= 0).sum()) > 20
+
+
+def test_dml_gbdt_panel_fused_root_same_bits(gpu, monkeypatch):
+    """The config-5 cross-fit with the fused root pass (the default) and with the two fits
+    of a fold one after the other (ATE_GBDT_FUSED_ROOT=0): the same ATE/SE bits."""
+    from ate_replication_causalml_amd.data.device_dgp import synthetic_panel
+    from ate_replication_causalml_amd.estimators.boosting import dml_plr_gbdt_panel
+    pan = synthetic_panel(60000, p=37, folds=5, seed=9, dtype="bf16", device=gpu,
+                          dgp="tutorial")
+    a = dml_plr_gbdt_panel(pan, n_trees=6, depth=5)
+    monkeypatch.setattr(G, "FUSED_ROOT", False)
+    b = dml_plr_gbdt_panel(pan, n_trees=6, depth=5)
+    assert a.ate == b.ate and a.se == b.se
