@@ -987,8 +987,12 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
     const char* e = getenv("ATE_GBDT_HIST_TARGET");
     return e ? (int64_t)std::max(64, atoi(e)) : (int64_t)0;
   }();
+  static const int64_t env_rows = [] {
+    const char* e = getenv("ATE_GBDT_HIST_ROWS");
+    return e ? (int64_t)std::max(1024, atoi(e)) : (int64_t)32768;
+  }();
   const int64_t target = env_target ? env_target
-                                    : std::max<int64_t>(512, (rows * ydim + 32767) / 32768);
+                                    : std::max<int64_t>(512, (rows * ydim + env_rows - 1) / env_rows);
   int64_t ch = (rows * ydim + target - 1) / target;
   ch = std::max<int64_t>(1024, (ch + 255) / 256 * 256);
   const int64_t wg = (((n_train + ch - 1) / ch + (1 << d)) + 7) / 8 * 8 * ydim;
@@ -999,7 +1003,13 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
 // fused root pass (gbdt_hist2_kernel): chunk length, chunk count, workgroups
 static void gbdt_hist2_geom(int64_t n_train, int p, int64_t* CH, int64_t* nchunk, int64_t* nwg) {
   const int ydim2 = (p + FB2 - 1) / FB2;
-  const int64_t target = std::max<int64_t>(512, (n_train * ydim2 + 32767) / 32768);
+  // ~R rows per chunk (ATE_GBDT_HIST2_ROWS; config-5 shard, 10 trees: 16384 3.05-3.46 s,
+  // 32768 2.905-2.914, 65536 2.874-2.879, 131072 2.889-2.894; tools/r06_fused3.sh)
+  static const int64_t R = [] {
+    const char* e = getenv("ATE_GBDT_HIST2_ROWS");
+    return e ? (int64_t)std::max(1024, atoi(e)) : (int64_t)65536;
+  }();
+  const int64_t target = std::max<int64_t>(512, (n_train * ydim2 + R - 1) / R);
   int64_t ch = (n_train * ydim2 + target - 1) / target;
   ch = std::max<int64_t>(1024, (ch + 255) / 256 * 256);
   *CH = ch;
