@@ -978,7 +978,7 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
   // (hessian rule) of them below; `target` workgroups of full chunks (two resident per
   // CU; each pays a fixed 64-KB LDS clear + slab store)
   const int64_t rows = (d == 0 || rule == 1) ? n_train : (n_train + 1) / 2;
-  // Chunks of ~32k rows: the ydim workgroups of a chunk read 16-byte slices of the same
+  // Chunks of ~64k rows: the ydim workgroups of a chunk read 16-byte slices of the same
   // row-major lines, and they only share them through L2 while they run close together --
   // short chunks keep them so (config-5 shard, 3 trees: 512 workgroups 4.46 s, 8192-65536
   // workgroups 2.7-3.2 s, the same bits; profiles/r03_cfg5). ATE_GBDT_HIST_TARGET = fixed
@@ -987,9 +987,12 @@ static void gbdt_hist_geom(int64_t n_train, int p, int d, int rule, int64_t* CH,
     const char* e = getenv("ATE_GBDT_HIST_TARGET");
     return e ? (int64_t)std::max(64, atoi(e)) : (int64_t)0;
   }();
+  // ~R rows per chunk (ATE_GBDT_HIST_ROWS; round 6, config-5 shard with the fused root, 10
+  // trees: 16384 3.13-3.58 s, 32768 2.86, 65536 2.77-2.79, 131072 2.81-2.82, 262144
+  // 3.07-3.09; tools/r06_fused4.sh)
   static const int64_t env_rows = [] {
     const char* e = getenv("ATE_GBDT_HIST_ROWS");
-    return e ? (int64_t)std::max(1024, atoi(e)) : (int64_t)32768;
+    return e ? (int64_t)std::max(1024, atoi(e)) : (int64_t)65536;
   }();
   const int64_t target = env_target ? env_target
                                     : std::max<int64_t>(512, (rows * ydim + env_rows - 1) / env_rows);
