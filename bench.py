@@ -134,8 +134,9 @@ def measure_inflight(args, comm, device, pan, inflight, fit_phases, agree, slot_
         slot_comms_cache["slots"] = slot_comms
     slot_comms = slot_comms_cache["slots"]
     # Gram workgroup count beside another fit's path solve (staggered: 824-4096 within 3 %,
-    # 2048 the default; profiles/r02_overlap/stagger_sweep.log)
-    os.environ.setdefault("ATE_GRAM_PAIR_WG", "2048")
+    # profiles/r02_overlap/stagger_sweep.log; with the one-byte columns 1024: 2.98-2.99 ms per
+    # fit, 2048: 3.02-3.04, 2560: 2.98-2.99, 3072: 3.01-3.03, profiles/r06_bench/inflight_wg)
+    os.environ.setdefault("ATE_GRAM_PAIR_WG", "1024")
     # --stagger 2: the Grams of all fits run on one low-priority stream, each fit's remaining
     # phases on its own high-priority stream, so its path solve gets CUs ahead of the next
     # Gram's workgroups (eager stream hooks between the Gram graph and the rest)
