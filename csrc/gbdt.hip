@@ -1077,8 +1077,9 @@ ATE_API int ate_gbdt_pair_root(const void* args_a, const void* args_b, const voi
       hipMemcpyAsync(B.idx[0], idx_root, bytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return -3;
   const dim3 gg((unsigned)((A.n_train + 4 * NT - 1) / (4 * NT)));
-  if (!gh2 || (n0 >= 0 && (a0 < 0 || n0 > A.n_train || a1 < a0 + n0 ||
-                           a1 + (A.n_train - n0) > A.n)))
+  // (rows are int32 in the kernel: a fit holds < 2^31 rows)
+  if (!gh2 || A.n >= (1LL << 31) ||
+      (n0 >= 0 && (a0 < 0 || n0 > A.n_train || a1 < a0 + n0 || a1 + (A.n_train - n0) > A.n)))
     return -1;
   int64_t* g2 = static_cast<int64_t*>(gh2);
   ATE_LAUNCH(gbdt_grad_kernel, gg, dim3(NT), 0, st, A.loss, A.f, A.y, A.idx[0], A.n_train,
