@@ -531,9 +531,11 @@ def dml_repeated_phases(pan, folds: int, repeats: int, lambda_rule="min", comm=N
     The panel holds K*K micro-segments (segment m = K a + b); partition s puts micro-segment m
     in fold (a + s b) mod K (micro_fold_map). So ONE Gram pass gives every partition's fold
     Grams: the K*K micro-Gram stack (K01, C01) is summed per partition into its K fold
-    Grams (a [K, K*K] 0/1 matrix times the stack, fp64), and each partition runs its CV-LASSO
-    paths (K08/K09) and the residual pass with its fold coefficients spread over the
-    micro-segments. Phases as dml_phases (SegmentedStep captures them: one graph at world 1);
+    Grams (a [K, K*K] 0/1 matrix times the stack, fp64). The S partitions' CV-LASSO paths
+    (K08/K09) are ONE path launch over S*K fold Grams (S * K * (K + 1) * 2 problems, each the
+    bits of its own partition's solve), then each partition's residual pass runs with its
+    fold coefficients spread over the micro-segments. Phases as dml_phases (SegmentedStep
+    captures them: one graph at world 1);
     the result state holds "res" [2] (the aggregate) and "splits" [S, 2]. Reference:
     the split-and-average DML of /root/reference/ate_functions.R:372-389, generalised."""
     from ..utils.graphs import Collective
@@ -563,13 +565,22 @@ def dml_repeated_phases(pan, folds: int, repeats: int, lambda_rule="min", comm=N
     def phase_gram_reduce(st):
         return {"G": gram(pan, stage="reduce", out=st["G"])}
 
+    # every partition's fold Grams as one stack of Sn * K segments; partition s's outer fold
+    # k trains on segments s K + j, j != k (disjoint per partition: no shared training set)
+    Mall = torch.cat(M)                                                     # [Sn K, K*K]
+    sets_all = [[s * K + j for j in fs] for s in range(Sn) for fs in full_sets]
+    counts_all = np.concatenate(fold_counts)
+
+    def phase_paths(st):
+        Gs = (Mall @ st["G"].view(K * K, P * P)).view(Sn * K, P, P)
+        cv = cv_enet_gaussian(Gs, pan, pan.xcols, ycols, full_sets=sets_all,
+                              seg_counts=counts_all)
+        coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(Sn, K, 2, -1)
+        return {**st, "coef": coef}
+
     def phase_split(s):
         def f(st):
-            Gs = (M[s] @ st["G"].view(K * K, P * P)).view(K, P, P)
-            cv = cv_enet_gaussian(Gs, pan, pan.xcols, ycols, full_sets=full_sets,
-                                  seg_counts=fold_counts[s])
-            coef = (cv.coef_min if lambda_rule == "min" else cv.coef_1se).reshape(K, 2, -1)
-            coef_m = coef.double().index_select(0, mi[s]).contiguous()
+            coef_m = st["coef"][s].double().index_select(0, mi[s]).contiguous()
             return {**st, f"mom{s}": dml_residual_moments(pan, coef_m)}
         return f
 
@@ -594,6 +605,7 @@ def dml_repeated_phases(pan, folds: int, repeats: int, lambda_rule="min", comm=N
     phases = [phase_gram, phase_gram_reduce]
     if dist:
         phases.append(reduce_sym("G"))
+    phases.append(phase_paths)
     for s in range(Sn):
         phases.append(phase_split(s))
         if dist:
