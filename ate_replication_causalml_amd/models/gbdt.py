@@ -14,6 +14,7 @@ for bit at every world size.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -328,39 +329,6 @@ class _GpuFit:
 
     def __init__(self, Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child,
                  min_gain, edges, dist, dev, slab_min=0):
-        self._init(Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
-                   edges, dist, dev, slab_min)
-
-    def model(self):
-        return GbdtModel(self.feat, self.thr, self.value, self.base, self.loss, self.depth,
-                         self.edges, "gpu", self.f)
-
-    def drive(self, dist):
-        """Run the stepper from its position until it returns 0, servicing the row-sharded
-        fit's pauses: level histograms all-reduced (C04) -- or, feature-sliced, reduce-
-        scattered, and after the slice's split search the candidates all-gathered -- on the
-        same stream (no host callback, no host sync)."""
-        a, st, nr = self.a, self.st, self.nr
-        run = _native.hip().ate_gbdt_run
-        while True:
-            rc = run(ctypes.addressof(a), ctypes.addressof(st),
-                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-            if rc == 0:
-                break
-            if rc not in (1, 2) or dist is None or (rc == 2 and nr == 1):
-                raise RuntimeError(f"ate_gbdt_run failed with status {rc}")
-            self.reduce(dist, rc, st.red_count)
-
-    def reduce(self, dist, rc, m):
-        if rc == 1 and self.nr == 1:
-            dist.sum_(self.Hs[:m])
-        elif rc == 1:
-            dist.comm.reduce_scatter_(self.Hl[:m // self.nr], self.Hs[:m])
-        else:
-            dist.comm.all_gather_into_(self.candg[:self.nr * m], self.cand[:m])
-
-    def _init(self, Xr, ldr, p, y, train, loss, n_trees, depth, lr, lam, min_child, min_gain,
-              edges, dist, dev, slab_min):
         yt = torch.as_tensor(y, device=dev, dtype=torch.float64)
         trn = torch.as_tensor(train, device=dev, dtype=torch.bool)
         n = yt.numel()
@@ -428,10 +396,38 @@ class _GpuFit:
         a.H = (P * 2)(self.H[0].data_ptr(), self.H[1].data_ptr())
         self.a, self.st = a, RunState()
 
+    def model(self):
+        return GbdtModel(self.feat, self.thr, self.value, self.base, self.loss, self.depth,
+                         self.edges, "gpu", self.f)
+
+    def drive(self, dist):
+        """Run the stepper from its position until it returns 0, servicing the row-sharded
+        fit's pauses: level histograms all-reduced (C04) -- or, feature-sliced, reduce-
+        scattered, and after the slice's split search the candidates all-gathered -- on the
+        same stream (no host callback, no host sync)."""
+        a, st, nr = self.a, self.st, self.nr
+        run = _native.hip().ate_gbdt_run
+        while True:
+            rc = run(ctypes.addressof(a), ctypes.addressof(st),
+                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            if rc == 0:
+                break
+            if rc not in (1, 2) or dist is None or (rc == 2 and nr == 1):
+                raise RuntimeError(f"ate_gbdt_run failed with status {rc}")
+            self.reduce(dist, rc, st.red_count)
+
+    def reduce(self, dist, rc, m):
+        if rc == 1 and self.nr == 1:
+            dist.sum_(self.Hs[:m])
+        elif rc == 1:
+            dist.comm.reduce_scatter_(self.Hl[:m // self.nr], self.Hs[:m])
+        else:
+            dist.comm.all_gather_into_(self.candg[:self.nr * m], self.cand[:m])
+
 
 # Lockstep pair fits with a fused root histogram pass (fit_gbdt_pair); ATE_GBDT_FUSED_ROOT=0
 # fits a pair one after the other (the A/B of profiles/r06_cfg5)
-FUSED_ROOT = __import__("os").environ.get("ATE_GBDT_FUSED_ROOT", "1") == "1"
+FUSED_ROOT = os.environ.get("ATE_GBDT_FUSED_ROOT", "1") == "1"
 
 
 def _two_ranges(rows):
