@@ -243,7 +243,6 @@ def c04_slices(p, dist):
     (rank r owns [r * pw, min(p, r * pw + pw))), or (1, p) for a single device, when
     ATE_GBDT_C04=allreduce, or when some rank's slice would be empty (p small next to
     the world size)."""
-    import os
     if dist is None or dist.world == 1 or os.environ.get("ATE_GBDT_C04", "") == "allreduce":
         return 1, p
     w = dist.world
