@@ -27,7 +27,9 @@ panel, captured as the library runs it (one stream, the default Gram plan). The 
 steps are K such calls back to back on one stream; stream order serialises them, so no
 two fits overlap. ``value`` = N / ms_per_step. ``single_fit_ms`` is the median of >= 5
 replays each bracketed by device syncs (the §7.5 latency). The panel uses the 64-row
-blocked layout (``--blocked 1``). With RCCL the all-reduces (C01 Gram stack, C08
+blocked layout (``--blocked 1``) with its 128 exactly-{0,1} columns also stored as bytes
+(``layout`` "blocked64+bytes8": the Gram reads 896 instead of 1,024 bytes per row, the
+same bits; data/device_dgp.py). With RCCL the all-reduces (C01 Gram stack, C08
 coefficients, C06 moments) are captured inside the call's graph
 (utils/graphs.SegmentedStep); if capture of the collectives fails they run eagerly between
 graph segments and the JSON says so (``collectives_captured``).
@@ -35,6 +37,9 @@ graph segments and the JSON says so (``collectives_captured``).
 Secondary, reported under ``throughput_inflight`` and never as ``value``: ``--inflight 3``
 identical calls overlapped on streams (each fit's Gram on one low-priority stream beside
 another fit's latency-bound path solve), with a check that they return the same bits.
+Secondary, under ``repeated`` (world 1, ``--repeats 3``): ``ate_dml(repeats=3)``, three
+DISTINCT 5-fold partitions of 25 micro-segments from one Gram pass and one path launch,
+median-aggregated (Chernozhukov et al. 2018 §3.4); the JSON lists the split ATEs.
 
 Parity (``--parity 1``, untimed): the same kept rows as a float64 panel, fp64 Gram and
 fp64 path solves; the JSON reports |dATE| / SE_f64 and the relative SE difference.
