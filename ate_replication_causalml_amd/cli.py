@@ -38,13 +38,24 @@ def _replicate(a):
 def _dml(a):
     import torch
     from .data.device_dgp import synthetic_panel
-    from .estimators.lasso import dml_crossfit_panel
+    from .estimators.lasso import dml_crossfit_panel, dml_repeated_panel
     from .estimators.common import read_result
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    pan = synthetic_panel(a.n, p=a.p, folds=a.folds, seed=a.seed, dtype=a.dtype, device=dev)
-    res, mom, cv = dml_crossfit_panel(pan, a.folds, a.lambda_rule)
-    r = read_result(res, "DML cross-fit (LASSO)", n=a.n)
-    print(json.dumps({"ate": r.ate, "se": r.se, "lower_ci": r.lower_ci, "upper_ci": r.upper_ci}))
+    if a.repeats > 1:
+        # repeated cross-fitting: K*K micro-segments, `repeats` distinct K-fold partitions
+        pan = synthetic_panel(a.n, p=a.p, folds=a.folds * a.folds, seed=a.seed, dtype=a.dtype,
+                              device=dev)
+        res, splits = dml_repeated_panel(pan, a.folds, a.repeats, a.lambda_rule,
+                                         aggregate=a.aggregate)
+        r = read_result(res, "DML cross-fit (LASSO, repeated)", n=a.n)
+        out = {"ate": r.ate, "se": r.se, "lower_ci": r.lower_ci, "upper_ci": r.upper_ci,
+               "repeats": a.repeats, "splits": splits.cpu().tolist()}
+    else:
+        pan = synthetic_panel(a.n, p=a.p, folds=a.folds, seed=a.seed, dtype=a.dtype, device=dev)
+        res, mom, cv = dml_crossfit_panel(pan, a.folds, a.lambda_rule)
+        r = read_result(res, "DML cross-fit (LASSO)", n=a.n)
+        out = {"ate": r.ate, "se": r.se, "lower_ci": r.lower_ci, "upper_ci": r.upper_ci}
+    print(json.dumps(out))
     return 0
 
 
@@ -84,6 +95,9 @@ def main(argv=None):
     d.add_argument("--dtype", default="bf16")
     d.add_argument("--seed", type=int, default=7)
     d.add_argument("--lambda-rule", default="min", choices=["min", "1se"])
+    d.add_argument("--repeats", type=int, default=1,
+                   help="> 1: repeated cross-fitting over that many distinct K-fold partitions")
+    d.add_argument("--aggregate", default="median", choices=["median", "mean"])
     d.set_defaults(fn=_dml)
     b = sub.add_parser("build")
     b.set_defaults(fn=_build)

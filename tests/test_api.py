@@ -77,6 +77,17 @@ def test_cli_replicate(tmp_path, capsys):
     assert "oracle" in capsys.readouterr().out
 
 
+def test_cli_dml_repeated(capsys):
+    """`dml --repeats 3`: three distinct partitions of 25 micro-segments, median-aggregated;
+    the aggregate is the median split ATE."""
+    import json
+    from ate_replication_causalml_amd.cli import main
+    rc = main(["dml", "--n", "12000", "--p", "24", "--dtype", "f64", "--repeats", "3"])
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert rc == 0 and out["repeats"] == 3 and len(out["splits"]) == 3
+    assert out["ate"] == sorted(s[0] for s in out["splits"])[1]
+
+
 def test_loader_reads_social_pressure_layout(tmp_path):
     """The CSV loader on a synthetic file with the reference's column names."""
     import pandas as pd
