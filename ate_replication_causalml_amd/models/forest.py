@@ -252,6 +252,22 @@ class Forest:
     Xb_train: object = None
     packed: object = None        # GPU: int2 per node (see csrc/forest.hip forest_pack_kernel)
     exact: ExactBins | None = None   # exact-split forests: uint16 value-rank bins
+    # GPU exact-split fits: (device count of trees with nnodes = -1, ntree, mc), checked at the
+    # first host read (check()), so that the fit itself never waits for the device
+    overflow: object = None
+
+    def check(self):
+        """Raise if the exact-split fit flagged trees whose in-bag count exceeded the host's
+        bound mc (csrc/forest_exact.hip sets nnodes = -1; exact_mcap is exact, so never
+        expected). Runs once, at the first host read of the forest's outputs."""
+        if self.overflow is None:
+            return
+        cnt, ntree, mc = self.overflow
+        self.overflow = None
+        bad = int(cnt)
+        if bad:
+            raise RuntimeError(f"exact forest: {bad} of {ntree} trees overflowed the in-bag "
+                               f"bound mc = {mc} (models/forest.exact_mcap)")
 
     @property
     def device(self):
@@ -309,6 +325,7 @@ class Forest:
                 if not host:
                     return out.view(n2, width) if width > 1 else out
                 res = out.cpu().numpy()
+                self.check()
                 return res.reshape(n2, width) if width > 1 else res
             if self.packed is None:
                 self.packed = torch.zeros(self.params.ntree * self.cap * 2, dtype=torch.int32,
@@ -366,6 +383,7 @@ class Forest:
 
     def tree_arrays(self):
         """(feat, thr, left, val, nnodes) as numpy (for parity tests)."""
+        self.check()
         f = lambda a: a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
         return f(self.feat), f(self.thr), f(self.left), f(self.val), f(self.nnodes)
 
@@ -629,17 +647,15 @@ def fit_forest_exact(Xb, eb, kind: int, y=None, r1=None, r2=None, ntree=500, mtr
                          val.data_ptr(), nnodes.data_ptr(), inbag.data_ptr(), p_(est),
                          scratch.data_ptr(), s)
         del scratch
-        if not torch.cuda.is_current_stream_capturing():
-            # a tree whose in-bag count exceeded the host's bound mc returns nnodes = -1
-            # (csrc/forest_exact.hip; exact_mcap is exact, so never expected): an empty tree
-            # must not pass silently (inside a graph capture the check runs on the eager
-            # first call of the estimator instead)
-            bad = int((nnodes < 0).sum())
-            if bad:
-                raise RuntimeError(f"exact forest: {bad} of {ntree} trees overflowed the in-bag "
-                                   f"bound mc = {mc} (models/forest.exact_mcap)")
+        # a tree whose in-bag count exceeded the host's bound mc returns nnodes = -1: an empty
+        # tree must not pass silently. The count stays on the device and Forest.check() reads
+        # it at the first host read (a host sync here made the next fit's host-side set-up
+        # wait for this fit: config 4 0.71 -> 0.78-0.82 s). Inside a graph capture the check
+        # runs on the eager first call of the estimator instead.
+        ovf = None if torch.cuda.is_current_stream_capturing() else \
+            ((nnodes < 0).sum(), ntree, mc)
         return Forest(fp, "gpu", cap, feat, thr, left, val, nnodes, inbag, est, None, None, Xb,
-                      exact=eb)
+                      exact=eb, overflow=ovf)
     Xbn = np.ascontiguousarray(h(Xb), dtype=np.uint16)
     ycls = None if y is None else h(y).astype(np.uint8)
     r1f = None if r1 is None else to_fix(h(r1))

@@ -357,3 +357,22 @@ def test_auto_splits_bound_the_exact_list_scratch():
     assert F.resolve_splits("auto", 65_536) == "exact"          # p unknown: rows only
     assert F.resolve_splits("exact", 65_536, 512) == "exact"
     assert F.exact_list_bytes(65_536, 512) == 268_435_456
+
+
+def test_exact_overflow_flag_raises_at_first_host_read():
+    """GPU exact-split fits keep the count of overflowed trees (nnodes = -1) on the device and
+    Forest.check() raises at the first host read of the outputs (predict_raw, tree_arrays),
+    so the fit itself never waits for the device; a clean count passes once and is dropped."""
+    import dataclasses
+    import torch
+    rs = np.random.RandomState(0)
+    X = rs.randn(300, 4)
+    y = (X[:, 0] > 0).astype(float)
+    fr = F.fit_forest(X, F.KIND_CLASS, y=y, ntree=4, seed=1, backend="cpu")
+    bad = dataclasses.replace(fr, overflow=(torch.tensor(2), 4, 100))
+    with pytest.raises(RuntimeError, match="2 of 4 trees overflowed"):
+        bad.tree_arrays()
+    assert bad.overflow is None
+    ok = dataclasses.replace(fr, overflow=(torch.tensor(0), 4, 100))
+    ok.tree_arrays()
+    assert ok.overflow is None
